@@ -1,0 +1,165 @@
+// ref_driver.cc -- our own driver over the REFERENCE libmerc (compiled from
+// /root/reference by oracle/Makefile.ref into oracle/_ref/merc_ref_drv).
+// Test infrastructure only: it produces golden vectors and times the
+// reference CPU path; nothing in mercury_amd/ links or calls it.
+//
+// Input: a classic pcap file, or our batch format (see tests/pcaplib.py:
+// "MFPB" magic, n, then n x {u64 off,u32 caplen,u16 linktype,u16 flags},
+// then the arena).
+// Output (mode "fp"): one TSV line per packet:
+//   idx  emit  fp_type  truncated  fp_string
+// Output (mode "an"): analysis_context path, one TSV line per packet:
+//   idx  valid  fp_type  status  process  score  malware  p_malware  fp_string
+// Mode "time": run write_json with T threads (one processor per thread over
+// contiguous shards), print packets/s.
+//
+// Uses the reference's public C API (libmerc.h:211-736) plus the processor's
+// analysis context (pkt_proc.h:132), exactly as the reference's own unit-test
+// fixture does (unit_tests/libmerc_fixture.cc:138).
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <thread>
+#include <chrono>
+#include "libmerc.h"
+#include "pkt_proc.h"
+
+struct pkt { const uint8_t *data; uint32_t len; uint16_t linktype; };
+
+static std::vector<uint8_t> slurp(const char *fn) {
+    std::vector<uint8_t> v;
+    FILE *f = fopen(fn, "rb");
+    if (!f) { perror(fn); exit(1); }
+    fseek(f, 0, SEEK_END); long n = ftell(f); fseek(f, 0, SEEK_SET);
+    v.resize(n);
+    if (n && fread(v.data(), 1, n, f) != (size_t)n) { perror("fread"); exit(1); }
+    fclose(f);
+    return v;
+}
+
+static std::vector<pkt> load(const std::vector<uint8_t> &buf) {
+    std::vector<pkt> out;
+    if (buf.size() >= 4 && memcmp(buf.data(), "MFPB", 4) == 0) {
+        uint64_t n; memcpy(&n, buf.data() + 8, 8);
+        const uint8_t *d = buf.data() + 16;
+        const uint8_t *arena = d + n * 16;
+        for (uint64_t i = 0; i < n; i++) {
+            uint64_t off; uint32_t cl; uint16_t lt;
+            memcpy(&off, d + 16 * i, 8); memcpy(&cl, d + 16 * i + 8, 4); memcpy(&lt, d + 16 * i + 12, 2);
+            out.push_back({arena + off, cl, lt});
+        }
+        return out;
+    }
+    // classic pcap
+    if (buf.size() < 24) { fprintf(stderr, "short pcap\n"); exit(1); }
+    uint32_t magic; memcpy(&magic, buf.data(), 4);
+    bool swap = (magic == 0xd4c3b2a1 || magic == 0x4d3cb2a1);
+    auto rd32 = [&](const uint8_t *p) { uint32_t x; memcpy(&x, p, 4); return swap ? __builtin_bswap32(x) : x; };
+    uint16_t lt = (uint16_t)rd32(buf.data() + 20);
+    size_t o = 24;
+    while (o + 16 <= buf.size()) {
+        uint32_t incl = rd32(buf.data() + o + 8);
+        o += 16;
+        if (o + incl > buf.size()) break;
+        out.push_back({buf.data() + o, incl, lt});
+        o += incl;
+    }
+    return out;
+}
+
+static int quiet(enum log_level, const char *, va_list) { return 0; }
+
+int main(int argc, char **argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: %s fp|an|time <input> <config-string> [resources] [threads] [seconds]\n", argv[0]);
+        return 2;
+    }
+    std::string mode = argv[1];
+    auto buf = slurp(argv[2]);
+    auto pkts = load(buf);
+    register_printf_err_callback(quiet);
+
+    libmerc_config cfg{};
+    std::string filt = argv[3];
+    cfg.packet_filter_cfg = (char *)filt.c_str();
+    std::string res;
+    if (argc > 4 && strlen(argv[4]) > 0 && strcmp(argv[4], "-") != 0) {
+        res = argv[4];
+        cfg.resources = (char *)res.c_str();
+        cfg.do_analysis = true;
+    }
+    mercury_context mc = mercury_init(&cfg, 0);
+    if (!mc) { fprintf(stderr, "mercury_init failed\n"); return 1; }
+
+    std::vector<char> out(1 << 16);
+    if (mode == "fp") {
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        for (size_t i = 0; i < pkts.size(); i++) {
+            struct timespec ts{1700000000, 0};
+            size_t n = mercury_packet_processor_write_json_linktype(p, out.data(), out.size(),
+                                                                   (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
+            std::string json(out.data(), n);
+            bool trunc = json.find("\"reassembly_properties\":{\"truncated\":true}") != std::string::npos;
+            // the processor's fingerprint is only (re)computed for packets that
+            // reach ip_write_json and emit a record (pkt_proc.cc:1157-1158)
+            int t = n > 0 ? p->analysis.fp.get_type() : 0;
+            printf("%zu\t%d\t%d\t%d\t%s\n", i, n > 0, t, (int)trunc, t ? p->analysis.fp.string() : "");
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "an") {
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        for (size_t i = 0; i < pkts.size(); i++) {
+            struct timespec ts{1700000000, 0};
+            const analysis_context *ac = mercury_packet_processor_get_analysis_context_linktype(
+                p, (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
+            if (!ac) {
+                int t = p->analysis.fp.get_type();
+                printf("%zu\t0\t%d\t0\t\t0\t0\t0\t%s\n", i, t, t ? p->analysis.fp.string() : "");
+                continue;
+            }
+            const char *proc = ""; double score = 0; bool mal = false; double pm = 0;
+            analysis_context_get_process_info(ac, &proc, &score);
+            analysis_context_get_malware_info(ac, &mal, &pm);
+            printf("%zu\t1\t%d\t%d\t%s\t%.17g\t%d\t%.17g\t%s\n", i,
+                   (int)analysis_context_get_fingerprint_type(ac),
+                   (int)analysis_context_get_fingerprint_status(ac),
+                   proc ? proc : "", score, (int)mal, pm,
+                   analysis_context_get_fingerprint_string(ac));
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "time") {
+        int threads = argc > 5 ? atoi(argv[5]) : 1;
+        double secs = argc > 6 ? atof(argv[6]) : 10.0;
+        std::vector<std::thread> th;
+        std::vector<unsigned long long> counts(threads, 0);
+        auto t0 = std::chrono::steady_clock::now();
+        for (int t = 0; t < threads; t++) {
+            th.emplace_back([&, t]() {
+                mercury_packet_processor p = mercury_packet_processor_construct(mc);
+                std::vector<char> o(1 << 16);
+                size_t lo = pkts.size() * t / threads, hi = pkts.size() * (t + 1) / threads;
+                unsigned long long c = 0;
+                auto start = std::chrono::steady_clock::now();
+                do {
+                    for (size_t i = lo; i < hi; i++) {
+                        struct timespec ts{1700000000, 0};
+                        mercury_packet_processor_write_json_linktype(p, o.data(), o.size(), (uint8_t *)pkts[i].data,
+                                                                     pkts[i].len, &ts, pkts[i].linktype);
+                    }
+                    c += hi - lo;
+                } while (std::chrono::duration<double>(std::chrono::steady_clock::now() - start).count() < secs);
+                counts[t] = c;
+                mercury_packet_processor_destruct(p);
+            });
+        }
+        for (auto &x : th) x.join();
+        double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        unsigned long long tot = 0; for (auto c : counts) tot += c;
+        printf("{\"threads\": %d, \"packets\": %llu, \"seconds\": %.6f, \"pps\": %.1f}\n", threads, tot, el, tot / el);
+    }
+    mercury_finalize(mc);
+    return 0;
+}
