@@ -1,0 +1,116 @@
+/*
+ * mfp.h -- C-ABI of libmercury_amd.so, the MI355X-native packet
+ * fingerprint/classify path.  Plain pointers and sizes only.
+ *
+ * Two layers:
+ *  1. the BATCH API below (mfp_*): packet batches in HBM or host memory,
+ *     one launch per batch; this is what the libmerc per-packet shims
+ *     (include/mercury_amd_libmerc.h) and our host pipeline call;
+ *  2. libmerc-compatible per-packet symbols, declared in
+ *     include/mercury_amd_libmerc.h, replacing src/libmerc/libmerc.h.
+ *
+ * The batch entry point replaces the reference's per-packet plugin call
+ * pkt_proc::apply(packet_info*, uint8_t*) (src/pkt_proc.hpp:26-33) as driven
+ * by pcap_file_dispatch_pkt_processor (src/pcap_file_io.c:470-512) and
+ * process_all_packets_in_block (src/af_packet_v3.c:174-210): instead of one
+ * C-ABI crossing per packet, the caller fills an arena + descriptor array
+ * and crosses once per batch.
+ */
+#ifndef MFP_H
+#define MFP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MFP_EXPORT __attribute__((visibility("default")))
+
+/* One packet of a batch (16 bytes).  `offset` is the byte offset of the
+ * captured frame in the arena; `linktype` is the pcap LINKTYPE (1 Ethernet,
+ * 9 PPP, 101 raw IP, 113 Linux SLL, 276 Linux SLL2, 0 BSD loopback), as in
+ * mercury_packet_processor_write_json_linktype (libmerc.h:293). */
+typedef struct {
+    uint64_t offset;
+    uint32_t caplen;
+    uint16_t linktype;
+    uint16_t flags;      /* reserved, 0 */
+} mfp_pkt_desc;
+
+/* Per-packet result (32 bytes). */
+typedef struct {
+    uint64_t fp_offset;  /* fingerprint string offset in the fp arena    */
+    uint32_t fp_len;     /* string length (no NUL), 0 when fp_type == 0  */
+    uint8_t  fp_type;    /* enum fingerprint_type (libmerc.h:351-373)     */
+    uint8_t  msg;        /* protocol tag, MFP_MSG_*                       */
+    uint8_t  flags;      /* MFP_FLAG_*                                    */
+    uint8_t  status;     /* enum fingerprint_status (libmerc.h:307-313)   */
+    /* classifier inputs (destination_context, result.h:346): offsets are
+     * relative to the packet start, len 0xffff = absent */
+    uint16_t sni_off, sni_len;
+    uint16_t ua_off, ua_len;
+    uint16_t src_port, dst_port;   /* host byte order */
+    uint32_t reserved;
+} mfp_record;
+
+enum {
+    MFP_FLAG_EMIT      = 1,  /* the reference's write_json emits a record   */
+    MFP_FLAG_TRUNCATED = 2,  /* reassembly_properties.truncated             */
+};
+
+enum {
+    MFP_MSG_NONE = 0, MFP_MSG_TLS_CH, MFP_MSG_TLS_SH, MFP_MSG_TLS_CERT,
+    MFP_MSG_SSH_INIT, MFP_MSG_SSH_KEX, MFP_MSG_HTTP_REQ, MFP_MSG_HTTP_RESP,
+    MFP_MSG_TCP_SYN, MFP_MSG_TCP_SYNACK, MFP_MSG_DTLS_CH, MFP_MSG_DTLS_SH,
+    MFP_MSG_DTLS_HVR,
+};
+
+/* semantics of the reference entry point to follow */
+enum {
+    MFP_MODE_WRITE_JSON = 0,  /* stateful_pkt_proc::write_json (pkt_proc.cc:1063)      */
+    MFP_MODE_ANALYSIS   = 1,  /* stateful_pkt_proc::analyze_ip_packet (pkt_proc.cc:1597) */
+};
+
+typedef struct mfp_context_s *mfp_context;
+
+/* Create a context on HIP device `device`.  `packet_filter_cfg` uses the
+ * reference's syntax (global_config.h:143-153): a bare protocol list, or
+ * "key=value;..." with select=/format=.  Supported selections: tls,
+ * tls.client_hello, tls.server_hello, tls.server_certificate, ssh,
+ * ssh.client, ssh.server, http, http.request, http.response, tcp,
+ * tcp.syn_ack, dtls; NULL/""/"all" select all of these.  Returns NULL on
+ * error (unknown protocol, no HIP device, extension not loadable). */
+MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode);
+MFP_EXPORT void mfp_finalize(mfp_context ctx);
+
+/* Device-resident batch: all pointers are device (HBM) pointers.  The fp
+ * arena receives the fingerprint strings (compact, each packet's string at
+ * rec[i].fp_offset; tile order, not packet order).  *d_fp_used (device u64,
+ * zeroed by the call) receives the bytes used.  `stream` is a hipStream_t
+ * (NULL = default stream).  The call is asynchronous; returns 0 or a
+ * negative error.  fp_cap must be >= mfp_fp_arena_bound(...). */
+MFP_EXPORT int mfp_process_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
+                                        size_t n, mfp_record *d_rec, char *d_fp_arena, size_t fp_cap,
+                                        uint64_t *d_fp_used, void *stream);
+
+/* Host batch: copies arena/descriptors to the device, runs, copies back.
+ * Synchronous.  Returns bytes of fp arena used, or a negative error. */
+MFP_EXPORT long long mfp_process_batch_host(mfp_context ctx, const uint8_t *arena, size_t arena_len,
+                                            const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                            char *fp_arena, size_t fp_cap);
+
+/* Upper bound on fp-arena bytes for packets totalling `total_caplen` bytes. */
+MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen);
+
+/* last error string for this thread */
+MFP_EXPORT const char *mfp_last_error(void);
+
+/* version: 0x00MMmmpp of the reference semantics implemented (2.18.0) */
+MFP_EXPORT uint32_t mfp_reference_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,46 @@
+"""In-tree build of libmercury_amd.so (hipcc, gfx950).  The built library is
+git-ignored and travels to the GPU box with the working-tree snapshot."""
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libmercury_amd.so")
+OBJ = os.path.join(HERE, "_obj")
+
+SOURCES = ["mfp_kernels.hip", "mfp_host.cpp"]
+HEADERS = ["mfp_device.hpp", "mfp_internal.h"]
+ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "mfp.h")]
+    objs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s + ".o")
+        objs.append(obj)
+        if _newer(obj, [src] + hdrs):
+            cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+                   "-Wall", "-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+    if _newer(LIB, objs):
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

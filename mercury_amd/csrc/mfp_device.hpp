@@ -1,0 +1,1289 @@
+// mfp_device.hpp -- device-side (gfx950) packet walk and fingerprint
+// construction for the MI355X-native mercury path.
+//
+// One lane owns one packet.  The same walker runs twice per tile:
+//   pass 1 (EMIT=false): protocol identification + exact fingerprint length;
+//   pass 2 (EMIT=true):  writes the fingerprint bytes with 8-byte
+//                        write-combined stores into the tile's arena slice.
+// Semantics follow the reference exactly (file:line cites are relative to
+// /root/reference/src/libmerc/); the C oracle (oracle/mfp_oracle.c) restates
+// the same rules on the CPU and the parity tests compare the two.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mfp.h"
+
+namespace mfp {
+
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------
+// cursor == struct datum (datum.h:220-850); null cursor has d == nullptr
+// ---------------------------------------------------------------------------
+struct Cur {
+    const uint8_t *d, *e;
+};
+
+DEV long clen(Cur c) { return c.d ? (long)(c.e - c.d) : 0; }
+DEV bool cnull(Cur c) { return c.d == nullptr; }
+DEV bool cnotempty(Cur c) { return c.d != nullptr && c.d < c.e; }
+DEV void cset_null(Cur &c) { c.d = c.e = nullptr; }
+DEV Cur cmk(const uint8_t *d, const uint8_t *e) { Cur c; c.d = d; c.e = e; return c; }
+
+DEV uint32_t ld(const uint8_t *p) { return *p; }
+
+DEV bool cskip(Cur &c, long n) {                       // datum::skip datum.h:365
+    if (!c.d) return false;
+    if (n > c.e - c.d) { c.d = c.e; return false; }
+    c.d += n;
+    return true;
+}
+DEV void cparse(Cur &dst, Cur &r, long n) {            // datum::parse datum.h:294
+    if (clen(r) < n || n < 0) { cset_null(r); cset_null(dst); return; }
+    dst.d = r.d; dst.e = r.d ? r.d + n : nullptr;
+    if (r.d) r.d += n;
+}
+DEV void cparse_soft(Cur &dst, Cur &r, long n) {       // datum::parse_soft_fail datum.h:305
+    long l = clen(r);
+    if (l < n) n = l;
+    dst.d = r.d; dst.e = r.d ? r.d + n : nullptr;
+    if (r.d) r.d += n;
+}
+DEV bool rd_uint(Cur &c, int n, uint64_t &out) {      // datum::read_uint datum.h:795
+    if (c.d && c.d + n <= c.e) {
+        uint64_t v = 0;
+        for (int i = 0; i < n; i++) v = (v << 8) | ld(c.d + i);
+        c.d += n; out = v; return true;
+    }
+    cset_null(c); out = 0; return false;
+}
+DEV uint32_t rd_u8(Cur &c) {                           // datum::read_uint8 datum.h:749
+    if (c.d && c.e > c.d) { uint32_t v = ld(c.d); c.d += 1; return v; }
+    cset_null(c); return 0;
+}
+DEV uint32_t look_u8(Cur &c) {                         // datum::lookahead_uint8 datum.h:702
+    if (c.d && c.e > c.d) return ld(c.d);
+    cset_null(c); return 0;
+}
+DEV bool look_uint(Cur &c, int n, uint64_t &out) {    // datum::lookahead_uint datum.h:712
+    if (c.d && c.d + n <= c.e) {
+        uint64_t v = 0;
+        for (int i = 0; i < n; i++) v = (v << 8) | ld(c.d + i);
+        out = v; return true;
+    }
+    return false;
+}
+DEV void cinit_outer(Cur &dst, Cur &outer, uint64_t len) {  // datum::init_from_outer_parser datum.h:825
+    if (!cnotempty(outer)) return;
+    const uint8_t *end = (len > (uint64_t)(outer.e - outer.d)) ? outer.e : outer.d + len;
+    dst.d = outer.d; dst.e = end; outer.d = end;
+}
+DEV const uint8_t *cget_ptr(Cur &c, long n) {          // datum::get_pointer datum.h:737
+    if (c.d && c.d + n <= c.e) { const uint8_t *p = c.d; c.d += n; return p; }
+    return nullptr;
+}
+DEV void ctrim_to_length(Cur &c, long len) {           // datum::trim_to_length datum.h:383
+    if (c.d && len <= (long)(c.e - c.d)) c.e = c.d + len;
+}
+DEV void cparse_to_delim(Cur &dst, Cur &r, uint8_t delim) {   // datum::parse_up_to_delim datum.h:313
+    if (!cnotempty(r)) { cset_null(r); cset_null(dst); return; }
+    dst.d = r.d;
+    for (const uint8_t *p = r.d; p < r.e; p++) {
+        if (ld(p) == delim) { dst.e = r.d = p; return; }
+    }
+    dst.e = r.e;
+}
+DEV uint32_t cparse_to_delims(Cur &dst, Cur &r, uint8_t d1, uint8_t d2) {   // datum.h:328
+    dst.d = r.d;
+    if (r.d) {
+        while (r.d < r.e) {
+            uint32_t c = ld(r.d);
+            if (c == d1) { dst.e = r.d; return d1; }
+            if (c == d2) { dst.e = r.d; return d2; }
+            r.d++;
+        }
+    }
+    dst.e = r.e;
+    return 0;
+}
+DEV bool ccompare_n(Cur c, const uint8_t *x, long n) {        // datum::compare_nbytes datum.h:873
+    if (!(c.d && clen(c) >= n)) return false;
+    for (long i = 0; i < n; i++) if (ld(c.d + i) != ld(x + i)) return false;
+    return true;
+}
+DEV int ccmp(Cur a, Cur b) {                                   // datum::cmp datum.h:456
+    if (cnull(a)) return cnull(b) ? 0 : -1;
+    if (cnull(b)) return 1;
+    long la = clen(a), lb = clen(b), m = la < lb ? la : lb;
+    for (long i = 0; i < m; i++) {
+        int x = (int)ld(a.d + i), y = (int)ld(b.d + i);
+        if (x != y) return x - y;
+    }
+    return (int)(la - lb);
+}
+DEV bool c_isupper(uint32_t c) { return c >= 'A' && c <= 'Z'; }
+DEV bool c_isalpha(uint32_t c) { return ((c | 0x20) >= 'a') && ((c | 0x20) <= 'z'); }
+DEV uint32_t c_tolower(uint32_t c) { return c_isupper(c) ? c + 32 : c; }
+
+// ---------------------------------------------------------------------------
+// emitter: restates buffer_stream's truncation rule (buffer_stream.h:100-240)
+// as a length count in pass 1; in pass 2 writes bytes with 8-byte stores
+// ---------------------------------------------------------------------------
+constexpr uint32_t FP_MAX = 8192;   // fingerprint::MAX_FP_STR_LEN fingerprint.h:15
+
+template <bool EMIT>
+struct Em {
+    uint32_t n = 0;          // bytes produced
+    bool last_putc = false;
+    static constexpr bool emit_pass() { return EMIT; }
+    // pass-2 write combining
+    uint8_t *out = nullptr;  // string start
+    uint64_t acc = 0;        // staged bytes of the current aligned word
+    uint32_t nacc = 0;       // bytes staged (including skipped lead bytes)
+    uintptr_t word = 0;      // aligned address of the staged word
+    uint32_t lead = 0;       // bytes of the first word not owned by us
+
+    DEV void begin(uint8_t *o) {
+        out = o;
+        uintptr_t a = (uintptr_t)o;
+        word = a & ~(uintptr_t)7;
+        lead = (uint32_t)(a & 7);
+        nacc = lead;
+        acc = 0;
+    }
+    DEV void flush_word(uint32_t upto) {       // write bytes [lead, upto) of word
+        if (lead == 0 && upto == 8) {
+            *(uint64_t *)word = acc;
+        } else {
+            for (uint32_t i = lead; i < upto; i++) ((uint8_t *)word)[i] = (uint8_t)(acc >> (8 * i));
+        }
+    }
+    DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v
+        if (EMIT) {
+            uint32_t room = 8 - nacc;
+            if (k < room) {
+                acc |= v << (8 * nacc);
+                nacc += k;
+            } else {
+                acc |= (room == 8) ? v : (v << (8 * nacc));
+                flush_word(8);
+                word += 8; lead = 0;
+                uint32_t rest = k - room;
+                acc = rest ? (v >> (8 * room)) : 0;
+                nacc = rest;
+            }
+        }
+        n += k;
+    }
+    DEV void finish() {
+        if (EMIT && nacc > lead) flush_word(nacc);
+    }
+    DEV void putc(uint32_t c) { push(c & 0xff, 1); last_putc = true; }
+    DEV static uint64_t hex2(uint32_t b) {
+        uint32_t hi = b >> 4, lo = b & 15;
+        uint32_t ch = hi + (hi < 10 ? '0' : 'a' - 10);
+        uint32_t cl = lo + (lo < 10 ? '0' : 'a' - 10);
+        return (uint64_t)ch | ((uint64_t)cl << 8);
+    }
+    // raw_as_hex buffer_stream.h:1087 (NULL data -> nothing)
+    DEV void hex(const uint8_t *p, long len) {
+        if (!p || len <= 0) return;
+        last_putc = false;
+        if (!EMIT) { n += (uint32_t)(2 * len); return; }
+        long i = 0;
+        for (; i + 4 <= len; i += 4) {
+            uint64_t v = hex2(ld(p + i)) | (hex2(ld(p + i + 1)) << 16) | (hex2(ld(p + i + 2)) << 32) |
+                         (hex2(ld(p + i + 3)) << 48);
+            push(v, 8);
+        }
+        for (; i < len; i++) push(hex2(ld(p + i)), 2);
+    }
+    DEV void hex16(uint32_t v) {                // append_uint16_hex buffer_stream.h:425
+        last_putc = false;
+        uint64_t w = hex2((v >> 8) & 0xff) | (hex2(v & 0xff) << 16);
+        push(w, 4);
+    }
+    DEV void hex8(uint32_t v) { last_putc = false; push(hex2(v & 0xff), 2); }
+    DEV void lit(const char *s) {               // puts (strncpy) of a literal
+        last_putc = false;
+        for (; *s; s++) push((uint8_t)*s, 1);
+    }
+    // valid iff no append truncated: end <= 8190, or 8191 reached by putc
+    DEV bool valid() const { return n <= FP_MAX - 2 || (n == FP_MAX - 1 && last_putc); }
+};
+
+// ---------------------------------------------------------------------------
+// TLS (tls.h)
+// ---------------------------------------------------------------------------
+DEV uint32_t degrease16(uint32_t x) {                   // degrease_uint16 tls.h:776
+    if ((x & 0x0f0f) == 0x0a0a && ((x >> 12) == ((x >> 4) & 15))) return 0x0a0a;
+    return x;
+}
+template <class E>
+DEV void hex_degrease(E &b, const uint8_t *p, long len) {   // raw_as_hex_degrease tls.h:802
+    if (len % 2) len--;
+    for (long i = 0; i < len; i += 2) b.hex16(degrease16((ld(p + i) << 8) | ld(p + i + 1)));
+}
+DEV bool is_static_ext(uint32_t t) {                    // static_extension_types tls.h:1000
+    switch (t) {
+    case 1: case 5: case 7: case 8: case 9: case 10: case 11: case 13: case 15: case 16: case 17:
+    case 24: case 27: case 28: case 0x39: case 43: case 45: case 50: case 21760: case 0xffa5:
+        return true;
+    }
+    return false;
+}
+struct Ext {
+    uint32_t type, length, encoded_type;
+    const uint8_t *type_ptr, *length_ptr;
+    Cur value;
+    bool ok;
+};
+DEV Ext ext_parse(Cur &p) {                             // tls_extension ctor tls.h:1383
+    Ext x;
+    x.type = x.length = x.encoded_type = 0;
+    x.type_ptr = p.d; x.length_ptr = nullptr; x.ok = false; cset_null(x.value);
+    uint64_t v;
+    if (!rd_uint(p, 2, v)) return x;
+    x.type = (uint32_t)v;
+    x.length_ptr = p.d;
+    if (!rd_uint(p, 2, v)) return x;
+    x.length = (uint32_t)v;
+    if ((long)x.length <= clen(p)) {
+        x.value.d = p.d; x.value.e = p.d + x.length; p.d += x.length; x.ok = true;
+    }
+    x.encoded_type = ((x.type & 0x0f0f) == 0x0a0a) ? 0x0a0a : x.type;
+    return x;
+}
+DEV bool ext_is_grease(uint32_t t) { return (t & 0x0f0f) == 0x0a0a; }
+
+template <class E>
+DEV void ext_degreased_value(E &b, const Ext &x, long ungreased) {   // tls.h:1513
+    if (!cnotempty(x.value)) return;
+    long vl = clen(x.value), skip, gl;
+    if (ungreased < vl) { skip = ungreased; gl = vl - ungreased; } else { skip = vl; gl = 0; }
+    b.hex(x.value.d, skip);
+    hex_degrease(b, x.value.d + skip, gl);
+}
+
+// QUIC transport parameters inside a TLS extension (tls.h:1237-1262,
+// quic_vli.hpp:30-113)
+DEV int vli_len(uint32_t b) { return (b & 0xc0) == 0xc0 ? 8 : (b & 0xc0) == 0x80 ? 4 : (b & 0xc0) == 0x40 ? 2 : 1; }
+DEV uint64_t vli_value(Cur c) {
+    uint32_t b = rd_u8(c);
+    int len = vli_len(b);
+    uint64_t v = b & 0x3f;
+    for (int i = 1; i < len; i++) v = v * 256 + rd_u8(c);
+    return v;
+}
+DEV bool qtp_parse(Cur &d, Cur &id) {                   // quic_transport_parameter ctor tls.h:1247
+    uint32_t b = look_u8(d);
+    cparse(id, d, vli_len(b));
+    uint32_t bb = rd_u8(d);
+    int l2 = vli_len(bb);
+    uint64_t v = bb & 0x3f;
+    for (int i = 1; i < l2; i++) v = v * 256 + rd_u8(d);
+    Cur val;
+    long vlen = (v > 0x7fffffffffffffffULL) ? -1 : (long)v;
+    cparse(val, d, vlen);
+    return !cnull(val);
+}
+DEV bool qtp_is_grease(Cur id) { return vli_value(id) % 31 == 27; }
+template <class E>
+DEV void qtp_write_id(E &b, Cur id) {
+    if (!qtp_is_grease(id)) b.hex(id.d, clen(id));
+    else { b.putc('1'); b.putc('b'); }
+}
+DEV bool qtp_less(Cur a, Cur b) {                       // fmt-1 id comparator tls.h:1453
+    bool ga = qtp_is_grease(a), gb = qtp_is_grease(b);
+    if (ga) { if (gb) return false; return 0x1b < vli_value(b); }
+    if (gb) return vli_value(a) < 0x1b;
+    return ccmp(a, b) < 0;
+}
+
+// fmt-1 output of one extension: tls_extension::fingerprint_format1 tls.h:1413
+template <class E>
+DEV void ext_fp1(E &b, Ext &x, int role) {
+    if (is_static_ext(x.type)) {
+        if (x.type == 0x000a || x.type == 0x002b) {
+            b.putc('('); b.hex16(x.encoded_type);
+            if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
+            ext_degreased_value(b, x, x.type == 0x000a ? 2 : (role == 0 ? 1 : 0));
+            b.putc(')');
+        } else if (x.type == 0x39 || x.type == 0xffa5) {
+            b.putc('('); b.putc('('); b.hex16(x.encoded_type); b.putc(')');
+            b.putc('[');
+            // selection order == std::sort order for the (consistent) comparator
+            Cur prev; cset_null(prev);
+            bool have_prev = false;
+            long prev_pos = -1;
+            while (true) {
+                Cur best; cset_null(best); long best_pos = -1;
+                Cur v = x.value; long pos = 0;
+                while (!cnull(v)) {
+                    Cur id;
+                    bool ok = qtp_parse(v, id);
+                    if (ok) {
+                        bool after = !have_prev || qtp_less(prev, id) ||
+                                     (!qtp_less(id, prev) && pos > prev_pos);
+                        if (after) {
+                            bool better = best_pos < 0 || qtp_less(id, best) ||
+                                          (!qtp_less(best, id) && pos < best_pos);
+                            if (better) { best = id; best_pos = pos; }
+                        }
+                        pos++;
+                    }
+                }
+                if (best_pos < 0) break;
+                b.putc('('); qtp_write_id(b, best); b.putc(')');
+                prev = best; prev_pos = best_pos; have_prev = true;
+            }
+            b.putc(']');
+            b.putc(')');
+        } else {
+            b.putc('('); b.hex16(x.encoded_type);
+            if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
+            if (cnotempty(x.value)) b.hex(x.value.d, clen(x.value));
+            b.putc(')');
+        }
+    } else {
+        b.putc('('); b.hex16(x.encoded_type); b.putc(')');
+    }
+}
+
+// format 0: tls_extensions::fingerprint tls.h:1549
+template <class E>
+DEV void exts_fp0(E &b, Cur exts, int role) {
+    Cur p = exts;
+    b.putc('(');
+    while (clen(p) > 0) {
+        Ext x = ext_parse(p);
+        if (!x.ok) break;
+        if (is_static_ext(x.type)) {
+            if (x.type == 0x000a || x.type == 0x002b) {
+                b.putc('(');
+                if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+                if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
+                ext_degreased_value(b, x, x.type == 0x000a ? 2 : (role == 0 ? 1 : 0));
+                b.putc(')');
+            } else if (x.type == 0x39 || x.type == 0xffa5) {
+                b.putc('('); b.putc('(');
+                if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+                b.putc(')');
+                b.putc('(');
+                Cur v = x.value;
+                while (!cnull(v)) {
+                    Cur id;
+                    if (qtp_parse(v, id)) { b.putc('('); qtp_write_id(b, id); b.putc(')'); }
+                }
+                b.putc(')'); b.putc(')');
+            } else {
+                b.putc('(');
+                if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+                if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
+                if (cnotempty(x.value)) b.hex(x.value.d, clen(x.value));
+                b.putc(')');
+            }
+        } else {
+            b.putc('(');
+            if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+            b.putc(')');
+        }
+    }
+    b.putc(')');
+}
+
+// tls_extensions_assign::get_index tls_extensions.h:15-110
+DEV int fmt2_index(uint32_t t) {
+    if (t <= 20) return (int)t;
+    if (t >= 22 && t <= 34) return (int)t - 1;
+    if (t >= 36 && t <= 40) return (int)t - 2;
+    if (t >= 43 && t <= 62) return (int)t - 4;
+    switch (t) {
+    case 2570: return 59; case 13172: return 60; case 21760: return 61; case 30031: return 62;
+    case 30032: return 63; case 64768: return 64; case 65037: return 65; case 65280: return 66;
+    case 65281: return 67; case 65283: return 68; case 65445: return 69; case 65486: return 70;
+    }
+    return -1;
+}
+// fmt-2 bucket after the private/unassigned remap (tls.h:1680-1693)
+DEV int fmt2_bucket(Ext &x) {
+    int idx = fmt2_index(x.type);
+    if (idx == -1) {
+        if (x.type == 65280 || x.type >= 65282) x.encoded_type = 65280;
+        else if (x.type >= 62 && x.type <= 65279 && !ext_is_grease(x.type)) x.encoded_type = 62;
+        idx = fmt2_index(x.encoded_type);
+    }
+    return idx;
+}
+
+// ordering key of an extension for formats 1 and 2.  Returns a 32-bit
+// primary key; ties (same primary) are broken by ext_tie_less.
+//   fmt 1 (tls.h:1637): grease == type 0x0a0a, then type, length, value
+//   fmt 2 (tls.h:1709): bucket, then (grease first...) length, value
+DEV uint32_t ext_key(const Ext &x, int fmt, int bucket) {
+    if (fmt == 1) {
+        bool g = ext_is_grease(x.type);
+        return g ? (0x0a0aU << 16) : ((x.type << 16) | x.length);
+    }
+    bool g = ext_is_grease(x.type);
+    return ((uint32_t)bucket << 24) | (g ? 0 : (1u << 23)) | (g ? 0 : x.length);
+}
+// strict "less" on full comparator given equal primary keys
+DEV bool ext_tie_less(const Ext &a, const Ext &b) {
+    if (ext_is_grease(a.type) || ext_is_grease(b.type)) return false;
+    return ccmp(a.value, b.value) < 0;
+}
+
+// per-lane LDS scratch for formats 1/2 (offset of each kept extension
+// relative to the extension block, and its primary key)
+constexpr int MAX_LDS_EXT = 32;
+
+// formats 1 and 2: sort kept extensions, then emit fingerprint_format1 each
+template <class E>
+DEV void exts_fp12(E &b, Cur exts, int role, int fmt, uint32_t *lds_key, uint16_t *lds_off, int stride) {
+    b.putc('[');
+    // gather
+    int n = 0;
+    bool overflow = false;
+    {
+        Cur p = exts;
+        while (clen(p) > 0) {
+            const uint8_t *start = p.d;
+            Ext x = ext_parse(p);
+            if (!x.ok) break;
+            int bucket = 0;
+            if (fmt == 2) {
+                bucket = fmt2_bucket(x);
+                if (bucket < 0) continue;
+                // keep the first three per bucket (tls.h:1695-1701)
+                int cnt = 0;
+                for (int j = 0; j < n; j++) if ((lds_key[j * stride] >> 24) == (uint32_t)bucket) cnt++;
+                if (cnt >= 3) continue;
+            }
+            if (n >= MAX_LDS_EXT) { overflow = true; break; }
+            lds_key[n * stride] = ext_key(x, fmt, bucket);
+            lds_off[n * stride] = (uint16_t)(start - exts.d);
+            n++;
+        }
+    }
+    if (!overflow) {
+        if (!E::emit_pass()) {
+            // pass 1: the length does not depend on the order
+            for (int j = 0; j < n; j++) {
+                Cur q = cmk(exts.d + lds_off[j * stride], exts.e);
+                Ext x = ext_parse(q);
+                if (fmt == 2) fmt2_bucket(x);
+                ext_fp1(b, x, role);
+            }
+        } else {
+            // insertion sort (LDS), ties broken by value bytes
+            for (int i = 1; i < n; i++) {
+                uint32_t k = lds_key[i * stride];
+                uint16_t o = lds_off[i * stride];
+                int j = i;
+                while (j > 0) {
+                    uint32_t kj = lds_key[(j - 1) * stride];
+                    bool less = k < kj;
+                    if (!less && k == kj) {
+                        Cur qa = cmk(exts.d + o, exts.e), qb = cmk(exts.d + lds_off[(j - 1) * stride], exts.e);
+                        Ext a = ext_parse(qa), bb = ext_parse(qb);
+                        less = ext_tie_less(a, bb);
+                    }
+                    if (!less) break;
+                    lds_key[j * stride] = kj;
+                    lds_off[j * stride] = lds_off[(j - 1) * stride];
+                    j--;
+                }
+                lds_key[j * stride] = k;
+                lds_off[j * stride] = o;
+            }
+            for (int j = 0; j < n; j++) {
+                Cur q = cmk(exts.d + lds_off[j * stride], exts.e);
+                Ext x = ext_parse(q);
+                if (fmt == 2) fmt2_bucket(x);
+                ext_fp1(b, x, role);
+            }
+        }
+    } else {
+        // rare path (> MAX_LDS_EXT kept extensions): selection over the wire
+        // list, O(n^2), same total order
+        uint32_t prev_key = 0; long prev_pos = -1; bool have_prev = false;
+        Ext prev_x; prev_x.type = 0; prev_x.length = 0; cset_null(prev_x.value);
+        while (true) {
+            long best_pos = -1; uint32_t best_key = 0; Ext best_x; best_x.type = 0; cset_null(best_x.value);
+            Cur p = exts; long pos = 0;
+            // for fmt 2 we must respect the first-three-per-bucket rule
+            while (clen(p) > 0) {
+                Ext x = ext_parse(p);
+                if (!x.ok) break;
+                long mypos = pos++;
+                int bucket = 0;
+                if (fmt == 2) {
+                    bucket = fmt2_bucket(x);
+                    if (bucket < 0) continue;
+                    // count earlier kept in bucket
+                    Cur q = exts; int cnt = 0; long qp = 0;
+                    while (qp < mypos && clen(q) > 0) {
+                        Ext y = ext_parse(q);
+                        if (!y.ok) break;
+                        qp++;
+                        if (fmt2_bucket(y) == bucket) cnt++;
+                    }
+                    if (cnt >= 3) continue;
+                }
+                uint32_t k = ext_key(x, fmt, bucket);
+                auto lt = [&](uint32_t ka, const Ext &xa, long pa, uint32_t kb, const Ext &xb, long pb) {
+                    if (ka != kb) return ka < kb;
+                    if (ext_tie_less(xa, xb)) return true;
+                    if (ext_tie_less(xb, xa)) return false;
+                    return pa < pb;
+                };
+                bool after = !have_prev || lt(prev_key, prev_x, prev_pos, k, x, mypos);
+                if (!after) continue;
+                if (best_pos < 0 || lt(k, x, mypos, best_key, best_x, best_pos)) {
+                    best_pos = mypos; best_key = k; best_x = x;
+                }
+            }
+            if (best_pos < 0) break;
+            ext_fp1(b, best_x, role);
+            prev_key = best_key; prev_pos = best_pos; prev_x = best_x; have_prev = true;
+        }
+    }
+    b.putc(']');
+}
+
+}  // namespace mfp
+
+namespace mfp {
+
+// ---------------------------------------------------------------------------
+// TLS handshake containers (tls.h:145-262), ClientHello/ServerHello/Cert
+// ---------------------------------------------------------------------------
+DEV Cur tls_record_fragment(Cur &d) {                   // tls_record::parse tls.h:153
+    Cur f; cset_null(f);
+    if (clen(d) < 5) return f;
+    uint64_t t, len;
+    rd_uint(d, 1, t); rd_uint(d, 2, t); rd_uint(d, 2, len);
+    cinit_outer(f, d, len);
+    return f;
+}
+struct Hs { uint32_t msg_type; uint64_t length; Cur body; uint64_t more; };
+DEV Hs tls_hs_parse(Cur &d) {                           // tls_handshake::parse tls.h:244
+    Hs h; h.msg_type = 0; h.length = 0; cset_null(h.body); h.more = 0;
+    if (clen(d) < 4) return h;
+    uint64_t t;
+    rd_uint(d, 1, t); h.msg_type = (uint32_t)t;
+    rd_uint(d, 3, t); h.length = t;
+    if (h.length > 32768) return h;
+    cinit_outer(h.body, d, h.length);
+    h.more = h.length - (uint64_t)clen(h.body);
+    return h;
+}
+struct Ch { Cur version, ciphers, compression, extensions; };
+DEV Ch tls_ch_parse(Cur p) {                            // tls_client_hello::parse tls.h:1811
+    Ch ch; cset_null(ch.version); cset_null(ch.ciphers); cset_null(ch.compression); cset_null(ch.extensions);
+    uint64_t l;
+    Cur t;
+    cparse(ch.version, p, 2);
+    if (!cnotempty(ch.version)) return ch;
+    bool dtls = ld(ch.version.d) == 0xfe;
+    cparse(t, p, 32);
+    if (!rd_uint(p, 1, l)) return ch;
+    cparse(t, p, (long)l);
+    if (dtls) {
+        if (!look_uint(p, 1, l)) return ch;
+        if (!cskip(p, (long)l + 1)) return ch;
+    }
+    if (!rd_uint(p, 2, l)) return ch;
+    if (l & 1) return ch;
+    cparse(ch.ciphers, p, (long)l);
+    if (!rd_uint(p, 1, l)) return ch;
+    cparse(ch.compression, p, (long)l);
+    if (!rd_uint(p, 2, l)) return ch;
+    cparse_soft(ch.extensions, p, (long)l);
+    return ch;
+}
+template <class E>
+DEV void tls_ch_fp(E &b, const Ch &ch, int fmt, uint32_t *lk, uint16_t *lo, int stride) {   // tls.h:1928
+    if (fmt >= 1 && fmt <= 2) { b.putc('0' + fmt); b.putc('/'); }
+    b.putc('('); b.hex(ch.version.d, clen(ch.version)); b.putc(')');
+    b.putc('('); hex_degrease(b, ch.ciphers.d, clen(ch.ciphers)); b.putc(')');
+    if (fmt == 0) exts_fp0(b, ch.extensions, 0);
+    else exts_fp12(b, ch.extensions, 0, fmt, lk, lo, stride);
+}
+// tls_extensions::set_meta_data tls.h:1316 (server_name; last one wins)
+DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len) {
+    Cur p = exts;
+    while (clen(p) > 0) {
+        const uint8_t *start = p.d;
+        uint64_t t, l;
+        if (!rd_uint(p, 2, t)) break;
+        if (!rd_uint(p, 2, l)) break;
+        if (!cskip(p, (long)l)) break;
+        if (t == 0) {
+            Cur e = cmk(start, p.d);
+            cskip(e, 9);
+            off = (uint32_t)(e.d - base); len = (uint32_t)clen(e);
+        }
+    }
+}
+struct Sh { Cur version, cipher, extensions; };
+DEV Sh tls_sh_parse(Cur &rec) {                         // parse_tls_server_hello tls.h:2097
+    Sh s; cset_null(s.version); cset_null(s.cipher); cset_null(s.extensions);
+    uint64_t l; Cur t;
+    cparse(s.version, rec, 2);
+    cparse(t, rec, 32);
+    if (!look_uint(rec, 1, l)) return s;
+    if (!cskip(rec, (long)l + 1)) return s;
+    cparse(s.cipher, rec, 2);
+    cparse(t, rec, 1);
+    if (!rd_uint(rec, 2, l)) return s;
+    cparse(s.extensions, rec, (long)l);
+    return s;
+}
+DEV bool tls_sh_not_empty(const Sh &s) {                // tls_server_hello::is_not_empty tls.h:513
+    Cur t = s.version; uint64_t v;
+    rd_uint(t, 2, v);
+    if (!(v == 0x0303 || v == 0x0302 || v == 0x0301 || v == 0x0300 || v == 0xfeff || v == 0xfefd)) return false;
+    return cnotempty(s.cipher);
+}
+template <class E>
+DEV void tls_sh_fp(E &b, const Sh &s) {                 // tls_server_hello::fingerprint tls.h:2126
+    b.putc('('); b.hex(s.version.d, clen(s.version)); b.putc(')');
+    b.putc('('); b.hex(s.cipher.d, clen(s.cipher)); b.putc(')');
+    exts_fp0(b, s.extensions, 1);
+}
+struct Cert { Cur list; uint64_t more; };
+DEV void tls_cert_parse(Cert &c, Cur &d) {              // tls_server_certificate::parse tls.h:281
+    uint64_t t = 0;
+    if (!rd_uint(d, 3, t)) return;
+    if (t > 65536) { cset_null(d); return; }
+    cinit_outer(c.list, d, t);
+    c.more = t - (uint64_t)clen(c.list);
+}
+
+// ---------------------------------------------------------------------------
+// SSH (ssh.h)
+// ---------------------------------------------------------------------------
+struct SshBin { Cur payload; uint64_t more; };
+DEV SshBin ssh_bin_parse(Cur &p) {                      // ssh_binary_packet ssh.h:56
+    SshBin b; cset_null(b.payload); b.more = 0;
+    uint64_t plen, pad;
+    rd_uint(p, 4, plen);
+    rd_uint(p, 1, pad);
+    if (plen > 16384 || plen < 1) { if (p.d) p.d = p.e; return b; }
+    if (!cnotempty(p)) return b;
+    long left = (long)plen - 1;
+    if (left > clen(p)) b.more = left - clen(p);
+    cparse_soft(b.payload, p, left);
+    return b;
+}
+// ssh_kex_init::parse ssh.h:190; returns the kex_algorithms name-list and
+// leaves the 10 name-lists' extents retrievable by re-walking
+DEV void name_list_parse(Cur &nl, Cur &p) {             // name_list::parse ssh.h:110
+    uint64_t l;
+    rd_uint(p, 4, l);
+    if (l > 2048) { if (p.d) p.d = p.e; return; }
+    cparse(nl, p, (long)l);
+}
+template <class E>
+DEV bool ssh_kex_fp(E *b, Cur payload) {                // ssh_kex_init::fingerprint ssh.h:240
+    Cur p = payload, t, nl[10];
+    cparse(t, p, 1);
+    cparse(t, p, 16);
+    for (int i = 0; i < 10; i++) { cset_null(nl[i]); name_list_parse(nl[i], p); }
+    if (!cnotempty(nl[0])) return false;
+    if (b) {
+        for (int i = 0; i < 10; i++) {
+            b->putc('(');
+            if (cnotempty(nl[i])) b->hex(nl[i].d, clen(nl[i]));
+            b->putc(')');
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// HTTP (http.h, http.cc) -- header-name tables in constant memory
+// ---------------------------------------------------------------------------
+struct HdrName { uint8_t len; uint8_t incl_value; uint8_t capture; char s[33]; };
+// http.cc:426-445 (request) and :487-536 (response); capture: 1 host, 2 user-agent
+__constant__ HdrName k_req_names[] = {
+    {6, 1, 0, "accept"}, {15, 1, 0, "accept-encoding"}, {10, 1, 0, "connection"}, {3, 1, 0, "dnt"},
+    {3, 1, 0, "dpr"}, {25, 1, 0, "upgrade-insecure-requests"}, {16, 1, 0, "x-requested-with"},
+    {14, 0, 0, "accept-charset"}, {15, 0, 0, "accept-language"}, {13, 0, 0, "authorization"},
+    {13, 0, 0, "cache-control"}, {4, 0, 1, "host"}, {17, 0, 0, "if-modified-since"}, {10, 0, 0, "keep-alive"},
+    {10, 0, 2, "user-agent"}, {15, 0, 0, "x-flash-version"}, {14, 0, 0, "x-p2p-peerdist"},
+};
+constexpr int N_REQ_NAMES = 17;
+__constant__ HdrName k_resp_names[] = {
+    {32, 1, 0, "access-control-allow-credentials"}, {28, 1, 0, "access-control-allow-headers"},
+    {28, 1, 0, "access-control-allow-methods"}, {29, 1, 0, "access-control-expose-headers"},
+    {13, 1, 0, "cache-control"}, {4, 1, 0, "code"}, {10, 1, 0, "connection"}, {16, 1, 0, "content-language"},
+    {25, 1, 0, "content-transfer-encoding"}, {3, 1, 0, "p3p"}, {6, 1, 0, "pragma"}, {6, 1, 0, "reason"},
+    {6, 1, 0, "server"}, {25, 1, 0, "strict-transport-security"}, {7, 1, 0, "version"},
+    {19, 1, 0, "x-aspnetmvc-version"}, {16, 1, 0, "x-aspnet-version"}, {5, 1, 0, "x-cid"},
+    {12, 1, 0, "x-ms-version"}, {16, 1, 0, "x-xss-protection"},
+    {17, 0, 0, "appex-activity-id"}, {7, 0, 0, "cdnuuid"}, {6, 0, 0, "cf-ray"}, {13, 0, 0, "content-range"},
+    {12, 0, 0, "content-type"}, {4, 0, 0, "date"}, {4, 0, 0, "etag"}, {7, 0, 0, "expires"},
+    {12, 0, 0, "flow_context"}, {5, 0, 0, "ms-cv"}, {8, 0, 0, "msregion"}, {12, 0, 0, "ms-requestid"},
+    {10, 0, 0, "request-id"}, {4, 0, 0, "vary"}, {12, 0, 0, "x-amz-cf-pop"}, {16, 0, 0, "x-amz-request-id"},
+    {24, 0, 0, "x-azure-ref-originshield"}, {7, 0, 0, "x-cache"}, {12, 0, 0, "x-cache-hits"},
+    {5, 0, 0, "x-ccc"}, {14, 0, 0, "x-diagnostic-s"}, {10, 0, 0, "x-feserver"}, {4, 0, 0, "x-hw"},
+    {12, 0, 0, "x-msedge-ref"}, {19, 0, 0, "x-ocsp-responder-id"}, {11, 0, 0, "x-requestid"},
+    {11, 0, 0, "x-served-by"}, {7, 0, 0, "x-timer"}, {15, 0, 0, "x-trace-context"},
+};
+constexpr int N_RESP_NAMES = 49;
+
+// perfect_hash::lookup perfect_hash.h:256: exact ASCII-case-insensitive match
+DEV int name_lookup(const HdrName *tab, int ntab, Cur n) {
+    long l = clen(n);
+    if (l <= 0 || l > 32) return -1;
+    uint32_t c0 = c_tolower(ld(n.d));
+    for (int i = 0; i < ntab; i++) {
+        if (tab[i].len != l || (uint8_t)tab[i].s[0] != c0) continue;
+        bool ok = true;
+        for (long j = 1; j < l; j++)
+            if (c_tolower(ld(n.d + j)) != (uint8_t)tab[i].s[j]) { ok = false; break; }
+        if (ok) return i;
+    }
+    return -1;
+}
+DEV bool http_delim(Cur &p, Cur del) {                  // delimiter(datum&, const datum&) http.h:113
+    Cur dl; cset_null(dl);
+    static const uint8_t crlf[2] = {'\r', '\n'};
+    if (ccompare_n(p, del.d, clen(del))) cparse(dl, p, clen(del));
+    else if (p.d && clen(p) >= 2 && ld(p.d) == '\r' && ld(p.d + 1) == '\n') cparse(dl, p, 2);
+    else if (p.d && clen(p) >= 1 && ld(p.d) == '\n') cparse(dl, p, 1);
+    (void)crlf;
+    return cnotempty(dl);
+}
+// new_http_headers::fingerprint http.h:335 + httpheader http.h:146
+template <class E>
+DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {
+    Cur tmp = body;
+    const HdrName *tab = req ? k_req_names : k_resp_names;
+    int ntab = req ? N_REQ_NAMES : N_RESP_NAMES;
+    while (true) {
+        if (http_delim(tmp, delim)) break;
+        Cur hdr_body = tmp, name; cset_null(name);
+        if (!cnotempty(tmp)) { cset_null(tmp); }
+        else {
+            name.d = tmp.d; name.e = tmp.e;
+            for (const uint8_t *q = tmp.d; q < tmp.e; q++) if (ld(q) == ':') { name.e = q; tmp.d = q; break; }
+        }
+        if (tmp.d && tmp.e > tmp.d && ld(tmp.d) == ':') tmp.d++; else cset_null(tmp);
+        while (tmp.d && tmp.d < tmp.e && (ld(tmp.d) == '\t' || ld(tmp.d) == ' ')) tmp.d++;
+        Cur value;
+        cparse_to_delims(value, tmp, '\r', '\n');
+        http_delim(tmp, delim);
+        hdr_body.e = value.e;
+        if (cnull(tmp)) break;
+        int idx = name_lookup(tab, ntab, name);
+        if (idx >= 0) {
+            b.putc('(');
+            if (tab[idx].incl_value) b.hex(hdr_body.d, clen(hdr_body)); else b.hex(name.d, clen(name));
+            b.putc(')');
+            if (req) {
+                if (tab[idx].capture == 1 && cnull(host)) host = value;
+                if (tab[idx].capture == 2 && cnull(ua)) ua = value;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-packet walk
+// ---------------------------------------------------------------------------
+struct Out {
+    uint32_t fp_type, msg, flags;
+    uint32_t sni_off, sni_len, ua_off, ua_len;
+    uint32_t src_port, dst_port;
+};
+struct Cfg {
+    uint32_t select, tls_format, mode;
+};
+enum : uint32_t {
+    SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
+    SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
+    SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9,
+};
+
+// masked 8/16-byte matchers (match.h:64-103)
+DEV bool m8(Cur p, uint64_t mask, uint64_t val) {
+    if (!p.d || clen(p) < 8) return false;
+    uint64_t w = 0;
+    for (int i = 0; i < 8; i++) w |= (uint64_t)ld(p.d + i) << (8 * i);
+    return (w & mask) == val;
+}
+#define LE8(a, b, c, d, e, f, g, h)                                                                    \
+    ((uint64_t)(a) | ((uint64_t)(b) << 8) | ((uint64_t)(c) << 16) | ((uint64_t)(d) << 24) |           \
+     ((uint64_t)(e) << 32) | ((uint64_t)(f) << 40) | ((uint64_t)(g) << 48) | ((uint64_t)(h) << 56))
+
+// HTTP request keywords that map to http_request (proto_identify.h:200-236)
+__constant__ uint32_t k_http_kw[] = {
+    0x41434c20, 0x42415345, 0x42494e44, 0x43484543, 0x434f4e4e, 0x434f5059, 0x44454c45, 0x47455420,
+    0x48454144, 0x4c414245, 0x4c494e4b, 0x4c4f434b, 0x4d455247, 0x4d4b4143, 0x4d4b4341, 0x4d4b434f,
+    0x4d4b5245, 0x4d4b574f, 0x4d4f5645, 0x4f505449, 0x4f524445, 0x50415443, 0x504f5354, 0x50524920,
+    0x50524f50, 0x50555420, 0x52454249, 0x5245504f, 0x53454152, 0x54524143, 0x554e4249, 0x554e4348,
+    0x554e4c49, 0x554e4c4f, 0x55504441, 0x56455253,
+};
+
+template <class E>
+DEV void fp_type_prefix(E &b, uint32_t t) {             // fingerprint::set_type fingerprint.h:44
+    switch (t) {
+    case 1: b.lit("tls/"); break;
+    case 2: b.lit("tls_server/"); break;
+    case 3: b.lit("http/"); break;
+    case 4: b.lit("http_server/"); break;
+    case 5: b.lit("ssh/"); break;
+    case 6: b.lit("ssh_kex/"); break;
+    case 7: b.lit("tcp/"); break;
+    case 10: b.lit("dtls/"); break;
+    case 11: b.lit("dtls_server/"); break;
+    case 13: b.lit("tcp_server/"); break;
+    case 17: b.lit("ssh_init/"); break;
+    case 18: b.lit("ssh_server/"); break;
+    case 19: b.lit("ssh_kex_server/"); break;
+    case 20: b.lit("ssh_init_server/"); break;
+    }
+    b.last_putc = true;   // set_type ends with write_char('/')
+}
+
+// HTTP request/response parse + fingerprint (http.cc:105-128, 369-383,
+// 426-553); returns false when the message is empty (no record)
+template <class E>
+DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
+    Cur f1, f2, f3;   // req: method, protocol ; resp: version, status, reason
+    cset_null(f1); cset_null(f2); cset_null(f3);
+    if (req) {
+        Cur uri;
+        cparse_to_delim(f1, p, ' ');
+        long ml = clen(f1);
+        if (ml < 3 || ml > 16) return false;
+        for (long i = 0; i < ml; i++) if (!c_isupper(ld(f1.d + i))) return false;
+        cskip(p, 1);
+        cparse_to_delim(uri, p, ' ');
+        cskip(p, 1);
+        cparse_to_delims(f2, p, '\r', '\n');
+        if (!(f2.d && clen(f2) >= 5 && ld(f2.d) == 'H' && ld(f2.d + 1) == 'T' && ld(f2.d + 2) == 'T' &&
+              ld(f2.d + 3) == 'P' && ld(f2.d + 4) == '/'))
+            return false;
+    } else {
+        cparse_to_delim(f1, p, ' ');
+        cskip(p, 1);
+        cparse_to_delim(f2, p, ' ');
+        cskip(p, 1);
+        cparse_to_delims(f3, p, '\r', '\n');
+        if (!cnotempty(f2)) return false;
+    }
+    Cur delim; delim.d = p.d;
+    while (p.d && p.d < p.e && !c_isalpha(ld(p.d))) p.d++;
+    delim.e = p.d;
+    fp_type_prefix(b, req ? 3 : 4);
+    b.putc('('); b.hex(f1.d, clen(f1)); b.putc(')');
+    b.putc('('); b.hex(f2.d, clen(f2)); b.putc(')');
+    if (!req) { b.putc('('); b.hex(f3.d, clen(f3)); b.putc(')'); }
+    b.putc('(');
+    Cur host, ua; cset_null(host); cset_null(ua);
+    http_headers_fp(b, p, delim, req, host, ua);
+    b.putc(')');
+    if (req) {
+        if (!cnull(host)) { o.sni_off = (uint32_t)(host.d - base); o.sni_len = (uint32_t)clen(host); }
+        if (!cnull(ua)) { o.ua_off = (uint32_t)(ua.d - base); o.ua_len = (uint32_t)clen(ua); }
+    }
+    return true;
+}
+
+// set_tcp_protocol pkt_proc.cc:488 (selection subset)
+template <class E>
+DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, const uint8_t *base,
+                  uint32_t *lk, uint16_t *lo, int stride) {
+    uint32_t sel = cfg.select;
+    uint32_t sport = (ld(tcph) << 8) | ld(tcph + 1), dport = (ld(tcph + 2) << 8) | ld(tcph + 3);
+    uint32_t msg = 0;
+    if (clen(pkt) >= 4) {
+        const uint64_t MT = LE8(0xff, 0xff, 0xfc, 0, 0, 0xff, 0, 0);
+        if ((sel & SEL_TLS_CH) && m8(pkt, MT, LE8(0x16, 0x03, 0, 0, 0, 0x01, 0, 0))) msg = MFP_MSG_TLS_CH;
+        else if ((sel & SEL_TLS_SH) && m8(pkt, MT, LE8(0x16, 0x03, 0, 0, 0, 0x02, 0, 0))) msg = MFP_MSG_TLS_SH;
+        else if ((sel & SEL_TLS_CERT) && m8(pkt, MT, LE8(0x16, 0x03, 0, 0, 0, 0x0b, 0, 0))) msg = MFP_MSG_TLS_CERT;
+        else if ((sel & (SEL_SSH_CLIENT | SEL_SSH_SERVER)) &&
+                 m8(pkt, LE8(0xff, 0xff, 0xff, 0xff, 0, 0, 0, 0), LE8('S', 'S', 'H', '-', 0, 0, 0, 0)))
+            msg = MFP_MSG_SSH_INIT;
+        else if ((sel & (SEL_SSH_CLIENT | SEL_SSH_SERVER)) &&
+                 m8(pkt, LE8(0xff, 0xff, 0xf0, 0, 0, 0xff, 0, 0), LE8(0, 0, 0, 0, 0, 0x14, 0, 0)))
+            msg = MFP_MSG_SSH_KEX;
+    }
+    if (msg == 0) {
+        if (clen(pkt) < 4) return;
+        uint32_t kw = (ld(pkt.d) << 24) | (ld(pkt.d + 1) << 16) | (ld(pkt.d + 2) << 8) | ld(pkt.d + 3);
+        if (sel & SEL_HTTP_REQ) {
+            bool hit = false;
+            for (int i = 0; i < 36; i++) hit |= (k_http_kw[i] == kw);
+            if (hit) {
+                o.msg = MFP_MSG_HTTP_REQ;
+                if (http_msg(b, pkt, true, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 3; }
+                else o.msg = 0;
+                return;
+            }
+        }
+        if ((sel & SEL_HTTP_RESP) && kw == 0x48545450u) {
+            o.msg = MFP_MSG_HTTP_RESP;
+            if (http_msg(b, pkt, false, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 4; }
+            else o.msg = 0;
+        }
+        return;
+    }
+    o.msg = msg;
+    switch (msg) {
+    case MFP_MSG_TLS_CH: {
+        Cur p = pkt;
+        Cur frag = tls_record_fragment(p);
+        Hs hs = tls_hs_parse(frag);
+        if (hs.more) o.flags |= MFP_FLAG_TRUNCATED;
+        Ch ch = tls_ch_parse(hs.body);
+        if (!cnotempty(ch.compression)) return;
+        o.flags |= MFP_FLAG_EMIT; o.fp_type = 1;
+        fp_type_prefix(b, 1);
+        tls_ch_fp(b, ch, (int)cfg.tls_format, lk, lo, stride);
+        tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+        return;
+    }
+    case MFP_MSG_TLS_SH: {                              // tls.h:573
+        Cur p = pkt;
+        Sh sh; cset_null(sh.version); cset_null(sh.cipher); cset_null(sh.extensions);
+        Cert cert; cset_null(cert.list); cert.more = 0;
+        Cur frag = tls_record_fragment(p);
+        Hs hs = tls_hs_parse(frag);
+        if (hs.msg_type == 2) {
+            sh = tls_sh_parse(hs.body);
+            if (cnotempty(frag)) { Hs h2 = tls_hs_parse(frag); tls_cert_parse(cert, h2.body); }
+        } else if (hs.msg_type == 11) {
+            tls_cert_parse(cert, hs.body);
+        }
+        Cur frag2 = tls_record_fragment(p);
+        Hs hs2 = tls_hs_parse(frag2);
+        if (hs2.msg_type == 11) tls_cert_parse(cert, hs2.body);
+        if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
+        bool hello = tls_sh_not_empty(sh);
+        if (hello || cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
+        if (hello) { o.fp_type = 2; fp_type_prefix(b, 2); tls_sh_fp(b, sh); }
+        return;
+    }
+    case MFP_MSG_TLS_CERT: {                            // tls.h:720
+        Cur p = pkt;
+        Cert cert; cset_null(cert.list); cert.more = 0;
+        Cur frag = tls_record_fragment(p);
+        Hs hs = tls_hs_parse(frag);
+        if (hs.msg_type == 11) tls_cert_parse(cert, hs.body);
+        if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
+        if (cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
+        return;
+    }
+    case MFP_MSG_SSH_INIT: {                            // ssh.h:342-430
+        bool server = !(dport <= sport);
+        if (!(sel & (server ? SEL_SSH_SERVER : SEL_SSH_CLIENT))) { o.msg = 0; return; }
+        Cur p = pkt, proto, comment; cset_null(comment);
+        uint32_t delim = cparse_to_delims(proto, p, '\n', ' ');
+        if (delim != '\n') { cskip(p, 1); cparse_to_delim(comment, p, '\n'); }
+        cskip(p, 1);
+        bool kex = false;
+        SshBin bin; cset_null(bin.payload); bin.more = 0;
+        if (cnotempty(p)) {
+            bin = ssh_bin_parse(p);
+            if (cnotempty(bin.payload)) kex = ssh_kex_fp<E>(nullptr, bin.payload);
+        }
+        uint64_t more = kex ? bin.more : 8192;
+        if (more) o.flags |= MFP_FLAG_TRUNCATED;
+        if (!cnotempty(proto)) return;
+        o.flags |= MFP_FLAG_EMIT;
+        if (kex) {
+            o.fp_type = server ? 18 : 5;
+            fp_type_prefix(b, o.fp_type);
+            ssh_kex_fp(&b, bin.payload);
+        } else {
+            o.fp_type = server ? 20 : 17;
+            fp_type_prefix(b, o.fp_type);
+            b.putc('(');
+            if (cnotempty(comment)) {
+                b.hex(proto.d, clen(proto));
+                b.putc('2'); b.putc('0');
+                Cur t = comment; t.e -= 1; if (t.e < t.d) t.e = t.d;
+                b.hex(t.d, clen(t));
+            } else {
+                Cur t = proto; t.e -= 1; if (t.e < t.d) t.e = t.d;
+                b.hex(t.d, clen(t));
+            }
+            b.putc(')');
+        }
+        // analysis: user agent = protocol + comment strings (ssh.h:480)
+        o.ua_off = (uint32_t)(proto.d - base); o.ua_len = (uint32_t)clen(proto);
+        return;
+    }
+    case MFP_MSG_SSH_KEX: {                             // pkt_proc.cc:586-601
+        bool server = !(dport <= sport);
+        if (!(sel & (server ? SEL_SSH_SERVER : SEL_SSH_CLIENT))) { o.msg = 0; return; }
+        Cur p = pkt;
+        SshBin bin = ssh_bin_parse(p);
+        if (bin.more) o.flags |= MFP_FLAG_TRUNCATED;
+        if (!ssh_kex_fp<E>(nullptr, bin.payload)) return;
+        o.flags |= MFP_FLAG_EMIT;
+        o.fp_type = server ? 19 : 6;
+        fp_type_prefix(b, o.fp_type);
+        ssh_kex_fp(&b, bin.payload);
+        return;
+    }
+    }
+}
+
+// set_udp_protocol pkt_proc.cc:677 (selection subset: DTLS, dtls.h)
+template <class E>
+DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uint32_t *lk, uint16_t *lo,
+                  int stride) {
+    if (!(cfg.select & SEL_DTLS) || clen(pkt) < 16) return;
+    uint64_t w0 = 0, w1 = 0;
+    for (int i = 0; i < 8; i++) { w0 |= (uint64_t)ld(pkt.d + i) << (8 * i); w1 |= (uint64_t)ld(pkt.d + 8 + i) << (8 * i); }
+    const uint64_t M0 = LE8(0xff, 0xff, 0xfd, 0, 0, 0, 0, 0), V0 = LE8(0x16, 0xfe, 0xfd, 0, 0, 0, 0, 0);
+    const uint64_t M1 = LE8(0, 0, 0, 0, 0, 0xff, 0, 0);
+    if ((w0 & M0) != V0) return;
+    uint32_t hb = (uint32_t)((w1 & M1) >> 40);
+    uint32_t msg = hb == 1 ? MFP_MSG_DTLS_CH : hb == 2 ? MFP_MSG_DTLS_SH : hb == 3 ? MFP_MSG_DTLS_HVR : 0;
+    if (!msg) return;
+    o.msg = msg;
+    Cur d = pkt, frag, body; cset_null(frag); cset_null(body);
+    uint64_t t, len = 0, foff = 0, flen = 0, more = 0;
+    if (clen(d) < 13) cset_null(d);
+    else {
+        rd_uint(d, 1, t); rd_uint(d, 2, t); rd_uint(d, 2, t); rd_uint(d, 6, t); rd_uint(d, 2, t);
+        cparse(frag, d, (long)t);
+    }
+    if (clen(frag) < 12) cset_null(frag);
+    else {
+        rd_uint(frag, 1, t); rd_uint(frag, 3, len); rd_uint(frag, 2, t);
+        rd_uint(frag, 3, foff); rd_uint(frag, 3, flen);
+        cparse(body, frag, (long)flen);
+        if (foff == 0) {
+            long bl = clen(body);
+            if (flen <= len && bl >= 0 && (uint64_t)bl <= len) more = len - (uint64_t)bl;
+        }
+    }
+    if (msg == MFP_MSG_DTLS_CH) {
+        if ((uint32_t)more) o.flags |= MFP_FLAG_TRUNCATED;
+        Ch ch = tls_ch_parse(body);
+        if (!cnotempty(ch.compression)) return;
+        o.flags |= MFP_FLAG_EMIT; o.fp_type = 10;
+        fp_type_prefix(b, 10);
+        tls_ch_fp(b, ch, (int)cfg.tls_format, lk, lo, stride);
+        tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+    } else if (msg == MFP_MSG_DTLS_SH) {
+        Cur b2 = body;
+        Sh sh = tls_sh_parse(b2);
+        if (!tls_sh_not_empty(sh)) return;
+        o.flags |= MFP_FLAG_EMIT; o.fp_type = 11;
+        fp_type_prefix(b, 11);
+        tls_sh_fp(b, sh);
+    } else {
+        Cur b2 = body; uint64_t cl; Cur ck;
+        rd_uint(b2, 2, t); rd_uint(b2, 1, cl);
+        cparse(ck, b2, (long)cl);
+        if (!cnull(b2)) o.flags |= MFP_FLAG_EMIT;
+    }
+}
+
+// IP header (ip.h:124, ip.h:448); returns transport protocol or 255
+DEV uint32_t ip_parse(Cur &p, const uint8_t *&iph, int &ipv) {
+    uint32_t v = look_u8(p);
+    iph = nullptr; ipv = 0;
+    if ((v & 0xf0) == 0x40) {
+        const uint8_t *h = cget_ptr(p, 20);
+        ipv = 4;
+        if (!h) return 255;
+        iph = h;
+        long tl = ((long)ld(h + 2) << 8) | ld(h + 3);
+        ctrim_to_length(p, tl - 20);
+        return ld(h + 9);
+    }
+    if ((v & 0xf0) == 0x60) {
+        const uint8_t *h = cget_ptr(p, 40);
+        ipv = 6;
+        if (!h) return 255;
+        iph = h;
+        ctrim_to_length(p, ((long)ld(h + 4) << 8) | ld(h + 5));
+        uint32_t nh = ld(h + 6);
+        while (clen(p) > 0) {
+            bool ext = (nh == 0 || nh == 43 || nh == 44 || nh == 51 || nh == 60 || nh == 135 || nh == 139 || nh == 140);
+            if (!ext) break;
+            uint32_t hdr = nh, nnh = rd_u8(p), hl; Cur dd;
+            if (hdr == 44) cparse(dd, p, 7);
+            else if (hdr == 51) { hl = rd_u8(p); cparse(dd, p, (long)hl * 4 + 6); }
+            else { hl = rd_u8(p); cparse(dd, p, (long)hl * 8 + 6); }
+            nh = nnh;
+        }
+        return nh;
+    }
+    return 255;
+}
+
+// TCP SYN fingerprint (tcpip.h:215-249, ip.h:141-163, 478-503)
+template <class E>
+DEV void tcp_syn_fp(E &b, int ipv, const uint8_t *iph, const uint8_t *tcph, Cur opts) {
+    if (ipv == 4) {
+        b.lit("(40)");
+        b.putc('(');
+        if (ld(iph + 4) == 0 && ld(iph + 5) == 0) { b.putc('0'); b.putc('0'); }
+        b.putc(')');
+        b.putc('('); b.hex8(ld(iph + 8) & 0xe0); b.putc(')');
+    } else {
+        b.lit("(60)");
+        b.putc('(');
+        if (ld(iph + 1) == 0 && ld(iph + 2) == 0 && ld(iph + 3) == 0) { b.putc('0'); b.putc('0'); }
+        b.putc(')');
+        b.putc('('); b.hex8(ld(iph + 7) & 0xe0); b.putc(')');
+    }
+    b.putc('('); b.hex(tcph + 14, 2); b.putc(')');
+    b.putc('(');
+    Cur tmp = opts;
+    while (clen(tmp) > 0) {
+        uint32_t kind = rd_u8(tmp), len = 0;
+        Cur od; cset_null(od);
+        if (!(kind == 0 || kind == 1)) {
+            len = rd_u8(tmp);
+            if (len >= 2) cparse(od, tmp, (long)len - 2);
+        }
+        b.putc('(');
+        b.hex8(kind);
+        if (kind == 2 || kind == 3) { b.hex8(len); b.hex(od.d, clen(od)); }
+        b.putc(')');
+    }
+    b.putc(')');
+}
+
+// IP layer: ip_write_json pkt_proc.cc:1063 / analyze_ip_packet pkt_proc.cc:1597
+template <class E>
+DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uint32_t *lk, uint16_t *lo,
+                 int stride) {
+    const uint8_t *iph; int ipv;
+    uint32_t proto = ip_parse(pkt, iph, ipv);
+    for (int n = 0; n < 4 && (proto == 4 || proto == 41); n++) proto = ip_parse(pkt, iph, ipv);  // pkt_proc.cc:959
+    if (proto == 6) {
+        const uint8_t *tcph = cget_ptr(pkt, 20);
+        if (!tcph) return;
+        Cur opts; cset_null(opts);
+        cparse(opts, pkt, (long)(ld(tcph + 12) >> 4) * 4 - 20);
+        o.src_port = (ld(tcph) << 8) | ld(tcph + 1);
+        o.dst_port = (ld(tcph + 2) << 8) | ld(tcph + 3);
+        uint32_t fl = ld(tcph + 13);
+        bool syn = fl & 0x02, ack = fl & 0x10;
+        if (cfg.mode == MFP_MODE_WRITE_JSON) {
+            if (syn && !ack) {
+                if (cfg.select & SEL_TCP_SYN) {
+                    o.msg = MFP_MSG_TCP_SYN; o.flags |= MFP_FLAG_EMIT; o.fp_type = 7;
+                    fp_type_prefix(b, 7);
+                    tcp_syn_fp(b, ipv, iph, tcph, opts);
+                }
+                return;
+            }
+            if (syn && ack) {
+                if ((cfg.select & SEL_TCP_SYN) && (cfg.select & SEL_TCP_SYNACK)) {
+                    o.msg = MFP_MSG_TCP_SYNACK; o.flags |= MFP_FLAG_EMIT; o.fp_type = 13;
+                    fp_type_prefix(b, 13);
+                    tcp_syn_fp(b, ipv, iph, tcph, opts);
+                }
+                return;
+            }
+            if (clen(pkt) == 0) return;
+        }
+        tcp_data(b, cfg, o, pkt, tcph, base, lk, lo, stride);
+    } else if (proto == 17) {
+        const uint8_t *udph = cget_ptr(pkt, 8);
+        if (udph) {
+            o.src_port = (ld(udph) << 8) | ld(udph + 1);
+            o.dst_port = (ld(udph + 2) << 8) | ld(udph + 3);
+        }
+        udp_data(b, cfg, o, pkt, base, lk, lo, stride);
+    }
+}
+
+DEV bool ppp_is_ip(Cur &p) {                            // ppp::is_ip ppp.h:76
+    uint32_t b = look_u8(p);
+    if (b == 0x7e) {
+        rd_u8(p);
+        b = look_u8(p);
+        if (b == 0xff) { rd_u8(p); rd_u8(p); }
+    } else if (b == 0xff) {
+        rd_u8(p); rd_u8(p);
+    }
+    uint32_t proto;
+    b = look_u8(p);
+    if (b & 1) { uint32_t x; if (!(p.d && p.e > p.d)) { cset_null(p); proto = 0; } else { x = rd_u8(p); proto = x; } }
+    else { uint32_t v = 0; for (int i = 0; i < 2; i++) { v *= 256; v += rd_u8(p); } proto = v; }
+    return proto == 0x21 || proto == 0x57;
+}
+
+// link layer: stateful_pkt_proc::write_json(..., linktype) pkt_proc.cc:1328
+// and analyze_packet pkt_proc.cc:1814
+template <class E>
+DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t len, uint32_t linktype,
+                     uint32_t *lk, uint16_t *lo, int stride) {
+    o.fp_type = 0; o.msg = 0; o.flags = 0;
+    o.sni_off = o.ua_off = 0; o.sni_len = o.ua_len = 0xffff;
+    o.src_port = o.dst_port = 0;
+    Cur p = cmk(data, data + len);
+    switch (linktype) {
+    case 1: {                                           // eth::eth eth.h:137
+        uint64_t et;
+        cskip(p, 12);
+        if (!rd_uint(p, 2, et)) return;
+        if (et == 0x88a8) { cskip(p, 2); if (!rd_uint(p, 2, et)) return; }
+        while (et == 0x8100) { cskip(p, 2); if (!rd_uint(p, 2, et)) return; }
+        if (et == 0x8847) {
+            uint64_t lbl = 0;
+            while (!(lbl & 0x100)) { if (!rd_uint(p, 4, lbl)) return; }
+            et = 0x0800;
+        }
+        if (et == 0x8909) { cskip(p, 6); if (!rd_uint(p, 2, et)) return; }
+        if (et == 0x0800 || et == 0x86dd) break;
+        if (et == 0x8864) {
+            Cur t; cparse(t, p, 1); cparse(t, p, 1); cparse(t, p, 2); cparse(t, p, 2);
+            if (!ppp_is_ip(p)) return;
+            break;
+        }
+        return;
+    }
+    case 9:
+        if (!ppp_is_ip(p)) return;
+        break;
+    case 101:
+        break;
+    case 113: {                                         // linux_sll.hpp
+        uint64_t pt, ar, al, pr; Cur lla;
+        rd_uint(p, 2, pt); rd_uint(p, 2, ar); rd_uint(p, 2, al); cparse(lla, p, 8); rd_uint(p, 2, pr);
+        if (cnull(p) || !((ar == 1 || ar == 772) && (pr == 0x0800 || pr == 0x86dd))) return;
+        break;
+    }
+    case 276: {                                         // linux_sll2.hpp
+        uint64_t pr, t, ar; Cur lla;
+        rd_uint(p, 2, pr); rd_uint(p, 2, t); rd_uint(p, 4, t); rd_uint(p, 2, ar);
+        rd_uint(p, 1, t); rd_uint(p, 1, t); cparse(lla, p, 8);
+        if (cnull(p) || !((ar == 1 || ar == 772) && (pr == 0x0800 || pr == 0x86dd))) return;
+        break;
+    }
+    case 0: {                                           // loopback.hpp
+        if (cfg.mode != MFP_MODE_WRITE_JSON) return;
+        uint64_t v; rd_uint(p, 4, v);
+        if (!cnull(p)) {
+            if (!(v == 2 || v == 0x02000000 || v == 24 || v == 0x18000000 || v == 28 || v == 0x1c000000 ||
+                  v == 30 || v == 0x1e000000))
+                return;
+        }
+        break;
+    }
+    default:
+        return;
+    }
+    if (cnull(p)) return;
+    ip_path(b, cfg, o, p, data, lk, lo, stride);
+}
+
+}  // namespace mfp

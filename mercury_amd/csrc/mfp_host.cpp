@@ -1,0 +1,257 @@
+// mfp_host.cpp -- host side of libmercury_amd.so: context, configuration
+// (the reference's packet_filter_cfg syntax, global_config.h:143-153,
+// 246-275, 348-368), device buffers and the C-ABI batch entry points of
+// include/mfp.h.  There is no CPU fallback: without a HIP device the calls
+// fail with an error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mfp.h"
+#include "mfp_internal.h"
+
+extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
+                                      const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
+                                      uint64_t fp_cap, unsigned long long *fp_used, hipStream_t stream);
+
+static thread_local std::string g_err;
+
+void mfp_set_error(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+extern "C" MFP_EXPORT const char *mfp_last_error(void) { return g_err.c_str(); }
+extern "C" MFP_EXPORT uint32_t mfp_reference_version(void) { return (2u << 16) | (18u << 8) | 0u; }
+
+// selection bits, mirrored in mfp_device.hpp (SEL_*) and oracle/mfp_oracle.h
+enum : uint32_t {
+    SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
+    SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
+    SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9,
+    SEL_ALL = (1u << 10) - 1,
+};
+
+static std::string strip(const std::string &s) {
+    std::string o;
+    for (char c : s) if (!isspace((unsigned char)c)) o += c;
+    return o;
+}
+static std::string trim(const std::string &s) {
+    size_t a = 0, b = s.size();
+    while (a < b && isspace((unsigned char)s[a])) a++;
+    while (b > a && isspace((unsigned char)s[b - 1])) b--;
+    return s.substr(a, b - a);
+}
+
+// global_config::set_protocols (global_config.h:246) restricted to the
+// protocols of this path; the reference's traffic_selector turns the map
+// into matchers (proto_identify.h:620-895)
+static bool parse_select(const std::string &list, uint32_t &sel) {
+    std::string s = list.empty() ? "all" : list;
+    std::map<std::string, uint32_t> known = {
+        {"all", SEL_ALL}, {"none", 0},
+        {"tls", SEL_TLS_CH | SEL_TLS_SH | SEL_TLS_CERT}, {"tls.client_hello", SEL_TLS_CH},
+        {"tls.server_hello", SEL_TLS_SH}, {"tls.server_certificate", SEL_TLS_CERT},
+        {"ssh", SEL_SSH_CLIENT | SEL_SSH_SERVER}, {"ssh.client", SEL_SSH_CLIENT}, {"ssh.server", SEL_SSH_SERVER},
+        {"http", SEL_HTTP_REQ | SEL_HTTP_RESP}, {"http.request", SEL_HTTP_REQ}, {"http.response", SEL_HTTP_RESP},
+        {"tcp", SEL_TCP_SYN}, {"tcp.syn_ack", SEL_TCP_SYNACK}, {"dtls", SEL_DTLS},
+    };
+    bool none = false;
+    size_t pos = 0;
+    while (true) {
+        size_t c = s.find(',', pos);
+        std::string tok = strip(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
+        auto it = known.find(tok);
+        if (it == known.end()) {
+            mfp_set_error("protocol selection \"%s\" is not supported by the device path", tok.c_str());
+            return false;
+        }
+        if (tok == "none") none = true;
+        sel |= it->second;
+        if (c == std::string::npos) break;
+        pos = c + 1;
+    }
+    if (none) sel = 0;   // proto_identify.h:611-615
+    return true;
+}
+
+// fingerprint_format::set_fingerprint_format (global_config.h:92)
+static bool parse_format(const std::string &s, uint32_t &tls_format) {
+    size_t pos = 0;
+    while (pos <= s.size()) {
+        size_t c = s.find(',', pos);
+        std::string tok = strip(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
+        if (!tok.empty()) {
+            size_t sl = tok.find('/');
+            std::string proto = tok.substr(0, sl), ver = sl == std::string::npos ? "" : tok.substr(sl + 1);
+            if (proto == "tls") {
+                if (ver == "") tls_format = 0;
+                else if (ver == "1") tls_format = 1;
+                else if (ver == "2") tls_format = 2;
+                else { mfp_set_error("unknown fingerprint format %s", tok.c_str()); return false; }
+            } else if (proto != "quic") {
+                mfp_set_error("unknown fingerprint format %s", tok.c_str());
+                return false;
+            }
+        }
+        if (c == std::string::npos) break;
+        pos = c + 1;
+    }
+    return true;
+}
+
+bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis) {
+    sel = 0; tls_format = 0;
+    std::string s = cfg ? cfg : "";
+    if (s.find(';') == std::string::npos) return parse_select(s, sel);   // global_config.h:148-152
+    // key=value;... (config_generator.cc parse_tokens); without select=
+    // nothing is selected, as in the reference
+    size_t pos = 0;
+    while (pos <= s.size()) {
+        size_t c = s.find(';', pos);
+        std::string tok = trim(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
+        if (!tok.empty()) {
+            size_t eq = tok.find('=');
+            std::string key = trim(tok.substr(0, eq)), val = eq == std::string::npos ? "" : trim(tok.substr(eq + 1));
+            if (key == "select") { if (!parse_select(val, sel)) return false; }
+            else if (key == "format") { if (!parse_format(val, tls_format)) return false; }
+            else if (key == "resources") { if (resources) *resources = val; }
+            else if (key == "analysis") { if (analysis) *analysis = val.empty() || val == "1"; }
+            else if (key == "reassembly" || key == "tcp-reassembly") {
+                mfp_set_error("reassembly is not part of the device path");
+                return false;
+            }
+            // other keys (metadata, stats, ...) do not affect fingerprints
+        }
+        if (c == std::string::npos) break;
+        pos = c + 1;
+    }
+    return true;
+}
+
+struct mfp_context_s {
+    int device = 0;
+    uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
+    unsigned long long *d_used = nullptr;
+    // host-batch staging buffers (grown on demand)
+    uint8_t *d_arena = nullptr; size_t cap_arena = 0;
+    mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
+    mfp_record *d_rec = nullptr; size_t cap_rec = 0;
+    char *d_fp = nullptr; size_t cap_fp = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+};
+
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            mfp_set_error("%s failed: %s", #x, hipGetErrorString(e_));              \
+            return -2;                                                              \
+        }                                                                           \
+    } while (0)
+
+extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode) {
+    uint32_t sel, fmt;
+    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, nullptr, nullptr)) return nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        mfp_set_error("no HIP device available: the mercury_amd fingerprint path runs only on the GPU");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) { mfp_set_error("bad device %d", device); return nullptr; }
+    auto *c = new mfp_context_s;
+    c->device = device; c->select = sel; c->tls_format = fmt; c->mode = mode;
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_used, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        mfp_set_error("device init failed");
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipFree(c->d_used); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen) {
+    // every byte of a captured frame yields at most 4 fingerprint characters
+    // (TCP NOP option "(01)"), plus the type prefix; 8 bytes of slack per packet
+    return 4 * total_caplen + 72 * n + 64;
+}
+
+int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode) {
+    c->select = select; c->tls_format = tls_format; c->mode = mode;
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
+                                                   size_t n, mfp_record *d_rec, char *d_fp_arena, size_t fp_cap,
+                                                   uint64_t *d_fp_used, void *stream) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(d_fp_used, 0, 2 * sizeof(unsigned long long), s));
+    if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
+                               fp_cap, (unsigned long long *)d_fp_used, s) != 0) {
+        mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -3;
+    }
+    return 0;
+}
+
+template <class T>
+static int grow(T *&p, size_t &cap, size_t need) {
+    if (need <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    size_t nc = std::max(need, cap * 2);
+    if (hipMalloc(&p, nc * sizeof(T)) != hipSuccess) { cap = 0; return -1; }
+    cap = nc;
+    return 0;
+}
+
+extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint8_t *arena, size_t arena_len,
+                                                       const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                                       char *fp_arena, size_t fp_cap) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    // 16 bytes of padding after the arena: the kernel may read the aligned
+    // word that contains a packet's last byte
+    if (grow(c->d_arena, c->cap_arena, arena_len + 64) || grow(c->d_desc, c->cap_desc, n + 1) ||
+        grow(c->d_rec, c->cap_rec, n + 1) || grow(c->d_fp, c->cap_fp, fp_cap + 64)) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_arena, arena, arena_len, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, c->stream));
+    int r = mfp_process_batch_device(c, c->d_arena, c->d_desc, n, c->d_rec, c->d_fp, fp_cap,
+                                     (uint64_t *)c->d_used, c->stream);
+    if (r) return r;
+    unsigned long long used[2];
+    HIPCHK(hipMemcpyAsync(used, c->d_used, sizeof used, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(rec, c->d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    if (used[0]) HIPCHK(hipMemcpy(fp_arena, c->d_fp, used[0], hipMemcpyDeviceToHost));
+    return (long long)used[0];
+}

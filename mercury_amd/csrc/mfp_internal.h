@@ -1,0 +1,12 @@
+// mfp_internal.h -- declarations shared by the host translation units of
+// libmercury_amd.so (not part of the public C-ABI).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/mfp.h"
+
+void mfp_set_error(const char *fmt, ...);
+bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis);
+int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode);
