@@ -104,6 +104,12 @@ MFP_EXPORT long long mfp_process_batch_host(mfp_context ctx, const uint8_t *aren
 /* Upper bound on fp-arena bytes for packets totalling `total_caplen` bytes. */
 MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen);
 
+/* Parse a packet_filter_cfg string exactly as mfp_init does (host only, no
+ * device needed): *select receives the MFP selection bits, *tls_format 0/1/2.
+ * Returns 0, or -1 with mfp_last_error() set.  Mirrors global_config's
+ * parser (global_config.h:143-153,246-275,348-368). */
+MFP_EXPORT int mfp_parse_filter(const char *packet_filter_cfg, uint32_t *select, uint32_t *tls_format);
+
 /* last error string for this thread */
 MFP_EXPORT const char *mfp_last_error(void);
 

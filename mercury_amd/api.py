@@ -57,6 +57,8 @@ def load_library():
     lib.mfp_fp_arena_bound.argtypes = [sz, sz]
     lib.mfp_last_error.restype = ctypes.c_char_p
     lib.mfp_reference_version.restype = ctypes.c_uint32
+    lib.mfp_parse_filter.restype = ctypes.c_int
+    lib.mfp_parse_filter.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     _lib = lib
     return lib
 
@@ -108,6 +110,15 @@ class Context:
         r = self.lib.mfp_process_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, fp_cap, d_used, stream)
         if r != 0:
             raise MercuryAmdError("mfp_process_batch_device failed: " + _err(self.lib))
+
+
+def parse_filter(cfg):
+    """packet_filter_cfg -> (selection bits, tls format); host only."""
+    lib = load_library()
+    sel, fmt = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    if lib.mfp_parse_filter(None if cfg is None else cfg.encode(), ctypes.byref(sel), ctypes.byref(fmt)) != 0:
+        raise MercuryAmdError(_err(lib))
+    return sel.value, fmt.value
 
 
 def fingerprints(rec, fp_arena):

@@ -142,6 +142,14 @@ bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std:
     return true;
 }
 
+extern "C" MFP_EXPORT int mfp_parse_filter(const char *cfg, uint32_t *select, uint32_t *tls_format) {
+    uint32_t sel = 0, fmt = 0;
+    if (!mfp_parse_config(cfg, sel, fmt, nullptr, nullptr)) return -1;
+    if (select) *select = sel;
+    if (tls_format) *tls_format = fmt;
+    return 0;
+}
+
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;

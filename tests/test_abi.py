@@ -1,0 +1,87 @@
+"""The drop-in boundary on the CPU: libmercury_amd.so loads, exports every
+symbol include/*.h declares, parses the reference's packet_filter_cfg syntax
+(global_config.h:143-153,246-275) and refuses to run without a HIP device
+(there is no CPU fallback).  No compute calls are made here."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+import mercury_amd
+from oracle import oracle
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def declared_symbols():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"#define[^\n]*", "", src)
+        for m in re.finditer(r"MFP_EXPORT[^;{(]*?\b(\w+)\s*\(", src):
+            names.add(m.group(1))
+    return names
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", mercury_amd.library_path()], capture_output=True,
+                         check=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_library_loads():
+    lib = mercury_amd.load_library()
+    assert lib.mfp_reference_version() == (2 << 16) | (18 << 8)
+
+
+def test_every_declared_symbol_is_exported():
+    decl = declared_symbols()
+    assert {"mfp_init", "mfp_process_batch_device", "mfp_process_batch_host", "mfp_parse_filter"} <= decl
+    missing = decl - exported_symbols()
+    assert not missing, missing
+
+
+def test_only_declared_symbols_are_exported():
+    extra = {s for s in exported_symbols() - declared_symbols() if not s.startswith("_")}
+    assert not extra, extra
+
+
+@pytest.mark.parametrize("cfg,sel,fmt", [
+    (None, oracle.SEL_ALL, 0),
+    ("", oracle.SEL_ALL, 0),
+    ("all", oracle.SEL_ALL, 0),
+    ("tls", oracle.SEL["tls"], 0),
+    ("tls,dtls,ssh,http,tcp,tcp.syn_ack", oracle.SEL_ALL, 0),
+    ("select=tls,http;format=tls/1", oracle.SEL["tls"] | oracle.SEL["http"], 1),
+    ("select=tls.client_hello;format=tls/2", oracle.SEL["tls.client_hello"], 2),
+    ("select=ssh.client;", oracle.SEL["ssh.client"], 0),
+    ("format=tls/1;", 0, 1),          # key=value form without select= selects nothing
+    ("tls,none", 0, 0),              # proto_identify.h:611-615
+])
+def test_parse_filter(cfg, sel, fmt):
+    assert mercury_amd.parse_filter(cfg) == (sel, fmt)
+
+
+@pytest.mark.parametrize("cfg", ["select=tls", "quic", "tls,dns", "select=tls;format=tls/9", "select=tls;reassembly"])
+def test_parse_filter_rejects(cfg):
+    with pytest.raises(mercury_amd.MercuryAmdError):
+        mercury_amd.parse_filter(cfg)
+
+
+def test_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(mercury_amd.MercuryAmdError, match="no HIP device"):
+        mercury_amd.Context("tls")
+
+
+def test_record_layout_matches_header():
+    hdr = open(os.path.join(ROOT, "include", "mfp.h")).read()
+    assert "uint64_t offset;" in hdr and mercury_amd.DESC_DTYPE.itemsize == 16
+    assert mercury_amd.RECORD_DTYPE.itemsize == 32
+    assert ctypes.sizeof(ctypes.c_void_p) == 8
