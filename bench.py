@@ -123,10 +123,11 @@ def main():
     # size the fp arena from the unique set (exact per replica)
     rec_u, fp_u = ctx.process_host(ua, ud)
     reps = (n + len(ud) - 1) // len(ud)
-    cap = int(len(fp_u) * reps * 1.02) + (1 << 20)
+    # strings are 16-byte aligned and each wave reserves 128 KiB chunks
+    cap = int(int(rec_u["fp_len"].astype(np.int64).sum() + 16 * len(ud)) * reps * 1.05) + (2 << 30)
     d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_fp = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    d_used = torch.zeros(2, dtype=torch.int64, device="cuda")
+    d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream()
 
     def step():
@@ -136,7 +137,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    used, overflow = [int(x) for x in d_used.cpu()]
+    reserved, overflow, used, n_fallback = [int(x) for x in d_used.cpu()]
     if overflow:
         raise RuntimeError("fp arena overflow")
 
@@ -203,6 +204,7 @@ def main():
             },
             "gb_per_s": round(caplen_bytes * world * args.steps / elapsed / 1e9, 3),
             "fingerprints_per_step": n_fp,
+            "fallback_packets_per_step": n_fallback,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),

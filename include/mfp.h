@@ -86,11 +86,16 @@ MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int m
 MFP_EXPORT void mfp_finalize(mfp_context ctx);
 
 /* Device-resident batch: all pointers are device (HBM) pointers.  The fp
- * arena receives the fingerprint strings (compact, each packet's string at
- * rec[i].fp_offset; tile order, not packet order).  *d_fp_used (device u64,
- * zeroed by the call) receives the bytes used.  `stream` is a hipStream_t
- * (NULL = default stream).  The call is asynchronous; returns 0 or a
- * negative error.  fp_cap must be >= mfp_fp_arena_bound(...). */
+ * arena receives the fingerprint strings (each string contiguous at
+ * rec[i].fp_offset, 16-byte aligned, in no particular order; the arena may
+ * contain unused gaps).  d_fp_used is a device u64[4], zeroed by the call:
+ * [0] arena bytes reserved (copy [0, d_fp_used[0]) to read every string),
+ * [1] overflow flag (arena too small: records without strings), [2] string
+ * bytes written (sum of fp_len), [3] packets handled by the fallback lane.
+ * Packets are read with aligned 16-byte loads: the 16-byte block holding a
+ * packet's last byte must be readable.  `stream` is a hipStream_t (NULL =
+ * default stream).  Asynchronous; returns 0 or a negative error.  For no
+ * overflow fp_cap must be >= mfp_fp_arena_bound(n, total caplen). */
 MFP_EXPORT int mfp_process_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
                                         size_t n, mfp_record *d_rec, char *d_fp_arena, size_t fp_cap,
                                         uint64_t *d_fp_used, void *stream);
@@ -100,6 +105,10 @@ MFP_EXPORT int mfp_process_batch_device(mfp_context ctx, const uint8_t *d_arena,
 MFP_EXPORT long long mfp_process_batch_host(mfp_context ctx, const uint8_t *arena, size_t arena_len,
                                             const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                             char *fp_arena, size_t fp_cap);
+
+/* Pre-allocate the context's device workspace for batches of up to n
+ * packets (otherwise grown on demand by the first larger batch). */
+MFP_EXPORT int mfp_reserve(mfp_context ctx, size_t n);
 
 /* Upper bound on fp-arena bytes for packets totalling `total_caplen` bytes. */
 MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen);

@@ -9,7 +9,7 @@ LIB = os.path.join(HERE, "libmercury_amd.so")
 OBJ = os.path.join(HERE, "_obj")
 
 SOURCES = ["mfp_kernels.hip", "mfp_host.cpp"]
-HEADERS = ["mfp_device.hpp", "mfp_internal.h"]
+HEADERS = ["mfp_device.hpp", "mfp_wave.hpp", "mfp_internal.h"]
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 
 

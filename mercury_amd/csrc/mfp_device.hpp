@@ -407,15 +407,16 @@ DEV int fmt2_index(uint32_t t) {
     return -1;
 }
 // fmt-2 bucket after the private/unassigned remap (tls.h:1680-1693)
-DEV int fmt2_bucket(Ext &x) {
-    int idx = fmt2_index(x.type);
+DEV int fmt2_bucket_t(uint32_t type, uint32_t &encoded_type) {
+    int idx = fmt2_index(type);
     if (idx == -1) {
-        if (x.type == 65280 || x.type >= 65282) x.encoded_type = 65280;
-        else if (x.type >= 62 && x.type <= 65279 && !ext_is_grease(x.type)) x.encoded_type = 62;
-        idx = fmt2_index(x.encoded_type);
+        if (type == 65280 || type >= 65282) encoded_type = 65280;
+        else if (type >= 62 && type <= 65279 && !ext_is_grease(type)) encoded_type = 62;
+        idx = fmt2_index(encoded_type);
     }
     return idx;
 }
+DEV int fmt2_bucket(Ext &x) { return fmt2_bucket_t(x.type, x.encoded_type); }
 
 // ordering key of an extension for formats 1 and 2.  Returns a 32-bit
 // primary key; ties (same primary) are broken by ext_tie_less.

@@ -9,6 +9,7 @@
 #include <cctype>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -20,7 +21,12 @@
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
-                                      uint64_t fp_cap, unsigned long long *fp_used, hipStream_t stream);
+                                      uint64_t fp_cap, unsigned long long *fp_used, uint32_t *fallback, int lane_only,
+                                      hipStream_t stream);
+
+// fp-arena reservation granule of the wave kernel and its grid (mfp_kernels.hip)
+static const uint64_t kWaveChunk = 128 * 1024;
+static const uint64_t kWaveGridWaves = 2048 * 4;
 
 static thread_local std::string g_err;
 
@@ -153,7 +159,9 @@ extern "C" MFP_EXPORT int mfp_parse_filter(const char *cfg, uint32_t *select, ui
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
+    int lane_only = 0;                   // MFP_LANE_ONLY=1: lane-per-packet kernel only (A/B, debugging)
     unsigned long long *d_used = nullptr;
+    uint32_t *d_fallback = nullptr; size_t cap_fallback = 0;
     // host-batch staging buffers (grown on demand)
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
@@ -183,7 +191,9 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     if (device < 0 || device >= ndev) { mfp_set_error("bad device %d", device); return nullptr; }
     auto *c = new mfp_context_s;
     c->device = device; c->select = sel; c->tls_format = fmt; c->mode = mode;
-    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_used, 2 * sizeof(unsigned long long)) != hipSuccess ||
+    const char *lo = getenv("MFP_LANE_ONLY");
+    c->lane_only = lo && lo[0] == '1';
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_used, 4 * sizeof(unsigned long long)) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         mfp_set_error("device init failed");
         delete c;
@@ -195,34 +205,22 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
 extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipFree(c->d_used); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
+    (void)hipFree(c->d_used); (void)hipFree(c->d_fallback); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
 extern "C" MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen) {
     // every byte of a captured frame yields at most 4 fingerprint characters
-    // (TCP NOP option "(01)"), plus the type prefix; 8 bytes of slack per packet
-    return 4 * total_caplen + 72 * n + 64;
+    // (TCP NOP option "(01)"), plus the type prefix; 16-byte alignment of each
+    // string; plus one partly used reservation chunk per wave of the grid
+    uint64_t waves = (n + 63) / 64;
+    if (waves > kWaveGridWaves) waves = kWaveGridWaves;
+    return 4 * total_caplen + 88 * n + (waves + 1) * kWaveChunk;
 }
 
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode) {
     c->select = select; c->tls_format = tls_format; c->mode = mode;
-    return 0;
-}
-
-extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
-                                                   size_t n, mfp_record *d_rec, char *d_fp_arena, size_t fp_cap,
-                                                   uint64_t *d_fp_used, void *stream) {
-    if (!c) { mfp_set_error("null context"); return -1; }
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(d_fp_used, 0, 2 * sizeof(unsigned long long), s));
-    if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
-                               fp_cap, (unsigned long long *)d_fp_used, s) != 0) {
-        mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-        return -3;
-    }
     return 0;
 }
 
@@ -237,12 +235,43 @@ static int grow(T *&p, size_t &cap, size_t need) {
     return 0;
 }
 
+extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (grow(c->d_fallback, c->cap_fallback, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    return 0;
+}
+
+static int process_device_locked(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
+                                 mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
+                                 hipStream_t s) {
+    HIPCHK(hipSetDevice(c->device));
+    if (grow(c->d_fallback, c->cap_fallback, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
+    if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
+                               fp_cap, (unsigned long long *)d_fp_used, c->d_fallback, c->lane_only, s) != 0) {
+        mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -3;
+    }
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
+                                                   size_t n, mfp_record *d_rec, char *d_fp_arena, size_t fp_cap,
+                                                   uint64_t *d_fp_used, void *stream) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    return process_device_locked(c, d_arena, d_desc, n, d_rec, d_fp_arena, fp_cap, d_fp_used, (hipStream_t)stream);
+}
+
 extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                        const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                        char *fp_arena, size_t fp_cap) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
+    if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
     // 16 bytes of padding after the arena: the kernel may read the aligned
     // word that contains a packet's last byte
     if (grow(c->d_arena, c->cap_arena, arena_len + 64) || grow(c->d_desc, c->cap_desc, n + 1) ||
@@ -252,10 +281,10 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint
     }
     HIPCHK(hipMemcpyAsync(c->d_arena, arena, arena_len, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, c->stream));
-    int r = mfp_process_batch_device(c, c->d_arena, c->d_desc, n, c->d_rec, c->d_fp, fp_cap,
-                                     (uint64_t *)c->d_used, c->stream);
+    int r = process_device_locked(c, c->d_arena, c->d_desc, n, c->d_rec, c->d_fp, fp_cap, (uint64_t *)c->d_used,
+                                  c->stream);
     if (r) return r;
-    unsigned long long used[2];
+    unsigned long long used[4];
     HIPCHK(hipMemcpyAsync(used, c->d_used, sizeof used, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(rec, c->d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "mfp_device.hpp"
+#include "mfp_wave.hpp"
 
 namespace mfp {
 
@@ -26,9 +27,14 @@ struct KParams {
     mfp_record *rec;
     uint8_t *fp_arena;
     uint64_t fp_cap;
-    unsigned long long *fp_used;     // [0] bytes used, [1] overflow flag
+    unsigned long long *fp_used;     // [0] bytes reserved, [1] overflow flag, [2] bytes written, [3] fallback count
+    const uint32_t *idx;             // fallback lane: packet indices (count = fp_used[3]); nullptr = all packets
 };
 
+// k_fingerprint -- lane-per-packet walker, grid-stride over tiles of TILE
+// packets.  Used as the fallback lane of k_wave_fp (packets larger than the
+// wave kernel's LDS staging buffer, or whose fingerprint overflows its segment
+// table); with idx == nullptr it processes the whole batch.
 __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
     // per-lane extension scratch for TLS formats 1/2 (dynamic: 0 bytes for
     // format 0, so the default path keeps full occupancy)
@@ -39,8 +45,12 @@ __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
     __shared__ unsigned long long tile_base;
 
     const int tid = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * TILE + tid;
-    const bool live = i < P.n;
+    const uint64_t count = P.idx ? (uint64_t)__hip_atomic_load(&P.fp_used[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : P.n;
+    for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
+    const uint64_t t = tile * TILE + tid;
+    const bool live = t < count;
+    const uint64_t i = live ? (P.idx ? (uint64_t)P.idx[t] : t) : 0;
 
     mfp_pkt_desc dsc;
     if (live) dsc = P.desc[i];
@@ -72,14 +82,15 @@ __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
     uint32_t wbase = 0, total = 0;
 #pragma unroll
     for (int w = 0; w < TILE / 64; w++) {
-        uint32_t t = wave_tot[w];
-        if (w < wid) wbase += t;
-        total += t;
+        uint32_t tt = wave_tot[w];
+        if (w < wid) wbase += tt;
+        total += tt;
     }
     const uint32_t excl = wbase + incl - len;
     if (tid == 0) {
         unsigned long long b = total ? atomicAdd(&P.fp_used[0], (unsigned long long)total) : 0ull;
         if (b + total > P.fp_cap) { atomicExch(&P.fp_used[1], 1ull); b = ~0ull; }
+        else if (total) atomicAdd(&P.fp_used[2], (unsigned long long)total);
         tile_base = b;
     }
     __syncthreads();
@@ -112,21 +123,166 @@ __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
         r.reserved = 0;
         P.rec[i] = r;
     }
+    __syncthreads();   // tile_base / wave_tot reuse
+    }
 }
 
 }  // namespace mfp
 
-// launcher used by the host library (mfp_host.cpp)
+
+#define MFP_WAVE_GRID 2048   // 8 workgroups of 4 waves per CU x 256 CUs
+
+namespace mfpw {
+
+constexpr uint64_t CHUNK = 128 * 1024;   // fp-arena bytes reserved per wave at a time
+
+struct WParams {
+    Cfg cfg;
+    const uint8_t *arena;
+    const mfp_pkt_desc *desc;
+    uint64_t n;
+    mfp_record *rec;
+    uint8_t *fp_arena;
+    uint64_t fp_cap;
+    unsigned long long *fp_used;     // see KParams
+    uint32_t *fallback;              // packet indices for the lane-per-packet kernel
+};
+
+WDEV uint64_t rfl64(uint64_t v) {
+    return (uint64_t)rfl((uint32_t)v) | ((uint64_t)rfl((uint32_t)(v >> 32)) << 32);
+}
+WDEV uint32_t rdl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
+
+// k_wave_fp: every wave takes groups of 64 consecutive packets (one
+// descriptor per lane, coalesced) in a grid-stride loop, then handles the
+// group's packets one at a time with the whole wave (mfp_wave.hpp).  Each
+// wave reserves fingerprint-arena space CHUNK bytes at a time (one atomic per
+// CHUNK); every string starts 16-byte aligned.  Records are gathered in the
+// lanes (lane j holds packet j's record) and stored coalesced.
+__global__ __launch_bounds__(64 * WAVES) void k_wave_fp(WParams P) {
+    __shared__ WaveLds lds[WAVES];
+    const int wid = threadIdx.x >> 6;
+    WaveLds &L = lds[wid];
+    const uint32_t lane = lane_id();
+    const uint64_t ngroups = (P.n + 63) / 64;
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    uint64_t cur = 0, end = 0;
+    bool dead = false;
+    unsigned long long exact = 0;
+
+    for (uint64_t g = (uint64_t)blockIdx.x * WAVES + wid; g < ngroups; g += nw) {
+        const uint64_t i = g * 64 + lane;
+        const bool live = i < P.n;
+        uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_lt = 0xffff;
+        if (live) {
+            const uint4 dv = *(const uint4 *)(P.desc + i);
+            d_lo = dv.x; d_hi = dv.y; d_len = dv.z; d_lt = dv.w & 0xffff;
+        }
+        const int npk = (int)min((uint64_t)64, P.n - g * 64);
+        // this lane's record
+        uint64_t r_off = 0;
+        uint32_t r_len = 0, r_w2 = 0, r_sni = 0xffff0000u, r_ua = 0xffff0000u, r_ports = 0;
+        bool fb = false;
+
+        for (int j = 0; j < npk; j++) {
+            const uint64_t off = (uint64_t)rdl(d_lo, j) | ((uint64_t)rdl(d_hi, j) << 32);
+            const uint32_t caplen = rdl(d_len, j), lt = rdl(d_lt, j);
+            if (caplen > (uint32_t)MAX_PKT) { fb |= (int)lane == j; continue; }
+            const uint32_t a = (uint32_t)(off & 15);
+            const uint32_t nvec = (a + caplen + 15) >> 4;
+            const uint8_t *src = P.arena + (off - a);
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t v = lane; v < nvec; v += 64) *(uint4 *)(L.buf + 16 * v) = *(const uint4 *)(src + 16 * v);
+            __builtin_amdgcn_wave_barrier();
+
+            W w(L, P.cfg);
+            w.packet_walk((int)a, caplen, lt);
+            w.flush();
+            if (w.ovf) { fb |= (int)lane == j; continue; }
+            uint32_t type = w.o.fp_type, T = 0;
+            uint64_t fpo = 0;
+            if (type) {
+                if (!w.valid()) {
+                    type = 0;                       // fingerprint::final drops truncated fingerprints
+                } else {
+                    T = w.n;
+                    const uint64_t slot = (T + 15) & ~15u;
+                    if (!dead && cur + slot > end) {
+                        uint64_t b = 0;
+                        if (lane == 0) b = atomicAdd(&P.fp_used[0], (unsigned long long)CHUNK);
+                        b = rfl64(b);
+                        if (b + CHUNK > P.fp_cap) {
+                            dead = true;
+                            if (lane == 0) atomicExch(&P.fp_used[1], 1ull);
+                        } else {
+                            cur = b; end = b + CHUNK;
+                        }
+                    }
+                    if (dead) {
+                        type = 0; T = 0;
+                    } else {
+                        fpo = cur; cur += slot;
+                        w.expand(P.fp_arena + fpo);
+                        exact += T;
+                    }
+                }
+            }
+            if ((int)lane == j) {
+                r_off = fpo; r_len = T;
+                r_w2 = type | (w.o.msg << 8) | (w.o.flags << 16);
+                r_sni = (w.o.sni_len == 0xffff ? 0 : (w.o.sni_off & 0xffff)) | (w.o.sni_len << 16);
+                r_ua = (w.o.ua_len == 0xffff ? 0 : (w.o.ua_off & 0xffff)) | (w.o.ua_len << 16);
+                r_ports = (w.o.src_port & 0xffff) | (w.o.dst_port << 16);
+            }
+        }
+        const uint64_t fbm = ballot(fb);
+        if (fbm) {
+            uint64_t b = 0;
+            if (lane == 0) b = atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(fbm));
+            b = rfl64(b);
+            if (fb) P.fallback[b + __builtin_popcountll(fbm & ((1ull << lane) - 1))] = (uint32_t)i;
+        }
+        if (live && !fb) {
+            uint4 *rp = (uint4 *)(P.rec + i);
+            rp[0] = make_uint4((uint32_t)r_off, (uint32_t)(r_off >> 32), r_len, r_w2);
+            rp[1] = make_uint4(r_sni, r_ua, r_ports, 0u);
+        }
+    }
+    if (lane == 0 && exact) atomicAdd(&P.fp_used[2], exact);
+}
+
+}  // namespace mfpw
+
+// launchers used by the host library (mfp_host.cpp)
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
-                                      uint64_t fp_cap, unsigned long long *fp_used, hipStream_t stream) {
+                                      uint64_t fp_cap, unsigned long long *fp_used, uint32_t *fallback, int lane_only,
+                                      hipStream_t stream) {
     if (n == 0) return 0;
+    size_t shmem = tls_format ? (size_t)mfp::MAX_LDS_EXT * mfp::TILE * 6 : 0;
     mfp::KParams P;
     P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
-    uint64_t blocks = (n + mfp::TILE - 1) / mfp::TILE;
-    size_t shmem = tls_format ? (size_t)mfp::MAX_LDS_EXT * mfp::TILE * 6 : 0;
-    hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)blocks), dim3(mfp::TILE), shmem, stream, P);
+    P.idx = nullptr;
+    if (lane_only) {
+        uint64_t blocks = (n + mfp::TILE - 1) / mfp::TILE;
+        hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)blocks), dim3(mfp::TILE), shmem, stream, P);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    mfpw::WParams W;
+    W.cfg.select = select; W.cfg.tls_format = tls_format; W.cfg.mode = mode;
+    W.arena = arena; W.desc = desc; W.n = n; W.rec = rec; W.fp_arena = fp_arena; W.fp_cap = fp_cap;
+    W.fp_used = fp_used; W.fallback = fallback;
+    uint64_t groups = (n + 63) / 64;
+    uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
+    if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
+    hipLaunchKernelGGL(mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+    if (hipGetLastError() != hipSuccess) return -1;
+    // fallback lane over the packets the wave kernel handed back
+    P.idx = fallback;
+    uint64_t fblocks = (n + mfp::TILE - 1) / mfp::TILE;
+    if (fblocks > 1024) fblocks = 1024;
+    hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

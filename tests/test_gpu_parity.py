@@ -162,16 +162,18 @@ def test_large_device_batch_properties():
     cap = ctx.fp_arena_bound(desc)
     d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_fp = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    d_used = torch.zeros(2, dtype=torch.int64, device="cuda")
+    d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
     ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(), cap,
                        d_used.data_ptr(), 0)
     torch.cuda.synchronize()
-    used, overflow = [int(x) for x in d_used.cpu()]
+    reserved, overflow, exact, n_fallback = [int(x) for x in d_used.cpu()]
     assert overflow == 0
     rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
-    assert int(rec["fp_len"].astype(np.int64).sum()) == used
-    # tile slices are disjoint: every string lies inside [0, used)
-    assert int((rec["fp_offset"] + rec["fp_len"]).max()) <= used
+    assert int(rec["fp_len"].astype(np.int64).sum()) == exact
+    # every string lies inside the reserved part of the arena, 16-byte aligned
+    assert int((rec["fp_offset"] + rec["fp_len"]).max()) <= reserved
+    assert int((rec["fp_offset"][rec["fp_len"] > 0] % 16).max()) == 0
+    used = reserved
     rng = np.random.default_rng(1)
     sample = rng.choice(n, 20000, replace=False)
     fp_host = d_fp[:used].cpu().numpy().tobytes()
