@@ -87,8 +87,8 @@ MFP_EXPORT void mfp_finalize(mfp_context ctx);
 
 /* Device-resident batch: all pointers are device (HBM) pointers.  The fp
  * arena receives the fingerprint strings (each string contiguous at
- * rec[i].fp_offset, 16-byte aligned, in no particular order; the arena may
- * contain unused gaps).  d_fp_used is a device u64[4], zeroed by the call:
+ * rec[i].fp_offset, in no particular order; the arena may contain unused
+ * gaps).  d_fp_used is a device u64[4], zeroed by the call:
  * [0] arena bytes reserved (copy [0, d_fp_used[0]) to read every string),
  * [1] overflow flag (arena too small: records without strings), [2] string
  * bytes written (sum of fp_len), [3] packets handled by the fallback lane.

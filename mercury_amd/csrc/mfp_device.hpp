@@ -804,6 +804,7 @@ struct Out {
 };
 struct Cfg {
     uint32_t select, tls_format, mode;
+    uint32_t classify;   // stop after protocol identification (o.msg), emit nothing
 };
 enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
@@ -924,6 +925,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
             for (int i = 0; i < 36; i++) hit |= (k_http_kw[i] == kw);
             if (hit) {
                 o.msg = MFP_MSG_HTTP_REQ;
+                if (cfg.classify) return;
                 if (http_msg(b, pkt, true, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 3; }
                 else o.msg = 0;
                 return;
@@ -931,12 +933,14 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         }
         if ((sel & SEL_HTTP_RESP) && kw == 0x48545450u) {
             o.msg = MFP_MSG_HTTP_RESP;
+            if (cfg.classify) return;
             if (http_msg(b, pkt, false, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 4; }
             else o.msg = 0;
         }
         return;
     }
     o.msg = msg;
+    if (cfg.classify) return;
     switch (msg) {
     case MFP_MSG_TLS_CH: {
         Cur p = pkt;
@@ -1052,6 +1056,7 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, ui
     uint32_t msg = hb == 1 ? MFP_MSG_DTLS_CH : hb == 2 ? MFP_MSG_DTLS_SH : hb == 3 ? MFP_MSG_DTLS_HVR : 0;
     if (!msg) return;
     o.msg = msg;
+    if (cfg.classify) return;
     Cur d = pkt, frag, body; cset_null(frag); cset_null(body);
     uint64_t t, len = 0, foff = 0, flen = 0, more = 0;
     if (clen(d) < 13) cset_null(d);
@@ -1179,7 +1184,9 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
         if (cfg.mode == MFP_MODE_WRITE_JSON) {
             if (syn && !ack) {
                 if (cfg.select & SEL_TCP_SYN) {
-                    o.msg = MFP_MSG_TCP_SYN; o.flags |= MFP_FLAG_EMIT; o.fp_type = 7;
+                    o.msg = MFP_MSG_TCP_SYN;
+                    if (cfg.classify) return;
+                    o.flags |= MFP_FLAG_EMIT; o.fp_type = 7;
                     fp_type_prefix(b, 7);
                     tcp_syn_fp(b, ipv, iph, tcph, opts);
                 }
@@ -1187,7 +1194,9 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
             }
             if (syn && ack) {
                 if ((cfg.select & SEL_TCP_SYN) && (cfg.select & SEL_TCP_SYNACK)) {
-                    o.msg = MFP_MSG_TCP_SYNACK; o.flags |= MFP_FLAG_EMIT; o.fp_type = 13;
+                    o.msg = MFP_MSG_TCP_SYNACK;
+                    if (cfg.classify) return;
+                    o.flags |= MFP_FLAG_EMIT; o.fp_type = 13;
                     fp_type_prefix(b, 13);
                     tcp_syn_fp(b, ipv, iph, tcph, opts);
                 }

@@ -21,11 +21,12 @@
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
-                                      uint64_t fp_cap, unsigned long long *fp_used, uint32_t *fallback, int lane_only,
+                                      uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
+                                      unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
                                       hipStream_t stream);
 
 // fp-arena reservation granule of the wave kernel and its grid (mfp_kernels.hip)
-static const uint64_t kWaveChunk = 128 * 1024;
+static const uint64_t kWaveChunk = 32 * 1024;
 static const uint64_t kWaveGridWaves = 2048 * 4;
 
 static thread_local std::string g_err;
@@ -159,9 +160,11 @@ extern "C" MFP_EXPORT int mfp_parse_filter(const char *cfg, uint32_t *select, ui
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
-    int lane_only = 0;                   // MFP_LANE_ONLY=1: lane-per-packet kernel only (A/B, debugging)
+    int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|wave|lane (A/B, debugging)
+    uint32_t bin_wave_mask = 0x2;        // bins fingerprinted by the wave kernel (MFP_BIN_WAVE_MASK)
     unsigned long long *d_used = nullptr;
-    uint32_t *d_fallback = nullptr; size_t cap_fallback = 0;
+    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass
+    uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list
     // host-batch staging buffers (grown on demand)
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
@@ -191,9 +194,13 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     if (device < 0 || device >= ndev) { mfp_set_error("bad device %d", device); return nullptr; }
     auto *c = new mfp_context_s;
     c->device = device; c->select = sel; c->tls_format = fmt; c->mode = mode;
-    const char *lo = getenv("MFP_LANE_ONLY");
-    c->lane_only = lo && lo[0] == '1';
+    const char *st = getenv("MFP_STRATEGY");
+    if (st && !strcmp(st, "wave")) c->strategy = MFP_STRATEGY_WAVE;
+    else if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
+    const char *bm = getenv("MFP_BIN_WAVE_MASK");
+    if (bm) c->bin_wave_mask = (uint32_t)strtoul(bm, nullptr, 0);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_used, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_bins, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         mfp_set_error("device init failed");
         delete c;
@@ -205,7 +212,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
 extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipFree(c->d_used); (void)hipFree(c->d_fallback); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
+    (void)hipFree(c->d_used); (void)hipFree(c->d_bins); (void)hipFree(c->d_work); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -214,9 +221,10 @@ extern "C" MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen) {
     // every byte of a captured frame yields at most 4 fingerprint characters
     // (TCP NOP option "(01)"), plus the type prefix; 16-byte alignment of each
     // string; plus one partly used reservation chunk per wave of the grid
+    // for each of the (up to 6) wave-kernel launches of a batch
     uint64_t waves = (n + 63) / 64;
     if (waves > kWaveGridWaves) waves = kWaveGridWaves;
-    return 4 * total_caplen + 88 * n + (waves + 1) * kWaveChunk;
+    return 4 * total_caplen + 88 * n + 6 * (waves + 1) * kWaveChunk;
 }
 
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode) {
@@ -239,7 +247,7 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_fallback, c->cap_fallback, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->d_work, c->cap_work, 6 * n + 1)) { mfp_set_error("device allocation failed"); return -2; }
     return 0;
 }
 
@@ -247,10 +255,11 @@ static int process_device_locked(mfp_context c, const uint8_t *d_arena, const mf
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
                                  hipStream_t s) {
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_fallback, c->cap_fallback, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->d_work, c->cap_work, 6 * n + 1)) { mfp_set_error("device allocation failed"); return -2; }
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(c->d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
-                               fp_cap, (unsigned long long *)d_fp_used, c->d_fallback, c->lane_only, s) != 0) {
+                               fp_cap, (unsigned long long *)d_fp_used, c->d_work, c->d_bins, c->strategy, c->bin_wave_mask, s) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

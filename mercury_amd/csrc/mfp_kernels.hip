@@ -28,7 +28,8 @@ struct KParams {
     uint8_t *fp_arena;
     uint64_t fp_cap;
     unsigned long long *fp_used;     // [0] bytes reserved, [1] overflow flag, [2] bytes written, [3] fallback count
-    const uint32_t *idx;             // fallback lane: packet indices (count = fp_used[3]); nullptr = all packets
+    const uint32_t *idx;             // packet indices (count = *count); nullptr = all n packets
+    const unsigned long long *count;
 };
 
 // k_fingerprint -- lane-per-packet walker, grid-stride over tiles of TILE
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
     __shared__ unsigned long long tile_base;
 
     const int tid = threadIdx.x;
-    const uint64_t count = P.idx ? (uint64_t)__hip_atomic_load(&P.fp_used[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    const uint64_t count = P.idx ? (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                  : P.n;
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
     const uint64_t t = tile * TILE + tid;
@@ -127,14 +128,62 @@ __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
     }
 }
 
+
+// protocol bins of the classify pass: each bin is then fingerprinted by its
+// own k_fingerprint launch over a compact index list, so the lanes of a wave
+// walk the same protocol (same parser, similar loop trip counts)
+constexpr int NBINS = 5;
+DEV int msg_bin(uint32_t msg) {
+    switch (msg) {
+    case MFP_MSG_TLS_CH: return 0;
+    case MFP_MSG_HTTP_REQ: return 1;
+    case MFP_MSG_TCP_SYN: case MFP_MSG_TCP_SYNACK: return 2;
+    case MFP_MSG_HTTP_RESP: return 3;
+    default: return 4;
+    }
+}
+
+// k_classify: lane-per-packet link/IP/transport walk + protocol
+// identification only (proto_identify.h:936-968); appends each packet index
+// to its bin with one wave-aggregated atomic per non-empty bin
+__global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, uint64_t bin_stride,
+                                                     unsigned long long *bin_count) {
+    const uint64_t i = (uint64_t)blockIdx.x * TILE + threadIdx.x;
+    const bool live = i < P.n;
+    int bin = -1;
+    if (live) {
+        mfp_pkt_desc dsc = P.desc[i];
+        Out o;
+        Em<false> e;
+        Cfg c = P.cfg;
+        c.classify = 1;
+        packet_walk(e, c, o, P.arena + dsc.offset, dsc.caplen, dsc.linktype, nullptr, nullptr, 0);
+        bin = msg_bin(o.msg);
+    }
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < NBINS; b++) {
+        const uint64_t m = __ballot(bin == b);
+        if (!m) continue;
+        const int leader = (int)__builtin_ctzll(m);
+        unsigned long long base = 0;
+        if ((int)lane == leader) base = atomicAdd(&bin_count[b], (unsigned long long)__builtin_popcountll(m));
+        base = __shfl(base, leader, 64);
+        if (bin == b) bins[b * bin_stride + base + __builtin_popcountll(m & ((1ull << lane) - 1))] = (uint32_t)i;
+    }
+}
+
 }  // namespace mfp
 
-
+#include "mfp_internal.h"
 #define MFP_WAVE_GRID 2048   // 8 workgroups of 4 waves per CU x 256 CUs
+#ifndef MFP_WAVE_MINW
+#define MFP_WAVE_MINW 4      // min waves per SIMD (caps VGPRs at 128)
+#endif
 
 namespace mfpw {
 
-constexpr uint64_t CHUNK = 128 * 1024;   // fp-arena bytes reserved per wave at a time
+constexpr uint64_t CHUNK = 32 * 1024;    // fp-arena bytes reserved per wave at a time
 
 struct WParams {
     Cfg cfg;
@@ -146,6 +195,8 @@ struct WParams {
     uint64_t fp_cap;
     unsigned long long *fp_used;     // see KParams
     uint32_t *fallback;              // packet indices for the lane-per-packet kernel
+    const uint32_t *idx;             // packet indices (count = *count); nullptr = all n packets
+    const unsigned long long *count;
 };
 
 WDEV uint64_t rfl64(uint64_t v) {
@@ -159,26 +210,30 @@ WDEV uint32_t rdl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlan
 // wave reserves fingerprint-arena space CHUNK bytes at a time (one atomic per
 // CHUNK); every string starts 16-byte aligned.  Records are gathered in the
 // lanes (lane j holds packet j's record) and stored coalesced.
-__global__ __launch_bounds__(64 * WAVES) void k_wave_fp(WParams P) {
+__global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P) {
     __shared__ WaveLds lds[WAVES];
-    const int wid = threadIdx.x >> 6;
+    // wave index made provably uniform: the compiler would otherwise treat the
+    // group loop as divergent and move all the scalar parse state to VGPRs
+    const int wid = (int)rfl(threadIdx.x >> 6);
     WaveLds &L = lds[wid];
     const uint32_t lane = lane_id();
-    const uint64_t ngroups = (P.n + 63) / 64;
+    const uint64_t n_eff = P.idx ? (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P.n;
+    const uint64_t ngroups = (n_eff + 63) / 64;
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
     uint64_t cur = 0, end = 0;
     bool dead = false;
     unsigned long long exact = 0;
 
     for (uint64_t g = (uint64_t)blockIdx.x * WAVES + wid; g < ngroups; g += nw) {
-        const uint64_t i = g * 64 + lane;
-        const bool live = i < P.n;
+        const uint64_t t = g * 64 + lane;
+        const bool live = t < n_eff;
+        const uint64_t i = live ? (P.idx ? (uint64_t)P.idx[t] : t) : 0;
         uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_lt = 0xffff;
         if (live) {
             const uint4 dv = *(const uint4 *)(P.desc + i);
             d_lo = dv.x; d_hi = dv.y; d_len = dv.z; d_lt = dv.w & 0xffff;
         }
-        const int npk = (int)min((uint64_t)64, P.n - g * 64);
+        const int npk = (int)min((uint64_t)64, n_eff - g * 64);
         // this lane's record
         uint64_t r_off = 0;
         uint32_t r_len = 0, r_w2 = 0, r_sni = 0xffff0000u, r_ua = 0xffff0000u, r_ports = 0;
@@ -256,33 +311,67 @@ __global__ __launch_bounds__(64 * WAVES) void k_wave_fp(WParams P) {
 // launchers used by the host library (mfp_host.cpp)
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
-                                      uint64_t fp_cap, unsigned long long *fp_used, uint32_t *fallback, int lane_only,
+                                      uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
+                                      unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
                                       hipStream_t stream) {
     if (n == 0) return 0;
     size_t shmem = tls_format ? (size_t)mfp::MAX_LDS_EXT * mfp::TILE * 6 : 0;
     mfp::KParams P;
-    P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode;
+    P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
-    P.idx = nullptr;
-    if (lane_only) {
-        uint64_t blocks = (n + mfp::TILE - 1) / mfp::TILE;
-        hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)blocks), dim3(mfp::TILE), shmem, stream, P);
+    P.idx = nullptr; P.count = nullptr;
+    const uint64_t tiles = (n + mfp::TILE - 1) / mfp::TILE;
+    if (strategy == MFP_STRATEGY_LANE) {
+        hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)tiles), dim3(mfp::TILE), shmem, stream, P);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     mfpw::WParams W;
     W.cfg.select = select; W.cfg.tls_format = tls_format; W.cfg.mode = mode;
     W.arena = arena; W.desc = desc; W.n = n; W.rec = rec; W.fp_arena = fp_arena; W.fp_cap = fp_cap;
-    W.fp_used = fp_used; W.fallback = fallback;
+    W.fp_used = fp_used; W.fallback = work + (strategy == MFP_STRATEGY_BINNED ? (uint64_t)mfp::NBINS * n : 0);
+    W.idx = nullptr; W.count = nullptr;
     uint64_t groups = (n + 63) / 64;
+    if (strategy == MFP_STRATEGY_BINNED) {
+        // classify, then one launch per protocol bin: the lane-per-packet
+        // walker or the wave-per-packet walker, whichever is faster for
+        // that protocol (bin_wave_mask bit b = wave kernel for bin b)
+        hipLaunchKernelGGL(mfp::k_classify, dim3((uint32_t)tiles), dim3(mfp::TILE), 0, stream, P, work, n, bin_count);
+        if (hipGetLastError() != hipSuccess) return -1;
+        uint64_t fblocks = tiles < 2048 ? tiles : 2048;
+        uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
+        if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
+        bool any_wave = false;
+        for (int b = 0; b < mfp::NBINS; b++) {
+            if (bin_wave_mask & (1u << b)) {
+                W.idx = work + (uint64_t)b * n;
+                W.count = bin_count + b;
+                hipLaunchKernelGGL(mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+                any_wave = true;
+            } else {
+                P.idx = work + (uint64_t)b * n;
+                P.count = bin_count + b;
+                hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
+            }
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
+        if (any_wave) {
+            // fallback lane for packets the wave kernel handed back
+            P.idx = W.fallback;
+            P.count = fp_used + 3;
+            uint64_t fb = tiles < 1024 ? tiles : 1024;
+            hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fb), dim3(mfp::TILE), shmem, stream, P);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
     if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
     hipLaunchKernelGGL(mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
     if (hipGetLastError() != hipSuccess) return -1;
     // fallback lane over the packets the wave kernel handed back
-    P.idx = fallback;
-    uint64_t fblocks = (n + mfp::TILE - 1) / mfp::TILE;
-    if (fblocks > 1024) fblocks = 1024;
+    P.idx = work;
+    P.count = fp_used + 3;
+    uint64_t fblocks = tiles < 1024 ? tiles : 1024;
     hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

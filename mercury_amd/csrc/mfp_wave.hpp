@@ -33,7 +33,7 @@ namespace mfpw {
 
 constexpr int WAVES = 4;            // waves per workgroup
 constexpr int PKT_CAP = 2048;       // staged packet bytes (incl. 16-byte alignment slack)
-constexpr int SCR_CAP = 768;        // literal / computed-byte pool
+constexpr int SCR_CAP = 768;        // literal / computed-byte pool (last 16 bytes: write sink)
 constexpr int SEG_CAP = 256;        // segments per fingerprint
 constexpr int MAX_PKT = PKT_CAP - 16;
 constexpr uint32_t FP_MAX = 8192;   // fingerprint::MAX_FP_STR_LEN fingerprint.h:15
@@ -94,16 +94,40 @@ struct W {
     WDEV W(WaveLds &l, const Cfg &c) : L(l), cfg(c) {
         lane = lane_id();
         n = 0; last_putc = false; nseg = 0; scr = 0; ovf = false; pk_kind = 0; pk_src = 0; pk_len = 0;
+        refill(0);
     }
 
     // ---- uniform byte reads from the staged packet ----
-    WDEV uint32_t ld(int o_) { return rfl(L.buf[o_]); }
-    WDEV uint32_t be16(int o_) { return (ld(o_) << 8) | ld(o_ + 1); }
-    WDEV uint64_t le8(int o_) {
-        uint64_t w = 0;
-        for (int i = 0; i < 8; i++) w |= (uint64_t)ld(o_ + i) << (8 * i);
-        return w;
+    // A 256-byte window of the packet is held in one VGPR (lane l holds the
+    // dword at wbase + 4 l); a uniform read is v_readlane + shift, and only
+    // a read outside the window goes back to LDS (one ds_read_b32 per lane).
+    uint32_t win;
+    int wbase;
+    WDEV void refill(int o_) {
+        wbase = o_ & ~3;
+        const int a = wbase + 4 * (int)lane;
+        win = a + 4 <= PKT_CAP + SCR_CAP ? *(const uint32_t *)(L.buf + a) : 0u;
     }
+    WDEV uint32_t rdlane(int k) { return (uint32_t)__builtin_amdgcn_readlane((int)win, k); }
+    WDEV uint32_t ld(int o_) {
+        uint32_t rel = (uint32_t)(o_ - wbase);
+        if (rel > 255) { refill(o_); rel = (uint32_t)(o_ - wbase); }
+        return (rdlane((int)(rel >> 2)) >> ((rel & 3) * 8)) & 0xff;
+    }
+    // 4 bytes at o_, little-endian order (byte o_ in bits 0..7)
+    WDEV uint32_t ld4le(int o_) {
+        uint32_t rel = (uint32_t)(o_ - wbase);
+        if (rel > 248) { refill(o_); rel = (uint32_t)(o_ - wbase); }
+        uint32_t lo = rdlane((int)(rel >> 2));
+        if ((rel & 3) == 0) return lo;
+        uint32_t hi = rdlane((int)(rel >> 2) + 1);
+        return (uint32_t)((((uint64_t)hi << 32) | lo) >> ((rel & 3) * 8));
+    }
+    // bswap lowers to v_perm_b32 (VALU); readfirstlane brings the result
+    // back to an SGPR so the parse arithmetic that follows stays scalar
+    WDEV uint32_t be32(int o_) { return rfl(__builtin_bswap32(ld4le(o_))); }
+    WDEV uint32_t be16(int o_) { return be32(o_) >> 16; }
+    WDEV uint64_t le8(int o_) { return (uint64_t)ld4le(o_) | ((uint64_t)ld4le(o_ + 4) << 32); }
 
     // ---- datum operations (datum.h) ----
     WDEV bool cskip(C &c, int k) {                       // datum::skip datum.h:365
@@ -123,11 +147,14 @@ struct W {
         dst.d = r.d; dst.e = r.d >= 0 ? r.d + (int)k : -1;
         if (r.d >= 0) r.d += (int)k;
     }
+    WDEV uint64_t rd_be(int o_, int k) {                 // k (1..8) bytes, big-endian
+        if (k <= 4) return be32(o_) >> (32 - 8 * k);
+        return ((uint64_t)be32(o_) << (8 * (k - 4))) | (be32(o_ + 4) >> (32 - 8 * (k - 4)));
+    }
     WDEV bool rd_uint(C &c, int k, uint64_t &out) {      // datum::read_uint datum.h:795
         if (c.d >= 0 && c.d + k <= c.e) {
-            uint64_t v = 0;
-            for (int i = 0; i < k; i++) v = (v << 8) | ld(c.d + i);
-            c.d += k; out = v; return true;
+            out = rd_be(c.d, k);
+            c.d += k; return true;
         }
         cset_null(c); out = 0; return false;
     }
@@ -141,9 +168,7 @@ struct W {
     }
     WDEV bool look_uint(C &c, int k, uint64_t &out) {    // datum::lookahead_uint datum.h:712
         if (c.d >= 0 && c.d + k <= c.e) {
-            uint64_t v = 0;
-            for (int i = 0; i < k; i++) v = (v << 8) | ld(c.d + i);
-            out = v; return true;
+            out = rd_be(c.d, k); return true;
         }
         return false;
     }
@@ -165,9 +190,8 @@ struct W {
     WDEV int scan(int a, int e, P pred) {
         for (int base = a; base < e; base += 64) {
             int q = base + (int)lane;
-            bool hit = false;
-            if (q < e) hit = pred((uint32_t)L.buf[q]);
-            uint64_t m = ballot(hit);
+            uint32_t c = L.buf[q < e ? q : base];
+            uint64_t m = ballot(q < e && pred(c));
             if (m) return base + (int)__builtin_ctzll(m);
         }
         return e;
@@ -194,7 +218,8 @@ struct W {
         if (!(c.d >= 0 && clen(c) >= k)) return false;
         for (int base = 0; base < k; base += 64) {
             int j = base + (int)lane;
-            bool bad = j < k && L.buf[c.d + j] != L.buf[x + j];
+            int jj = j < k ? j : 0;
+            bool bad = j < k && L.buf[c.d + jj] != L.buf[x + jj];
             if (ballot(bad)) return false;
         }
         return true;
@@ -206,7 +231,8 @@ struct W {
         int la = clen(a), lb = clen(b), m = la < lb ? la : lb;
         for (int base = 0; base < m; base += 64) {
             int j = base + (int)lane;
-            bool diff = j < m && L.buf[a.d + j] != L.buf[b.d + j];
+            int jj = j < m ? j : 0;
+            bool diff = j < m && L.buf[a.d + jj] != L.buf[b.d + jj];
             uint64_t bm = ballot(diff);
             if (bm) {
                 int k = base + (int)__builtin_ctzll(bm);
@@ -219,10 +245,9 @@ struct W {
     // ---- emitter ----
     WDEV void seg_store(uint32_t end_chars) {
         if (nseg >= SEG_CAP) { ovf = true; return; }
-        if (lane == 0) {
-            L.seg_end[nseg] = (uint16_t)end_chars;
-            L.seg_info[nseg] = (uint32_t)pk_src | (pk_kind << 16);
-        }
+        // every lane stores the same value: no exec-mask region in the walk
+        L.seg_end[nseg] = (uint16_t)end_chars;
+        L.seg_info[nseg] = (uint32_t)pk_src | (pk_kind << 16);
         nseg++;
     }
     WDEV void add(uint32_t kind, int src, int len) {
@@ -243,8 +268,15 @@ struct W {
     }
     // write k (1..8) bytes of v (little-endian) to the scratch pool as RAW
     WDEV void raw_bytes(uint64_t v, int k) {
-        if (scr + k > SCR_CAP) { ovf = true; n += (uint32_t)k; return; }
-        if ((int)lane < k) L.buf[PKT_CAP + scr + (int)lane] = (uint8_t)(v >> (8 * lane));
+        if (scr + k > SCR_CAP - 16) { ovf = true; n += (uint32_t)k; return; }
+        // lanes >= k store into the sink at the end of the scratch pool.  The
+        // lane id goes through an opaque move so the per-lane byte shifts of
+        // literal strings are not hoisted out of the packet loop (LICM would
+        // keep one VGPR pair per literal live across the whole kernel).
+        uint32_t ln;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+        const int dst = (int)ln < k ? PKT_CAP + scr + (int)ln : PKT_CAP + SCR_CAP - 16;
+        L.buf[dst] = (uint8_t)(v >> (8 * (ln & 7)));
         add(K_RAW, PKT_CAP + scr, k);
         scr += k;
     }
@@ -445,6 +477,9 @@ struct W {
     // formats 1 and 2: kept extensions in lanes, rank by the reference's
     // comparator (tls.h:1637-1655, 1709-1724), emit in rank order
     WDEV void exts_fp12(C exts, int role, int fmt) {
+#ifdef MFP_PROBE_NOFMT12
+        return;
+#endif
         putc('[');
         uint32_t my_key = 0xffffffffu;
         int my_off = 0, nk = 0;
@@ -511,6 +546,216 @@ struct W {
         putc(']');
     }
 
+    // -----------------------------------------------------------------------
+    // Extension list, lane-parallel: lane k owns extension k.  The offset
+    // chain (type, length) is walked once with window reads; each lane then
+    // formats its own extension (tls.h:1549-1616 format 0, 1413-1499 format
+    // 1, 1664-1732 format 2), the wave orders them (wire order, or the rank
+    // under the reference's comparator for formats 1/2), and exclusive
+    // prefix sums place every lane's characters, scratch bytes and segments.
+    // Returns false (nothing emitted) when the list needs the serial path:
+    // more than 64 extensions or a QUIC transport-parameter extension.
+    // -----------------------------------------------------------------------
+    WDEV static uint32_t wave_excl_scan(uint32_t v, uint32_t lane_) {
+        uint32_t incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint32_t y = __shfl_up(incl, d, 64);
+            if ((int)lane_ >= d) incl += y;
+        }
+        return incl - v;
+    }
+    WDEV bool exts_par(C exts, int role, int fmt) {
+#ifdef MFP_PROBE_NOPAR
+        return false;
+#endif
+        // 1. offset chain (ext_parse semantics: header and value must fit)
+        int my_off = 0, nk = 0;
+        {
+            int p = exts.d, e = exts.e;
+            if (p < 0) { p = 0; e = 0; }
+            while (p < e) {
+                if (e - p < 4) break;
+                uint32_t h = be32(p);
+                int len = (int)(h & 0xffff);
+                if (len > e - p - 4) break;
+                uint32_t t = h >> 16;
+                if (t == 0x39 || t == 0xffa5 || nk == 64) return false;
+                my_off = ((int)lane == nk) ? p : my_off;
+                nk++;
+                p += 4 + len;
+            }
+        }
+        const bool mine = (int)lane < nk;
+        // 2. per-lane extension fields
+        uint32_t type = 0, len = 0;
+        if (mine) {
+            const uint8_t *b = L.buf + my_off;
+            type = ((uint32_t)b[0] << 8) | b[1];
+            len = ((uint32_t)b[2] << 8) | b[3];
+        }
+        const bool grease = (type & 0x0f0f) == 0x0a0a;
+        uint32_t enc = grease ? 0x0a0a : type;
+        int bucket = 0;
+        bool keep = mine;
+        if (fmt == 2 && mine) {
+            bucket = mfp::fmt2_bucket_t(type, enc);
+            keep = bucket >= 0;
+        }
+        if (fmt == 2) {
+            // the first three per bucket in wire order are kept (tls.h:1695-1701)
+            int seen = 0;
+            for (int j = 0; j < nk; j++) {
+                int bj = __builtin_amdgcn_readlane(bucket, j);
+                int kj = __builtin_amdgcn_readlane((int)keep, j);
+                if (kj && bj == bucket && j < (int)lane) seen++;
+            }
+            if (seen >= 3) keep = false;
+        }
+        // 3. order: wire order (fmt 0) or rank under the fmt 1/2 comparator
+        int pos = (int)lane;
+        if (fmt != 0) {
+            uint32_t key = 0xffffffffu;
+            if (keep) {
+                if (fmt == 1) key = grease ? (0x0a0aU << 16) : ((type << 16) | len);
+                else key = ((uint32_t)bucket << 24) | (grease ? 0 : (1u << 23)) | (grease ? 0 : len);
+            }
+            int rank = 0;
+            for (int j = 0; j < nk; j++) {
+                uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key, j);
+                if (kj == 0xffffffffu) continue;
+                bool less = false;
+                if (keep && j != (int)lane) {
+                    if (kj != key) less = kj < key;
+                    else less = j < (int)lane;
+                }
+                // equal keys of non-grease extensions: value bytes decide
+                uint64_t eq = ballot(keep && j != (int)lane && kj == key && !grease && (kj >> 16) != 0x0a0a);
+                if (eq && fmt == 2) eq = ballot(keep && j != (int)lane && kj == key && !grease);
+                while (eq) {
+                    int i = (int)__builtin_ctzll(eq);
+                    eq &= eq - 1;
+                    int oj = __builtin_amdgcn_readlane(my_off, j), oi = __builtin_amdgcn_readlane(my_off, i);
+                    uint32_t tj = be16(oj);
+                    if ((tj & 0x0f0f) == 0x0a0a) continue;
+                    int c = ccmp(cmk(oj + 4, oj + 4 + (int)be16(oj + 2)), cmk(oi + 4, oi + 4 + (int)be16(oi + 2)));
+                    if ((int)lane == i) less = c < 0 || (c == 0 && j < i);
+                }
+                rank += less ? 1 : 0;
+            }
+            pos = keep ? rank : 64;
+        }
+        // 4. per-extension output shape
+        //   non-static: "(" hex16(t) ")"                          6 chars, 6 scratch, 1 segment
+        //   static:     "(" hex16(t) hex16(dg len) | value | ")"  9 scratch + value hex + 1 scratch
+        //   type printed: fmt 0 degrease16(type), fmt 1/2 encoded type
+        const bool st = keep && mfp::is_static_ext(type);
+        uint32_t tprint = fmt == 0 ? mfp::degrease16(type) : enc;
+        int skip = 0, gl = 0;
+        if (st) {
+            if (type == 0x000a || type == 0x002b) {
+                int ug = type == 0x000a ? 2 : (role == 0 ? 1 : 0);
+                skip = (int)len < ug ? (int)len : ug;
+                gl = ((int)len - skip) & ~1;
+            } else {
+                skip = (int)len;
+            }
+        }
+        uint32_t chars = !keep ? 0u : st ? (uint32_t)(10 + 2 * skip + 2 * gl) : 6u;
+        uint32_t sbytes = !keep ? 0u : st ? 10u : 6u;
+        uint32_t segs = !keep ? 0u : st ? (uint32_t)(2 + (skip > 0) + (gl > 0)) : 1u;
+        // values in output order: lane r holds the extension of rank r
+        const int nout = fmt == 0 ? nk : (int)__builtin_popcountll(ballot(keep));
+        if (fmt != 0) {
+            // inverse permutation through LDS scratch is avoided: bpermute pulls
+            // each output slot's values from the lane that owns that rank
+            int src = 64;
+            for (int j = 0; j < nk; j++) {
+                int pj = __builtin_amdgcn_readlane(pos, j);
+                if (pj == (int)lane) src = j;
+            }
+            int sl = src < 64 ? src : 0;
+            uint32_t c2 = __builtin_amdgcn_ds_bpermute(sl << 2, (int)chars);
+            uint32_t s2 = __builtin_amdgcn_ds_bpermute(sl << 2, (int)sbytes);
+            uint32_t g2 = __builtin_amdgcn_ds_bpermute(sl << 2, (int)segs);
+            if (src == 64) { c2 = 0; s2 = 0; g2 = 0; }
+            uint32_t ec = wave_excl_scan(c2, lane), es = wave_excl_scan(s2, lane), eg = wave_excl_scan(g2, lane);
+            // back to the owning lane
+            int ps = pos < 64 ? pos : 0;
+            uint32_t c3 = __builtin_amdgcn_ds_bpermute(ps << 2, (int)ec);
+            uint32_t s3 = __builtin_amdgcn_ds_bpermute(ps << 2, (int)es);
+            uint32_t g3 = __builtin_amdgcn_ds_bpermute(ps << 2, (int)eg);
+            return exts_par_write(fmt, nout, keep, my_off, len, tprint, st, skip, gl, chars, sbytes, segs, c3, s3, g3);
+        }
+        uint32_t ec = wave_excl_scan(chars, lane), es = wave_excl_scan(sbytes, lane), eg = wave_excl_scan(segs, lane);
+        return exts_par_write(fmt, nout, keep, my_off, len, tprint, st, skip, gl, chars, sbytes, segs, ec, es, eg);
+    }
+    WDEV bool exts_par_write(int fmt, int nout, bool keep, int off, uint32_t len, uint32_t tprint, bool st, int skip,
+                             int gl, uint32_t chars, uint32_t sbytes, uint32_t segs, uint32_t ec, uint32_t es,
+                             uint32_t eg) {
+        // totals (sum over all lanes; lanes without an extension add zeros)
+        uint32_t tc = chars, ts = sbytes, tg = segs;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            tc += __shfl_xor(tc, d, 64);
+            ts += __shfl_xor(ts, d, 64);
+            tg += __shfl_xor(tg, d, 64);
+        }
+        tc = rfl(tc); ts = rfl(ts); tg = rfl(tg);
+        (void)nout; (void)len; (void)fmt;
+        flush();
+        const uint32_t lead = fmt == 0 ? '(' : '[', trail = fmt == 0 ? ')' : ']';
+        putc(lead);
+        flush();
+        if (n + tc > FP_MAX) { n += tc; putc(trail); return true; }
+        if (nseg + (int)tg > SEG_CAP || scr + (int)ts > SCR_CAP - 16) { ovf = true; return true; }
+        if (keep) {
+            const int sbase = PKT_CAP + scr + (int)es;
+            uint8_t *sp = L.buf + sbase;
+            sp[0] = '(';
+            sp[1] = (uint8_t)hexc((tprint >> 12) & 15);
+            sp[2] = (uint8_t)hexc((tprint >> 8) & 15);
+            sp[3] = (uint8_t)hexc((tprint >> 4) & 15);
+            sp[4] = (uint8_t)hexc(tprint & 15);
+            uint32_t c0 = n + ec;
+            int g = nseg + (int)eg;
+            if (!st) {
+                sp[5] = ')';
+                L.seg_end[g] = (uint16_t)(c0 + 6);
+                L.seg_info[g] = (uint32_t)sbase | (K_RAW << 16);
+            } else {
+                uint32_t ldg = mfp::degrease16(len);
+                sp[5] = (uint8_t)hexc((ldg >> 12) & 15);
+                sp[6] = (uint8_t)hexc((ldg >> 8) & 15);
+                sp[7] = (uint8_t)hexc((ldg >> 4) & 15);
+                sp[8] = (uint8_t)hexc(ldg & 15);
+                sp[9] = ')';
+                uint32_t c = c0 + 9;
+                L.seg_end[g] = (uint16_t)c;
+                L.seg_info[g] = (uint32_t)sbase | (K_RAW << 16);
+                g++;
+                if (skip > 0) {
+                    c += 2 * skip;
+                    L.seg_end[g] = (uint16_t)c;
+                    L.seg_info[g] = (uint32_t)(off + 4) | (K_HEX << 16);
+                    g++;
+                }
+                if (gl > 0) {
+                    c += 2 * gl;
+                    L.seg_end[g] = (uint16_t)c;
+                    L.seg_info[g] = (uint32_t)(off + 4 + skip) | (K_HEXDG << 16);
+                    g++;
+                }
+                c += 1;
+                L.seg_end[g] = (uint16_t)c;
+                L.seg_info[g] = (uint32_t)(sbase + 9) | (K_RAW << 16);
+            }
+        }
+        n += tc; nseg += (int)tg; scr += (int)ts;
+        putc(trail);
+        return true;
+    }
+
     WDEV C tls_record_fragment(C &d) {                   // tls_record::parse tls.h:153
         C f = cnul();
         if (clen(d) < 5) return f;
@@ -559,6 +804,7 @@ struct W {
         if (fmt >= 1 && fmt <= 2) put2('0' + fmt, '/');
         putc('('); hex_c(ch.version); putc(')');
         putc('('); hex_degrease(ch.ciphers.d, clen(ch.ciphers)); putc(')');
+        if (exts_par(ch.extensions, 0, fmt)) return;
         if (fmt == 0) exts_fp0(ch.extensions, 0);
         else exts_fp12(ch.extensions, 0, fmt);
     }
@@ -601,7 +847,7 @@ struct W {
     WDEV void tls_sh_fp(const Sh &s) {                   // tls_server_hello::fingerprint tls.h:2126
         putc('('); hex_c(s.version); putc(')');
         putc('('); hex_c(s.cipher); putc(')');
-        exts_fp0(s.extensions, 1);
+        if (!exts_par(s.extensions, 1, 0)) exts_fp0(s.extensions, 1);
     }
     struct Cert { C list; uint64_t more; };
     WDEV void tls_cert_parse(Cert &c, C &d) {            // tls_server_certificate::parse tls.h:281
@@ -658,8 +904,7 @@ struct W {
     WDEV int name_lookup(const mfp::HdrName *tab, int ntab, C nm) {
         int l = clen(nm);
         if (l <= 0 || l > 32) return -1;
-        uint32_t mine = 0;
-        if ((int)lane < l) mine = mfp::c_tolower(L.buf[nm.d + (int)lane]);
+        uint32_t mine = (int)lane < l ? mfp::c_tolower(L.buf[nm.d + (int)(lane & 31)]) : 0u;
         uint64_t live = l == 64 ? ~0ull : ((1ull << l) - 1);
         for (int i = 0; i < ntab; i++) {
             if (tab[i].len != l) continue;
@@ -729,6 +974,9 @@ struct W {
     }
     // HTTP request/response parse + fingerprint (http.cc:105-128, 369-383, 426-553)
     WDEV bool http_msg(C p, bool req, int base) {
+#ifdef MFP_PROBE_NOHTTP
+        return false;
+#endif
         C f1 = cnul(), f2 = cnul(), f3 = cnul();
         if (req) {
             C uri;
@@ -816,6 +1064,9 @@ struct W {
         o.msg = msg;
         switch (msg) {
         case MFP_MSG_TLS_CH: {
+#ifdef MFP_PROBE_NOCH
+            return;
+#endif
             C p = pkt;
             C frag = tls_record_fragment(p);
             Hs hs = tls_hs_parse(frag);
@@ -829,6 +1080,9 @@ struct W {
             return;
         }
         case MFP_MSG_TLS_SH: {                           // tls.h:573
+#ifdef MFP_PROBE_NOSH
+            return;
+#endif
             C p = pkt;
             Sh sh; cset_null(sh.version); cset_null(sh.cipher); cset_null(sh.extensions);
             Cert cert; cset_null(cert.list); cert.more = 0;
@@ -860,6 +1114,9 @@ struct W {
             return;
         }
         case MFP_MSG_SSH_INIT: {                         // ssh.h:342-430
+#ifdef MFP_PROBE_NOSSH
+            return;
+#endif
             bool server = !(dport <= sport);
             if (!(sel & (server ? SEL_SSH_SERVER : SEL_SSH_CLIENT))) { o.msg = 0; return; }
             C p = pkt, proto, comment = cnul();
@@ -915,6 +1172,9 @@ struct W {
     }
     // set_udp_protocol pkt_proc.cc:677 (DTLS, dtls.h)
     WDEV void udp_data(C pkt, int base) {
+#ifdef MFP_PROBE_NOUDP
+        return;
+#endif
         if (!(cfg.select & SEL_DTLS) || clen(pkt) < 16) return;
         uint64_t w0 = le8(pkt.d), w1 = le8(pkt.d + 8);
         const uint64_t M0 = LE8(0xff, 0xff, 0xfd, 0, 0, 0, 0, 0), V0 = LE8(0x16, 0xfe, 0xfd, 0, 0, 0, 0, 0);
@@ -1153,6 +1413,9 @@ struct W {
     // string: lane l of round r writes characters [512 r + 8 l, +8)
     // =======================================================================
     WDEV void expand(uint8_t *out) {
+#ifdef MFP_PROBE_NOEXPAND
+        return;
+#endif
         const uint32_t T = n;
         for (uint32_t r0 = 0; r0 < T; r0 += 512) {
             uint32_t p0 = r0 + 8 * lane;

@@ -170,9 +170,8 @@ def test_large_device_batch_properties():
     assert overflow == 0
     rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
     assert int(rec["fp_len"].astype(np.int64).sum()) == exact
-    # every string lies inside the reserved part of the arena, 16-byte aligned
+    # every string lies inside the reserved part of the arena
     assert int((rec["fp_offset"] + rec["fp_len"]).max()) <= reserved
-    assert int((rec["fp_offset"][rec["fp_len"] > 0] % 16).max()) == 0
     used = reserved
     rng = np.random.default_rng(1)
     sample = rng.choice(n, 20000, replace=False)
