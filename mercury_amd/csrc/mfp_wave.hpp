@@ -921,6 +921,134 @@ struct W {
         return cnotempty(dl);
     }
     // new_http_headers::fingerprint http.h:335 + httpheader http.h:146
+    // -----------------------------------------------------------------------
+    // Header block, lane-parallel (new_http_headers::fingerprint http.h:335,
+    // httpheader http.h:146): lane k owns header line k.  Taken only when
+    // the delimiter is "\r\n" and the block is well formed -- every CR is
+    // followed by LF and every LF preceded by CR, every line before the empty
+    // line has a ':' -- which is exactly when the reference's loop visits the
+    // lines one after another; anything else returns false before emitting
+    // and the serial loop below runs.
+    // -----------------------------------------------------------------------
+    WDEV bool http_headers_par(C body, bool req, C &host, C &ua) {
+        if (body.d < 0) return false;
+        const mfp::HdrName *tab = req ? mfp::k_req_names : mfp::k_resp_names;
+        const int ntab = req ? mfp::N_REQ_NAMES : mfp::N_RESP_NAMES;
+        // 1. line ends: LF positions up to the empty line (CRLF CRLF) or the end
+        int my_start = 0, my_end = 0, nl = 0;     // line [start, end) excludes CRLF
+        bool partial = false, done = false;
+        int p = body.d;
+        const int e = body.e;
+        uint32_t carry_cr = 0;
+        int base = p;
+        for (; base < e && !done; base += 64) {
+            const int q = base + (int)lane;
+            const uint32_t c = L.buf[q < e ? q : base];
+            const uint64_t lf = ballot(q < e && c == '\n');
+            const uint64_t cr = ballot(q < e && c == '\r');
+            // CR/LF pairing: every LF sits right after a CR and vice versa
+            if (((cr << 1) | carry_cr) != lf) return false;
+            carry_cr = (uint32_t)(cr >> 63);
+            uint64_t m = lf;
+            while (m) {
+                const int pos = base + (int)__builtin_ctzll(m);
+                m &= m - 1;
+                const int ls = p, le = pos - 1;       // exclude CR
+                if (le == ls) { done = true; break; }  // empty line ends the block
+                if (nl == 64) return false;
+                if ((int)lane == nl) { my_start = ls; my_end = le; }
+                nl++;
+                p = pos + 1;
+            }
+        }
+        if (!done) {
+            if (carry_cr) return false;                // data ends with a bare CR
+            if (p < e) {                                // last line without CRLF
+                if (nl == 64) return false;
+                if ((int)lane == nl) { my_start = p; my_end = e; }
+                nl++;
+                partial = true;
+            }
+        }
+        const bool mine = (int)lane < nl;
+        // 2. per line: colon, LWS, value
+        int colon = -1;
+        if (mine) {
+            for (int x = my_start; x < my_end; x++) {
+                if (L.buf[x] == ':') { colon = x; break; }
+            }
+        }
+        // a line without ':' makes the reference's name scan run into the
+        // next line; the final partial line without ':' just ends the loop
+        const bool lastp = partial && (int)lane == nl - 1;
+        if (ballot(mine && colon < 0 && !lastp)) return false;
+        const bool valid = mine && colon >= 0;
+        int vs = 0;
+        if (valid) {
+            vs = colon + 1;
+            while (vs < my_end && (L.buf[vs] == ' ' || L.buf[vs] == '\t')) vs++;
+        }
+        // 3. name lookup: ASCII case-insensitive exact match (perfect_hash.h:256)
+        int idx = -1;
+        const int nlen = valid ? colon - my_start : 0;
+        if (valid && nlen > 0 && nlen <= 32) {
+            const uint32_t c0 = mfp::c_tolower(L.buf[my_start]);
+            for (int i = 0; i < ntab; i++) {
+                if (tab[i].len != nlen || (uint8_t)tab[i].s[0] != c0) continue;
+                bool ok = true;
+                for (int j = 1; j < nlen; j++)
+                    if (mfp::c_tolower(L.buf[my_start + j]) != (uint8_t)tab[i].s[j]) { ok = false; break; }
+                if (ok) { idx = i; break; }
+            }
+        }
+        const bool emit = idx >= 0;
+        // host / user-agent: first occurrence wins (http.h:364-366)
+        if (req) {
+            const bool is_host = emit && tab[idx].capture == 1, is_ua = emit && tab[idx].capture == 2;
+            const uint64_t hm = ballot(is_host), um = ballot(is_ua);
+            if (hm) {
+                int k = (int)__builtin_ctzll(hm);
+                host = cmk(__builtin_amdgcn_readlane(vs, k), __builtin_amdgcn_readlane(my_end, k));
+            }
+            if (um) {
+                int k = (int)__builtin_ctzll(um);
+                ua = cmk(__builtin_amdgcn_readlane(vs, k), __builtin_amdgcn_readlane(my_end, k));
+            }
+        }
+        // 4. "(" hex(span) ")" per emitted line, in line order
+        const int span_end = emit ? (tab[idx].incl_value ? my_end : colon) : 0;
+        const uint32_t chars = emit ? (uint32_t)(2 + 2 * (span_end - my_start)) : 0u;
+        const uint32_t sbytes = emit ? 2u : 0u, segs = emit ? 3u : 0u;
+        const uint32_t ec = wave_excl_scan(chars, lane), es = wave_excl_scan(sbytes, lane),
+                       eg = wave_excl_scan(segs, lane);
+        uint32_t tc = chars, ts = sbytes, tg = segs;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            tc += __shfl_xor(tc, d, 64);
+            ts += __shfl_xor(ts, d, 64);
+            tg += __shfl_xor(tg, d, 64);
+        }
+        tc = rfl(tc); ts = rfl(ts); tg = rfl(tg);
+        flush();
+        if (n + tc > FP_MAX) { n += tc; return true; }
+        if (nseg + (int)tg > SEG_CAP || scr + (int)ts > SCR_CAP - 16) { ovf = true; return true; }
+        if (emit) {
+            const int sbase = PKT_CAP + scr + (int)es;
+            L.buf[sbase] = '(';
+            L.buf[sbase + 1] = ')';
+            const int g = nseg + (int)eg;
+            const uint32_t c0 = n + ec;
+            L.seg_end[g] = (uint16_t)(c0 + 1);
+            L.seg_info[g] = (uint32_t)sbase | (K_RAW << 16);
+            L.seg_end[g + 1] = (uint16_t)(c0 + chars - 1);
+            L.seg_info[g + 1] = (uint32_t)my_start | (K_HEX << 16);
+            L.seg_end[g + 2] = (uint16_t)(c0 + chars);
+            L.seg_info[g + 2] = (uint32_t)(sbase + 1) | (K_RAW << 16);
+        }
+        n += tc; nseg += (int)tg; scr += (int)ts;
+        if (tc) last_putc = true;
+        return true;
+    }
     WDEV void http_headers_fp(C body, C delim, bool req, C &host, C &ua) {
         C tmp = body;
         const mfp::HdrName *tab = req ? mfp::k_req_names : mfp::k_resp_names;
@@ -1008,7 +1136,8 @@ struct W {
         if (!req) { putc('('); hex_c(f3); putc(')'); }
         putc('(');
         C host = cnul(), ua = cnul();
-        http_headers_fp(p, delim, req, host, ua);
+        const bool crlf = clen(delim) == 2 && ld(delim.d) == '\r' && ld(delim.d + 1) == '\n';
+        if (!(crlf && http_headers_par(p, req, host, ua))) http_headers_fp(p, delim, req, host, ua);
         putc(')');
         if (req) {
             if (!cnull(host)) { o.sni_off = (uint32_t)(host.d - base); o.sni_len = (uint32_t)clen(host); }
