@@ -52,8 +52,28 @@ typedef struct {
     uint16_t sni_off, sni_len;
     uint16_t ua_off, ua_len;
     uint16_t src_port, dst_port;   /* host byte order */
-    uint32_t reserved;
+    uint32_t net;        /* innermost IP header: offset (bits 0-15), version (16-19) */
 } mfp_record;
+
+/* Per-packet classifier result (analysis_result, result.h:174-300), written
+ * by the --analysis pass for packets whose fingerprint type the resource
+ * archive covers. */
+typedef struct {
+    double   score;          /* analysis_result::max_score                      */
+    double   malware_prob;   /* analysis_result::malware_prob (-1 if none)      */
+    uint32_t process;        /* process-name id (mfp_process_name), or ~0u     */
+    uint16_t attr;           /* attribute_result tags (mfp_attribute_name bits) */
+    uint8_t  status;         /* enum fingerprint_status (libmerc.h:307-313)     */
+    uint8_t  flags;          /* MFP_AN_*                                        */
+} mfp_analysis;
+
+enum {
+    MFP_AN_VALID     = 1,    /* analysis_result::is_valid() (result.h:254)  */
+    MFP_AN_MALWARE   = 2,    /* max_mal                                      */
+    MFP_AN_CLASSIFY_MALWARE = 4,   /* malware fields meaningful (malware db) */
+    MFP_AN_PENDING   = 8,    /* internal: unknown TLS, status resolved later */
+};
+#define MFP_NO_PROCESS 0xffffffffu
 
 enum {
     MFP_FLAG_EMIT      = 1,  /* the reference's write_json emits a record   */
@@ -118,6 +138,45 @@ MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen);
  * Returns 0, or -1 with mfp_last_error() set.  Mirrors global_config's
  * parser (global_config.h:143-153,246-275,348-368). */
 MFP_EXPORT int mfp_parse_filter(const char *packet_filter_cfg, uint32_t *select, uint32_t *tls_format);
+
+/* ---- --analysis: the process classifier (classifier, analysis.h) ----
+ * Enabled by mfp_init when packet_filter_cfg holds "resources=<archive.tgz>"
+ * and "analysis" (key=value form), mirroring libmerc_config.resources and
+ * do_analysis; the TLS fingerprint format is then the archive's
+ * (pkt_proc.h:93-99). */
+MFP_EXPORT int mfp_analysis_enabled(mfp_context ctx);
+
+/* Classify a device-resident batch already fingerprinted by
+ * mfp_process_batch_device on the same stream (records and fp arena as it
+ * left them).  d_out: n mfp_analysis records; rec[i].status is set too.
+ * Batches must be submitted in stream order: the unknown-TLS status
+ * (randomized / unlabeled) depends on earlier sightings. */
+MFP_EXPORT int mfp_analyze_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
+                                        mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, void *stream);
+
+/* mfp_process_batch_host plus classification into analysis[n] (NULL: none). */
+MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context ctx, const uint8_t *arena, size_t arena_len,
+                                               const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                               char *fp_arena, size_t fp_cap, mfp_analysis *analysis);
+
+/* names behind mfp_analysis.process and the bits of mfp_analysis.attr */
+MFP_EXPORT const char *mfp_process_name(mfp_context ctx, uint32_t id);
+MFP_EXPORT const char *mfp_attribute_name(mfp_context ctx, uint32_t bit);
+
+/* last analysis batch: [0] packets classified, [1] unknown-TLS sightings,
+ * [2] fingerprints with more processes than the kernel handles (512),
+ * [3] distinct unknown TLS fingerprints seen so far (the reference's LRU
+ * holds 100000; beyond that its evictions are not reproduced) */
+MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
+
+/* host only (tests): load an archive; out = {fingerprints, entries,
+ * processes, feature updates, known-prevalence, asn prefixes, disabled,
+ * distinct process names} */
+MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]);
+
+/* host only (tests): server_identifier::get_normalized_domain_name (the
+ * normalisation the device applies to server names); returns the length */
+MFP_EXPORT int mfp_normalize_server_name(const char *name, size_t len, char *out, size_t cap);
 
 /* last error string for this thread */
 MFP_EXPORT const char *mfp_last_error(void);

@@ -8,8 +8,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmercury_amd.so")
 OBJ = os.path.join(HERE, "_obj")
 
-SOURCES = ["mfp_kernels.hip", "mfp_host.cpp"]
-HEADERS = ["mfp_device.hpp", "mfp_wave.hpp", "mfp_internal.h"]
+SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_host.cpp", "mfp_classifier.cpp"]
+HEADERS = ["mfp_device.hpp", "mfp_wave.hpp", "mfp_internal.h", "mfp_analysis.h", "mfp_common.hpp"]
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 
 
@@ -35,7 +35,7 @@ def build(verbose=False):
                 print(" ".join(cmd))
             subprocess.run(cmd, check=True)
     if _newer(LIB, objs):
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lz"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -10,8 +10,12 @@ DESC_DTYPE = np.dtype([("offset", "<u8"), ("caplen", "<u4"), ("linktype", "<u2")
 RECORD_DTYPE = np.dtype([("fp_offset", "<u8"), ("fp_len", "<u4"), ("fp_type", "u1"), ("msg", "u1"),
                          ("flags", "u1"), ("status", "u1"), ("sni_off", "<u2"), ("sni_len", "<u2"),
                          ("ua_off", "<u2"), ("ua_len", "<u2"), ("src_port", "<u2"), ("dst_port", "<u2"),
-                         ("reserved", "<u4")])
-assert DESC_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 32
+                         ("net", "<u4")])
+ANALYSIS_DTYPE = np.dtype([("score", "<f8"), ("malware_prob", "<f8"), ("process", "<u4"), ("attr", "<u2"),
+                           ("status", "u1"), ("flags", "u1")])
+assert DESC_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 32 and ANALYSIS_DTYPE.itemsize == 24
+NO_PROCESS = 0xFFFFFFFF
+STATUS_NAMES = ["no_info_available", "labeled", "randomized", "unlabeled", "unanalyzed"]
 
 # fingerprint::get_type_name (src/libmerc/fingerprint.h:159-192)
 FP_TYPE_NAMES = ["unknown", "tls", "tls_server", "http", "http_server", "ssh", "ssh_kex", "tcp", "dhcp",
@@ -57,6 +61,22 @@ def load_library():
     lib.mfp_fp_arena_bound.argtypes = [sz, sz]
     lib.mfp_last_error.restype = ctypes.c_char_p
     lib.mfp_reference_version.restype = ctypes.c_uint32
+    lib.mfp_analysis_enabled.restype = ctypes.c_int
+    lib.mfp_analysis_enabled.argtypes = [vp]
+    lib.mfp_analyze_batch_device.restype = ctypes.c_int
+    lib.mfp_analyze_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
+    lib.mfp_process_batch_host_ex.restype = ctypes.c_longlong
+    lib.mfp_process_batch_host_ex.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp]
+    lib.mfp_process_name.restype = ctypes.c_char_p
+    lib.mfp_process_name.argtypes = [vp, ctypes.c_uint32]
+    lib.mfp_attribute_name.restype = ctypes.c_char_p
+    lib.mfp_attribute_name.argtypes = [vp, ctypes.c_uint32]
+    lib.mfp_analysis_stats.restype = ctypes.c_int
+    lib.mfp_analysis_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    lib.mfp_resource_stats.restype = ctypes.c_int
+    lib.mfp_resource_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+    lib.mfp_normalize_server_name.restype = ctypes.c_int
+    lib.mfp_normalize_server_name.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
     lib.mfp_parse_filter.restype = ctypes.c_int
     lib.mfp_parse_filter.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     _lib = lib
@@ -105,11 +125,73 @@ class Context:
             raise MercuryAmdError("mfp_process_batch_host failed: " + _err(self.lib))
         return rec, fp[:used].tobytes()
 
+    @property
+    def analysis_enabled(self):
+        return bool(self.lib.mfp_analysis_enabled(self.h))
+
+    def process_host_analysis(self, arena, desc):
+        """Fingerprint + classify a host batch -> (records, fp arena bytes, analysis records)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        n = len(desc)
+        rec = np.zeros(n, dtype=RECORD_DTYPE)
+        an = np.zeros(n, dtype=ANALYSIS_DTYPE)
+        cap = self.fp_arena_bound(desc)
+        fp = np.zeros(cap, dtype=np.uint8)
+        used = self.lib.mfp_process_batch_host_ex(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
+                                                  rec.ctypes.data, fp.ctypes.data, cap, an.ctypes.data)
+        if used < 0:
+            raise MercuryAmdError("mfp_process_batch_host_ex failed: " + _err(self.lib))
+        return rec, fp[:used].tobytes(), an
+
+    def analyze_device(self, d_arena, d_desc, n, d_rec, d_fp, d_out, stream=0):
+        r = self.lib.mfp_analyze_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out, stream)
+        if r != 0:
+            raise MercuryAmdError("mfp_analyze_batch_device failed: " + _err(self.lib))
+
+    def process_name(self, pid):
+        if pid == NO_PROCESS:
+            return ""
+        s = self.lib.mfp_process_name(self.h, int(pid))
+        return s.decode() if s else None
+
+    def attribute_name(self, bit):
+        s = self.lib.mfp_attribute_name(self.h, int(bit))
+        return s.decode() if s else None
+
+    def analysis_stats(self):
+        out = (ctypes.c_uint64 * 4)()
+        if self.lib.mfp_analysis_stats(self.h, out) != 0:
+            raise MercuryAmdError(_err(self.lib))
+        return list(out)
+
     def process_device(self, d_arena, d_desc, n, d_rec, d_fp, fp_cap, d_used, stream=0):
         """All arguments are device pointers (ints, e.g. torch data_ptr())."""
         r = self.lib.mfp_process_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, fp_cap, d_used, stream)
         if r != 0:
             raise MercuryAmdError("mfp_process_batch_device failed: " + _err(self.lib))
+
+
+def resource_stats(path):
+    """Host-only load of a resource archive: {fingerprints, entries, processes, updates, ...}."""
+    lib = load_library()
+    out = (ctypes.c_uint64 * 8)()
+    if lib.mfp_resource_stats(path.encode(), out) != 0:
+        raise MercuryAmdError(_err(lib))
+    keys = ["fingerprints", "entries", "processes", "updates", "known_prevalence", "asn_prefixes", "disabled",
+            "process_names"]
+    return dict(zip(keys, list(out)))
+
+
+def normalize_server_name(name):
+    """server_identifier::get_normalized_domain_name as the device applies it (host)."""
+    lib = load_library()
+    b = name if isinstance(name, bytes) else name.encode("latin-1")
+    buf = ctypes.create_string_buffer(512)
+    n = lib.mfp_normalize_server_name(b, len(b), buf, 512)
+    if n < 0:
+        raise MercuryAmdError("normalize_server_name failed")
+    return buf.raw[:n].decode("latin-1")
 
 
 def parse_filter(cfg):

@@ -1,0 +1,82 @@
+// mfp_analysis.h -- device-table layout of the --analysis classifier, shared
+// by the host loader (mfp_classifier.cpp) and the classifier kernels
+// (mfp_analysis.hip).  Internal to libmercury_amd.so.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mfp.h"
+
+// open-addressing string table slot (fingerprint DB, known-prevalence set)
+struct mfp_fp_slot {
+    uint64_t hash;      // mfpc::str_hash of the string
+    uint32_t id;        // entry id (0xffffffff = empty)
+    uint32_t str_off;   // string in the pool, for exact verification
+    uint32_t str_len;
+    uint32_t pad;
+};
+
+// one fingerprint entry (fingerprint_data, analysis.h:123-218)
+struct mfp_entry {
+    uint32_t proc_off;      // first process in prior/proc_* arrays
+    uint32_t nproc;         // P
+    uint32_t malware_db;    // fingerprint_data::malware_db
+    uint32_t generic_dmz;   // index of "generic dmz process" or 0xffffffff
+};
+
+// feature-table slot, keyed by (entry, kind, key) -- key is the value itself
+// for ASN / port / IPv4, a str_hash for strings and IPv6 (verified)
+struct mfp_feat_slot {
+    uint64_t key;
+    uint32_t entry;     // 0xffffffff = empty
+    uint32_t kind;      // mfpc::FeatureKind
+    uint32_t upd_off, upd_cnt;
+    uint32_t str_off, str_len;
+};
+
+struct mfp_update {     // class update (naive_bayes.hpp:21-41)
+    uint32_t idx, pad;
+    double value;
+};
+
+struct mfp_asn4 { uint32_t lo, hi, asn, pad; };             // host-order address interval
+struct mfp_asn6 { uint64_t lo_hi, lo_lo, hi_hi, hi_lo; uint32_t asn, pad; };   // 128-bit host-order interval
+
+struct mfp_seen_slot {  // fingerprint_prevalence, adaptive part
+    unsigned long long hash;
+    unsigned long long first;   // (batch << 32) | packet index of the first sighting
+};
+
+struct mfp_classifier_dev {
+    mfp_fp_slot *fp_slots = nullptr;   uint64_t fp_mask = 0;
+    mfp_fp_slot *prev_slots = nullptr; uint64_t prev_mask = 0;
+    mfp_entry *entry = nullptr;
+    double *prior = nullptr;
+    uint32_t *proc_id = nullptr;
+    uint8_t *proc_mal = nullptr;
+    uint32_t *proc_attr = nullptr;
+    mfp_feat_slot *feat_slots = nullptr; uint64_t feat_mask = 0;
+    mfp_update *upd = nullptr;
+    char *pool = nullptr;
+    mfp_asn4 *asn4 = nullptr; uint32_t n_asn4 = 0;
+    mfp_asn6 *asn6 = nullptr; uint32_t n_asn6 = 0;
+    uint32_t types_mask = 0;           // analyzable fingerprint types (fp_types)
+    uint32_t enc_channel_idx = 7, faketls_idx = 9;
+    uint32_t randomized_entry[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};   // "tls/", "tls/1/", "tls/2/" + "randomized"
+    mfp_seen_slot *seen = nullptr; uint32_t seen_cap = 0;
+    unsigned long long *seen_count = nullptr;
+    uint32_t batch = 0;
+};
+
+typedef struct mfp_classifier_s mfp_classifier;
+
+mfp_classifier *mfp_classifier_load(const char *path);
+int mfp_classifier_upload(mfp_classifier *c, int device);
+void mfp_classifier_free(mfp_classifier *c);
+void mfp_classifier_free_device(mfp_classifier_dev &d);
+int mfp_classifier_tls_format(const mfp_classifier *c);
+bool mfp_classifier_disabled(const mfp_classifier *c);
+const char *mfp_classifier_process_name(const mfp_classifier *c, uint32_t id);
+const char *mfp_classifier_attr_name(const mfp_classifier *c, uint32_t i);
+void mfp_classifier_stats(const mfp_classifier *c, uint64_t out[8]);
+const mfp_classifier_dev *mfp_classifier_device(const mfp_classifier *c);
+mfp_classifier_dev *mfp_classifier_device_mut(mfp_classifier *c);

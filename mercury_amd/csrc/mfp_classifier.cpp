@@ -1,0 +1,839 @@
+// mfp_classifier.cpp -- host side of the --analysis process classifier:
+// reads the reference's resource archive (.tgz: VERSION, fingerprint_db.json,
+// fp_prevalence_tls.txt, pyasn.db; analysis.h:821-980) and turns it into the
+// flat device tables the classifier kernel (mfp_analysis.hip) reads.
+//
+// Model restated from the reference (file:line relative to
+// /root/reference/src/libmerc/):
+//   * fingerprint_data / naive_bayes_tls_quic_http ctor  analysis.h:143-218,
+//     naive_bayes.hpp:710-750: per fingerprint, P processes, a prior vector
+//     (add_class naive_bayes.hpp:657-663) and six categorical features whose
+//     updates are precomputed as (log(count/total) - log(0.1/total)) * weight
+//     (feature::add_update naive_bayes.hpp:103-118; domain/sni updates of the
+//     same process combine, update::combine naive_bayes.hpp:34-40);
+//   * classifier::process_fp_db_line analysis.h:646-743 (validate_fp
+//     analysis.h:598-640, MALWARE_DB, feature_weights, str_repr_array);
+//   * attribute name indices (attribute_names result.h:133-172, reserved in
+//     the order of pkt_proc.h:72 and analysis.h:830).
+// The loader runs once per context; the per-packet work is on the device.
+#include <hip/hip_runtime.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/mfp.h"
+#include "mfp_analysis.h"
+#include "mfp_common.hpp"
+#include "mfp_internal.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// minimal JSON (one fingerprint_db.json line at a time; keeps member order)
+// ---------------------------------------------------------------------------
+struct JV {
+    enum T { NUL, BOOL, NUM, STR, ARR, OBJ } t = NUL;
+    bool b = false;
+    std::string s;                       // string value, or the number's text
+    double num = 0;
+    bool is_uint = false;
+    uint64_t u = 0;
+    std::vector<JV> a;
+    std::vector<std::pair<std::string, JV>> o;
+    const JV *get(const char *k) const {
+        for (auto &kv : o) if (kv.first == k) return &kv.second;
+        return nullptr;
+    }
+};
+
+struct JP {
+    const char *p, *e;
+    bool ok = true;
+    void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
+    bool str(std::string &out) {
+        if (p >= e || *p != '"') return ok = false;
+        p++;
+        while (p < e && *p != '"') {
+            if (*p == '\\') {
+                p++;
+                if (p >= e) return ok = false;
+                char c = *p++;
+                switch (c) {
+                case 'n': out += '\n'; break;
+                case 't': out += '\t'; break;
+                case 'r': out += '\r'; break;
+                case 'b': out += '\b'; break;
+                case 'f': out += '\f'; break;
+                case 'u': {
+                    if (e - p < 4) return ok = false;
+                    unsigned v = (unsigned)strtoul(std::string(p, 4).c_str(), nullptr, 16);
+                    p += 4;
+                    if (v >= 0xd800 && v < 0xdc00 && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+                        unsigned lo = (unsigned)strtoul(std::string(p + 2, 4).c_str(), nullptr, 16);
+                        p += 6;
+                        v = 0x10000 + ((v - 0xd800) << 10) + (lo - 0xdc00);
+                    }
+                    if (v < 0x80) out += (char)v;
+                    else if (v < 0x800) { out += (char)(0xc0 | v >> 6); out += (char)(0x80 | (v & 63)); }
+                    else if (v < 0x10000) { out += (char)(0xe0 | v >> 12); out += (char)(0x80 | (v >> 6 & 63)); out += (char)(0x80 | (v & 63)); }
+                    else { out += (char)(0xf0 | v >> 18); out += (char)(0x80 | (v >> 12 & 63)); out += (char)(0x80 | (v >> 6 & 63)); out += (char)(0x80 | (v & 63)); }
+                    break;
+                }
+                default: out += c;
+                }
+            } else {
+                out += *p++;
+            }
+        }
+        if (p >= e) return ok = false;
+        p++;
+        return true;
+    }
+    bool val(JV &v, int depth = 0) {
+        if (depth > 64) return ok = false;
+        ws();
+        if (p >= e) return ok = false;
+        char c = *p;
+        if (c == '{') {
+            v.t = JV::OBJ; p++; ws();
+            if (p < e && *p == '}') { p++; return true; }
+            while (true) {
+                ws();
+                std::string k;
+                if (!str(k)) return false;
+                ws();
+                if (p >= e || *p != ':') return ok = false;
+                p++;
+                v.o.emplace_back(std::move(k), JV());
+                if (!val(v.o.back().second, depth + 1)) return false;
+                ws();
+                if (p < e && *p == ',') { p++; continue; }
+                if (p < e && *p == '}') { p++; return true; }
+                return ok = false;
+            }
+        }
+        if (c == '[') {
+            v.t = JV::ARR; p++; ws();
+            if (p < e && *p == ']') { p++; return true; }
+            while (true) {
+                v.a.emplace_back();
+                if (!val(v.a.back(), depth + 1)) return false;
+                ws();
+                if (p < e && *p == ',') { p++; continue; }
+                if (p < e && *p == ']') { p++; return true; }
+                return ok = false;
+            }
+        }
+        if (c == '"') { v.t = JV::STR; return str(v.s); }
+        if (e - p >= 4 && !strncmp(p, "true", 4)) { v.t = JV::BOOL; v.b = true; p += 4; return true; }
+        if (e - p >= 5 && !strncmp(p, "false", 5)) { v.t = JV::BOOL; v.b = false; p += 5; return true; }
+        if (e - p >= 4 && !strncmp(p, "null", 4)) { v.t = JV::NUL; p += 4; return true; }
+        const char *s = p;
+        while (p < e && (isdigit((unsigned char)*p) || *p == '-' || *p == '+' || *p == '.' || *p == 'e' || *p == 'E')) p++;
+        if (p == s) return ok = false;
+        v.t = JV::NUM;
+        v.s.assign(s, p);
+        v.num = strtod(v.s.c_str(), nullptr);
+        bool integral = v.s.find_first_of(".eE-") == std::string::npos;
+        if (integral) { v.is_uint = true; v.u = strtoull(v.s.c_str(), nullptr, 10); }
+        return true;
+    }
+};
+
+bool parse_json(const std::string &line, JV &out) {
+    JP jp{line.data(), line.data() + line.size()};
+    return jp.val(out) && jp.ok;
+}
+
+// ---------------------------------------------------------------------------
+// .tgz reader (gzip via zlib, ustar headers): calls f(name, contents)
+// ---------------------------------------------------------------------------
+template <class F>
+bool read_tgz(const char *path, F f) {
+    gzFile gz = gzopen(path, "rb");
+    if (!gz) return false;
+    std::string all;
+    char buf[1 << 16];
+    int r;
+    while ((r = gzread(gz, buf, sizeof buf)) > 0) all.append(buf, r);
+    gzclose(gz);
+    if (r < 0) return false;
+    size_t off = 0;
+    std::string longname;
+    while (off + 512 <= all.size()) {
+        const char *h = all.data() + off;
+        if (h[0] == 0) break;
+        std::string name(h, strnlen(h, 100));
+        std::string prefix(h + 345, strnlen(h + 345, 155));
+        if (!prefix.empty() && !memcmp(h + 257, "ustar", 5)) name = prefix + "/" + name;
+        uint64_t size = strtoull(std::string(h + 124, 12).c_str(), nullptr, 8);
+        char type = h[156];
+        off += 512;
+        if (off + size > all.size()) return false;
+        if (type == 'L') {
+            longname.assign(all.data() + off, strnlen(all.data() + off, size));
+        } else {
+            if (!longname.empty()) { name = longname; longname.clear(); }
+            if (type == '0' || type == 0) {
+                size_t sl = name.rfind('/');
+                f(sl == std::string::npos ? name : name.substr(sl + 1), std::string(all.data() + off, size));
+            }
+        }
+        off += (size + 511) / 512 * 512;
+    }
+    return true;
+}
+
+template <class F>
+void for_lines(const std::string &s, F f) {
+    size_t a = 0;
+    while (a < s.size()) {
+        size_t b = s.find('\n', a);
+        if (b == std::string::npos) b = s.size();
+        std::string line = s.substr(a, b - a);
+        f(line);
+        a = b + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host model
+// ---------------------------------------------------------------------------
+struct Upd { uint32_t idx; double val; };
+struct FeatMap {
+    std::map<std::string, std::vector<Upd>> by_str;     // ua, domain, sni
+    std::map<uint64_t, std::vector<Upd>> by_int;        // asn, port, ipv4
+    std::map<std::string, std::vector<Upd>> by_v6;      // 16-byte keys
+};
+struct Entry {
+    std::vector<std::string> proc_name;
+    std::vector<uint8_t> malware;
+    std::vector<uint32_t> attr;
+    std::vector<double> prior;
+    bool malware_db = false;
+    FeatMap f[7];
+};
+
+struct Weights { double as, domain, port, ip, sni, ua; double sum() const { return as + domain + port + ip + sni + ua; } };
+const Weights kDefaultWeights{0.13924, 0.15590, 0.00528, 0.56735, 0.96941, 1.0};   // naive_bayes.hpp:697-704
+
+const char *kReservedAttrs[] = {   // pkt_proc.h:72 then analysis.h:830
+    "residential_proxy", "exposed_credentials_plaintext", "exposed_credentials_token",
+    "exposed_credentials_derived", "cnsa_2_0_non_conformant", "nist_sp_800_52_2_non_conformant",
+    "encrypted_dns", "encrypted_channel", "domain_faking", "faketls",
+};
+
+}  // namespace
+
+struct mfp_classifier_s {
+    // host model
+    std::vector<std::string> attr_names;
+    bool accept_attr = true;
+    std::vector<std::unique_ptr<Entry>> entries;
+    std::unordered_map<std::string, uint32_t> fpdb;           // fingerprint string -> entry
+    std::vector<std::string> fp_order;                         // strings in insertion order
+    std::unordered_set<std::string> known_prevalence;
+    std::vector<uint32_t> fp_types;
+    std::map<std::string, std::pair<uint32_t, size_t>> fp_count_and_format;
+    std::string version;
+    bool malware_db = false;
+    bool disabled = false;
+    std::vector<std::pair<uint64_t, uint32_t>> asn4;           // (prefix<<8 | len, asn)
+    std::vector<std::pair<std::string, uint32_t>> asn6;        // (16 bytes + len byte, asn)
+    std::vector<std::string> proc_names;                       // global process-name table
+    std::unordered_map<std::string, uint32_t> proc_name_id;
+    mfp_classifier_dev dev;                                    // device tables (mfp_analysis.h)
+    int device = -1;
+};
+
+namespace {
+
+int attr_index(mfp_classifier_s &c, const std::string &name) {   // attribute_names::get_index
+    if (c.accept_attr) {
+        c.attr_names.push_back(name);
+        if (c.attr_names.size() > 16) throw std::runtime_error("too many attributes in attribute_names");
+        return (int)c.attr_names.size() - 1;
+    }
+    for (size_t i = 0; i < c.attr_names.size(); i++) if (c.attr_names[i] == name) return (int)i;
+    return -1;
+}
+
+std::string normalized_sni(const std::string &s) {
+    char out[400];
+    int n = mfpc::normalize_server_name((const uint8_t *)s.data(), (int)s.size(), out);
+    return std::string(out, n);
+}
+
+bool ipv4_key(const std::string &s, uint32_t &key) {   // lookahead<ipv4_address_string> + normalize
+    int pos = 0;
+    uint32_t v;
+    if (!mfpc::parse_ipv4((const uint8_t *)s.data(), (int)s.size(), pos, v)) return false;
+    key = mfpc::normalize_ipv4(v);
+    return true;
+}
+
+bool ipv6_key(const std::string &s, std::string &key) {
+    int pos = 0;
+    uint8_t a[16];
+    if (!mfpc::parse_ipv6((const uint8_t *)s.data(), (int)s.size(), pos, a)) return false;
+    mfpc::normalize_ipv6(a);
+    key.assign((const char *)a, 16);
+    return true;
+}
+
+uint64_t stoul_like(const std::string &s, uint64_t max) {   // feature<T>::convert
+    char *end = nullptr;
+    errno = 0;
+    unsigned long long v = strtoull(s.c_str(), &end, 10);
+    if (end == s.c_str()) return 0;
+    if (v > max) return 0;
+    return v;
+}
+
+void add_update(std::vector<Upd> &lst, uint32_t idx, uint64_t count, uint64_t total, double w) {
+    double base_prior = log(0.1 / (double)total);
+    lst.push_back(Upd{idx, (log((double)count / (double)total) - base_prior) * w});
+}
+
+// domain_name_model::add_domain_update / add_sni_update (naive_bayes.hpp:422-490)
+void add_combining_update(std::vector<Upd> &lst, uint32_t idx, uint64_t count, uint64_t total, double w) {
+    double base_prior = log(0.1 / (double)total);
+    for (auto it = lst.rbegin(); it != lst.rend(); ++it) {
+        if (it->idx == idx) {   // update::combine naive_bayes.hpp:34-40
+            long double old_count = expl((long double)(it->val / w + base_prior)) * (long double)total;
+            size_t old_int = (size_t)roundl(old_count);
+            it->val = (log((double)(count + old_int) / (double)total) - base_prior) * w;
+            return;
+        }
+    }
+    lst.push_back(Upd{idx, (log((double)count / (double)total) - base_prior) * w});
+}
+
+uint32_t fp_type_code(const std::string &s) {   // classifier::get_fingerprint_type analysis.h:448
+    if (s == "tls") return 1;
+    if (s == "http") return 3;
+    if (s == "quic") return 12;
+    if (s == "stun") return 16;
+    if (s == "tofsee") return 15;
+    if (s == "ssh") return 5;
+    return 0;
+}
+
+// get_fingerprint_type_and_version analysis.h:501-541
+std::pair<uint32_t, size_t> type_and_version(const std::string &s) {
+    size_t idx = s.find('/');
+    if (idx == std::string::npos) return {0, 0};
+    uint32_t t = fp_type_code(s.substr(0, idx));
+    if (!t) return {0, 0};
+    std::string tail = s.substr(idx + 1);
+    if (tail.empty()) return {0, 0};
+    if (tail[0] == '(' || tail.compare(0, 10, "randomized") == 0) return {t, 0};
+    char *end = nullptr;
+    long v = strtol(tail.c_str(), &end, 10);
+    if (end == tail.c_str()) return {0, 0};
+    return {t, (size_t)v};
+}
+
+bool validate_fp(mfp_classifier_s &c, std::string &fp, uint32_t code, const std::string &type_str) {
+    if (fp.empty() || fp.size() >= 8192) return false;
+    if (code == 1 && (fp[0] == '(' || fp == "randomized")) fp = "tls/" + fp;
+    auto tv = type_and_version(fp);
+    if (tv.first != code) return false;
+    auto it = c.fp_count_and_format.find(type_str);
+    if (it != c.fp_count_and_format.end()) {
+        if (it->second.first == 1) it->second.second = tv.second;
+        else if (tv.second != it->second.second) return false;
+    }
+    return true;
+}
+
+void process_fp_db_line(mfp_classifier_s &c, const std::string &line) {
+    JV fp;
+    if (!parse_json(line, fp) || fp.t != JV::OBJ) return;
+    uint32_t code = 1;
+    std::string type_str;
+    if (const JV *t = fp.get("fp_type"); t && t->t == JV::STR) {
+        type_str = t->s;
+        code = fp_type_code(type_str);
+        auto &cf = c.fp_count_and_format[type_str];
+        cf.first++;
+        if (cf.first == 1) cf.second = 0;
+    }
+    if (code && std::find(c.fp_types.begin(), c.fp_types.end(), code) == c.fp_types.end()) c.fp_types.push_back(code);
+    uint64_t total = 0;
+    if (const JV *t = fp.get("total_count"); t && t->t == JV::NUM && t->is_uint) total = t->u;
+    Weights w = kDefaultWeights;
+    if (const JV *fw = fp.get("feature_weights"); fw && fw->t == JV::OBJ) {
+        for (auto &kv : fw->o) {
+            double v = (double)(float)kv.second.num;   // rapidjson GetFloat()
+            if (kv.first == "as") w.as = v;
+            else if (kv.first == "domain") w.domain = v;
+            else if (kv.first == "port") w.port = v;
+            else if (kv.first == "ip") w.ip = v;
+            else if (kv.first == "sni") w.sni = v;
+            else if (kv.first == "ua") w.ua = v;
+        }
+    }
+    const JV *pi = fp.get("process_info");
+    if (!pi || pi->t != JV::ARR) return;
+    if (!pi->a.empty()) {
+        if (pi->a[0].get("malware")) c.malware_db = true;
+    }
+    if (total == 0) throw std::runtime_error("total_count==0 in naive_bayes");
+    auto e = std::make_unique<Entry>();
+    e->malware_db = c.malware_db;
+    uint32_t idx = 0;
+    for (auto &x : pi->a) {
+        if (const JV *p = x.get("process"); p && p->t == JV::STR) e->proc_name.push_back(p->s);
+        if (const JV *m = x.get("malware"); m && m->t == JV::BOOL) e->malware.push_back(m->b);
+        uint32_t bits = 0;
+        if (const JV *a = x.get("attributes"); a && a->t == JV::OBJ) {
+            for (auto &kv : a->o) {
+                int ai = attr_index(c, kv.first);
+                if (ai < 0) throw std::runtime_error("unknown attribute " + kv.first);
+                if (kv.second.t == JV::BOOL && kv.second.b) bits |= 1u << ai;
+            }
+            c.accept_attr = false;
+        }
+        e->attr.push_back(bits);
+        if (x.t == JV::OBJ) {
+            // domain_name_model: sni (normalized keys) then domains
+            const JV *sni = x.get("classes_hostname_sni");
+            const JV *dom = x.get("classes_hostname_domains");
+            const JV *port = x.get("classes_port_port");
+            const JV *as = x.get("classes_ip_as");
+            const JV *ua = x.get("classes_user_agent");
+            const JV *ip = x.get("classes_ip_ip");
+            if (!sni || !dom || !port || !as || !ip) throw std::runtime_error("missing feature in process_info");
+            if (sni->t == JV::OBJ)
+                for (auto &kv : sni->o)
+                    if (kv.second.is_uint)
+                        add_combining_update(e->f[mfpc::F_SNI].by_str[normalized_sni(kv.first)], idx, kv.second.u, total, w.sni);
+            if (dom->t == JV::OBJ)
+                for (auto &kv : dom->o)
+                    if (kv.second.is_uint)
+                        add_combining_update(e->f[mfpc::F_DOMAIN].by_str[kv.first], idx, kv.second.u, total, w.domain);
+            if (port->t != JV::OBJ || as->t != JV::OBJ || ip->t != JV::OBJ) throw std::runtime_error("feature not an object");
+            for (auto &kv : port->o) {
+                if (!kv.second.is_uint) throw std::runtime_error("expected uint64");
+                add_update(e->f[mfpc::F_PORT].by_int[stoul_like(kv.first, 65535)], idx, kv.second.u, total, w.port);
+            }
+            for (auto &kv : as->o) {
+                if (!kv.second.is_uint) throw std::runtime_error("expected uint64");
+                uint64_t k = kv.first == "unknown" ? 0 : stoul_like(kv.first, 0xffffffffULL);
+                add_update(e->f[mfpc::F_ASN].by_int[k], idx, kv.second.u, total, w.as);
+            }
+            if (ua && ua->t == JV::OBJ) {
+                for (auto &kv : ua->o) {
+                    if (!kv.second.is_uint) throw std::runtime_error("expected uint64");
+                    add_update(e->f[mfpc::F_UA].by_str[kv.first == "None" ? std::string() : kv.first], idx, kv.second.u,
+                               total, w.ua);
+                }
+            }
+            for (auto &kv : ip->o) {
+                if (!kv.second.is_uint) throw std::runtime_error("expected uint64");
+                uint32_t k4;
+                std::string k6;
+                if (ipv4_key(kv.first, k4)) add_update(e->f[mfpc::F_IPV4].by_int[k4], idx, kv.second.u, total, w.ip);
+                else if (ipv6_key(kv.first, k6)) add_update(e->f[mfpc::F_IPV6].by_v6[k6], idx, kv.second.u, total, w.ip);
+            }
+        }
+        // naive_bayes::add_class_from_count naive_bayes.hpp:665-680
+        const JV *cnt = x.get("count");
+        if (!cnt || !cnt->is_uint || cnt->u == 0) throw std::runtime_error("bad process count");
+        double base_prior = log(0.1 / (double)total);
+        double score = log((double)cnt->u / (double)total);
+        e->prior.push_back(fmax(score, log(.1)) + base_prior * w.sum());
+        idx++;
+    }
+    if (e->proc_name.size() != idx || e->malware.size() != idx) {
+        // the reference asserts these; a DB without "malware" members gives
+        // malware = false for every process in non-malware databases
+        if (e->malware.size() != idx) e->malware.assign(idx, 0);
+        if (e->proc_name.size() != idx) return;
+    }
+    uint32_t eid = (uint32_t)c.entries.size();
+    bool used = false;
+    if (const JV *s = fp.get("str_repr"); s && s->t == JV::STR) {
+        std::string fs = s->s;
+        if (!validate_fp(c, fs, code, type_str)) return;
+        if (c.fpdb.count(fs)) return;
+        c.fpdb[fs] = eid; c.fp_order.push_back(fs); used = true;
+    }
+    if (const JV *arr = fp.get("str_repr_array"); arr && arr->t == JV::ARR) {
+        for (auto &x : arr->a) {
+            if (x.t != JV::STR) continue;
+            std::string fs = x.s;
+            if (!validate_fp(c, fs, code, type_str)) { if (used) break; return; }
+            if (c.fpdb.count(fs)) continue;
+            c.fpdb[fs] = eid; c.fp_order.push_back(fs); used = true;
+        }
+    }
+    if (used) c.entries.push_back(std::move(e));
+}
+
+// pyasn.db line "a.b.c.d/len<ws>asn" (lct_subnet_set_from_string)
+void process_asn_line(mfp_classifier_s &c, const std::string &line) {
+    size_t sl = line.find('/');
+    if (sl == std::string::npos) return;
+    std::string addr = line.substr(0, sl);
+    char *end = nullptr;
+    long len = strtol(line.c_str() + sl + 1, &end, 10);
+    while (end && (*end == ' ' || *end == '\t')) end++;
+    unsigned long asn = end ? strtoul(end, nullptr, 10) : 0;
+    if (addr.find('.') != std::string::npos) {
+        int pos = 0;
+        uint32_t v;
+        if (!mfpc::parse_ipv4((const uint8_t *)addr.data(), (int)addr.size(), pos, v) || len < 0 || len > 32) return;
+        uint32_t be = (v & 0xff) << 24 | (v >> 8 & 0xff) << 16 | (v >> 16 & 0xff) << 8 | (v >> 24);
+        uint32_t mask = len == 0 ? 0 : (0xffffffffu << (32 - len));
+        c.asn4.push_back({(uint64_t)(be & mask) << 8 | (uint64_t)len, (uint32_t)asn});
+    } else {
+        int pos = 0;
+        uint8_t a[16];
+        if (!mfpc::parse_ipv6((const uint8_t *)addr.data(), (int)addr.size(), pos, a) || len < 0 || len > 128) return;
+        for (int b = (int)len; b < 128; b++) a[b / 8] &= (uint8_t)~(0x80u >> (b % 8));
+        std::string k((const char *)a, 16);
+        k.push_back((char)len);
+        c.asn6.push_back({k, (uint32_t)asn});
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C++ API used by mfp_host.cpp
+// ---------------------------------------------------------------------------
+mfp_classifier *mfp_classifier_load(const char *path) {
+    auto c = std::make_unique<mfp_classifier_s>();
+    for (const char *a : kReservedAttrs) attr_index(*c, a);
+    bool got_db = false, got_prev = false, got_ver = false, got_asn = false;
+    std::string db_text;
+    try {
+        bool ok = read_tgz(path, [&](const std::string &name, const std::string &data) {
+            if (name == "fp_prevalence_tls.txt") {
+                for_lines(data, [&](std::string l) {
+                    if (!l.empty() && l.back() == '\n') l.pop_back();
+                    if (l.empty()) return;
+                    if (l[0] == '(') l = "tls/" + l;
+                    c->known_prevalence.insert(l);
+                });
+                got_prev = true;
+            } else if (name == "fingerprint_db.json") {
+                db_text = data;
+                got_db = true;
+            } else if (name == "VERSION") {
+                for_lines(data, [&](const std::string &l) { c->version += l; });
+                got_ver = true;
+            } else if (name == "pyasn.db") {
+                for_lines(data, [&](const std::string &l) { process_asn_line(*c, l); });
+                got_asn = true;
+            }
+        });
+        if (!ok) { mfp_set_error("cannot read resource archive %s", path); return nullptr; }
+        c->fp_types.push_back(1);   // tls is always expected (analysis.h:833)
+        bool dual = c->version.find("dual") != std::string::npos, lite = c->version.find("lite") != std::string::npos,
+             full = c->version.find("full") != std::string::npos;
+        if (!dual && !lite && !full) c->disabled = true;   // legacy archive
+        if (!c->disabled) for_lines(db_text, [&](const std::string &l) { if (!l.empty()) process_fp_db_line(*c, l); });
+    } catch (const std::exception &ex) {
+        mfp_set_error("resource archive %s: %s", path, ex.what());
+        return nullptr;
+    }
+    if (std::count(c->version.begin(), c->version.end(), ';') != 1) c->disabled = true;
+    if (!got_db || !got_prev || !got_ver || !got_asn) c->disabled = true;
+    c->accept_attr = false;
+    // global process-name table
+    for (auto &e : c->entries)
+        for (auto &n : e->proc_name)
+            if (!c->proc_name_id.count(n)) {
+                c->proc_name_id[n] = (uint32_t)c->proc_names.size();
+                c->proc_names.push_back(n);
+            }
+    return c.release();
+}
+
+void mfp_classifier_free(mfp_classifier *c) {
+    if (!c) return;
+    mfp_classifier_free_device(c->dev);
+    delete c;
+}
+
+int mfp_classifier_tls_format(const mfp_classifier *c) {
+    auto it = c->fp_count_and_format.find("tls");
+    return it == c->fp_count_and_format.end() ? 0 : (int)it->second.second;
+}
+bool mfp_classifier_disabled(const mfp_classifier *c) { return c->disabled; }
+const char *mfp_classifier_process_name(const mfp_classifier *c, uint32_t id) {
+    return id < c->proc_names.size() ? c->proc_names[id].c_str() : nullptr;
+}
+const char *mfp_classifier_attr_name(const mfp_classifier *c, uint32_t i) {
+    return i < c->attr_names.size() ? c->attr_names[i].c_str() : nullptr;
+}
+void mfp_classifier_stats(const mfp_classifier *c, uint64_t out[8]) {
+    uint64_t procs = 0, upd = 0;
+    for (auto &e : c->entries) {
+        procs += e->prior.size();
+        for (auto &f : e->f) {
+            for (auto &kv : f.by_str) upd += kv.second.size();
+            for (auto &kv : f.by_int) upd += kv.second.size();
+            for (auto &kv : f.by_v6) upd += kv.second.size();
+        }
+    }
+    out[0] = c->fpdb.size(); out[1] = c->entries.size(); out[2] = procs; out[3] = upd;
+    out[4] = c->known_prevalence.size(); out[5] = c->asn4.size() + c->asn6.size();
+    out[6] = c->disabled; out[7] = c->proc_names.size();
+}
+
+// ---------------------------------------------------------------------------
+// flatten the model into device tables (layout: mfp_analysis.h)
+// ---------------------------------------------------------------------------
+namespace {
+
+uint64_t pow2_at_least(uint64_t n) {
+    uint64_t p = 16;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+struct HostTables {
+    std::vector<mfp_fp_slot> fp_slots;
+    std::vector<mfp_entry> entry;
+    std::vector<double> prior;
+    std::vector<uint32_t> proc_id;
+    std::vector<uint8_t> proc_mal;
+    std::vector<uint32_t> proc_attr;
+    std::vector<mfp_feat_slot> feat_slots;
+    std::vector<mfp_update> upd;
+    std::vector<char> pool;
+    std::vector<mfp_fp_slot> prev_slots;   // known prevalence set
+    std::vector<mfp_asn4> asn4;
+    std::vector<mfp_asn6> asn6;
+};
+
+uint32_t pool_add(HostTables &t, const std::string &s) {
+    uint32_t off = (uint32_t)t.pool.size();
+    t.pool.insert(t.pool.end(), s.begin(), s.end());
+    while (t.pool.size() % 8) t.pool.push_back(0);
+    return off;
+}
+
+void insert_string_slot(std::vector<mfp_fp_slot> &slots, uint64_t h, uint32_t id, uint32_t off, uint32_t len) {
+    uint64_t mask = slots.size() - 1;
+    for (uint64_t k = h & mask;; k = (k + 1) & mask) {
+        if (slots[k].id == 0xffffffffu) {
+            slots[k].hash = h; slots[k].id = id; slots[k].str_off = off; slots[k].str_len = len;
+            return;
+        }
+    }
+}
+
+}  // namespace
+
+static mfp_asn4 mk4(uint32_t lo, uint32_t hi, uint32_t asn) { mfp_asn4 r; r.lo = lo; r.hi = hi; r.asn = asn; r.pad = 0; return r; }
+
+int mfp_classifier_upload(mfp_classifier *c, int device) {
+    HostTables t;
+    // fingerprint table
+    t.fp_slots.assign(pow2_at_least(2 * c->fpdb.size() + 2), mfp_fp_slot{0, 0xffffffffu, 0, 0});
+    for (auto &fs : c->fp_order) {
+        uint32_t off = pool_add(t, fs);
+        insert_string_slot(t.fp_slots, mfpc::str_hash((const uint8_t *)fs.data(), (uint32_t)fs.size()), c->fpdb[fs], off,
+                           (uint32_t)fs.size());
+    }
+    // known prevalence set
+    t.prev_slots.assign(pow2_at_least(2 * c->known_prevalence.size() + 2), mfp_fp_slot{0, 0xffffffffu, 0, 0});
+    for (auto &fs : c->known_prevalence) {
+        uint32_t off = pool_add(t, fs);
+        insert_string_slot(t.prev_slots, mfpc::str_hash((const uint8_t *)fs.data(), (uint32_t)fs.size()), 0, off,
+                           (uint32_t)fs.size());
+    }
+    // entries, processes, features
+    uint64_t nfeat = 0;
+    for (auto &e : c->entries)
+        for (auto &f : e->f) nfeat += f.by_str.size() + f.by_int.size() + f.by_v6.size();
+    t.feat_slots.assign(pow2_at_least(2 * nfeat + 2), mfp_feat_slot{0, 0xffffffffu, 0, 0, 0, 0, 0});
+    auto put_feat = [&](uint32_t eid, uint32_t kind, uint64_t key, const std::vector<Upd> &lst, const std::string *str) {
+        mfp_feat_slot s;
+        s.key = key; s.entry = eid; s.kind = kind;
+        s.upd_off = (uint32_t)t.upd.size(); s.upd_cnt = (uint32_t)lst.size();
+        s.str_off = str ? pool_add(t, *str) : 0; s.str_len = str ? (uint32_t)str->size() : 0;
+        for (auto &u : lst) t.upd.push_back(mfp_update{u.idx, 0, u.val});
+        uint64_t mask = t.feat_slots.size() - 1;
+        for (uint64_t k = mfpc::feat_slot_hash(eid, kind, key) & mask;; k = (k + 1) & mask)
+            if (t.feat_slots[k].entry == 0xffffffffu) { t.feat_slots[k] = s; break; }
+    };
+    for (uint32_t eid = 0; eid < c->entries.size(); eid++) {
+        Entry &e = *c->entries[eid];
+        mfp_entry me;
+        me.proc_off = (uint32_t)t.prior.size();
+        me.nproc = (uint32_t)e.prior.size();
+        me.malware_db = e.malware_db;
+        me.generic_dmz = 0xffffffffu;
+        for (uint32_t i = 0; i < me.nproc; i++) {
+            t.prior.push_back(e.prior[i]);
+            t.proc_id.push_back(c->proc_name_id[e.proc_name[i]]);
+            t.proc_mal.push_back(e.malware[i]);
+            t.proc_attr.push_back(e.attr[i]);
+            if (e.proc_name[i] == "generic dmz process") me.generic_dmz = i;
+        }
+        t.entry.push_back(me);
+        for (uint32_t k = 0; k < 7; k++) {
+            for (auto &kv : e.f[k].by_int) put_feat(eid, k, kv.first, kv.second, nullptr);
+            for (auto &kv : e.f[k].by_str)
+                put_feat(eid, k, mfpc::str_hash((const uint8_t *)kv.first.data(), (uint32_t)kv.first.size()), kv.second,
+                         &kv.first);
+            for (auto &kv : e.f[k].by_v6)
+                put_feat(eid, k, mfpc::str_hash((const uint8_t *)kv.first.data(), 16), kv.second, &kv.first);
+        }
+    }
+    // ASN: disjoint intervals of the IPv4 prefixes, longest prefix wins
+    // (lct_find semantics); prefixes are nested or disjoint, so one sweep
+    // with a stack of open prefixes emits the elementary intervals
+    {
+        struct P { uint64_t lo, hi; uint32_t asn; int len; };
+        std::vector<P> ps;
+        for (auto &p : c->asn4) {
+            int len = (int)(p.first & 0xff);
+            uint64_t lo = p.first >> 8, hi = lo + (len == 0 ? (1ULL << 32) : (1ULL << (32 - len))) - 1;
+            ps.push_back({lo, hi, p.second, len});
+        }
+        std::stable_sort(ps.begin(), ps.end(), [](const P &a, const P &b) {
+            return a.lo != b.lo ? a.lo < b.lo : a.len < b.len;
+        });
+        std::vector<P> st;
+        uint64_t cursor = 0;
+        auto emit = [&](uint64_t lo, uint64_t hi, uint32_t asn) {
+            if (lo <= hi) t.asn4.push_back(mk4((uint32_t)lo, (uint32_t)hi, asn));
+        };
+        for (auto &p : ps) {
+            while (!st.empty() && st.back().hi < p.lo) {
+                emit(std::max(cursor, st.back().lo), st.back().hi, st.back().asn);
+                cursor = std::max(cursor, st.back().hi + 1);
+                st.pop_back();
+            }
+            if (!st.empty() && p.lo > 0) emit(std::max(cursor, st.back().lo), p.lo - 1, st.back().asn);
+            cursor = std::max(cursor, p.lo);
+            st.push_back(p);
+        }
+        while (!st.empty()) {
+            emit(std::max(cursor, st.back().lo), st.back().hi, st.back().asn);
+            cursor = std::max(cursor, st.back().hi + 1);
+            st.pop_back();
+        }
+    }
+    // IPv6: the same sweep on 128-bit keys
+    {
+        typedef unsigned __int128 u128;
+        struct P { u128 lo, hi; uint32_t asn; int len; };
+        std::vector<P> ps;
+        for (auto &p : c->asn6) {
+            u128 lo = 0;
+            for (int k = 0; k < 16; k++) lo = lo << 8 | (uint8_t)p.first[k];
+            int len = (uint8_t)p.first[16];
+            u128 span = len == 0 ? ~(u128)0 : (((u128)1 << (128 - len)) - 1);
+            ps.push_back({lo, lo + span, p.second, len});
+        }
+        std::stable_sort(ps.begin(), ps.end(), [](const P &a, const P &b) {
+            return a.lo != b.lo ? a.lo < b.lo : a.len < b.len;
+        });
+        std::vector<P> st;
+        u128 cursor = 0;
+        bool wrapped = false;   // cursor passed the top of the space
+        auto emit = [&](u128 lo, u128 hi, uint32_t asn) {
+            if (lo > hi) return;
+            mfp_asn6 r;
+            r.lo_hi = (uint64_t)(lo >> 64); r.lo_lo = (uint64_t)lo;
+            r.hi_hi = (uint64_t)(hi >> 64); r.hi_lo = (uint64_t)hi;
+            r.asn = asn; r.pad = 0;
+            t.asn6.push_back(r);
+        };
+        auto close_top = [&]() {
+            P &b = st.back();
+            if (!wrapped) emit(std::max(cursor, b.lo), b.hi, b.asn);
+            if (b.hi == ~(u128)0) wrapped = true;
+            else cursor = std::max(cursor, b.hi + 1);
+            st.pop_back();
+        };
+        for (auto &p : ps) {
+            while (!st.empty() && st.back().hi < p.lo) close_top();
+            if (!st.empty() && p.lo > 0 && !wrapped) emit(std::max(cursor, st.back().lo), p.lo - 1, st.back().asn);
+            cursor = std::max(cursor, p.lo);
+            st.push_back(p);
+        }
+        while (!st.empty()) close_top();
+    }
+    if (t.pool.empty()) t.pool.push_back(0);
+    if (t.upd.empty()) t.upd.push_back(mfp_update{0, 0, 0});
+    if (t.prior.empty()) { t.prior.push_back(0); t.proc_id.push_back(0); t.proc_mal.push_back(0); t.proc_attr.push_back(0); }
+    if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0});
+    if (t.asn4.empty()) t.asn4.push_back(mk4(1, 0, 0));
+    if (t.asn6.empty()) { mfp_asn6 r{}; r.lo_lo = 1; t.asn6.push_back(r); }
+
+    mfp_classifier_dev &d = c->dev;
+    mfp_classifier_free_device(d);
+    if (hipSetDevice(device) != hipSuccess) return -1;
+    c->device = device;
+    auto up = [&](auto *&dst, const auto &vec) -> bool {
+        size_t bytes = vec.size() * sizeof(vec[0]);
+        if (hipMalloc((void **)&dst, bytes) != hipSuccess) return false;
+        return hipMemcpy((void *)dst, vec.data(), bytes, hipMemcpyHostToDevice) == hipSuccess;
+    };
+    bool ok = up(d.fp_slots, t.fp_slots) && up(d.prev_slots, t.prev_slots) && up(d.entry, t.entry) &&
+              up(d.prior, t.prior) && up(d.proc_id, t.proc_id) && up(d.proc_mal, t.proc_mal) &&
+              up(d.proc_attr, t.proc_attr) && up(d.feat_slots, t.feat_slots) && up(d.upd, t.upd) && up(d.pool, t.pool) &&
+              up(d.asn4, t.asn4) && up(d.asn6, t.asn6);
+    if (!ok) { mfp_set_error("classifier device upload failed"); return -2; }
+    d.fp_mask = t.fp_slots.size() - 1;
+    d.prev_mask = t.prev_slots.size() - 1;
+    d.feat_mask = t.feat_slots.size() - 1;
+    d.n_asn4 = (uint32_t)t.asn4.size();
+    d.n_asn6 = c->asn6.empty() ? 0 : (uint32_t)t.asn6.size();
+    const char *rnd[3] = {"tls/randomized", "tls/1/randomized", "tls/2/randomized"};
+    for (int k = 0; k < 3; k++) {
+        auto it = c->fpdb.find(rnd[k]);
+        d.randomized_entry[k] = it == c->fpdb.end() ? 0xffffffffu : it->second;
+    }
+    d.types_mask = 0;
+    for (uint32_t ty : c->fp_types) d.types_mask |= 1u << ty;
+    d.enc_channel_idx = 7;
+    d.faketls_idx = 9;
+    // adaptive "seen" set of unknown TLS fingerprints (fingerprint_prevalence LRU)
+    d.seen_cap = 1u << 18;
+    if (hipMalloc((void **)&d.seen, (size_t)d.seen_cap * sizeof(mfp_seen_slot)) != hipSuccess) return -2;
+    if (hipMemset(d.seen, 0xff, (size_t)d.seen_cap * sizeof(mfp_seen_slot)) != hipSuccess) return -2;
+    if (hipMalloc((void **)&d.seen_count, sizeof(unsigned long long)) != hipSuccess) return -2;
+    if (hipMemset(d.seen_count, 0, sizeof(unsigned long long)) != hipSuccess) return -2;
+    d.batch = 0;
+    return 0;
+}
+
+void mfp_classifier_free_device(mfp_classifier_dev &d) {
+    void *ptrs[] = {d.fp_slots, d.prev_slots, d.entry, d.prior, d.proc_id, d.proc_mal, d.proc_attr,
+                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn6, d.seen, d.seen_count};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    d = mfp_classifier_dev{};
+}
+
+const mfp_classifier_dev *mfp_classifier_device(const mfp_classifier *c) { return &c->dev; }
+mfp_classifier_dev *mfp_classifier_device_mut(mfp_classifier *c) { return &c->dev; }
+
+// host-only helper exported for tests: the normalisation the device uses
+extern "C" MFP_EXPORT int mfp_normalize_server_name(const char *name, size_t len, char *out, size_t cap) {
+    char buf[400];
+    int n = mfpc::normalize_server_name((const uint8_t *)name, (int)len, buf);
+    if ((size_t)n + 1 > cap) return -1;
+    memcpy(out, buf, n);
+    out[n] = 0;
+    return n;
+}

@@ -801,6 +801,7 @@ struct Out {
     uint32_t fp_type, msg, flags;
     uint32_t sni_off, sni_len, ua_off, ua_len;
     uint32_t src_port, dst_port;
+    uint32_t net;        // innermost IP header offset | version << 16 (flow key, flow_key.h:71)
 };
 struct Cfg {
     uint32_t select, tls_format, mode;
@@ -1172,6 +1173,7 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
     const uint8_t *iph; int ipv;
     uint32_t proto = ip_parse(pkt, iph, ipv);
     for (int n = 0; n < 4 && (proto == 4 || proto == 41); n++) proto = ip_parse(pkt, iph, ipv);  // pkt_proc.cc:959
+    if (iph) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16);
     if (proto == 6) {
         const uint8_t *tcph = cget_ptr(pkt, 20);
         if (!tcph) return;
@@ -1239,6 +1241,7 @@ DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t
     o.fp_type = 0; o.msg = 0; o.flags = 0;
     o.sni_off = o.ua_off = 0; o.sni_len = o.ua_len = 0xffff;
     o.src_port = o.dst_port = 0;
+    o.net = 0;
     Cur p = cmk(data, data + len);
     switch (linktype) {
     case 1: {                                           // eth::eth eth.h:137

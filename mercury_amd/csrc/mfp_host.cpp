@@ -17,7 +17,12 @@
 #include <vector>
 
 #include "../../include/mfp.h"
+#include "mfp_analysis.h"
 #include "mfp_internal.h"
+
+extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                   uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
+                                   unsigned long long *stats, hipStream_t stream);
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
@@ -165,6 +170,9 @@ struct mfp_context_s {
     unsigned long long *d_used = nullptr;
     unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass
     uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list
+    mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
+    unsigned long long *d_an_stats = nullptr;
+    mfp_analysis *d_an = nullptr; size_t cap_an = 0;
     // host-batch staging buffers (grown on demand)
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
@@ -185,7 +193,9 @@ struct mfp_context_s {
 
 extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode) {
     uint32_t sel, fmt;
-    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, nullptr, nullptr)) return nullptr;
+    std::string resources;
+    bool analysis = false;
+    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis)) return nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         mfp_set_error("no HIP device available: the mercury_amd fingerprint path runs only on the GPU");
@@ -206,12 +216,33 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
         delete c;
         return nullptr;
     }
+    if (analysis && !resources.empty()) {
+        // mercury ctor (pkt_proc.h:76-110): load the archive, force the TLS
+        // fingerprint format to the database's, keep parsing if the
+        // classifier is disabled
+        mfp_classifier *clf = mfp_classifier_load(resources.c_str());
+        if (!clf) { mfp_finalize(c); return nullptr; }
+        if (mfp_classifier_disabled(clf)) {
+            mfp_classifier_free(clf);
+        } else {
+            c->tls_format = (uint32_t)mfp_classifier_tls_format(clf);
+            if (mfp_classifier_upload(clf, device) != 0 ||
+                hipMalloc(&c->d_an_stats, 4 * sizeof(unsigned long long)) != hipSuccess) {
+                mfp_classifier_free(clf);
+                mfp_finalize(c);
+                return nullptr;
+            }
+            c->clf = clf;
+        }
+    }
     return c;
 }
 
 extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->clf) mfp_classifier_free(c->clf);
+    (void)hipFree(c->d_an_stats); (void)hipFree(c->d_an);
     (void)hipFree(c->d_used); (void)hipFree(c->d_bins); (void)hipFree(c->d_work); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -300,4 +331,75 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint
     if (used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
     if (used[0]) HIPCHK(hipMemcpy(fp_arena, c->d_fp, used[0], hipMemcpyDeviceToHost));
     return (long long)used[0];
+}
+
+// ---------------------------------------------------------------------------
+// --analysis (process classifier) entry points
+// ---------------------------------------------------------------------------
+extern "C" MFP_EXPORT int mfp_analysis_enabled(mfp_context c) { return c && c->clf ? 1 : 0; }
+
+extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
+                                                   size_t n, mfp_record *d_rec, const char *d_fp_arena,
+                                                   mfp_analysis *d_out, void *stream) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(c->device));
+    mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
+    D->batch++;                                   // stream order across batches (fingerprint_prevalence)
+    HIPCHK(hipMemsetAsync(c->d_an_stats, 0, 4 * sizeof(unsigned long long), s));
+    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_an_stats, s) != 0) {
+        mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -3;
+    }
+    return 0;
+}
+
+extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const uint8_t *arena, size_t arena_len,
+                                                          const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                                          char *fp_arena, size_t fp_cap, mfp_analysis *analysis) {
+    long long used = mfp_process_batch_host(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap);
+    if (used < 0 || !analysis) return used;
+    if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        if (grow(c->d_an, c->cap_an, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    }
+    int r = mfp_analyze_batch_device(c, c->d_arena, c->d_desc, n, c->d_rec, c->d_fp, c->d_an, c->stream);
+    if (r) return r;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipMemcpyAsync(analysis, c->d_an, n * sizeof(mfp_analysis), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(rec, c->d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return used;
+}
+
+extern "C" MFP_EXPORT const char *mfp_process_name(mfp_context c, uint32_t id) {
+    return c && c->clf ? mfp_classifier_process_name(c->clf, id) : nullptr;
+}
+
+extern "C" MFP_EXPORT const char *mfp_attribute_name(mfp_context c, uint32_t bit) {
+    return c && c->clf ? mfp_classifier_attr_name(c->clf, bit) : nullptr;
+}
+
+extern "C" MFP_EXPORT int mfp_analysis_stats(mfp_context c, uint64_t out[4]) {
+    if (!c || !c->clf) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    unsigned long long h[4];
+    HIPCHK(hipMemcpy(h, c->d_an_stats, sizeof h, hipMemcpyDeviceToHost));
+    unsigned long long seen = 0;
+    HIPCHK(hipMemcpy(&seen, mfp_classifier_device(c->clf)->seen_count, sizeof seen, hipMemcpyDeviceToHost));
+    out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = seen;
+    return 0;
+}
+
+// host-only: load a resource archive and report its size (no device needed)
+extern "C" MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]) {
+    mfp_classifier *clf = mfp_classifier_load(path);
+    if (!clf) return -1;
+    mfp_classifier_stats(clf, out);
+    mfp_classifier_free(clf);
+    return 0;
 }

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
         r.ua_len = (uint16_t)o.ua_len;
         r.src_port = (uint16_t)o.src_port;
         r.dst_port = (uint16_t)o.dst_port;
-        r.reserved = 0;
+        r.net = o.net;
         P.rec[i] = r;
     }
     __syncthreads();   // tile_base / wave_tot reuse
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P
         const int npk = (int)min((uint64_t)64, n_eff - g * 64);
         // this lane's record
         uint64_t r_off = 0;
-        uint32_t r_len = 0, r_w2 = 0, r_sni = 0xffff0000u, r_ua = 0xffff0000u, r_ports = 0;
+        uint32_t r_len = 0, r_w2 = 0, r_sni = 0xffff0000u, r_ua = 0xffff0000u, r_ports = 0, r_net = 0;
         bool fb = false;
 
         for (int j = 0; j < npk; j++) {
@@ -288,6 +288,7 @@ __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P
                 r_sni = (w.o.sni_len == 0xffff ? 0 : (w.o.sni_off & 0xffff)) | (w.o.sni_len << 16);
                 r_ua = (w.o.ua_len == 0xffff ? 0 : (w.o.ua_off & 0xffff)) | (w.o.ua_len << 16);
                 r_ports = (w.o.src_port & 0xffff) | (w.o.dst_port << 16);
+                r_net = w.o.net;
             }
         }
         const uint64_t fbm = ballot(fb);
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P
         if (live && !fb) {
             uint4 *rp = (uint4 *)(P.rec + i);
             rp[0] = make_uint4((uint32_t)r_off, (uint32_t)(r_off >> 32), r_len, r_w2);
-            rp[1] = make_uint4(r_sni, r_ua, r_ports, 0u);
+            rp[1] = make_uint4(r_sni, r_ua, r_ports, r_net);
         }
     }
     if (lane == 0 && exact) atomicAdd(&P.fp_used[2], exact);

@@ -65,6 +65,7 @@ struct Out {
     uint32_t fp_type, msg, flags;
     uint32_t sni_off, sni_len, ua_off, ua_len;
     uint32_t src_port, dst_port;
+    uint32_t net;        // innermost IP header offset | version << 16
 };
 struct Cfg {
     uint32_t select, tls_format, mode;
@@ -1421,6 +1422,7 @@ struct W {
         int iph, ipv;
         uint32_t proto = ip_parse(pkt, iph, ipv);
         for (int k = 0; k < 4 && (proto == 4 || proto == 41); k++) proto = ip_parse(pkt, iph, ipv);  // pkt_proc.cc:959
+        if (iph >= 0) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16);
         if (proto == 6) {
             int tcph = cget_ptr(pkt, 20);
             if (tcph < 0) return;
@@ -1480,6 +1482,7 @@ struct W {
         o.fp_type = 0; o.msg = 0; o.flags = 0;
         o.sni_off = o.ua_off = 0; o.sni_len = o.ua_len = 0xffff;
         o.src_port = o.dst_port = 0;
+        o.net = 0;
         C p = cmk(base, base + (int)len);
         switch (linktype) {
         case 1: {                                        // eth::eth eth.h:137

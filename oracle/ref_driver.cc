@@ -72,7 +72,24 @@ static std::vector<pkt> load(const std::vector<uint8_t> &buf) {
 
 static int quiet(enum log_level, const char *, va_list) { return 0; }
 
+// mode "sni": server_identifier normalisation (watchlist.hpp:326-390) of
+// each line of <input>, one output line each: <name>\t<normalized>
+static int sni_mode(const char *path) {
+    FILE *f = fopen(path, "rb");
+    if (!f) { perror(path); return 1; }
+    char line[4096];
+    while (fgets(line, sizeof line, f)) {
+        size_t n = strlen(line);
+        if (n && line[n - 1] == '\n') line[--n] = 0;
+        server_identifier si{std::string(line, n)};
+        printf("%s\t%s\n", line, si.get_normalized_domain_name(server_identifier::detail::on).c_str());
+    }
+    fclose(f);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 3 && std::string(argv[1]) == "sni") return sni_mode(argv[2]);
     if (argc < 4) {
         fprintf(stderr, "usage: %s fp|an|time <input> <config-string> [resources] [threads] [seconds]\n", argv[0]);
         return 2;

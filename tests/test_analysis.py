@@ -1,0 +1,189 @@
+"""The --analysis process classifier (classifier, analysis.h) on the device,
+compared with the REFERENCE's own results (tests/golden/an_*.tsv.gz, made by
+tests/golden/make_golden_analysis.py from libmerc built out of
+/root/reference).
+
+Bar: status, process name and malware flag identical; score and p_malware
+within |delta| <= 1e-6 (expf is fp32 in the reference, the
+sums are fp64 in both).
+"""
+import gzip
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import mercury_amd
+from tests import synth
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SELECT = "tls,dtls,ssh,http,tcp,tcp.syn_ack"
+TOL = 1e-6
+
+
+def load_ref_an(name):
+    rows = []
+    with gzip.open(os.path.join(GOLD, name), "rt", encoding="latin-1") as f:
+        for line in f:
+            p = line.rstrip("\n").split("\t")
+            rows.append(dict(valid=int(p[1]), fp_type=int(p[2]), status=int(p[3]), process=p[4], score=float(p[5]),
+                             malware=int(p[6]), p_malware=float(p[7])))
+    return rows
+
+
+def synth_batch():
+    m = json.load(open(os.path.join(GOLD, "an_manifest.json")))["synth"]
+    a, d = synth.batch(m["n"], seed=m["seed"], workload=m["workload"], n_templates=m["n_templates"])
+    h = hashlib.sha256()
+    h.update(a.tobytes())
+    h.update(d.tobytes())
+    assert h.hexdigest() == m["sha256"], "synthetic generator drifted from the golden batch"
+    return a, d
+
+
+# ---------------------------------------------------------------------------
+# CPU: the resource-archive loader and the server-name normalisation
+# ---------------------------------------------------------------------------
+def test_resource_archive_loader_reference_archive():
+    st = mercury_amd.resource_stats(os.path.join(GOLD, "resources-test.tgz"))
+    # resources-test.tgz: 6 fingerprints (tls x2, quic, http, stun, tofsee), <= 3 processes each
+    assert st["fingerprints"] == 6 and st["entries"] == 6
+    assert 6 <= st["processes"] <= 18
+    assert st["disabled"] == 0
+
+
+def test_resource_archive_loader_synthetic_archive():
+    st = mercury_amd.resource_stats(os.path.join(GOLD, "synth_resources.tgz"))
+    m = json.load(open(os.path.join(GOLD, "an_manifest.json")))["synth"]["db"]
+    assert st["fingerprints"] == m["labeled"] + 1          # + tls/1/randomized
+    assert st["known_prevalence"] > 0 and st["asn_prefixes"] == 8
+
+
+@pytest.mark.parametrize("name,want", [
+    ("outlook.office365.com", "outlook.office365.com"),
+    ("example.com.", "example.com"),
+    ("*.example.com", "*.example.com"),
+    ("localhost", "localhost"),
+    ("intranet", "unqualified.alt"),
+    ("None", "missing.alt"),
+    ("", "missing.alt"),
+    ("1.1.1.1:443", "_443.1-1-1-1.address.alt"),
+    ("10.1.2.3", "10-0-0-1.address.alt"),            # private -> 10.0.0.1 (ip_address.hpp:404)
+    ("[::1]:443", "_443.fd00--1.address.alt"),       # non-global -> fd00::1
+    ("2001:db8::1", "2001-db8--1.address.alt"),
+    ("www.example.com:8443", "_8443.www.example.com"),
+    ("bad name", "other.alt"),
+    ("x..y", "other.alt"),
+    (":443", "_443.missing.alt"),
+    ("host:99999", "other.alt"),
+])
+def test_server_name_normalisation(name, want):
+    """server_identifier::get_normalized_domain_name(detail::on), watchlist.hpp:326-390
+    (expected values confirmed with the reference: merc_ref_drv sni)."""
+    assert mercury_amd.normalize_server_name(name) == want
+
+
+def test_server_name_normalisation_reference_golden():
+    """6 855 names (synthetic, mutated, address-like) normalised by the REFERENCE
+    (tests/golden/make_golden_sni.py) -- the device runs the same code."""
+    bad = []
+    with gzip.open(os.path.join(GOLD, "sni_norm.tsv.gz"), "rt", encoding="latin-1") as f:
+        for line in f:
+            name, want = line.rstrip("\n").split("\t")
+            got = mercury_amd.normalize_server_name(name)
+            if got != want:
+                bad.append((name, got, want))
+    assert not bad, bad[:10]
+
+
+# ---------------------------------------------------------------------------
+# GPU: per-packet parity with the reference's classifier
+# ---------------------------------------------------------------------------
+def run_analysis(arena, desc, resources):
+    cfg = f"select={SELECT};resources={os.path.join(GOLD, resources)};analysis"
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        assert ctx.analysis_enabled
+        rec, fp, an = ctx.process_host_analysis(arena, desc)
+        names = [ctx.process_name(int(p)) for p in an["process"]]
+        stats = ctx.analysis_stats()
+    finally:
+        ctx.close()
+    return rec, fp, an, names, stats
+
+
+def compare(ref, rec, an, names):
+    bad = []
+    for i, r in enumerate(ref):
+        valid = int(an["flags"][i] & 1)
+        if valid != r["valid"]:
+            bad.append((i, "valid", valid, r))
+            continue
+        if not valid:
+            continue
+        if int(an["status"][i]) != r["status"] or int(rec["fp_type"][i]) != r["fp_type"]:
+            bad.append((i, "status", int(an["status"][i]), r))
+            continue
+        if names[i] != r["process"]:
+            bad.append((i, "process", names[i], r))
+            continue
+        if abs(float(an["score"][i]) - r["score"]) > TOL:
+            bad.append((i, "score", float(an["score"][i]), r))
+            continue
+        mal = int((an["flags"][i] >> 1) & 1)
+        if mal != r["malware"]:
+            bad.append((i, "malware", mal, r))
+            continue
+        pm = float(an["malware_prob"][i]) if an["flags"][i] & 4 else 0.0
+        if r["process"] and abs(pm - r["p_malware"]) > TOL:
+            bad.append((i, "p_malware", pm, r))
+    return bad
+
+
+@pytest.mark.gpu
+def test_analysis_synthetic_archive_vs_reference():
+    a, d = synth_batch()
+    ref = load_ref_an("an_synth.tsv.gz")
+    rec, fp, an, names, stats = run_analysis(a, d, "synth_resources.tgz")
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+    # the fixture exercises labeled TLS and HTTP, unlabeled, randomized, unanalyzed, malware
+    st = [(r["fp_type"], r["status"]) for r in ref if r["valid"]]
+    assert {(1, 1), (3, 1), (1, 3), (3, 3), (5, 4), (1, 2)} <= set(st)
+    assert sum(r["malware"] for r in ref) > 50
+    assert stats[0] > 5000
+
+
+@pytest.mark.gpu
+def test_analysis_reference_archive_and_pcaps():
+    z = np.load(os.path.join(GOLD, "ref_packets.npz"))
+    ref = load_ref_an("an_ref.tsv.gz")
+    rec, fp, an, names, _ = run_analysis(z["arena"], z["desc"], "resources-test.tgz")
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+
+
+@pytest.mark.gpu
+def test_analysis_stream_order_across_batches():
+    """fingerprint_prevalence: an unknown TLS fingerprint is 'randomized' at its
+    first sighting and 'unlabeled' afterwards, also across batches."""
+    a, d = synth_batch()
+    ref = load_ref_an("an_synth.tsv.gz")
+    cfg = f"select={SELECT};resources={os.path.join(GOLD, 'synth_resources.tgz')};analysis"
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        half = len(d) // 2
+        out = []
+        for lo, hi in ((0, half), (half, len(d))):
+            dd = d[lo:hi].copy()
+            rec, fp, an = ctx.process_host_analysis(a, dd)
+            out.append((rec, an, [ctx.process_name(int(p)) for p in an["process"]]))
+    finally:
+        ctx.close()
+    rec = np.concatenate([o[0] for o in out])
+    an = np.concatenate([o[1] for o in out])
+    names = out[0][2] + out[1][2]
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
