@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmercury_amd.so")
 OBJ = os.path.join(HERE, "_obj")
 
-SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_host.cpp", "mfp_classifier.cpp"]
+SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp"]
 HEADERS = ["mfp_device.hpp", "mfp_wave.hpp", "mfp_internal.h", "mfp_analysis.h", "mfp_common.hpp"]
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 
@@ -22,7 +22,8 @@ def _newer(target, deps):
 
 def build(verbose=False):
     os.makedirs(OBJ, exist_ok=True)
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "mfp.h")]
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", h)
+                                                       for h in ("mfp.h", "mercury_amd_libmerc.h")]
     objs = []
     for s in SOURCES:
         src = os.path.join(CSRC, s)

@@ -348,6 +348,10 @@ __global__ __launch_bounds__(256) void k_analyze(AParams P) {
                     if ((res.flags & MFP_AN_MALWARE) && ft == 1) res.attr |= (uint16_t)(1u << D.enc_channel_idx);
                 }
             }
+            // analyze_ip_packet: a truncated message reports "unlabeled" and
+            // keeps its classification (pkt_proc.cc:1716-1719)
+            const uint32_t rflags = rfl(__shfl((uint32_t)r.flags, j, 64));
+            if (P.mode == MFP_MODE_ANALYSIS && (rflags & MFP_FLAG_TRUNCATED) && !pending) res.status = 3;
             if (lane == 0) atomicAdd(&P.stats[0], 1ull);
             if (pending && lane == 0) atomicAdd(&P.stats[1], 1ull);
             if (lane == (uint32_t)j) a = res;
@@ -384,6 +388,7 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
         a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0;
         a.flags = MFP_AN_VALID;
     }
+    if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
     P.out[i] = a;
     P.rec[i].status = a.status;
 }
@@ -392,11 +397,11 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   unsigned long long *stats, hipStream_t stream) {
+                                   unsigned long long *stats, uint32_t mode, hipStream_t stream) {
     if (n == 0) return 0;
     mfpa::AParams P;
     P.D = *D;
-    P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = 0;
+    P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = mode;
     P.stats = stats;
     uint64_t groups = (n + 63) / 64, blocks = (groups + 3) / 4;
     if (blocks > 2048) blocks = 2048;

@@ -22,7 +22,7 @@
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   unsigned long long *stats, hipStream_t stream);
+                                   unsigned long long *stats, uint32_t mode, hipStream_t stream);
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
@@ -349,7 +349,8 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
     D->batch++;                                   // stream order across batches (fingerprint_prevalence)
     HIPCHK(hipMemsetAsync(c->d_an_stats, 0, 4 * sizeof(unsigned long long), s));
-    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_an_stats, s) != 0) {
+    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_an_stats, c->mode,
+                            s) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
