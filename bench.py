@@ -1,21 +1,34 @@
-"""bench.py -- device-resident fingerprint throughput of the MI355X path.
+"""bench.py -- device-resident fingerprint + classify throughput of the MI355X path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mixed|tls_ch] [--packets P]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mixed|tls_ch]
+                    [--packets P] [--no-analysis]
 
-A step is one pass of the hot path (libmercury_amd.so, k_fingerprint) over
-one batch of P synthetic packets already resident in HBM (BASELINE.json
-config 2: 50 M mixed TLS/HTTP/SSH/TCP packets, protocol identification +
-fingerprint; `--workload tls_ch --packets 10000000` is config 1).  Packets
-are independent, so for N > 1 every rank processes its own batch (weak
-scaling, no data-path collective); the barrier and the max-over-ranks timing
-use torch.distributed only for measurement.
+A step is one pass of the hot path (libmercury_amd.so) over one batch of P
+synthetic packets already resident in HBM:
 
-Rank 0 prints one JSON line with the roofline of the dominant kernel
-(k_fingerprint, HIP events on its stream) and the CPU baseline (the
-reference libmerc compiled from /root/reference when oracle/_ref travelled
-with the snapshot, else the C oracle port), timed on a bounded sample.
+  default       BASELINE config 4: 50 M mixed TLS/HTTP/SSH/TCP packets,
+                protocol identification + fingerprint + the --analysis
+                process classifier (synthetic resource archive
+                tests/golden/synth_resources.tgz, built for this traffic)
+  --no-analysis config 3: protocol identification + fingerprint only
+  --workload tls_ch --packets 10000000 --no-analysis   config 2
+
+Packets are independent, so for N > 1 every rank processes its own shard
+(weak scaling, no data-path collective; all ranks draw from one template pool
+so the classifier's label rate is the same on every shard); the barrier and
+the max-over-ranks timing use torch.distributed only for measurement.
+
+Rank 0 prints one JSON line.  `roofline` covers the kernels of one step
+(timed with HIP events on the stream they run on, mfp_profile_enable) against
+the HBM peak; `kernels` breaks the step down per launch.  `roofline.traffic`
+comes from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the same command
+(profiles/*traffic*.json, tools/pmc_traffic.py) when one matches this
+configuration.  `cpu_baseline` is the reference libmerc compiled from
+/root/reference (oracle/_ref, travels with the snapshot) or else the C oracle
+port, timed on a bounded sample on the host cores.
 """
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -30,17 +43,22 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 CONTRACT = "tls,dtls,ssh,http,tcp,tcp.syn_ack"
+RESOURCES = os.path.join(ROOT, "tests", "golden", "synth_resources.tgz")
+TEMPLATE_SEED = {"mixed": 0x5EED0003, "tls_ch": 0x5EED0001}
+N_TEMPLATES = 4096
+METRIC = "device-resident Mpkt/s + GB/s, fingerprint+classify, mixed-protocol batch"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_device_batch(torch, n, workload, seed, unique):
-    """Unique packets generated on the host, replicated on the device."""
+def build_device_batch(torch, n, workload, draw_seed, unique):
+    """`unique` distinct packets generated on the host, replicated on the device."""
     from tests import synth
     u = min(unique, n)
-    ua, ud = synth.batch(u, seed=seed, workload=workload, n_templates=4096)
+    ua, ud = synth.batch(u, seed=TEMPLATE_SEED[workload], workload=workload, n_templates=N_TEMPLATES,
+                         draw_seed=draw_seed)
     span = int(ud["offset"][-1] + ud["caplen"][-1])
     stride = (span + 64 + 255) // 256 * 256
     reps = (n + u - 1) // u
@@ -48,37 +66,55 @@ def build_device_batch(torch, n, workload, seed, unique):
     host[:span] = ua[:span]
     d_unique = torch.from_numpy(host).cuda()
     d_arena = d_unique.repeat(reps)
+    del d_unique
     desc = np.tile(ud, reps)[:n].copy()
     desc["offset"] += (np.arange(reps, dtype=np.uint64) * np.uint64(stride)).repeat(u)[:n]
     d_desc = torch.from_numpy(desc.view(np.uint8)).cuda()
     return ua, ud, d_arena, desc, d_desc
 
 
-def cpu_baseline(workload, seed, sample_n, threads, seconds):
+def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis):
     """Reference libmerc (oracle/_ref) if present, else the C oracle port."""
     from tests import pcaplib, synth
-    a, d = synth.batch(sample_n, seed=seed, workload=workload, n_templates=4096)
+    a, d = synth.batch(sample_n, seed=TEMPLATE_SEED[workload], workload=workload, n_templates=N_TEMPLATES,
+                       draw_seed=draw_seed)
     ref = os.path.join(ROOT, "oracle", "_ref", "merc_ref_drv")
     if os.path.exists(ref):
         with tempfile.NamedTemporaryFile(suffix=".mfpb", delete=False) as t:
             path = t.name
         pcaplib.write_mfpb(path, a, d)
         try:
-            out = subprocess.run([ref, "time", path, CONTRACT, "-", str(threads), str(seconds)],
+            out = subprocess.run([ref, "time", path, CONTRACT, RESOURCES if analysis else "-", str(threads),
+                                  str(seconds)],
                                  capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
             r = json.loads(out.decode().strip().splitlines()[-1])
+            what = "write_json with --analysis (resources loaded)" if analysis else "write_json"
             return {"value": r["pps"] / 1e6, "unit": "Mpkt/s", "cores": threads, "kind": "reference",
-                    "sample": f"{sample_n} {workload} packets (seed {seed:#x}) looped for {r['seconds']:.1f} s, "
-                              f"libmerc write_json, one processor per thread, {r['packets']} packets"}
+                    "sample": f"{sample_n} {workload} packets looped for {r['seconds']:.1f} s, libmerc {what}, "
+                              f"one processor per thread, {r['packets']} packets"}
         finally:
             os.unlink(path)
+    if analysis:
+        return None   # the C oracle port restates the fingerprint path only
     from oracle import oracle
-    reps = 1
     t, _ = oracle.time_batch(a, d, oracle.config(), threads=threads, reps=1)
     reps = max(1, int(seconds / max(t, 1e-3)))
     t, _ = oracle.time_batch(a, d, oracle.config(), threads=threads, reps=reps)
     return {"value": sample_n * reps / t / 1e6, "unit": "Mpkt/s", "cores": threads, "kind": "port",
             "sample": f"{sample_n} {workload} packets x {reps} passes, C oracle, {threads} threads"}
+
+
+def find_traffic(cfg_key):
+    """Counter-derived HBM bytes per step for this configuration, if profiled."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
+        try:
+            t = json.load(open(f))
+        except Exception:
+            continue
+        if t.get("config") == cfg_key:
+            best = (f, t)
+    return best
 
 
 def main():
@@ -89,10 +125,12 @@ def main():
     ap.add_argument("--workload", default="mixed", choices=["mixed", "tls_ch"])
     ap.add_argument("--packets", type=int, default=None)
     ap.add_argument("--unique", type=int, default=1_000_000)
-    ap.add_argument("--tls-format", type=int, default=0)
+    ap.add_argument("--tls-format", type=int, default=0, help="without --analysis (else the archive's)")
+    ap.add_argument("--no-analysis", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    analysis = not args.no_analysis
 
     import torch
     import mercury_amd
@@ -110,29 +148,38 @@ def main():
 
     workload = args.workload
     n = args.packets or (50_000_000 if workload == "mixed" else 10_000_000)
-    seed = 0x5EED0003 if workload == "mixed" else 0x5EED0001
-    seed += rank * 7919   # different packets per rank
+    draw_seed = TEMPLATE_SEED[workload] + 1 + rank * 7919   # different packets per rank, one template pool
 
     t0 = time.time()
-    ua, ud, d_arena, desc, d_desc = build_device_batch(torch, n, workload, seed, args.unique)
+    ua, ud, d_arena, desc, d_desc = build_device_batch(torch, n, workload, draw_seed, args.unique)
     log(f"[rank {rank}] batch: {n} packets, {int(desc['caplen'].astype(np.int64).sum()) / 1e9:.2f} GB "
         f"({time.time() - t0:.1f} s to build)")
 
-    cfg = CONTRACT if args.tls_format == 0 else f"select={CONTRACT};format=tls/{args.tls_format}"
-    ctx = mercury_amd.Context(cfg, device=torch.cuda.current_device())
+    if analysis:
+        cfg = f"select={CONTRACT};resources={RESOURCES};analysis"
+        ctx = mercury_amd.Context(cfg, device=torch.cuda.current_device())
+        assert ctx.analysis_enabled
+    else:
+        cfg = CONTRACT if args.tls_format == 0 else f"select={CONTRACT};format=tls/{args.tls_format}"
+        ctx = mercury_amd.Context(cfg, device=torch.cuda.current_device())
+    tls_format = mercury_amd.parse_filter(cfg)[1] if not analysis else None
+
     # size the fp arena from the unique set (exact per replica)
     rec_u, fp_u = ctx.process_host(ua, ud)
     reps = (n + len(ud) - 1) // len(ud)
-    # strings are 16-byte aligned and each wave reserves 128 KiB chunks
     cap = int(int(rec_u["fp_len"].astype(np.int64).sum() + 16 * len(ud)) * reps * 1.05) + (2 << 30)
     d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_fp = torch.empty(cap, dtype=torch.uint8, device="cuda")
     d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
+    d_an = torch.empty(n * 24 if analysis else 1, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
 
     def step():
         ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(), cap,
                            d_used.data_ptr(), stream.cuda_stream)
+        if analysis:
+            ctx.analyze_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(),
+                               d_an.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -141,20 +188,19 @@ def main():
     if overflow:
         raise RuntimeError("fp arena overflow")
 
+    ctx.profile(True)   # HIP events around every kernel launch, on `stream`
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t_start = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
+    for _ in range(args.steps):
         step()
-        ev[k][1].record(stream)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t_start
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    prof = ctx.profile_read()
+    ctx.profile(False)
     if dist:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -164,23 +210,51 @@ def main():
     caplen_bytes = int(desc["caplen"].astype(np.int64).sum())
     fp_bytes = int(rec["fp_len"].astype(np.int64).sum())
     assert fp_bytes == used
-    alg_bytes = caplen_bytes + 16 * n + 32 * n + fp_bytes     # SURVEY 8(d)
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # algorithmic bytes per step: every packet
+    # read once, its descriptor, its 32-B record and its fingerprint written;
+    # the classifier re-reads the record and the fingerprint of each
+    # classified packet and writes a 24-B analysis record per packet
+    alg_bytes = caplen_bytes + 16 * n + 32 * n + fp_bytes
+    an_info = None
+    if analysis:
+        an = d_an.cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)
+        valid = (an["flags"] & 1) != 0
+        alg_bytes += 32 * n + 24 * n + int(rec["fp_len"][valid].astype(np.int64).sum())
+        st = np.bincount(an["status"][valid], minlength=5)
+        an_info = {"classified": int(valid.sum()),
+                   "status": {mercury_amd.api.STATUS_NAMES[i]: int(st[i]) for i in range(5)},
+                   "malware": int(((an["flags"] & 2) != 0).sum())}
+    kern_ms = {k: v[1] / args.steps for k, v in prof.items()}
+    step_kern_ms = sum(kern_ms.values())
+    dominant = max(kern_ms, key=kern_ms.get)
+    achieved = alg_bytes / (step_kern_ms * 1e-3) / 1e9
 
     total_pkts = n * world
     value = total_pkts * args.steps / elapsed / 1e6
-    out = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, len(os.sched_getaffinity(0)))
             try:
-                cpu = cpu_baseline(workload, seed, 200_000, threads, args.cpu_seconds)
+                cpu = cpu_baseline(workload, draw_seed, 200_000, threads, args.cpu_seconds, analysis)
             except Exception as e:   # baseline is reported, never the target
                 log(f"cpu baseline failed: {e}")
+        cfg_key = f"{workload}/{n}/{'analysis' if analysis else 'fp'}"
+        tr = find_traffic(cfg_key)
+        traffic = None
+        if tr:
+            traffic = tr[1]["hbm_bytes_per_step"]
         n_fp = int((rec["fp_type"] > 0).sum())
+        if workload == "mixed":
+            wl = ("config 4: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint + --analysis classifier "
+                  "(synthetic resource archive)") if analysis else \
+                 "config 3: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint"
+        else:
+            wl = "config 2: 10M TLS ClientHello, fingerprint" + (" + classifier" if analysis else "")
+        if n != (50_000_000 if workload == "mixed" else 10_000_000):
+            wl += f" (at {n} packets)"
         out = {
-            "metric": "device-resident Mpkt/s + GB/s, fingerprint+classify, mixed-protocol batch",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mpkt/s",
             "n_gpus": world,
@@ -193,29 +267,35 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": ("config 2: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint (classifier not "
-                             "yet on device)") if workload == "mixed" else "config 1: 10M TLS ClientHello, fingerprint",
+                "workload": wl,
                 "packets_per_gpu": n,
                 "unique_packets": len(ud),
                 "packet_bytes_per_gpu": caplen_bytes,
                 "select": CONTRACT,
-                "tls_format": args.tls_format,
+                "analysis": analysis,
+                "resources": os.path.relpath(RESOURCES, ROOT) if analysis else None,
+                "tls_format": "archive's (tls/1)" if analysis else tls_format,
                 "parallelism": f"shard{world}",
             },
             "gb_per_s": round(caplen_bytes * world * args.steps / elapsed / 1e9, 3),
             "fingerprints_per_step": n_fp,
             "fallback_packets_per_step": n_fallback,
+            "analysis": an_info,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
-                "kernel": "k_fingerprint",
-                "kernel_ms": round(kern_ms, 4),
+                "traffic": traffic,
+                "traffic_source": os.path.relpath(tr[0], ROOT) if tr else None,
+                "kernel": "step pipeline (every kernel of one step, back to back on one stream)",
+                "kernel_ms": round(step_kern_ms, 4),
+                "dominant_kernel": dominant,
                 "algorithmic_bytes_per_launch": alg_bytes,
             },
+            "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4)}
+                        for k, v in kern_ms.items()},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -178,6 +178,18 @@ MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]);
  * normalisation the device applies to server names); returns the length */
 MFP_EXPORT int mfp_normalize_server_name(const char *name, size_t len, char *out, size_t cap);
 
+/* ---- per-kernel timing (bench.py's roofline; the rocprofv3 cross-check) ----
+ * on != 0: from now on every kernel launch of this context is bracketed by
+ * HIP events recorded on its launch stream (totals reset); on == 0: off. */
+MFP_EXPORT int mfp_profile_enable(mfp_context ctx, int on);
+
+/* Kernel i (first-launch order) since mfp_profile_enable: its name
+ * ("k_classify", "k_fingerprint/<bin>", "k_wave_fp/<bin>", "k_analyze", ...),
+ * launch count and summed duration in ms.  Waits for the recorded events.
+ * Returns 0, 1 when i is past the last kernel, or a negative error. */
+MFP_EXPORT int mfp_profile_read(mfp_context ctx, uint32_t i, char *name, size_t cap, uint64_t *launches,
+                                double *total_ms);
+
 /* last error string for this thread */
 MFP_EXPORT const char *mfp_last_error(void);
 

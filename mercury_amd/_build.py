@@ -24,7 +24,7 @@ def build(verbose=False):
     os.makedirs(OBJ, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", h)
                                                        for h in ("mfp.h", "mercury_amd_libmerc.h")]
-    objs = []
+    objs, procs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OBJ, s + ".o")
@@ -34,7 +34,10 @@ def build(verbose=False):
                    "-Wall", "-c", src, "-o", obj]
             if verbose:
                 print(" ".join(cmd))
-            subprocess.run(cmd, check=True)
+            procs.append((cmd, subprocess.Popen(cmd)))   # objects are independent: compile in parallel
+    for cmd, p in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     if _newer(LIB, objs):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lz"]
         if verbose:

@@ -79,6 +79,11 @@ def load_library():
     lib.mfp_normalize_server_name.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
     lib.mfp_parse_filter.restype = ctypes.c_int
     lib.mfp_parse_filter.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    lib.mfp_profile_enable.restype = ctypes.c_int
+    lib.mfp_profile_enable.argtypes = [vp, ctypes.c_int]
+    lib.mfp_profile_read.restype = ctypes.c_int
+    lib.mfp_profile_read.argtypes = [vp, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_double)]
     _lib = lib
     return lib
 
@@ -164,6 +169,26 @@ class Context:
         if self.lib.mfp_analysis_stats(self.h, out) != 0:
             raise MercuryAmdError(_err(self.lib))
         return list(out)
+
+    def profile(self, on=True):
+        """Bracket every kernel launch of this context with HIP events (resets the totals)."""
+        if self.lib.mfp_profile_enable(self.h, 1 if on else 0) != 0:
+            raise MercuryAmdError(_err(self.lib))
+
+    def profile_read(self):
+        """{kernel name: (launches, total ms)} since profile(True), in first-launch order."""
+        out = {}
+        name = ctypes.create_string_buffer(64)
+        cnt, ms = ctypes.c_uint64(0), ctypes.c_double(0.0)
+        i = 0
+        while True:
+            r = self.lib.mfp_profile_read(self.h, i, name, 64, ctypes.byref(cnt), ctypes.byref(ms))
+            if r == 1:
+                return out
+            if r != 0:
+                raise MercuryAmdError(_err(self.lib))
+            out[name.value.decode()] = (int(cnt.value), float(ms.value))
+            i += 1
 
     def process_device(self, d_arena, d_desc, n, d_rec, d_fp, fp_cap, d_used, stream=0):
         """All arguments are device pointers (ints, e.g. torch data_ptr())."""

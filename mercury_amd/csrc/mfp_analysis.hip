@@ -30,6 +30,7 @@
 
 #include "mfp_analysis.h"
 #include "mfp_common.hpp"
+#include "mfp_internal.h"
 
 namespace mfpa {
 
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   unsigned long long *stats, uint32_t mode, hipStream_t stream) {
+                                   unsigned long long *stats, uint32_t mode, hipStream_t stream, mfp_prof *prof) {
     if (n == 0) return 0;
     mfpa::AParams P;
     P.D = *D;
@@ -405,8 +406,12 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *a
     P.stats = stats;
     uint64_t groups = (n + 63) / 64, blocks = (groups + 3) / 4;
     if (blocks > 2048) blocks = 2048;
+    if (prof) mfp_prof_begin(prof, "k_analyze", stream);
     hipLaunchKernelGGL(mfpa::k_analyze, dim3((uint32_t)blocks), dim3(256), 0, stream, P);
+    if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (prof) mfp_prof_begin(prof, "k_analyze_status", stream);
     hipLaunchKernelGGL(mfpa::k_analyze_status, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, P);
+    if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -22,13 +22,13 @@
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   unsigned long long *stats, uint32_t mode, hipStream_t stream);
+                                   unsigned long long *stats, uint32_t mode, hipStream_t stream, mfp_prof *prof);
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
-                                      hipStream_t stream);
+                                      hipStream_t stream, mfp_prof *prof);
 
 // fp-arena reservation granule of the wave kernel and its grid (mfp_kernels.hip)
 static const uint64_t kWaveChunk = 32 * 1024;
@@ -162,6 +162,56 @@ extern "C" MFP_EXPORT int mfp_parse_filter(const char *cfg, uint32_t *select, ui
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// per-kernel timing: HIP events recorded on the launch stream around every
+// kernel launch of a context (mfp_profile_enable); read back by name
+// ---------------------------------------------------------------------------
+struct mfp_prof {
+    struct Pending { const char *name; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    std::vector<std::string> names;                  // first-launch order
+    std::map<std::string, std::pair<uint64_t, double>> acc;   // launches, total ms
+
+    hipEvent_t get() {
+        hipEvent_t e = nullptr;
+        if (!pool.empty()) { e = pool.back(); pool.pop_back(); return e; }
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    int collect() {
+        int rc = 0;
+        for (auto &p : pending) {
+            float ms = 0.f;
+            if (hipEventSynchronize(p.b) != hipSuccess || hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) rc = -1;
+            auto it = acc.find(p.name);
+            if (it == acc.end()) { names.push_back(p.name); it = acc.emplace(p.name, std::make_pair(0ull, 0.0)).first; }
+            it->second.first++;
+            it->second.second += ms;
+            pool.push_back(p.a); pool.push_back(p.b);
+        }
+        pending.clear();
+        return rc;
+    }
+    void reset() { (void)collect(); acc.clear(); names.clear(); }
+    ~mfp_prof() {
+        (void)collect();
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+void mfp_prof_begin(mfp_prof *p, const char *kernel, hipStream_t s) {
+    hipEvent_t a = p->get();
+    (void)hipEventRecord(a, s);
+    p->pending.push_back({kernel, a, nullptr});
+}
+
+void mfp_prof_end(mfp_prof *p, hipStream_t s) {
+    hipEvent_t b = p->get();
+    (void)hipEventRecord(b, s);
+    p->pending.back().b = b;
+}
+
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
@@ -179,6 +229,7 @@ struct mfp_context_s {
     mfp_record *d_rec = nullptr; size_t cap_rec = 0;
     char *d_fp = nullptr; size_t cap_fp = 0;
     hipStream_t stream = nullptr;
+    mfp_prof *prof = nullptr;            // mfp_profile_enable
     std::mutex mu;
 };
 
@@ -244,6 +295,7 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (c->clf) mfp_classifier_free(c->clf);
     (void)hipFree(c->d_an_stats); (void)hipFree(c->d_an);
     (void)hipFree(c->d_used); (void)hipFree(c->d_bins); (void)hipFree(c->d_work); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
+    delete c->prof;
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -290,7 +342,7 @@ static int process_device_locked(mfp_context c, const uint8_t *d_arena, const mf
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(c->d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
-                               fp_cap, (unsigned long long *)d_fp_used, c->d_work, c->d_bins, c->strategy, c->bin_wave_mask, s) != 0) {
+                               fp_cap, (unsigned long long *)d_fp_used, c->d_work, c->d_bins, c->strategy, c->bin_wave_mask, s, c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
@@ -350,7 +402,7 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     D->batch++;                                   // stream order across batches (fingerprint_prevalence)
     HIPCHK(hipMemsetAsync(c->d_an_stats, 0, 4 * sizeof(unsigned long long), s));
     if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_an_stats, c->mode,
-                            s) != 0) {
+                            s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
@@ -402,5 +454,34 @@ extern "C" MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]) 
     if (!clf) return -1;
     mfp_classifier_stats(clf, out);
     mfp_classifier_free(clf);
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_profile_enable(mfp_context c, int on) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (on) {
+        if (!c->prof) c->prof = new mfp_prof;
+        c->prof->reset();
+    } else {
+        delete c->prof;
+        c->prof = nullptr;
+    }
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_profile_read(mfp_context c, uint32_t i, char *name, size_t cap, uint64_t *launches,
+                                           double *total_ms) {
+    if (!c || !c->prof) { mfp_set_error("profiling is not enabled"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (c->prof->collect() != 0) { mfp_set_error("event timing failed"); return -2; }
+    if (i >= c->prof->names.size()) return 1;
+    const std::string &k = c->prof->names[i];
+    if (name && cap) snprintf(name, cap, "%s", k.c_str());
+    const auto &v = c->prof->acc[k];
+    if (launches) *launches = v.first;
+    if (total_ms) *total_ms = v.second;
     return 0;
 }

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
 #include <string>
 
 #include "../../include/mfp.h"
@@ -13,3 +15,9 @@ int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t
 
 // kernel strategies of the fingerprint pass (mfp_kernels.hip)
 enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_WAVE = 1, MFP_STRATEGY_LANE = 2 };
+
+// per-kernel HIP-event timing (mfp_profile_enable): the launchers bracket
+// every launch with begin/end when `p` is non-null
+struct mfp_prof;
+void mfp_prof_begin(mfp_prof *p, const char *kernel, hipStream_t s);
+void mfp_prof_end(mfp_prof *p, hipStream_t s);

@@ -314,7 +314,13 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
-                                      hipStream_t stream) {
+                                      hipStream_t stream, mfp_prof *prof) {
+#define MFP_LAUNCH(name, ...)                                \
+    do {                                                     \
+        if (prof) mfp_prof_begin(prof, name, stream);        \
+        hipLaunchKernelGGL(__VA_ARGS__);                     \
+        if (prof) mfp_prof_end(prof, stream);                \
+    } while (0)
     if (n == 0) return 0;
     size_t shmem = tls_format ? (size_t)mfp::MAX_LDS_EXT * mfp::TILE * 6 : 0;
     mfp::KParams P;
@@ -324,7 +330,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     P.idx = nullptr; P.count = nullptr;
     const uint64_t tiles = (n + mfp::TILE - 1) / mfp::TILE;
     if (strategy == MFP_STRATEGY_LANE) {
-        hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)tiles), dim3(mfp::TILE), shmem, stream, P);
+        MFP_LAUNCH("k_fingerprint", mfp::k_fingerprint, dim3((uint32_t)tiles), dim3(mfp::TILE), shmem, stream, P);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     mfpw::WParams W;
@@ -337,22 +343,26 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
         // classify, then one launch per protocol bin: the lane-per-packet
         // walker or the wave-per-packet walker, whichever is faster for
         // that protocol (bin_wave_mask bit b = wave kernel for bin b)
-        hipLaunchKernelGGL(mfp::k_classify, dim3((uint32_t)tiles), dim3(mfp::TILE), 0, stream, P, work, n, bin_count);
+        MFP_LAUNCH("k_classify", mfp::k_classify, dim3((uint32_t)tiles), dim3(mfp::TILE), 0, stream, P, work, n, bin_count);
         if (hipGetLastError() != hipSuccess) return -1;
         uint64_t fblocks = tiles < 2048 ? tiles : 2048;
         uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
         if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
         bool any_wave = false;
         for (int b = 0; b < mfp::NBINS; b++) {
+            static const char *const wave_name[mfp::NBINS] = {"k_wave_fp/tls_ch", "k_wave_fp/http_req",
+                "k_wave_fp/tcp_syn", "k_wave_fp/http_resp", "k_wave_fp/other"};
+            static const char *const lane_name[mfp::NBINS] = {"k_fingerprint/tls_ch", "k_fingerprint/http_req",
+                "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other"};
             if (bin_wave_mask & (1u << b)) {
                 W.idx = work + (uint64_t)b * n;
                 W.count = bin_count + b;
-                hipLaunchKernelGGL(mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+                MFP_LAUNCH(wave_name[b], mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
                 any_wave = true;
             } else {
                 P.idx = work + (uint64_t)b * n;
                 P.count = bin_count + b;
-                hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
+                MFP_LAUNCH(lane_name[b], mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
             }
             if (hipGetLastError() != hipSuccess) return -1;
         }
@@ -361,18 +371,19 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
             P.idx = W.fallback;
             P.count = fp_used + 3;
             uint64_t fb = tiles < 1024 ? tiles : 1024;
-            hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fb), dim3(mfp::TILE), shmem, stream, P);
+            MFP_LAUNCH("k_fingerprint/fallback", mfp::k_fingerprint, dim3((uint32_t)fb), dim3(mfp::TILE), shmem, stream, P);
         }
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
     if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
-    hipLaunchKernelGGL(mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+    MFP_LAUNCH("k_wave_fp", mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
     if (hipGetLastError() != hipSuccess) return -1;
     // fallback lane over the packets the wave kernel handed back
     P.idx = work;
     P.count = fp_used + 3;
     uint64_t fblocks = tiles < 1024 ? tiles : 1024;
-    hipLaunchKernelGGL(mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
+    MFP_LAUNCH("k_fingerprint/fallback", mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#undef MFP_LAUNCH

@@ -357,10 +357,12 @@ def templates(seed, n_templates, workload="mixed"):
     return [make_template(rng, c) for c in classes], classes
 
 
-def batch(n, seed=0x5EED0003, workload="mixed", n_templates=4096, randomize=True, align=1):
-    """n packets drawn from a seeded template pool; returns (arena, desc)."""
+def batch(n, seed=0x5EED0003, workload="mixed", n_templates=4096, randomize=True, align=1, draw_seed=None):
+    """n packets drawn from a seeded template pool; returns (arena, desc).
+    `draw_seed` (default seed + 1) drives which templates are drawn and the
+    per-packet randomisation, so shards can share one template pool."""
     tpl, _ = templates(seed, n_templates, workload)
-    rng = np.random.default_rng(seed + 1)
+    rng = np.random.default_rng(seed + 1 if draw_seed is None else draw_seed)
     tid = rng.integers(0, len(tpl), n)
     lens = np.array([len(t) for t in tpl], dtype=np.int64)
     plen = lens[tid]
