@@ -33,6 +33,9 @@ struct mfp_feat_slot {
     uint32_t str_off, str_len;
 };
 
+// mfp_feat_slot::upd_cnt flag: the list repeats a process index, apply it in order
+#define MFP_UPD_SERIAL 0x80000000u
+
 struct mfp_update {     // class update (naive_bayes.hpp:21-41)
     uint32_t idx, pad;
     double value;

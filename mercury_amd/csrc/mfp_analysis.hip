@@ -118,7 +118,8 @@ ADEV uint32_t asn_v6(const mfp_classifier_dev &D, uint64_t xh, uint64_t xl) {
 
 // apply one feature's update list to the per-lane scores
 ADEV void apply(const mfp_classifier_dev &D, Hit h, double (&sc)[MAXP_CHUNKS], uint32_t lane) {
-    for (uint32_t u = 0; u < h.cnt; u++) {
+    const uint32_t cnt = h.cnt & ~MFP_UPD_SERIAL;   // applied in list order either way
+    for (uint32_t u = 0; u < cnt; u++) {
         const mfp_update up = D.upd[h.off + u];
         const uint32_t idx = rfl(up.idx);
         const double v = __hiloint2double((int)rfl((uint32_t)(__double_as_longlong(up.value) >> 32)),
@@ -129,6 +130,199 @@ ADEV void apply(const mfp_classifier_dev &D, Hit h, double (&sc)[MAXP_CHUNKS], u
     }
 }
 
+// ---------------------------------------------------------------------------
+// lane-serial helpers: one packet per lane (phase A of k_analyze)
+// ---------------------------------------------------------------------------
+// little-endian 8-byte word j of s[0, len) (bytes past len read as 0) from
+// aligned 8-byte loads; never reads the aligned word after the last byte
+ADEV uint64_t word_at(const uint8_t *s, uint32_t len, uint32_t j) {
+    const uintptr_t p = (uintptr_t)s + 8u * j;
+    const uint32_t rem = len - 8u * j;                 // >= 1
+    const uintptr_t a = p & ~(uintptr_t)7;
+    const uint32_t sh = (uint32_t)(p & 7) * 8u;
+    uint64_t w = *(const uint64_t *)a;
+    if (sh) {
+        w >>= sh;
+        if (p + (rem < 8 ? rem : 8) > a + 8) w |= *(const uint64_t *)(a + 8) << (64 - sh);
+    }
+    if (rem < 8) w &= (1ull << (8 * rem)) - 1;
+    return w;
+}
+
+// string-relative 8-byte words j0 .. j0+B-1 of s[0, len) (bytes past len read
+// as 0), from B+1 aligned 8-byte loads issued together: one memory round
+// trip per 8*B bytes; never reads an aligned word past the last byte
+template <int B>
+ADEV void load_words(const uint8_t *s, uint32_t len, uint32_t j0, uint64_t (&w)[B]) {
+    const uintptr_t base = (uintptr_t)s & ~(uintptr_t)7;
+    const uint32_t sh = (uint32_t)((uintptr_t)s & 7) * 8;
+    const uintptr_t end = (uintptr_t)s + len;
+    uint64_t a[B + 1];
+#pragma unroll
+    for (int k = 0; k <= B; k++) {
+        const uintptr_t p = base + 8 * (uintptr_t)(j0 + k);
+        a[k] = p < end ? *(const uint64_t *)p : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+        uint64_t x = sh ? (a[k] >> sh) | (a[k + 1] << (64 - sh)) : a[k];
+        const uint32_t pos = 8 * (j0 + k);
+        if (pos >= len) x = 0;
+        else if (len - pos < 8) x &= (1ull << (8 * (len - pos))) - 1;
+        w[k] = x;
+    }
+}
+constexpr int LB = 8;   // words per batch
+
+// mfpc::str_hash, one lane
+ADEV uint64_t lane_hash(const uint8_t *s, uint32_t len) {
+    uint64_t acc = 0;
+    for (uint32_t j0 = 0; 8 * j0 < len; j0 += LB) {
+        uint64_t w[LB];
+        load_words<LB>(s, len, j0, w);
+#pragma unroll
+        for (int k = 0; k < LB; k++)
+            if (8 * (j0 + k) < len) acc ^= word_term(w[k], j0 + k);
+    }
+    return hash_final(acc, len);
+}
+
+ADEV bool lane_eq(const uint8_t *a, const uint8_t *b, uint32_t len) {
+    for (uint32_t j0 = 0; 8 * j0 < len; j0 += LB) {
+        uint64_t x[LB], y[LB];
+        load_words<LB>(a, len, j0, x);
+        load_words<LB>(b, len, j0, y);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < LB; k++) same &= x[k] == y[k];
+        if (!same) return false;
+    }
+    return true;
+}
+
+// C-string view of s[0, n) (strncpy into the destination context stops at a
+// NUL): its length, and its str_hash
+ADEV uint32_t cstr_hash(const uint8_t *s, uint32_t n, uint64_t &h) {
+    uint64_t acc = 0;
+    for (uint32_t j0 = 0; 8 * j0 < n; j0 += LB) {
+        uint64_t w[LB];
+        load_words<LB>(s, n, j0, w);
+#pragma unroll
+        for (int k = 0; k < LB; k++) {
+            const uint32_t pos = 8 * (j0 + k);
+            if (pos < n) {
+                uint64_t v = w[k];
+                if (n - pos < 8) v |= ~0ull << (8 * (n - pos));   // bytes past n are not NUL
+                const uint64_t z = (v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull;
+                if (z) {   // a NUL inside: the C string is shorter (rare)
+                    const uint32_t m = pos + (uint32_t)(__builtin_ctzll(z) >> 3);
+                    h = lane_hash(s, m);
+                    return m;
+                }
+                acc ^= word_term(w[k], j0 + k);
+            }
+        }
+    }
+    h = hash_final(acc, n);
+    return n;
+}
+
+ADEV uint32_t probe_string_lane(const mfp_fp_slot *slots, uint64_t mask, const char *pool, const uint8_t *s,
+                                uint32_t len, uint64_t h) {
+    for (uint64_t k = h & mask;; k = (k + 1) & mask) {
+        const mfp_fp_slot sl = slots[k];
+        if (sl.id == 0xffffffffu) return 0xffffffffu;
+        if (sl.hash == h && sl.str_len == len && lane_eq(s, (const uint8_t *)pool + sl.str_off, len)) return sl.id;
+    }
+}
+
+// feature slot of (entry, kind, key); s/len: the string to verify (len ==
+// ~0u: integer key, nothing to verify)
+ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_t kind, uint64_t key,
+                            const uint8_t *s, uint32_t len) {
+    for (uint64_t k = feat_slot_hash(entry, kind, key) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
+        const mfp_feat_slot sl = D.feat_slots[k];
+        if (sl.entry == 0xffffffffu) return Hit{0, 0};
+        if (sl.entry == entry && sl.kind == kind && sl.key == key &&
+            (len == 0xffffffffu || (sl.str_len == len && lane_eq(s, (const uint8_t *)D.pool + sl.str_off, len))))
+            return Hit{sl.upd_off, sl.upd_cnt};
+    }
+}
+
+ADEV uint32_t asn_v4_lane(const mfp_classifier_dev &D, uint32_t addr_host) {
+    int lo = 0, hi = (int)D.n_asn4 - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const mfp_asn4 r = D.asn4[mid];
+        if (addr_host < r.lo) hi = mid - 1;
+        else if (addr_host > r.hi) lo = mid + 1;
+        else return r.asn;
+    }
+    return 0;
+}
+ADEV uint32_t asn_v6_lane(const mfp_classifier_dev &D, uint64_t xh, uint64_t xl) {
+    int lo = 0, hi = (int)D.n_asn6 - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const mfp_asn6 r = D.asn6[mid];
+        if (!le128(r.lo_hi, r.lo_lo, xh, xl)) hi = mid - 1;
+        else if (!le128(xh, xl, r.hi_hi, r.hi_lo)) lo = mid + 1;
+        else return r.asn;
+    }
+    return 0;
+}
+
+// A server name that server_identifier::get_normalized_domain_name leaves
+// unchanged (watchlist.hpp:326-390): 1..256 bytes of label characters and
+// dots, no empty label, at least two labels, the last one with a letter.
+// Such a name is no IPv6 literal (a dot ends the hex run), a dns_string
+// consuming every byte, neither "None" nor "localhost" and not unqualified,
+// so the normalized name is the input itself.  *tld: offset of the top two
+// labels (get_tld_domain_name, naive_bayes.hpp:557).  Anything else takes the
+// wave path (normalize_server_name, mfp_common.hpp).
+ADEV bool plain_server_name(const uint8_t *s, uint32_t n, uint32_t &tld, uint64_t &h) {
+    if (n == 0 || n > 256) return false;
+    int last_dot = -1, prev_dot = -1;
+    bool ok = true, alpha_last = false;
+    uint32_t prevc = '.';
+    uint64_t acc = 0;
+    for (uint32_t j0 = 0; 8 * j0 < n; j0 += LB) {
+        uint64_t w[LB];
+        load_words<LB>(s, n, j0, w);
+#pragma unroll
+        for (int q = 0; q < LB; q++) {
+            if (8 * (j0 + q) < n) acc ^= word_term(w[q], j0 + q);
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) {
+                const uint32_t k = 8 * (j0 + q) + b;
+                if (k < n) {
+                    const uint32_t c = (uint32_t)(w[q] >> (8 * b)) & 0xff;
+                    if (c == '.') {
+                        ok &= prevc != '.';
+                        prev_dot = last_dot;
+                        last_dot = (int)k;
+                        alpha_last = false;
+                    } else {
+                        ok &= is_label_char(c);
+                        alpha_last |= is_alpha(c);
+                    }
+                    prevc = c;
+                }
+            }
+        }
+    }
+    ok &= prevc != '.' && last_dot >= 0 && alpha_last;
+    tld = (uint32_t)(prev_dot + 1);
+    h = hash_final(acc, n);
+    return ok;
+}
+
+// a packet k_analyze hands to k_analyze_wave, with its feature lookups done
+struct Deferred {
+    uint32_t i, entry, slow_sni, pad;   // slow_sni: domain / SNI lookups still to do
+    uint32_t off[6], cnt[6];
+};
+
 struct AParams {
     mfp_classifier_dev D;
     const uint8_t *arena;
@@ -137,26 +331,43 @@ struct AParams {
     mfp_record *rec;
     const uint8_t *fp_arena;
     mfp_analysis *out;
+    uint32_t *pending;           // indices of unknown-TLS sightings (k_analyze_status)
+    struct Deferred *deferred;   // packets scored by k_analyze_wave
     uint32_t mode;
-    unsigned long long *stats;   // [0] analyzed, [1] pending unknown-TLS, [2] over-size P
+    uint32_t lane_max_p;         // phase L takes fingerprints with P <= min(lane_max_p, PL)
+    unsigned long long *stats;   // [0] analyzed, [1] pending unknown-TLS, [2] over-size P, [3] deferred
 };
 
-__global__ __launch_bounds__(256) void k_analyze(AParams P) {
-    __shared__ char sni_buf[4][336];
+constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.hpp:752-772 order
+
+// k_analyze, in two phases per group of 64 fingerprint records:
+//  A. lane per packet (64 packets in flight per wave): fingerprint hash,
+//     verified fingerprint-table lookup and status, destination context,
+//     ASN, server-name normalisation (plain names; the rest are marked for
+//     phase B) and the six feature-table lookups -> per lane: entry and six
+//     (update list offset, count) pairs;
+//  B. wave per scored packet: prior + update lists loaded lane-parallel,
+//     applied feature by feature as LDS scatters (one update per process per
+//     list, so a feature is one conflict-free scatter and each process sees
+//     the reference's addition order), max / second max, fp32 softmax, result.
+constexpr uint32_t PL = 32;       // phase L: fingerprints with at most PL processes, scored lane per packet
+constexpr int AW = 2;             // waves per k_analyze block (LDS: 16 KiB of score rows per wave)
+
+__global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
+    __shared__ double sc_lds[AW][64 * PL];   // per wave: phase L's lane-private score rows S[p][lane]
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
-    char *nbuf = sni_buf[wid];
+    double *scl = sc_lds[wid];
     const mfp_classifier_dev &D = P.D;
     const uint64_t ngroups = (P.n + 63) / 64;
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t g = (uint64_t)blockIdx.x * 4 + wid; g < ngroups; g += nw) {
+    const uint64_t nw = (uint64_t)gridDim.x * AW;
+    for (uint64_t g = (uint64_t)blockIdx.x * AW + wid; g < ngroups; g += nw) {
         const uint64_t i = g * 64 + lane;
         const bool live = i < P.n;
         mfp_record r;
         if (live) r = P.rec[i];
-        else { r.fp_len = 0; r.fp_type = 0; }
-        // default result: no information (analysis_result())
-        mfp_analysis a;
+        else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; }
+        mfp_analysis a;   // default: no information (analysis_result())
         a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.status = 0; a.flags = 0;
         // messages whose do_analysis calls the classifier: TLS ClientHello
         // (tls.h:1977), HTTP request (http.cc:571), SSH client KEXINIT
@@ -164,198 +375,226 @@ __global__ __launch_bounds__(256) void k_analyze(AParams P) {
         const bool typed = live && r.fp_len != 0 && (r.fp_type == 1 || r.fp_type == 3 || r.fp_type == 5);
         const bool analyzable = typed && ((D.types_mask >> r.fp_type) & 1u);
         if (typed && !analyzable) { a.status = 4; a.flags = MFP_AN_VALID; }   // fingerprint_status_unanalyzed
-        uint64_t todo = __ballot(analyzable);
-        while (todo) {
-            const int j = (int)__builtin_ctzll(todo);
-            todo &= todo - 1;
-            // ---- this packet's inputs, wave-uniform
-            const uint64_t fpo = ((uint64_t)rfl(__shfl((uint32_t)(r.fp_offset >> 32), j, 64)) << 32) |
-                                 rfl(__shfl((uint32_t)r.fp_offset, j, 64));
-            const uint32_t fl = rfl(__shfl(r.fp_len, j, 64));
-            const uint32_t ft = rfl(__shfl((uint32_t)r.fp_type, j, 64));
-            const uint32_t sni = rfl(__shfl((uint32_t)r.sni_off | ((uint32_t)r.sni_len << 16), j, 64));
-            const uint32_t ua = rfl(__shfl((uint32_t)r.ua_off | ((uint32_t)r.ua_len << 16), j, 64));
-            const uint32_t dport = rfl(__shfl((uint32_t)r.dst_port, j, 64));
-            const uint32_t net = rfl(__shfl(r.net, j, 64));
-            const uint64_t pidx = g * 64 + (uint64_t)j;
-            const mfp_pkt_desc dsc = P.desc[pidx];
-            const uint8_t *pkt = P.arena + dsc.offset;
-            const uint8_t *fp = P.fp_arena + fpo;
+        const uint64_t am = __ballot(analyzable);
+        if (!am) {
+            if (live) { P.out[i] = a; P.rec[i].status = a.status; }
+            continue;
+        }
+        if (lane == 0) atomicAdd(&P.stats[0], (unsigned long long)__builtin_popcountll(am));
 
-            // ---- 1. fingerprint lookup / status (perform_analysis_common)
-            uint32_t status = 0, entry = 0xffffffffu;
-            bool pending = false;
-            const uint64_t fh = wave_hash(fp, fl, lane);
-            entry = probe_string(D.fp_slots, D.fp_mask, D.pool, fp, fl, fh, lane);
+        // ================= phase A: lane per packet =================
+        uint32_t status = 0, entry = 0xffffffffu, np = 0, po = 0, mdb = 0, dmz = 0;
+        bool pending = false;
+        uint32_t hoff[NFEAT], hcnt[NFEAT];
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) { hoff[f] = 0; hcnt[f] = 0; }
+        if (analyzable) {
+            // ---- 1. fingerprint lookup / status (perform_analysis_common, analysis.h:1043-1083)
+            const uint8_t *fp = P.fp_arena + r.fp_offset;
+            const uint32_t fl = r.fp_len;
+            const uint64_t fh = lane_hash(fp, fl);
+            entry = probe_string_lane(D.fp_slots, D.fp_mask, D.pool, fp, fl, fh);
+            const uint64_t w0 = word_at(fp, fl, 0);
             if (entry != 0xffffffffu) {
-                status = 1;                                         // labeled
-            } else if (fl >= 4 && fp[0] == 't' && fp[1] == 'l' && fp[2] == 's' && fp[3] == '/') {
-                if (probe_string(D.prev_slots, D.prev_mask, D.pool, fp, fl, fh, lane) != 0xffffffffu) {
-                    status = 3;                                     // unlabeled (known set; no LRU update)
+                status = 1;                                                   // labeled
+            } else if (fl >= 4 && (uint32_t)w0 == 0x2f736c74u) {              // "tls/"
+                if (probe_string_lane(D.prev_slots, D.prev_mask, D.pool, fp, fl, fh) != 0xffffffffu) {
+                    status = 3;                    // unlabeled (known set; no LRU update)
                 } else {
                     // adaptive set: record the sighting; k_analyze_status decides
                     pending = true;
                     status = 2;
-                    if (lane == 0) {
-                        uint64_t k = fh & (D.seen_cap - 1);
-                        for (uint32_t t = 0; t < D.seen_cap; t++, k = (k + 1) & (D.seen_cap - 1)) {
-                            unsigned long long prev = atomicCAS(&D.seen[k].hash, ~0ull, (unsigned long long)fh);
-                            if (prev == ~0ull) atomicAdd(D.seen_count, 1ull);
-                            if (prev == ~0ull || prev == fh) {
-                                atomicMin(&D.seen[k].first, ((unsigned long long)D.batch << 32) | (uint32_t)pidx);
-                                break;
-                            }
+                    uint64_t k = fh & (D.seen_cap - 1);
+                    for (uint32_t t = 0; t < D.seen_cap; t++, k = (k + 1) & (D.seen_cap - 1)) {
+                        const unsigned long long prev = atomicCAS(&D.seen[k].hash, ~0ull, (unsigned long long)fh);
+                        if (prev == ~0ull) atomicAdd(D.seen_count, 1ull);
+                        if (prev == ~0ull || prev == fh) {
+                            atomicMin(&D.seen[k].first, ((unsigned long long)D.batch << 32) | (uint32_t)i);
+                            break;
                         }
                     }
                     // classify with "<prefix>randomized" when the DB has it
-                    const uint32_t pre = fl > 5 && fp[4] == '1' && fp[5] == '/' ? 1u : fl > 5 && fp[4] == '2' && fp[5] == '/' ? 2u : 0u;
+                    const uint32_t c4 = (uint32_t)(w0 >> 32) & 0xff, c5 = (uint32_t)(w0 >> 40) & 0xff;
+                    const uint32_t pre = fl > 5 && c5 == '/' ? (c4 == '1' ? 1u : c4 == '2' ? 2u : 0u) : 0u;
                     entry = D.randomized_entry[pre];
                 }
             } else {
-                status = 3;                                         // unlabeled
+                status = 3;                                                   // unlabeled
             }
-            mfp_analysis res;
-            res.score = 0.0; res.malware_prob = -1.0; res.process = MFP_NO_PROCESS; res.attr = 0;
-            res.status = (uint8_t)status; res.flags = MFP_AN_VALID | (pending ? MFP_AN_PENDING : 0);
-            if (entry != 0xffffffffu) {
-                const mfp_entry E = D.entry[entry];
-                const uint32_t np = rfl(E.nproc), po = rfl(E.proc_off), mdb = rfl(E.malware_db), dmz = rfl(E.generic_dmz);
-                if (np > 64 * MAXP_CHUNKS) {
-                    if (lane == 0) atomicAdd(&P.stats[2], 1ull);
-                } else {
-                    // ---- 2. destination context
-                    uint32_t ipv = (net >> 16) & 15, ipo = net & 0xffff;
-                    uint32_t v4 = 0, asn = 0;
-                    uint8_t v6[16];
-                    uint64_t v6h = 0, v6l = 0;
-                    if (ipv == 4) {
-                        const uint8_t *d = pkt + ipo + 16;
-                        v4 = (uint32_t)d[0] | (uint32_t)d[1] << 8 | (uint32_t)d[2] << 16 | (uint32_t)d[3] << 24;
-                        asn = asn_v4(D, (uint32_t)d[0] << 24 | (uint32_t)d[1] << 16 | (uint32_t)d[2] << 8 | d[3]);
-                    } else if (ipv == 6) {
-                        const uint8_t *d = pkt + ipo + 24;
-                        for (int k = 0; k < 16; k++) v6[k] = d[k];
-                        for (int k = 0; k < 8; k++) { v6h = v6h << 8 | v6[k]; v6l = v6l << 8 | v6[k + 8]; }
-                        if (D.n_asn6) asn = asn_v6(D, v6h, v6l);
-                    }
-                    // server name: TLS SNI, HTTP Host (strncpy 256, NUL stops)
-                    const uint32_t sl = (sni >> 16) == 0xffff ? 0 : (sni >> 16);
-                    const uint8_t *sp = pkt + (sni & 0xffff);
-                    int nlen = 0;
-                    if (lane == 0) nlen = normalize_server_name(sp, (int)sl, nbuf);
-                    nlen = (int)rfl((uint32_t)nlen);
-                    __builtin_amdgcn_wave_barrier();
-                    const int tld = (int)rfl((uint32_t)(lane == 0 ? tld_domain_offset(nbuf, nlen) : 0));
-                    // user agent (strncpy 511, NUL stops); TLS has none
-                    uint32_t ul = (ua >> 16) == 0xffff ? 0 : (ua >> 16);
-                    const uint8_t *up = pkt + (ua & 0xffff);
-                    if (ul > 511) ul = 511;
-                    {
-                        uint32_t z = 0xffffffffu;
-                        for (uint32_t k = lane; k < ul; k += 64) if (up[k] == 0 && k < z) z = k;
-                        for (int d = 32; d >= 1; d >>= 1) z = min(z, (uint32_t)__shfl_xor((int)z, d, 64));
-                        z = rfl(z);
-                        if (z < ul) ul = z;
-                    }
+        }
+        {   // queue unknown-TLS sightings for k_analyze_status
+            const uint64_t pm = __ballot(pending);
+            if (pm) {
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(&P.stats[1], (unsigned long long)__builtin_popcountll(pm));
+                base = rfl64(base);
+                if (pending) P.pending[base + __builtin_popcountll(pm & ((1ull << lane) - 1))] = (uint32_t)i;
+            }
+        }
+        bool scored = analyzable && entry != 0xffffffffu;
+        if (scored) {
+            const mfp_entry E = D.entry[entry];
+            np = E.nproc; po = E.proc_off; mdb = E.malware_db; dmz = E.generic_dmz;
+            if (np > 64 * MAXP_CHUNKS) {
+                atomicAdd(&P.stats[2], 1ull);
+                scored = false;
+            }
+        }
+        bool plain = false;
+        if (scored) {
+            // ---- 2. destination context (destination_context::init, result.h:346)
+            const uint8_t *pkt = P.arena + P.desc[i].offset;
+            const uint32_t ipv = (r.net >> 16) & 15, ipo = r.net & 0xffff;
+            uint32_t asn = 0;
+            uint64_t ipkey = 0, v6w0 = 0, v6w1 = 0;
+            if (ipv == 4) {
+                const uint32_t v4 = (uint32_t)word_at(pkt + ipo + 16, 4, 0);   // network order, as bytes
+                asn = asn_v4_lane(D, __builtin_bswap32(v4));
+                ipkey = normalize_ipv4(v4);
+            } else if (ipv == 6) {
+                v6w0 = word_at(pkt + ipo + 24, 16, 0);
+                v6w1 = word_at(pkt + ipo + 24, 16, 1);
+                if (D.n_asn6) asn = asn_v6_lane(D, __builtin_bswap64(v6w0), __builtin_bswap64(v6w1));
+                // normalize_ipv6 (mfp_common.hpp) on the two words
+                const bool gu = (v6w0 & 0xe0) == 0x20;
+                const bool mapped = v6w0 == 0 && (v6w1 & 0xffffffffull) == 0xffff0000ull;
+                if (!(gu || mapped)) { v6w0 = 0xfd; v6w1 = 1ull << 56; }
+                ipkey = hash_final(word_term(v6w0, 0) ^ word_term(v6w1, 1), 16);
+            }
+            // server name: TLS SNI / HTTP Host (strncpy 256, NUL stops)
+            const uint32_t sl = r.sni_len == 0xffff ? 0u : r.sni_len;
+            const uint8_t *sp = pkt + r.sni_off;
+            uint32_t tld = 0;
+            uint64_t nh = 0;
+            plain = plain_server_name(sp, sl, tld, nh);   // no NUL in a plain name
+            // user agent (strncpy 511, NUL stops); TLS has none
+            uint32_t ul = r.ua_len == 0xffff ? 0u : r.ua_len;
+            if (ul > 511) ul = 511;
+            const uint8_t *up = pkt + r.ua_off;
+            uint64_t uh = 0;
+            ul = cstr_hash(up, ul, uh);
+            const uint32_t dport = r.dst_port;
 
-                    // ---- 3. scores (lane i = process i)
-                    double sc[MAXP_CHUNKS];
-#pragma unroll
-                    for (int c = 0; c < MAXP_CHUNKS; c++) {
-                        const uint32_t pi = (uint32_t)c * 64 + lane;
-                        sc[c] = pi < np ? D.prior[po + pi] : 0.0;
-                    }
-                    apply(D, probe_feature(D, entry, F_ASN, asn, nullptr, 0, false, lane), sc, lane);
-                    apply(D, probe_feature(D, entry, F_PORT, dport, nullptr, 0, false, lane), sc, lane);
-                    if (ipv == 4) {
-                        apply(D, probe_feature(D, entry, F_IPV4, normalize_ipv4(v4), nullptr, 0, false, lane), sc, lane);
-                    } else if (ipv == 6) {
-                        normalize_ipv6(v6);
-                        uint64_t k6 = str_hash(v6, 16);
-                        apply(D, probe_feature(D, entry, F_IPV6, k6, v6, 16, true, lane), sc, lane);
-                    }
-                    apply(D, probe_feature(D, entry, F_UA, wave_hash(up, ul, lane), up, ul, true, lane), sc, lane);
-                    const uint8_t *dom = (const uint8_t *)nbuf + tld;
-                    apply(D, probe_feature(D, entry, F_DOMAIN, wave_hash(dom, (uint32_t)(nlen - tld), lane), dom,
-                                           (uint32_t)(nlen - tld), true, lane), sc, lane);
-                    apply(D, probe_feature(D, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
-                                           (const uint8_t *)nbuf, (uint32_t)nlen, true, lane), sc, lane);
-
-                    // ---- 4. max / second max (sequential first-index rule)
-                    double mx = -1.7976931348623157e308;
-                    uint32_t imx = 0xffffffffu;
-#pragma unroll
-                    for (int c = 0; c < MAXP_CHUNKS; c++) {
-                        const uint32_t pi = (uint32_t)c * 64 + lane;
-                        if (pi < np && (imx == 0xffffffffu || sc[c] > mx)) { mx = sc[c]; imx = pi; }
-                    }
-                    for (int d = 32; d >= 1; d >>= 1) {
-                        double om = __shfl_xor(mx, d, 64);
-                        uint32_t oi = (uint32_t)__shfl_xor((int)imx, d, 64);
-                        if (oi != 0xffffffffu && (imx == 0xffffffffu || om > mx || (om == mx && oi < imx))) { mx = om; imx = oi; }
-                    }
-                    imx = rfl(imx);
-                    mx = __hiloint2double((int)rfl((uint32_t)(__double_as_longlong(mx) >> 32)),
-                                          (int)rfl((uint32_t)__double_as_longlong(mx)));
-                    double sx = -1.7976931348623157e308;
-                    uint32_t isx = 0xffffffffu;
-#pragma unroll
-                    for (int c = 0; c < MAXP_CHUNKS; c++) {
-                        const uint32_t pi = (uint32_t)c * 64 + lane;
-                        if (pi < np && pi != imx && (isx == 0xffffffffu || sc[c] > sx)) { sx = sc[c]; isx = pi; }
-                    }
-                    for (int d = 32; d >= 1; d >>= 1) {
-                        double om = __shfl_xor(sx, d, 64);
-                        uint32_t oi = (uint32_t)__shfl_xor((int)isx, d, 64);
-                        if (oi != 0xffffffffu && (isx == 0xffffffffu || om > sx || (om == sx && oi < isx))) { sx = om; isx = oi; }
-                    }
-                    isx = rfl(isx);
-                    if (isx == 0xffffffffu) isx = 0;   // P == 1: index_sec stays 0
-
-                    // ---- softmax (expf in fp32, stored as double), sums
-                    double ssum = 0.0, swo = 0.0, mal = 0.0, p_imx = 0.0, p_isx = 0.0;
-#pragma unroll
-                    for (int c = 0; c < MAXP_CHUNKS; c++) {
-                        const uint32_t pi = (uint32_t)c * 64 + lane;
-                        if (pi < np) {
-                            const double p = (double)expf((float)(sc[c] - mx));
-                            ssum += p;
-                            if (pi != imx) swo += p;
-                            if (D.proc_mal[po + pi]) mal += p;
-                            if (pi == imx) p_imx = p;
-                            if (pi == isx) p_isx = p;
+            // ---- 3. the six feature lookups
+            Hit h;
+            h = probe_feature_lane(D, entry, F_ASN, asn, nullptr, 0xffffffffu);
+            hoff[0] = h.off; hcnt[0] = h.cnt;
+            h = probe_feature_lane(D, entry, F_PORT, dport, nullptr, 0xffffffffu);
+            hoff[1] = h.off; hcnt[1] = h.cnt;
+            if (ipv == 4) {
+                h = probe_feature_lane(D, entry, F_IPV4, ipkey, nullptr, 0xffffffffu);
+                hoff[2] = h.off; hcnt[2] = h.cnt;
+            } else if (ipv == 6) {
+                // the 16 normalized bytes, verified against the pool
+                for (uint64_t k = feat_slot_hash(entry, F_IPV6, ipkey) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
+                    const mfp_feat_slot s6 = D.feat_slots[k];
+                    if (s6.entry == 0xffffffffu) break;
+                    if (s6.entry == entry && s6.kind == F_IPV6 && s6.key == ipkey && s6.str_len == 16) {
+                        const uint8_t *ps = (const uint8_t *)D.pool + s6.str_off;
+                        if (word_at(ps, 16, 0) == v6w0 && word_at(ps, 16, 1) == v6w1) {
+                            hoff[2] = s6.upd_off; hcnt[2] = s6.upd_cnt;
+                            break;
                         }
                     }
-                    ssum = sum_all(ssum); swo = sum_all(swo); mal = sum_all(mal);
-                    p_imx = sum_all(p_imx); p_isx = sum_all(p_isx);
-                    double max_score = p_imx, sec_score = p_isx;
-                    if (ssum > 0.0 && mdb) mal /= ssum;
-                    uint32_t ibest = imx;
-                    if (mdb && dmz == imx && !D.proc_mal[po + isx]) {
-                        ibest = isx;
-                        ssum = swo;
-                        max_score = sec_score;
-                    }
-                    if (ssum > 0.0) max_score /= ssum;
-                    res.score = max_score;
-                    res.process = D.proc_id[po + ibest];
-                    res.attr = (uint16_t)D.proc_attr[po + ibest];
-                    if (mdb) {
-                        res.malware_prob = mal;
-                        res.flags |= MFP_AN_CLASSIFY_MALWARE;
-                        if (D.proc_mal[po + ibest]) res.flags |= MFP_AN_MALWARE;
-                    }
-                    // encrypted_channel (analysis.h:1161-1163)
-                    if ((res.flags & MFP_AN_MALWARE) && ft == 1) res.attr |= (uint16_t)(1u << D.enc_channel_idx);
                 }
             }
+            h = probe_feature_lane(D, entry, F_UA, uh, up, ul);
+            hoff[3] = h.off; hcnt[3] = h.cnt;
+            if (plain) {   // else k_analyze_wave normalises the name (wave, LDS)
+                h = probe_feature_lane(D, entry, F_DOMAIN, lane_hash(sp + tld, sl - tld), sp + tld, sl - tld);
+                hoff[4] = h.off; hcnt[4] = h.cnt;
+                h = probe_feature_lane(D, entry, F_SNI, nh, sp, sl);
+                hoff[5] = h.off; hcnt[5] = h.cnt;
+            }
+        }
+
+        // ================= phase L: lane per packet, P <= PL =================
+        // the reference's own sequential loops (naive_bayes.hpp:752-772,
+        // compute_score_and_probability analysis.h:222-277, softmax
+        // softmax.hpp:227-264) on lane-private LDS rows
+        const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain;
+        if (lanep) {
+            double *S = scl + lane;                    // S[p * 64]
+            for (uint32_t p = 0; p < np; p++) S[p * 64] = D.prior[po + p];
+#pragma unroll
+            for (uint32_t f = 0; f < NFEAT; f++) {
+                const uint32_t c = hcnt[f] & ~MFP_UPD_SERIAL;
+                const mfp_update *ul = D.upd + hoff[f];
+                uint32_t k = 0;
+                for (; k + 4 <= c; k += 4) {
+                    const mfp_update x0 = ul[k], x1 = ul[k + 1], x2 = ul[k + 2], x3 = ul[k + 3];
+                    S[x0.idx * 64] += x0.value;
+                    S[x1.idx * 64] += x1.value;
+                    S[x2.idx * 64] += x2.value;
+                    S[x3.idx * 64] += x3.value;
+                }
+                for (; k < c; k++) { const mfp_update x = ul[k]; S[x.idx * 64] += x.value; }
+            }
+            double mx = -1.7976931348623157e308, sx = -1.7976931348623157e308;
+            uint32_t imx = 0, isx = 0;
+            for (uint32_t p = 0; p < np; p++) {
+                const double v = S[p * 64];
+                if (v > mx) { sx = mx; isx = imx; mx = v; imx = p; }
+                else if (v > sx) { sx = v; isx = p; }
+            }
+            double ssum = 0.0, swo = 0.0, mal = 0.0, p_imx = 0.0, p_isx = 0.0;
+            for (uint32_t p = 0; p < np; p++) {
+                const double e = (double)expf((float)(S[p * 64] - mx));
+                ssum += e;
+                if (p != imx) swo += e;
+                if (D.proc_mal[po + p]) mal += e;
+                if (p == imx) p_imx = e;
+                if (p == isx) p_isx = e;
+            }
+            double max_score = p_imx;
+            if (ssum > 0.0 && mdb) mal /= ssum;
+            uint32_t ibest = imx;
+            if (mdb && dmz == imx && !D.proc_mal[po + isx]) {
+                ibest = isx;
+                ssum = swo;
+                max_score = p_isx;
+            }
+            if (ssum > 0.0) max_score /= ssum;
+            a.score = max_score;
+            a.process = D.proc_id[po + ibest];
+            a.attr = (uint16_t)D.proc_attr[po + ibest];
+            a.malware_prob = -1.0;
+            a.flags = MFP_AN_VALID;
+            if (mdb) {
+                a.malware_prob = mal;
+                a.flags |= MFP_AN_CLASSIFY_MALWARE;
+                if (D.proc_mal[po + ibest]) a.flags |= MFP_AN_MALWARE;
+            }
+            if ((a.flags & MFP_AN_MALWARE) && r.fp_type == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+
+        // ================= the rest: queued for k_analyze_wave =================
+        {
+            const bool defer = scored && !lanep;
+            const uint64_t dm = __ballot(defer);
+            if (dm) {
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(&P.stats[3], (unsigned long long)__builtin_popcountll(dm));
+                base = rfl64(base);
+                if (defer) {
+                    Deferred &d = P.deferred[base + __builtin_popcountll(dm & ((1ull << lane) - 1))];
+                    d.i = (uint32_t)i; d.entry = entry; d.slow_sni = plain ? 0u : 1u; d.pad = 0;
+#pragma unroll
+                    for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
+                }
+            }
+        }
+        if (analyzable) {
+            if (!lanep) {   // no process distribution (yet: k_analyze_wave scores the deferred ones)
+                a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.flags = MFP_AN_VALID;
+            }
+            a.status = (uint8_t)status;
+            if (pending) a.flags |= MFP_AN_PENDING;
             // analyze_ip_packet: a truncated message reports "unlabeled" and
             // keeps its classification (pkt_proc.cc:1716-1719)
-            const uint32_t rflags = rfl(__shfl((uint32_t)r.flags, j, 64));
-            if (P.mode == MFP_MODE_ANALYSIS && (rflags & MFP_FLAG_TRUNCATED) && !pending) res.status = 3;
-            if (lane == 0) atomicAdd(&P.stats[0], 1ull);
-            if (pending && lane == 0) atomicAdd(&P.stats[1], 1ull);
-            if (lane == (uint32_t)j) a = res;
+            if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED) && !pending) a.status = 3;
         }
         if (live) {
             P.out[i] = a;
@@ -364,54 +603,237 @@ __global__ __launch_bounds__(256) void k_analyze(AParams P) {
     }
 }
 
-// k_analyze_status: unknown TLS fingerprints -- the first sighting in stream
-// order is "randomized" (classified with the randomized entry, if any),
-// every later one "unlabeled" (no process)
-__global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= P.n) return;
-    mfp_analysis a = P.out[i];
-    if (!(a.flags & MFP_AN_PENDING)) return;
-    const mfp_record r = P.rec[i];
-    const uint8_t *fp = P.fp_arena + r.fp_offset;
-    const uint64_t h = str_hash(fp, r.fp_len);
+// k_analyze_wave: the packets k_analyze deferred (more than PL processes, or a
+// server name that needs the full normalisation) -- one wavefront per packet,
+// lane i holds process i (up to 64 * MAXP_CHUNKS processes).  Scores live in
+// LDS: the prior and the first 64 updates of every list are loaded in one
+// round trip, then the lists are applied feature by feature as lane-parallel
+// scatters (a list names each process at most once, so every process sees the
+// reference's addition order; lists flagged MFP_UPD_SERIAL go one by one).
+__global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
+    __shared__ char sni_buf[4][336];
+    __shared__ double sc_lds[4][64 * MAXP_CHUNKS];
+    const uint32_t lane = lane_id();
+    const int wid = (int)rfl(threadIdx.x >> 6);
+    char *nbuf = sni_buf[wid];
+    double *scl = sc_lds[wid];
     const mfp_classifier_dev &D = P.D;
-    uint64_t k = h & (D.seen_cap - 1);
-    bool first = false;
-    for (uint32_t t = 0; t < D.seen_cap; t++, k = (k + 1) & (D.seen_cap - 1)) {
-        const unsigned long long sh = D.seen[k].hash;
-        if (sh == h) { first = D.seen[k].first == (((unsigned long long)D.batch << 32) | (uint32_t)i); break; }
-        if (sh == ~0ull) break;
+    const uint64_t total = P.stats[3];
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t q = (uint64_t)blockIdx.x * 4 + wid; q < total; q += nw) {
+        const Deferred &dq = P.deferred[q];
+        const uint32_t i = rfl(dq.i), entry = rfl(dq.entry), slow = rfl(dq.slow_sni);
+        uint32_t off[NFEAT], cnt[NFEAT];
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) { off[f] = rfl(dq.off[f]); cnt[f] = rfl(dq.cnt[f]); }
+        const mfp_entry E = D.entry[entry];
+        const uint32_t np = rfl(E.nproc), po = rfl(E.proc_off), mdb = rfl(E.malware_db), dmz = rfl(E.generic_dmz);
+        const uint32_t ft = rfl((uint32_t)P.rec[i].fp_type);
+        if (slow) {
+            // server name: full normalisation on lane 0 into LDS, hashed and
+            // verified lane-parallel (strncpy 256, NUL stops)
+            const mfp_record r = P.rec[i];
+            const uint32_t sni = rfl((uint32_t)r.sni_off | ((uint32_t)r.sni_len << 16));
+            const uint32_t sl = (sni >> 16) == 0xffff ? 0 : (sni >> 16);
+            const uint8_t *sp = P.arena + P.desc[i].offset + (sni & 0xffff);
+            int nlen = 0;
+            if (lane == 0) nlen = normalize_server_name(sp, (int)sl, nbuf);
+            nlen = (int)rfl((uint32_t)nlen);
+            __builtin_amdgcn_wave_barrier();
+            const int tld = (int)rfl((uint32_t)(lane == 0 ? tld_domain_offset(nbuf, nlen) : 0));
+            const uint8_t *dom = (const uint8_t *)nbuf + tld;
+            Hit h = probe_feature(D, entry, F_DOMAIN, wave_hash(dom, (uint32_t)(nlen - tld), lane), dom,
+                                  (uint32_t)(nlen - tld), true, lane);
+            off[4] = h.off; cnt[4] = h.cnt;
+            h = probe_feature(D, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
+                              (const uint8_t *)nbuf, (uint32_t)nlen, true, lane);
+            off[5] = h.off; cnt[5] = h.cnt;
+            __builtin_amdgcn_wave_barrier();
+        }
+        // ---- scores: prior, then the six features in the reference's order
+        uint32_t anylong = 0;
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) anylong |= (cnt[f] & ~MFP_UPD_SERIAL) > 64 ? 1u : 0u;
+        mfp_update u[NFEAT];
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) {
+            u[f].idx = 0; u[f].value = 0.0;
+            if (lane < (cnt[f] & ~MFP_UPD_SERIAL)) u[f] = D.upd[off[f] + lane];
+        }
+        uint32_t malbits = 0;
+#pragma unroll
+        for (int c = 0; c < MAXP_CHUNKS; c++) {
+            const uint32_t pi = (uint32_t)c * 64 + lane;
+            if ((uint32_t)c * 64 < np) {
+                scl[pi] = pi < np ? D.prior[po + pi] : 0.0;
+                if (pi < np && D.proc_mal[po + pi]) malbits |= 1u << c;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) {
+            const uint32_t c = cnt[f] & ~MFP_UPD_SERIAL;
+            if (cnt[f] & MFP_UPD_SERIAL) {
+                for (uint32_t k = 0; k < c; k++) {
+                    const mfp_update x = k < 64 && !anylong ? mfp_update{(uint32_t)__shfl((int)u[f].idx, (int)k, 64), 0,
+                                                                        __shfl(u[f].value, (int)k, 64)}
+                                                            : D.upd[off[f] + k];
+                    if (lane == 0) scl[x.idx] += x.value;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+            } else {
+                if (lane < c) scl[u[f].idx] += u[f].value;
+                for (uint32_t b = 64; b < c; b += 64) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    if (b + lane < c) { const mfp_update x = D.upd[off[f] + b + lane]; scl[x.idx] += x.value; }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        double sc[MAXP_CHUNKS];
+#pragma unroll
+        for (int c = 0; c < MAXP_CHUNKS; c++) sc[c] = (uint32_t)c * 64 < np ? scl[c * 64 + lane] : 0.0;
+        __builtin_amdgcn_wave_barrier();
+
+        // ---- max / second max (sequential first-index rule)
+        double mx = -1.7976931348623157e308;
+        uint32_t imx = 0xffffffffu;
+#pragma unroll
+        for (int c = 0; c < MAXP_CHUNKS; c++) {
+            const uint32_t pi = (uint32_t)c * 64 + lane;
+            if (pi < np && (imx == 0xffffffffu || sc[c] > mx)) { mx = sc[c]; imx = pi; }
+        }
+        for (int d = 32; d >= 1; d >>= 1) {
+            const double om = __shfl_xor(mx, d, 64);
+            const uint32_t oi = (uint32_t)__shfl_xor((int)imx, d, 64);
+            if (oi != 0xffffffffu && (imx == 0xffffffffu || om > mx || (om == mx && oi < imx))) { mx = om; imx = oi; }
+        }
+        imx = rfl(imx);
+        mx = __hiloint2double((int)rfl((uint32_t)(__double_as_longlong(mx) >> 32)),
+                              (int)rfl((uint32_t)__double_as_longlong(mx)));
+        double sx = -1.7976931348623157e308;
+        uint32_t isx = 0xffffffffu;
+#pragma unroll
+        for (int c = 0; c < MAXP_CHUNKS; c++) {
+            const uint32_t pi = (uint32_t)c * 64 + lane;
+            if (pi < np && pi != imx && (isx == 0xffffffffu || sc[c] > sx)) { sx = sc[c]; isx = pi; }
+        }
+        for (int d = 32; d >= 1; d >>= 1) {
+            const double om = __shfl_xor(sx, d, 64);
+            const uint32_t oi = (uint32_t)__shfl_xor((int)isx, d, 64);
+            if (oi != 0xffffffffu && (isx == 0xffffffffu || om > sx || (om == sx && oi < isx))) { sx = om; isx = oi; }
+        }
+        isx = rfl(isx);
+        if (isx == 0xffffffffu) isx = 0;   // P == 1: index_sec stays 0
+
+        // ---- softmax (expf in fp32, stored as double), sums
+        double ssum = 0.0, swo = 0.0, mal = 0.0, p_imx = 0.0, p_isx = 0.0;
+#pragma unroll
+        for (int c = 0; c < MAXP_CHUNKS; c++) {
+            const uint32_t pi = (uint32_t)c * 64 + lane;
+            if (pi < np) {
+                const double p = (double)expf((float)(sc[c] - mx));
+                ssum += p;
+                if (pi != imx) swo += p;
+                if (malbits & (1u << c)) mal += p;
+                if (pi == imx) p_imx = p;
+                if (pi == isx) p_isx = p;
+            }
+        }
+        ssum = sum_all(ssum); swo = sum_all(swo); mal = sum_all(mal);
+        p_imx = sum_all(p_imx); p_isx = sum_all(p_isx);
+        double max_score = p_imx;
+        if (ssum > 0.0 && mdb) mal /= ssum;
+        uint32_t ibest = imx;
+        if (mdb && dmz == imx && !D.proc_mal[po + isx]) {
+            ibest = isx;
+            ssum = swo;
+            max_score = p_isx;
+        }
+        if (ssum > 0.0) max_score /= ssum;
+        if (lane == 0) {
+            mfp_analysis a = P.out[i];   // status and pending flag from k_analyze
+            a.score = max_score;
+            a.process = D.proc_id[po + ibest];
+            a.attr = (uint16_t)D.proc_attr[po + ibest];
+            a.malware_prob = -1.0;
+            a.flags = (uint8_t)(MFP_AN_VALID | (a.flags & MFP_AN_PENDING));
+            if (mdb) {
+                a.malware_prob = mal;
+                a.flags |= MFP_AN_CLASSIFY_MALWARE;
+                if (D.proc_mal[po + ibest]) a.flags |= MFP_AN_MALWARE;
+            }
+            // encrypted_channel (analysis.h:1161-1163)
+            if ((a.flags & MFP_AN_MALWARE) && ft == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
+            P.out[i] = a;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    a.flags &= (uint8_t)~MFP_AN_PENDING;
-    if (!first) {
-        a.status = 3;
-        a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0;
-        a.flags = MFP_AN_VALID;
+}
+
+// k_analyze_status: unknown TLS fingerprints (the sightings k_analyze queued)
+// -- the first sighting in stream order is "randomized" (classified with the
+// randomized entry, if any), every later one "unlabeled" (no process)
+__global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
+    const uint64_t cnt = P.stats[1];
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < cnt; q += (uint64_t)gridDim.x * 256) {
+        const uint32_t i = P.pending[q];
+        mfp_analysis a = P.out[i];
+        const mfp_record r = P.rec[i];
+        const uint8_t *fp = P.fp_arena + r.fp_offset;
+        const uint64_t h = lane_hash(fp, r.fp_len);
+        const mfp_classifier_dev &D = P.D;
+        uint64_t k = h & (D.seen_cap - 1);
+        bool first = false;
+        for (uint32_t t = 0; t < D.seen_cap; t++, k = (k + 1) & (D.seen_cap - 1)) {
+            const unsigned long long sh = D.seen[k].hash;
+            if (sh == h) { first = D.seen[k].first == (((unsigned long long)D.batch << 32) | i); break; }
+            if (sh == ~0ull) break;
+        }
+        a.flags &= (uint8_t)~MFP_AN_PENDING;
+        if (!first) {
+            a.status = 3;
+            a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0;
+            a.flags = MFP_AN_VALID;
+        }
+        if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
+        P.out[i] = a;
+        P.rec[i].status = a.status;
     }
-    if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
-    P.out[i] = a;
-    P.rec[i].status = a.status;
 }
 
 }  // namespace mfpa
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   unsigned long long *stats, uint32_t mode, hipStream_t stream, mfp_prof *prof) {
+                                   uint32_t *pending, void *deferred, unsigned long long *stats, uint32_t mode,
+                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof) {
     if (n == 0) return 0;
     mfpa::AParams P;
     P.D = *D;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = mode;
+    P.pending = pending;
+    P.deferred = (mfpa::Deferred *)deferred;
+    P.lane_max_p = lane_max_p;
     P.stats = stats;
-    uint64_t groups = (n + 63) / 64, blocks = (groups + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
+    uint64_t groups = (n + 63) / 64, blocks = (groups + mfpa::AW - 1) / mfpa::AW;
+    if (blocks > 4096) blocks = 4096;
     if (prof) mfp_prof_begin(prof, "k_analyze", stream);
-    hipLaunchKernelGGL(mfpa::k_analyze, dim3((uint32_t)blocks), dim3(256), 0, stream, P);
+    hipLaunchKernelGGL(mfpa::k_analyze, dim3((uint32_t)blocks), dim3(64 * mfpa::AW), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (prof) mfp_prof_begin(prof, "k_analyze_wave", stream);
+    hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(1024), dim3(256), 0, stream, P);
+    if (prof) mfp_prof_end(prof, stream);
+    if (hipGetLastError() != hipSuccess) return -1;
+    uint64_t sblocks = (n + 255) / 256;
+    if (sblocks > 1024) sblocks = 1024;
     if (prof) mfp_prof_begin(prof, "k_analyze_status", stream);
-    hipLaunchKernelGGL(mfpa::k_analyze_status, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, P);
+    hipLaunchKernelGGL(mfpa::k_analyze_status, dim3((uint32_t)sblocks), dim3(256), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -667,6 +667,15 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
         mfp_feat_slot s;
         s.key = key; s.entry = eid; s.kind = kind;
         s.upd_off = (uint32_t)t.upd.size(); s.upd_cnt = (uint32_t)lst.size();
+        // a list whose process indices are distinct can be applied as one
+        // lane-parallel scatter; repeated indices (e.g. two private IPv4
+        // addresses normalised to one key) keep the reference's serial order
+        {
+            std::vector<uint32_t> ix;
+            for (auto &u : lst) ix.push_back(u.idx);
+            std::sort(ix.begin(), ix.end());
+            if (std::adjacent_find(ix.begin(), ix.end()) != ix.end()) s.upd_cnt |= MFP_UPD_SERIAL;
+        }
         s.str_off = str ? pool_add(t, *str) : 0; s.str_len = str ? (uint32_t)str->size() : 0;
         for (auto &u : lst) t.upd.push_back(mfp_update{u.idx, 0, u.val});
         uint64_t mask = t.feat_slots.size() - 1;

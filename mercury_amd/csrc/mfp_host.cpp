@@ -22,7 +22,8 @@
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   unsigned long long *stats, uint32_t mode, hipStream_t stream, mfp_prof *prof);
+                                   uint32_t *pending, void *deferred, unsigned long long *stats, uint32_t mode,
+                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof);
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
@@ -217,12 +218,15 @@ struct mfp_context_s {
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|wave|lane (A/B, debugging)
     uint32_t bin_wave_mask = 0x2;        // bins fingerprinted by the wave kernel (MFP_BIN_WAVE_MASK)
+    uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
     unsigned long long *d_used = nullptr;
     unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass
     uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
     unsigned long long *d_an_stats = nullptr;
     mfp_analysis *d_an = nullptr; size_t cap_an = 0;
+    uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings of a batch
+    uint4 *d_deferred = nullptr; size_t cap_deferred = 0;    // packets for the wave-per-packet scorer (64 B each)
     // host-batch staging buffers (grown on demand)
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
@@ -260,6 +264,8 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     else if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
     const char *bm = getenv("MFP_BIN_WAVE_MASK");
     if (bm) c->bin_wave_mask = (uint32_t)strtoul(bm, nullptr, 0);
+    const char *lm = getenv("MFP_AN_LANE_MAX_P");
+    if (lm) c->an_lane_max_p = (uint32_t)strtoul(lm, nullptr, 0);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_used, 4 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_bins, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -293,7 +299,7 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->clf) mfp_classifier_free(c->clf);
-    (void)hipFree(c->d_an_stats); (void)hipFree(c->d_an);
+    (void)hipFree(c->d_an_stats); (void)hipFree(c->d_an); (void)hipFree(c->d_pending); (void)hipFree(c->d_deferred);
     (void)hipFree(c->d_used); (void)hipFree(c->d_bins); (void)hipFree(c->d_work); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
     delete c->prof;
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -398,11 +404,15 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     std::lock_guard<std::mutex> lk(c->mu);
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(c->device));
+    if (grow(c->d_pending, c->cap_pending, n + 1) || grow(c->d_deferred, c->cap_deferred, 4 * (n + 1))) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
     D->batch++;                                   // stream order across batches (fingerprint_prevalence)
     HIPCHK(hipMemsetAsync(c->d_an_stats, 0, 4 * sizeof(unsigned long long), s));
-    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_an_stats, c->mode,
-                            s, c->prof) != 0) {
+    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_pending,
+                            c->d_deferred, c->d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

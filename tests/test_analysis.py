@@ -143,7 +143,13 @@ def compare(ref, rec, an, names):
 
 
 @pytest.mark.gpu
-def test_analysis_synthetic_archive_vs_reference():
+@pytest.mark.parametrize("lane_max_p", [None, "0", "2"])
+def test_analysis_synthetic_archive_vs_reference(lane_max_p, monkeypatch):
+    """lane_max_p: MFP_AN_LANE_MAX_P -- None = default split (lane-per-packet
+    scoring for small P), "0" = every packet on the wave-per-packet scorer,
+    "2" = both kernels in one batch."""
+    if lane_max_p is not None:
+        monkeypatch.setenv("MFP_AN_LANE_MAX_P", lane_max_p)
     a, d = synth_batch()
     ref = load_ref_an("an_synth.tsv.gz")
     rec, fp, an, names, stats = run_analysis(a, d, "synth_resources.tgz")
