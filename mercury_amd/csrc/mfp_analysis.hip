@@ -331,7 +331,7 @@ struct AParams {
     mfp_record *rec;
     const uint8_t *fp_arena;
     mfp_analysis *out;
-    uint32_t *pending;           // indices of unknown-TLS sightings (k_analyze_status)
+    uint64_t *pend_bits;         // per group of 64 packets: unknown-TLS sightings (k_analyze_status)
     struct Deferred *deferred;   // packets scored by k_analyze_wave
     uint32_t mode;
     uint32_t lane_max_p;         // phase L takes fingerprints with P <= min(lane_max_p, PL)
@@ -361,6 +361,7 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
     const mfp_classifier_dev &D = P.D;
     const uint64_t ngroups = (P.n + 63) / 64;
     const uint64_t nw = (uint64_t)gridDim.x * AW;
+    uint32_t n_an = 0, n_pend = 0;   // per-wave counts, one atomic each at the end
     for (uint64_t g = (uint64_t)blockIdx.x * AW + wid; g < ngroups; g += nw) {
         const uint64_t i = g * 64 + lane;
         const bool live = i < P.n;
@@ -378,9 +379,10 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
         const uint64_t am = __ballot(analyzable);
         if (!am) {
             if (live) { P.out[i] = a; P.rec[i].status = a.status; }
+            if (lane == 0) P.pend_bits[g] = 0;
             continue;
         }
-        if (lane == 0) atomicAdd(&P.stats[0], (unsigned long long)__builtin_popcountll(am));
+        n_an += (uint32_t)__builtin_popcountll(am);
 
         // ================= phase A: lane per packet =================
         uint32_t status = 0, entry = 0xffffffffu, np = 0, po = 0, mdb = 0, dmz = 0;
@@ -422,14 +424,10 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
                 status = 3;                                                   // unlabeled
             }
         }
-        {   // queue unknown-TLS sightings for k_analyze_status
+        {   // unknown-TLS sightings of this group, for k_analyze_status
             const uint64_t pm = __ballot(pending);
-            if (pm) {
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(&P.stats[1], (unsigned long long)__builtin_popcountll(pm));
-                base = rfl64(base);
-                if (pending) P.pending[base + __builtin_popcountll(pm & ((1ull << lane) - 1))] = (uint32_t)i;
-            }
+            if (lane == 0) P.pend_bits[g] = pm;
+            n_pend += (uint32_t)__builtin_popcountll(pm);
         }
         bool scored = analyzable && entry != 0xffffffffu;
         if (scored) {
@@ -601,6 +599,8 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
             P.rec[i].status = a.status;
         }
     }
+    if (lane == 0 && n_an) atomicAdd(&P.stats[0], (unsigned long long)n_an);
+    if (lane == 0 && n_pend) atomicAdd(&P.stats[1], (unsigned long long)n_pend);
 }
 
 // k_analyze_wave: the packets k_analyze deferred (more than PL processes, or a
@@ -779,9 +779,10 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
 // -- the first sighting in stream order is "randomized" (classified with the
 // randomized entry, if any), every later one "unlabeled" (no process)
 __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
-    const uint64_t cnt = P.stats[1];
-    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < cnt; q += (uint64_t)gridDim.x * 256) {
-        const uint32_t i = P.pending[q];
+    const uint64_t ngroups = (P.n + 63) / 64;
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += (uint64_t)gridDim.x * 256) {
+    for (uint64_t w = P.pend_bits[g]; w; w &= w - 1) {
+        const uint32_t i = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(w));
         mfp_analysis a = P.out[i];
         const mfp_record r = P.rec[i];
         const uint8_t *fp = P.fp_arena + r.fp_offset;
@@ -804,6 +805,7 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
         P.out[i] = a;
         P.rec[i].status = a.status;
     }
+    }
 }
 
 }  // namespace mfpa
@@ -816,7 +818,7 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *a
     mfpa::AParams P;
     P.D = *D;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = mode;
-    P.pending = pending;
+    P.pend_bits = (uint64_t *)pending;
     P.deferred = (mfpa::Deferred *)deferred;
     P.lane_max_p = lane_max_p;
     P.stats = stats;
@@ -830,7 +832,7 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *a
     hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(1024), dim3(256), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
-    uint64_t sblocks = (n + 255) / 256;
+    uint64_t sblocks = (groups + 255) / 256;
     if (sblocks > 1024) sblocks = 1024;
     if (prof) mfp_prof_begin(prof, "k_analyze_status", stream);
     hipLaunchKernelGGL(mfpa::k_analyze_status, dim3((uint32_t)sblocks), dim3(256), 0, stream, P);

@@ -336,7 +336,7 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_work, c->cap_work, 6 * n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->d_work, c->cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     return 0;
 }
 
@@ -344,7 +344,7 @@ static int process_device_locked(mfp_context c, const uint8_t *d_arena, const mf
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
                                  hipStream_t s) {
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_work, c->cap_work, 6 * n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->d_work, c->cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(c->d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,

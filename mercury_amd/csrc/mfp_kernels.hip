@@ -146,30 +146,85 @@ DEV int msg_bin(uint32_t msg) {
 // k_classify: lane-per-packet link/IP/transport walk + protocol
 // identification only (proto_identify.h:936-968); appends each packet index
 // to its bin with one wave-aggregated atomic per non-empty bin
+// The walk runs on the first CLS_WIN bytes of each packet, staged in LDS with
+// nine independent 16-byte loads per lane (one memory round trip instead of a
+// dependent byte load per header field).  The bin only decides which kernel
+// walks the whole packet, and every bin's kernel handles any packet, so a
+// packet that needs more than the window to be identified is merely binned
+// less well, never fingerprinted differently.
+//
+// Persistent blocks, two phases, so that the bin counters see one atomic per
+// bin per BLOCK (same-address atomics serialise in one L2 channel): phase 1
+// classifies the block's tiles (bin id per packet to `cls`, counts in LDS),
+// then each non-empty bin reserves the block's span, and phase 2 re-reads the
+// bin ids and scatters the packet indices in tile order.
+constexpr int CLS_WIN = 128;
 __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, uint64_t bin_stride,
-                                                     unsigned long long *bin_count) {
-    const uint64_t i = (uint64_t)blockIdx.x * TILE + threadIdx.x;
-    const bool live = i < P.n;
-    int bin = -1;
-    if (live) {
-        mfp_pkt_desc dsc = P.desc[i];
-        Out o;
-        Em<false> e;
-        Cfg c = P.cfg;
-        c.classify = 1;
-        packet_walk(e, c, o, P.arena + dsc.offset, dsc.caplen, dsc.linktype, nullptr, nullptr, 0);
-        bin = msg_bin(o.msg);
-    }
-    const uint32_t lane = threadIdx.x & 63;
+                                                     unsigned long long *bin_count, uint8_t *cls) {
+    __shared__ uint4 win[TILE][CLS_WIN / 16 + 1];
+    __shared__ uint32_t blk_cnt[NBINS], run[NBINS];
+    __shared__ unsigned long long blk_base[NBINS];
+    __shared__ uint32_t wcnt[TILE / 64][NBINS];
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    if (tid < NBINS) { blk_cnt[tid] = 0; run[tid] = 0; }
+    __syncthreads();
+    for (uint64_t tile = blockIdx.x; tile * TILE < P.n; tile += gridDim.x) {
+        const uint64_t i = tile * TILE + tid;
+        int bin = -1;
+        if (i < P.n) {
+            const mfp_pkt_desc dsc = P.desc[i];
+            const uint8_t *pkt = P.arena + dsc.offset;
+            const uint32_t sh = (uint32_t)((uintptr_t)pkt & 15);
+            const uint32_t take = dsc.caplen < (uint32_t)CLS_WIN ? dsc.caplen : (uint32_t)CLS_WIN;
+            const uint32_t nch = (sh + take + 15) / 16;      // aligned blocks holding bytes [0, take)
+            const uint4 *src = (const uint4 *)((uintptr_t)pkt - sh);
+            uint4 v[CLS_WIN / 16 + 1];
 #pragma unroll
-    for (int b = 0; b < NBINS; b++) {
-        const uint64_t m = __ballot(bin == b);
-        if (!m) continue;
-        const int leader = (int)__builtin_ctzll(m);
-        unsigned long long base = 0;
-        if ((int)lane == leader) base = atomicAdd(&bin_count[b], (unsigned long long)__builtin_popcountll(m));
-        base = __shfl(base, leader, 64);
-        if (bin == b) bins[b * bin_stride + base + __builtin_popcountll(m & ((1ull << lane) - 1))] = (uint32_t)i;
+            for (int k = 0; k <= CLS_WIN / 16; k++) v[k] = (uint32_t)k < nch ? src[k] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k <= CLS_WIN / 16; k++) win[tid][k] = v[k];
+            Out o;
+            Em<false> e;
+            Cfg c = P.cfg;
+            c.classify = 1;
+            packet_walk(e, c, o, (const uint8_t *)&win[tid][0] + sh, take, dsc.linktype, nullptr, nullptr, 0);
+            bin = msg_bin(o.msg);
+            cls[i] = (uint8_t)bin;
+        }
+#pragma unroll
+        for (int b = 0; b < NBINS; b++) {
+            const uint64_t m = __ballot(bin == b);
+            if (m && lane == 0) atomicAdd(&blk_cnt[b], (uint32_t)__builtin_popcountll(m));
+        }
+    }
+    __syncthreads();
+    if (tid < NBINS) blk_base[tid] = blk_cnt[tid] ? atomicAdd(&bin_count[tid], (unsigned long long)blk_cnt[tid]) : 0ull;
+    __syncthreads();
+    for (uint64_t tile = blockIdx.x; tile * TILE < P.n; tile += gridDim.x) {
+        const uint64_t i = tile * TILE + tid;
+        const int bin = i < P.n ? (int)cls[i] : -1;
+        uint64_t mine = 0;
+#pragma unroll
+        for (int b = 0; b < NBINS; b++) {
+            const uint64_t m = __ballot(bin == b);
+            if (bin == b) mine = m;
+            if (lane == 0) wcnt[wid][b] = (uint32_t)__builtin_popcountll(m);
+        }
+        __syncthreads();
+        if (bin >= 0) {
+            uint32_t off = run[bin];
+            for (uint32_t w = 0; w < wid; w++) off += wcnt[w][bin];
+            off += (uint32_t)__builtin_popcountll(mine & ((1ull << lane) - 1));
+            bins[(uint64_t)bin * bin_stride + blk_base[bin] + off] = (uint32_t)i;
+        }
+        __syncthreads();
+        if (tid < NBINS) {
+            uint32_t t = 0;
+            for (int w = 0; w < TILE / 64; w++) t += wcnt[w][tid];
+            run[tid] += t;
+        }
+        __syncthreads();
     }
 }
 
@@ -343,7 +398,9 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
         // classify, then one launch per protocol bin: the lane-per-packet
         // walker or the wave-per-packet walker, whichever is faster for
         // that protocol (bin_wave_mask bit b = wave kernel for bin b)
-        MFP_LAUNCH("k_classify", mfp::k_classify, dim3((uint32_t)tiles), dim3(mfp::TILE), 0, stream, P, work, n, bin_count);
+        const uint64_t cblocks = tiles < 2048 ? tiles : 2048;
+        MFP_LAUNCH("k_classify", mfp::k_classify, dim3((uint32_t)cblocks), dim3(mfp::TILE), 0, stream, P, work, n, bin_count,
+                   (uint8_t *)(work + (uint64_t)(mfp::NBINS + 1) * n + 1));
         if (hipGetLastError() != hipSuccess) return -1;
         uint64_t fblocks = tiles < 2048 ? tiles : 2048;
         uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
