@@ -34,7 +34,8 @@ class MercuryAmdError(RuntimeError):
 
 
 def library_path():
-    return os.path.join(_HERE, "libmercury_amd.so")
+    # MFP_LIB: an alternative build of the same library (profiling variants)
+    return os.environ.get("MFP_LIB") or os.path.join(_HERE, "libmercury_amd.so")
 
 
 _lib = None

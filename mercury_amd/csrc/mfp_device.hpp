@@ -737,6 +737,55 @@ __constant__ HdrName k_resp_names[] = {
 };
 constexpr int N_RESP_NAMES = 49;
 
+// the same tables as lowercase names packed into four little-endian words
+// (zero past the name), for word-at-a-time lookups in the wave walker
+struct HdrKey { uint64_t w[4]; uint32_t len, info; };   // info: incl_value | capture << 8
+constexpr uint64_t pack_name(const char *s, int len, int k) {
+    uint64_t w = 0;
+    for (int i = 0; i < 8; i++)
+        if (8 * k + i < len) w |= (uint64_t)(uint8_t)s[8 * k + i] << (8 * i);
+    return w;
+}
+#define MFP_HK(len, incl, cap, str) \
+    HdrKey{{pack_name(str, len, 0), pack_name(str, len, 1), pack_name(str, len, 2), pack_name(str, len, 3)}, \
+           len, (incl) | ((cap) << 8)}
+__constant__ HdrKey k_req_keys[] = {
+    MFP_HK(6, 1, 0, "accept"), MFP_HK(15, 1, 0, "accept-encoding"), MFP_HK(10, 1, 0, "connection"),
+    MFP_HK(3, 1, 0, "dnt"), MFP_HK(3, 1, 0, "dpr"), MFP_HK(25, 1, 0, "upgrade-insecure-requests"),
+    MFP_HK(16, 1, 0, "x-requested-with"), MFP_HK(14, 0, 0, "accept-charset"), MFP_HK(15, 0, 0, "accept-language"),
+    MFP_HK(13, 0, 0, "authorization"), MFP_HK(13, 0, 0, "cache-control"), MFP_HK(4, 0, 1, "host"),
+    MFP_HK(17, 0, 0, "if-modified-since"), MFP_HK(10, 0, 0, "keep-alive"), MFP_HK(10, 0, 2, "user-agent"),
+    MFP_HK(15, 0, 0, "x-flash-version"), MFP_HK(14, 0, 0, "x-p2p-peerdist"),
+};
+__constant__ HdrKey k_resp_keys[] = {
+    MFP_HK(32, 1, 0, "access-control-allow-credentials"), MFP_HK(28, 1, 0, "access-control-allow-headers"),
+    MFP_HK(28, 1, 0, "access-control-allow-methods"), MFP_HK(29, 1, 0, "access-control-expose-headers"),
+    MFP_HK(13, 1, 0, "cache-control"), MFP_HK(4, 1, 0, "code"), MFP_HK(10, 1, 0, "connection"),
+    MFP_HK(16, 1, 0, "content-language"), MFP_HK(25, 1, 0, "content-transfer-encoding"), MFP_HK(3, 1, 0, "p3p"),
+    MFP_HK(6, 1, 0, "pragma"), MFP_HK(6, 1, 0, "reason"), MFP_HK(6, 1, 0, "server"),
+    MFP_HK(25, 1, 0, "strict-transport-security"), MFP_HK(7, 1, 0, "version"),
+    MFP_HK(19, 1, 0, "x-aspnetmvc-version"), MFP_HK(16, 1, 0, "x-aspnet-version"), MFP_HK(5, 1, 0, "x-cid"),
+    MFP_HK(12, 1, 0, "x-ms-version"), MFP_HK(16, 1, 0, "x-xss-protection"),
+    MFP_HK(17, 0, 0, "appex-activity-id"), MFP_HK(7, 0, 0, "cdnuuid"), MFP_HK(6, 0, 0, "cf-ray"),
+    MFP_HK(13, 0, 0, "content-range"), MFP_HK(12, 0, 0, "content-type"), MFP_HK(4, 0, 0, "date"),
+    MFP_HK(4, 0, 0, "etag"), MFP_HK(7, 0, 0, "expires"), MFP_HK(12, 0, 0, "flow_context"), MFP_HK(5, 0, 0, "ms-cv"),
+    MFP_HK(8, 0, 0, "msregion"), MFP_HK(12, 0, 0, "ms-requestid"), MFP_HK(10, 0, 0, "request-id"),
+    MFP_HK(4, 0, 0, "vary"), MFP_HK(12, 0, 0, "x-amz-cf-pop"), MFP_HK(16, 0, 0, "x-amz-request-id"),
+    MFP_HK(24, 0, 0, "x-azure-ref-originshield"), MFP_HK(7, 0, 0, "x-cache"), MFP_HK(12, 0, 0, "x-cache-hits"),
+    MFP_HK(5, 0, 0, "x-ccc"), MFP_HK(14, 0, 0, "x-diagnostic-s"), MFP_HK(10, 0, 0, "x-feserver"),
+    MFP_HK(4, 0, 0, "x-hw"), MFP_HK(12, 0, 0, "x-msedge-ref"), MFP_HK(19, 0, 0, "x-ocsp-responder-id"),
+    MFP_HK(11, 0, 0, "x-requestid"), MFP_HK(11, 0, 0, "x-served-by"), MFP_HK(7, 0, 0, "x-timer"),
+    MFP_HK(15, 0, 0, "x-trace-context"),
+};
+#undef MFP_HK
+// ASCII A-Z -> a-z in each byte of w (bytes >= 0x80 unchanged)
+DEV uint64_t swar_tolower(uint64_t w) {
+    const uint64_t x = w & 0x7f7f7f7f7f7f7f7full;
+    const uint64_t ge_a = x + 0x3f3f3f3f3f3f3f3full, gt_z = x + 0x2525252525252525ull;
+    const uint64_t upper = ge_a & ~gt_z & ~w & 0x8080808080808080ull;
+    return w | (upper >> 2);
+}
+
 // perfect_hash::lookup perfect_hash.h:256: exact ASCII-case-insensitive match
 DEV int name_lookup(const HdrName *tab, int ntab, Cur n) {
     long l = clen(n);

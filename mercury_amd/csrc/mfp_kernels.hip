@@ -265,6 +265,7 @@ WDEV uint32_t rdl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlan
 // wave reserves fingerprint-arena space CHUNK bytes at a time (one atomic per
 // CHUNK); every string starts 16-byte aligned.  Records are gathered in the
 // lanes (lane j holds packet j's record) and stored coalesced.
+template <uint32_t SPEC>
 __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P) {
     __shared__ WaveLds lds[WAVES];
     // wave index made provably uniform: the compiler would otherwise treat the
@@ -305,10 +306,10 @@ __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P
             for (uint32_t v = lane; v < nvec; v += 64) *(uint4 *)(L.buf + 16 * v) = *(const uint4 *)(src + 16 * v);
             __builtin_amdgcn_wave_barrier();
 
-            W w(L, P.cfg);
+            W<SPEC> w(L, P.cfg);
             w.packet_walk((int)a, caplen, lt);
             w.flush();
-            if (w.ovf) { fb |= (int)lane == j; continue; }
+            if (w.ovf || w.punt) { fb |= (int)lane == j; continue; }
             uint32_t type = w.o.fp_type, T = 0;
             uint64_t fpo = 0;
             if (type) {
@@ -414,7 +415,11 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
             if (bin_wave_mask & (1u << b)) {
                 W.idx = work + (uint64_t)b * n;
                 W.count = bin_count + b;
-                MFP_LAUNCH(wave_name[b], mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+                // the bin's protocol families only (others -> fallback lane)
+                auto kw = b == 0 ? mfpw::k_wave_fp<mfpw::SPEC_TLS>
+                        : (b == 1 || b == 3) ? mfpw::k_wave_fp<mfpw::SPEC_HTTP>
+                        : b == 2 ? mfpw::k_wave_fp<0u> : mfpw::k_wave_fp<mfpw::SPEC_ALL>;
+                MFP_LAUNCH(wave_name[b], kw, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
                 any_wave = true;
             } else {
                 P.idx = work + (uint64_t)b * n;
@@ -434,7 +439,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     }
     uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
     if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
-    MFP_LAUNCH("k_wave_fp", mfpw::k_wave_fp, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+    MFP_LAUNCH("k_wave_fp", mfpw::k_wave_fp<mfpw::SPEC_ALL>, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
     if (hipGetLastError() != hipSuccess) return -1;
     // fallback lane over the packets the wave kernel handed back
     P.idx = work;

@@ -40,6 +40,7 @@ constexpr uint32_t FP_MAX = 8192;   // fingerprint::MAX_FP_STR_LEN fingerprint.h
 
 struct WaveLds {
     uint8_t buf[PKT_CAP + SCR_CAP];  // [0,PKT_CAP) packet, then scratch
+    uint64_t cmask[PKT_CAP / 64 + 2];   // HTTP header block: ':' positions per 64-byte chunk
     uint16_t seg_end[SEG_CAP];       // exclusive end (characters) of each segment
     uint32_t seg_info[SEG_CAP];      // src offset in buf | kind << 16
 };
@@ -78,6 +79,12 @@ using mfp::SEL_TCP_SYNACK; using mfp::SEL_DTLS;
 // the wave walker: parse state + segment emitter (buffer_stream semantics,
 // buffer_stream.h:100-240: a fingerprint longer than FP_MAX-2 is dropped)
 // ---------------------------------------------------------------------------
+// protocol families a W instance can fingerprint (per-bin specialisations
+// keep the hot code of a bin kernel small; a packet of a family that is
+// compiled out is handed to the fallback lane, `punt`)
+enum : uint32_t { SPEC_TLS = 1, SPEC_SSH = 2, SPEC_HTTP = 4, SPEC_DTLS = 8, SPEC_ALL = 15 };
+
+template <uint32_t SPEC = SPEC_ALL>
 struct W {
     WaveLds &L;
     Cfg cfg;
@@ -88,13 +95,14 @@ struct W {
     bool last_putc;
     int nseg, scr;
     bool ovf;            // segment table / scratch overflow -> fallback lane
+    bool punt;           // protocol family not compiled into this instance -> fallback lane
     // pending (not yet stored) segment
     uint32_t pk_kind;
     int pk_src, pk_len;  // pk_len in source bytes; 0 = none
 
     WDEV W(WaveLds &l, const Cfg &c) : L(l), cfg(c) {
         lane = lane_id();
-        n = 0; last_putc = false; nseg = 0; scr = 0; ovf = false; pk_kind = 0; pk_src = 0; pk_len = 0;
+        n = 0; last_putc = false; nseg = 0; scr = 0; ovf = false; punt = false; pk_kind = 0; pk_src = 0; pk_len = 0;
         refill(0);
     }
 
@@ -931,9 +939,16 @@ struct W {
     // lines one after another; anything else returns false before emitting
     // and the serial loop below runs.
     // -----------------------------------------------------------------------
+    // 8 bytes of the staged buffer at byte offset x (any alignment)
+    WDEV uint64_t lds_u64(int x) {
+        const int a = x & ~7;
+        const uint32_t sh = (uint32_t)(x & 7) * 8;
+        const uint64_t lo = *(const uint64_t *)(L.buf + a), hi = *(const uint64_t *)(L.buf + a + 8);
+        return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    }
     WDEV bool http_headers_par(C body, bool req, C &host, C &ua) {
         if (body.d < 0) return false;
-        const mfp::HdrName *tab = req ? mfp::k_req_names : mfp::k_resp_names;
+        const mfp::HdrKey *tab = req ? mfp::k_req_keys : mfp::k_resp_keys;
         const int ntab = req ? mfp::N_REQ_NAMES : mfp::N_RESP_NAMES;
         // 1. line ends: LF positions up to the empty line (CRLF CRLF) or the end
         int my_start = 0, my_end = 0, nl = 0;     // line [start, end) excludes CRLF
@@ -942,11 +957,14 @@ struct W {
         const int e = body.e;
         uint32_t carry_cr = 0;
         int base = p;
+        const int p0 = p;
         for (; base < e && !done; base += 64) {
             const int q = base + (int)lane;
             const uint32_t c = L.buf[q < e ? q : base];
             const uint64_t lf = ballot(q < e && c == '\n');
             const uint64_t cr = ballot(q < e && c == '\r');
+            const uint64_t cm = ballot(q < e && c == ':');
+            if (lane == 0) L.cmask[(base - p0) >> 6] = cm;
             // CR/LF pairing: every LF sits right after a CR and vice versa
             if (((cr << 1) | carry_cr) != lf) return false;
             carry_cr = (uint32_t)(cr >> 63);
@@ -972,11 +990,20 @@ struct W {
             }
         }
         const bool mine = (int)lane < nl;
-        // 2. per line: colon, LWS, value
+        // 2. per line: colon (first ':' of the line, from the chunk masks), LWS, value
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         int colon = -1;
         if (mine) {
-            for (int x = my_start; x < my_end; x++) {
-                if (L.buf[x] == ':') { colon = x; break; }
+            for (int x = my_start; x < my_end;) {
+                const int rel = x - p0;
+                const uint64_t m = L.cmask[rel >> 6] >> (rel & 63);
+                if (m) {
+                    const int pos = x + (int)__builtin_ctzll(m);
+                    if (pos < my_end) colon = pos;
+                    break;
+                }
+                x = p0 + ((rel >> 6) + 1) * 64;
             }
         }
         // a line without ':' makes the reference's name scan run into the
@@ -989,23 +1016,34 @@ struct W {
             vs = colon + 1;
             while (vs < my_end && (L.buf[vs] == ' ' || L.buf[vs] == '\t')) vs++;
         }
-        // 3. name lookup: ASCII case-insensitive exact match (perfect_hash.h:256)
+        // 3. name lookup: ASCII case-insensitive exact match (perfect_hash.h:256),
+        // the lowercased name as four words against the packed tables
         int idx = -1;
+        uint32_t info = 0;
         const int nlen = valid ? colon - my_start : 0;
         if (valid && nlen > 0 && nlen <= 32) {
-            const uint32_t c0 = mfp::c_tolower(L.buf[my_start]);
+            uint64_t nw[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint64_t w = 8 * k < nlen ? mfp::swar_tolower(lds_u64(my_start + 8 * k)) : 0ull;
+                if (nlen - 8 * k < 8 && nlen > 8 * k) w &= (1ull << (8 * (nlen - 8 * k))) - 1;
+                nw[k] = w;
+            }
             for (int i = 0; i < ntab; i++) {
-                if (tab[i].len != nlen || (uint8_t)tab[i].s[0] != c0) continue;
-                bool ok = true;
-                for (int j = 1; j < nlen; j++)
-                    if (mfp::c_tolower(L.buf[my_start + j]) != (uint8_t)tab[i].s[j]) { ok = false; break; }
-                if (ok) { idx = i; break; }
+                const mfp::HdrKey &k = tab[i];
+                if (idx < 0 && k.len == (uint32_t)nlen && k.w[0] == nw[0] && k.w[1] == nw[1] && k.w[2] == nw[2] &&
+                    k.w[3] == nw[3]) {
+                    idx = i;
+                    info = k.info;
+                }
             }
         }
         const bool emit = idx >= 0;
+        const bool incl_value = (info & 0xff) != 0;
+        const uint32_t capture = info >> 8;
         // host / user-agent: first occurrence wins (http.h:364-366)
         if (req) {
-            const bool is_host = emit && tab[idx].capture == 1, is_ua = emit && tab[idx].capture == 2;
+            const bool is_host = emit && capture == 1, is_ua = emit && capture == 2;
             const uint64_t hm = ballot(is_host), um = ballot(is_ua);
             if (hm) {
                 int k = (int)__builtin_ctzll(hm);
@@ -1017,7 +1055,7 @@ struct W {
             }
         }
         // 4. "(" hex(span) ")" per emitted line, in line order
-        const int span_end = emit ? (tab[idx].incl_value ? my_end : colon) : 0;
+        const int span_end = emit ? (incl_value ? my_end : colon) : 0;
         const uint32_t chars = emit ? (uint32_t)(2 + 2 * (span_end - my_start)) : 0u;
         const uint32_t sbytes = emit ? 2u : 0u, segs = emit ? 3u : 0u;
         const uint32_t ec = wave_excl_scan(chars, lane), es = wave_excl_scan(sbytes, lane),
@@ -1138,7 +1176,9 @@ struct W {
         putc('(');
         C host = cnul(), ua = cnul();
         const bool crlf = clen(delim) == 2 && ld(delim.d) == '\r' && ld(delim.d + 1) == '\n';
+#ifndef MFP_PROBE_NOHDR
         if (!(crlf && http_headers_par(p, req, host, ua))) http_headers_fp(p, delim, req, host, ua);
+#endif
         putc(')');
         if (req) {
             if (!cnull(host)) { o.sni_off = (uint32_t)(host.d - base); o.sni_len = (uint32_t)clen(host); }
@@ -1178,6 +1218,7 @@ struct W {
                 bool hit = false;
                 for (int i = 0; i < 36; i++) hit |= (mfp::k_http_kw[i] == kw);
                 if (hit) {
+                    if constexpr (!(SPEC & SPEC_HTTP)) { punt = true; return; }
                     o.msg = MFP_MSG_HTTP_REQ;
                     if (http_msg(pkt, true, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 3; }
                     else o.msg = 0;
@@ -1185,6 +1226,7 @@ struct W {
                 }
             }
             if ((sel & SEL_HTTP_RESP) && kw == 0x48545450u) {
+                if constexpr (!(SPEC & SPEC_HTTP)) { punt = true; return; }
                 o.msg = MFP_MSG_HTTP_RESP;
                 if (http_msg(pkt, false, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 4; }
                 else o.msg = 0;
@@ -1192,6 +1234,12 @@ struct W {
             return;
         }
         o.msg = msg;
+        if constexpr (!(SPEC & SPEC_TLS)) {
+            if (msg == MFP_MSG_TLS_CH || msg == MFP_MSG_TLS_SH || msg == MFP_MSG_TLS_CERT) { punt = true; return; }
+        }
+        if constexpr (!(SPEC & SPEC_SSH)) {
+            if (msg == MFP_MSG_SSH_INIT || msg == MFP_MSG_SSH_KEX) { punt = true; return; }
+        }
         switch (msg) {
         case MFP_MSG_TLS_CH: {
 #ifdef MFP_PROBE_NOCH
@@ -1313,6 +1361,7 @@ struct W {
         uint32_t hb = (uint32_t)((w1 & M1) >> 40);
         uint32_t msg = hb == 1 ? MFP_MSG_DTLS_CH : hb == 2 ? MFP_MSG_DTLS_SH : hb == 3 ? MFP_MSG_DTLS_HVR : 0;
         if (!msg) return;
+        if constexpr (!(SPEC & SPEC_DTLS)) { punt = true; return; }
         o.msg = msg;
         C d = pkt, frag = cnul(), body = cnul();
         uint64_t t, len = 0, foff = 0, flen = 0, more = 0;

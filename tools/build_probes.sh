@@ -1,0 +1,15 @@
+#!/bin/bash
+# profiling variants of libmercury_amd.so (never shipped: mercury_amd/_probe/)
+# usage: tools/build_probes.sh NAME:MACRO[,MACRO] ...
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p mercury_amd/_probe
+OBJ=mercury_amd/_obj
+for spec in "$@"; do
+  name=${spec%%:*}; macros=${spec#*:}
+  defs=""; for m in ${macros//,/ }; do defs="$defs -D$m"; done
+  ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/mfp_kernels.hip -o mercury_amd/_probe/k_$name.o &&
+    hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so mercury_amd/_probe/k_$name.o \
+      $OBJ/mfp_analysis.hip.o $OBJ/mfp_host.cpp.o $OBJ/mfp_classifier.cpp.o $OBJ/mfp_libmerc.cpp.o -lz && echo built $name ) &
+done
+wait
