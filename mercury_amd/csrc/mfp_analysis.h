@@ -21,6 +21,8 @@ struct mfp_entry {
     uint32_t nproc;         // P
     uint32_t malware_db;    // fingerprint_data::malware_db
     uint32_t generic_dmz;   // index of "generic dmz process" or 0xffffffff
+    uint32_t mal_bits;      // bit p: process p is malware (p < 32)
+    uint32_t pad[3];
 };
 
 // feature-table slot, keyed by (entry, kind, key) -- key is the value itself

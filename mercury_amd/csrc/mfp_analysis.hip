@@ -232,8 +232,73 @@ ADEV uint32_t probe_string_lane(const mfp_fp_slot *slots, uint64_t mask, const c
     for (uint64_t k = h & mask;; k = (k + 1) & mask) {
         const mfp_fp_slot sl = slots[k];
         if (sl.id == 0xffffffffu) return 0xffffffffu;
+#ifdef MFP_PROBE_AN_NOVERIFY
+        if (sl.hash == h && sl.str_len == len) return sl.id;
+#else
         if (sl.hash == h && sl.str_len == len && lane_eq(s, (const uint8_t *)pool + sl.str_off, len)) return sl.id;
+#endif
     }
+}
+
+// first slot whose hash and length match (no byte comparison): the
+// candidate that wave_verify then checks; ~0u when the probe hits an empty slot
+ADEV uint32_t cand_string_lane(const mfp_fp_slot *slots, uint64_t mask, uint64_t h, uint32_t len, uint32_t &str_off) {
+    for (uint64_t k = h & mask;; k = (k + 1) & mask) {
+        const mfp_fp_slot sl = slots[k];
+        if (sl.id == 0xffffffffu) return 0xffffffffu;
+        if (sl.hash == h && sl.str_len == len) { str_off = sl.str_off; return sl.id; }
+    }
+}
+ADEV bool cand_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_t kind, uint64_t key, uint32_t len,
+                            Hit &hit, uint32_t &str_off) {
+    for (uint64_t k = feat_slot_hash(entry, kind, key) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
+        const mfp_feat_slot sl = D.feat_slots[k];
+        if (sl.entry == 0xffffffffu) return false;
+        if (sl.entry == entry && sl.kind == kind && sl.key == key && sl.str_len == len) {
+            hit = Hit{sl.upd_off, sl.upd_cnt};
+            str_off = sl.str_off;
+            return true;
+        }
+    }
+}
+
+ADEV uint64_t rl64(uint64_t v, int j) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j) << 32);
+}
+
+// Byte-exact comparison of a[0, len) with b[0, len) for every lane with
+// `has`, done by the whole wave one string (up to four at a time) after the
+// other: lane k compares word k, so each string is read with coalesced loads
+// instead of a lane walking its own string.  Returns false on lanes whose
+// strings differ (true on lanes without `has`).
+ADEV bool wave_verify(bool has, const uint8_t *a, const uint8_t *b, uint32_t len, uint32_t lane) {
+    bool ok = true;
+    uint64_t m = __ballot(has);
+    while (m) {
+        int js[4];
+        int nj = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            js[t] = 0;
+            if (m) { js[t] = (int)__builtin_ctzll(m); m &= m - 1; nj = t + 1; }
+        }
+        bool bad[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            bad[t] = false;
+            if (t < nj) {
+                const uint8_t *aj = (const uint8_t *)rl64((uint64_t)a, js[t]);
+                const uint8_t *bj = (const uint8_t *)rl64((uint64_t)b, js[t]);
+                const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, js[t]);
+                for (uint32_t k = lane; 8 * k < lj; k += 64) bad[t] |= word_at(aj, lj, k) != word_at(bj, lj, k);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (t < nj && __ballot(bad[t]) && (int)lane == js[t]) ok = false;
+    }
+    return ok;
 }
 
 // feature slot of (entry, kind, key); s/len: the string to verify (len ==
@@ -244,7 +309,11 @@ ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_
         const mfp_feat_slot sl = D.feat_slots[k];
         if (sl.entry == 0xffffffffu) return Hit{0, 0};
         if (sl.entry == entry && sl.kind == kind && sl.key == key &&
+#ifdef MFP_PROBE_AN_NOVERIFY
+            (len == 0xffffffffu || sl.str_len == len))
+#else
             (len == 0xffffffffu || (sl.str_len == len && lane_eq(s, (const uint8_t *)D.pool + sl.str_off, len))))
+#endif
             return Hit{sl.upd_off, sl.upd_cnt};
     }
 }
@@ -385,22 +454,43 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
         n_an += (uint32_t)__builtin_popcountll(am);
 
         // ================= phase A: lane per packet =================
-        uint32_t status = 0, entry = 0xffffffffu, np = 0, po = 0, mdb = 0, dmz = 0;
+        uint32_t status = 0, entry = 0xffffffffu, np = 0, po = 0, mdb = 0, dmz = 0, mbits = 0;
         bool pending = false;
         uint32_t hoff[NFEAT], hcnt[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) { hoff[f] = 0; hcnt[f] = 0; }
+        // ---- 1. fingerprint lookup / status (perform_analysis_common, analysis.h:1043-1083):
+        // hash and candidate slot per lane, byte-exact check by the wave
+        const uint8_t *fp = P.fp_arena + r.fp_offset;
+        const uint32_t fl = analyzable ? r.fp_len : 0u;
+        uint64_t fh = 0, w0 = 0;
+        uint32_t cid = 0xffffffffu, coff = 0;
         if (analyzable) {
-            // ---- 1. fingerprint lookup / status (perform_analysis_common, analysis.h:1043-1083)
-            const uint8_t *fp = P.fp_arena + r.fp_offset;
-            const uint32_t fl = r.fp_len;
-            const uint64_t fh = lane_hash(fp, fl);
-            entry = probe_string_lane(D.fp_slots, D.fp_mask, D.pool, fp, fl, fh);
-            const uint64_t w0 = word_at(fp, fl, 0);
+#ifdef MFP_PROBE_AN_NOHASH
+            fh = fl;
+#else
+            fh = lane_hash(fp, fl);
+#endif
+            w0 = word_at(fp, fl, 0);
+            cid = cand_string_lane(D.fp_slots, D.fp_mask, fh, fl, coff);
+        }
+        {
+            const bool ok = wave_verify(cid != 0xffffffffu, fp, (const uint8_t *)D.pool + coff, fl, lane);
+            if (cid != 0xffffffffu && !ok) cid = probe_string_lane(D.fp_slots, D.fp_mask, D.pool, fp, fl, fh);
+        }
+        entry = cid;
+        const bool tls_unknown = analyzable && entry == 0xffffffffu && fl >= 4 && (uint32_t)w0 == 0x2f736c74u;  // "tls/"
+        uint32_t pid = 0xffffffffu, poff = 0;
+        if (tls_unknown) pid = cand_string_lane(D.prev_slots, D.prev_mask, fh, fl, poff);
+        {
+            const bool ok = wave_verify(pid != 0xffffffffu, fp, (const uint8_t *)D.pool + poff, fl, lane);
+            if (pid != 0xffffffffu && !ok) pid = probe_string_lane(D.prev_slots, D.prev_mask, D.pool, fp, fl, fh);
+        }
+        if (analyzable) {
             if (entry != 0xffffffffu) {
                 status = 1;                                                   // labeled
-            } else if (fl >= 4 && (uint32_t)w0 == 0x2f736c74u) {              // "tls/"
-                if (probe_string_lane(D.prev_slots, D.prev_mask, D.pool, fp, fl, fh) != 0xffffffffu) {
+            } else if (tls_unknown) {
+                if (pid != 0xffffffffu) {
                     status = 3;                    // unlabeled (known set; no LRU update)
                 } else {
                     // adaptive set: record the sighting; k_analyze_status decides
@@ -432,13 +522,19 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
         bool scored = analyzable && entry != 0xffffffffu;
         if (scored) {
             const mfp_entry E = D.entry[entry];
-            np = E.nproc; po = E.proc_off; mdb = E.malware_db; dmz = E.generic_dmz;
+            np = E.nproc; po = E.proc_off; mdb = E.malware_db; dmz = E.generic_dmz; mbits = E.mal_bits;
             if (np > 64 * MAXP_CHUNKS) {
                 atomicAdd(&P.stats[2], 1ull);
                 scored = false;
             }
         }
         bool plain = false;
+        // string features UA, domain, SNI (hoff/hcnt slots 3..5)
+        const uint8_t *vs[3] = {nullptr, nullptr, nullptr};
+        uint32_t vl[3] = {0, 0, 0}, voff[3] = {0, 0, 0};
+        uint64_t vk[3] = {0, 0, 0};
+        Hit vh[3] = {Hit{0, 0}, Hit{0, 0}, Hit{0, 0}};
+        bool has[3] = {false, false, false};
         if (scored) {
             // ---- 2. destination context (destination_context::init, result.h:346)
             const uint8_t *pkt = P.arena + P.desc[i].offset;
@@ -496,13 +592,25 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
                     }
                 }
             }
-            h = probe_feature_lane(D, entry, F_UA, uh, up, ul);
-            hoff[3] = h.off; hcnt[3] = h.cnt;
+            // string features: candidate slots here, byte-exact check by the wave below
+            vs[0] = up; vl[0] = ul; vk[0] = uh;
+            has[0] = cand_feature_lane(D, entry, F_UA, uh, ul, vh[0], voff[0]);
             if (plain) {   // else k_analyze_wave normalises the name (wave, LDS)
-                h = probe_feature_lane(D, entry, F_DOMAIN, lane_hash(sp + tld, sl - tld), sp + tld, sl - tld);
-                hoff[4] = h.off; hcnt[4] = h.cnt;
-                h = probe_feature_lane(D, entry, F_SNI, nh, sp, sl);
-                hoff[5] = h.off; hcnt[5] = h.cnt;
+                vs[1] = sp + tld; vl[1] = sl - tld; vk[1] = lane_hash(sp + tld, sl - tld);
+                has[1] = cand_feature_lane(D, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
+                vs[2] = sp; vl[2] = sl; vk[2] = nh;
+                has[2] = cand_feature_lane(D, entry, F_SNI, nh, sl, vh[2], voff[2]);
+            }
+        }
+
+#pragma unroll
+        for (int v = 0; v < 3; v++) {
+            const bool ok = wave_verify(has[v], vs[v], (const uint8_t *)D.pool + voff[v], vl[v], lane);
+            if (has[v]) {
+                // a hash collision (ok == false) takes the full probe, which keeps looking
+                const Hit h = ok ? vh[v] : probe_feature_lane(D, entry, v == 0 ? F_UA : v == 1 ? F_DOMAIN : F_SNI, vk[v],
+                                                              vs[v], vl[v]);
+                hoff[3 + v] = h.off; hcnt[3 + v] = h.cnt;
             }
         }
 
@@ -510,7 +618,11 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
         // the reference's own sequential loops (naive_bayes.hpp:752-772,
         // compute_score_and_probability analysis.h:222-277, softmax
         // softmax.hpp:227-264) on lane-private LDS rows
+#ifdef MFP_PROBE_AN_NOSCORE
+        const bool lanep = false;
+#else
         const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain;
+#endif
         if (lanep) {
             double *S = scl + lane;                    // S[p * 64]
             for (uint32_t p = 0; p < np; p++) S[p * 64] = D.prior[po + p];
@@ -540,14 +652,14 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
                 const double e = (double)expf((float)(S[p * 64] - mx));
                 ssum += e;
                 if (p != imx) swo += e;
-                if (D.proc_mal[po + p]) mal += e;
+                if ((mbits >> p) & 1u) mal += e;
                 if (p == imx) p_imx = e;
                 if (p == isx) p_isx = e;
             }
             double max_score = p_imx;
             if (ssum > 0.0 && mdb) mal /= ssum;
             uint32_t ibest = imx;
-            if (mdb && dmz == imx && !D.proc_mal[po + isx]) {
+            if (mdb && dmz == imx && !((mbits >> isx) & 1u)) {
                 ibest = isx;
                 ssum = swo;
                 max_score = p_isx;
@@ -561,7 +673,7 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
             if (mdb) {
                 a.malware_prob = mal;
                 a.flags |= MFP_AN_CLASSIFY_MALWARE;
-                if (D.proc_mal[po + ibest]) a.flags |= MFP_AN_MALWARE;
+                if ((mbits >> ibest) & 1u) a.flags |= MFP_AN_MALWARE;
             }
             if ((a.flags & MFP_AN_MALWARE) && r.fp_type == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
         }

@@ -689,7 +689,9 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
         me.nproc = (uint32_t)e.prior.size();
         me.malware_db = e.malware_db;
         me.generic_dmz = 0xffffffffu;
+        me.mal_bits = 0; me.pad[0] = me.pad[1] = me.pad[2] = 0;
         for (uint32_t i = 0; i < me.nproc; i++) {
+            if (i < 32 && e.malware[i]) me.mal_bits |= 1u << i;
             t.prior.push_back(e.prior[i]);
             t.proc_id.push_back(c->proc_name_id[e.proc_name[i]]);
             t.proc_mal.push_back(e.malware[i]);
@@ -785,7 +787,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     if (t.pool.empty()) t.pool.push_back(0);
     if (t.upd.empty()) t.upd.push_back(mfp_update{0, 0, 0});
     if (t.prior.empty()) { t.prior.push_back(0); t.proc_id.push_back(0); t.proc_mal.push_back(0); t.proc_attr.push_back(0); }
-    if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0});
+    if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0, 0, {0, 0, 0}});
     if (t.asn4.empty()) t.asn4.push_back(mk4(1, 0, 0));
     if (t.asn6.empty()) { mfp_asn6 r{}; r.lo_lo = 1; t.asn6.push_back(r); }
 
