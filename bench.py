@@ -25,7 +25,9 @@ comes from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the same command
 (profiles/*traffic*.json, tools/pmc_traffic.py) when one matches this
 configuration.  `cpu_baseline` is the reference libmerc compiled from
 /root/reference (oracle/_ref, travels with the snapshot) or else the C oracle
-port, timed on a bounded sample on the host cores.
+port, timed on a bounded sample on the host cores.  `end_to_end` is the
+H2D/D2H-inclusive rate of the same configuration on --e2e-packets packets in
+page-locked host memory (mfp_process_pipelined), reported beside `value`.
 """
 import argparse
 import glob
@@ -104,6 +106,44 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis):
             "sample": f"{sample_n} {workload} packets x {reps} passes, C oracle, {threads} threads"}
 
 
+def end_to_end(torch, ctx, ua, ud, n, analysis, steps, chunk):
+    """Host-resident rate: packets in page-locked host memory, records,
+    fingerprints (and classifier results) back in host memory, through
+    mfp_process_pipelined (two streams: H2D, kernels, D2H overlapped)."""
+    from mercury_amd.api import ANALYSIS_DTYPE, DESC_DTYPE, RECORD_DTYPE
+    u = len(ud)
+    span = int(ud["offset"][-1] + ud["caplen"][-1])
+    stride = (span + 255) // 256 * 256
+    reps = (n + u - 1) // u
+    h_arena = torch.empty(stride * reps + 64, dtype=torch.uint8, pin_memory=True)
+    av = h_arena.numpy()
+    for r in range(reps):
+        av[r * stride:r * stride + span] = ua[:span]
+    desc = np.tile(ud, reps)[:n].copy()
+    desc["offset"] += (np.arange(reps, dtype=np.uint64) * np.uint64(stride)).repeat(u)[:n]
+    h_desc = torch.empty(n * 16, dtype=torch.uint8, pin_memory=True)
+    h_desc.numpy()[:] = desc.view(np.uint8)
+    rec_u, fp_u = ctx.process_host(ua, ud)
+    fp_cap = int((int(rec_u["fp_len"].astype(np.int64).sum()) + 16 * u) * reps * 1.05) + (64 << 20)
+    h_rec = torch.empty(n * 32, dtype=torch.uint8, pin_memory=True)
+    h_fp = torch.empty(fp_cap, dtype=torch.uint8, pin_memory=True)
+    h_an = torch.empty(n * 24 if analysis else 8, dtype=torch.uint8, pin_memory=True)
+    out = (h_rec.numpy().view(RECORD_DTYPE), h_fp.numpy(), h_an.numpy().view(ANALYSIS_DTYPE) if analysis else None)
+    d = h_desc.numpy().view(DESC_DTYPE)
+    ctx.process_pipelined(av, d, chunk=chunk, analysis=analysis, out=out)   # warm-up (device buffers)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, used, _ = ctx.process_pipelined(av, d, chunk=chunk, analysis=analysis, out=out)
+    el = (time.perf_counter() - t0) / steps
+    in_bytes = int(desc["caplen"].astype(np.int64).sum()) + 16 * n
+    out_bytes = 32 * n + used + (24 * n if analysis else 0)
+    return {"value": round(n / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "steps": steps, "chunk": chunk,
+            "ms_per_step": round(el * 1e3, 3), "h2d_gb_per_s": round(in_bytes / el / 1e9, 3),
+            "d2h_gb_per_s": round(out_bytes / el / 1e9, 3), "pinned": True,
+            "path": "mfp_process_pipelined: pinned host arena -> 2 HIP streams (H2D | kernels | D2H) -> pinned "
+                    "records + fingerprints" + (" + classifier results" if analysis else "")}
+
+
 def find_traffic(cfg_key):
     """Counter-derived HBM bytes per step for this configuration, if profiled."""
     best = None
@@ -129,6 +169,9 @@ def main():
     ap.add_argument("--no-analysis", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-packets", type=int, default=10_000_000,
+                    help="host-resident (H2D/D2H-inclusive) leg on this many packets; 0 = skip")
+    ap.add_argument("--e2e-chunk", type=int, default=2_000_000)
     args = ap.parse_args()
     analysis = not args.no_analysis
 
@@ -202,9 +245,8 @@ def main():
     prof = ctx.profile_read()
     ctx.profile(False)
     if dist:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from mercury_amd import shard
+        elapsed = shard.max_over_ranks(elapsed, device="cuda")
 
     rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
     caplen_bytes = int(desc["caplen"].astype(np.int64).sum())
@@ -245,6 +287,14 @@ def main():
         if tr:
             traffic = tr[1]["hbm_bytes_per_step"]
         n_fp = int((rec["fp_type"] > 0).sum())
+        e2e = None
+        if world == 1 and args.e2e_packets:
+            del d_arena, d_desc, d_fp          # room for the pipeline's staging buffers
+            torch.cuda.empty_cache()
+            try:
+                e2e = end_to_end(torch, ctx, ua, ud, args.e2e_packets, analysis, 3, args.e2e_chunk)
+            except Exception as e:   # reported beside the device-resident number, never instead of it
+                log(f"end-to-end leg failed: {e}")
         if workload == "mixed":
             wl = ("config 4: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint + --analysis classifier "
                   "(synthetic resource archive)") if analysis else \
@@ -297,6 +347,7 @@ def main():
             "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4)}
                         for k, v in kern_ms.items()},
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -121,7 +121,9 @@ MFP_EXPORT int mfp_process_batch_device(mfp_context ctx, const uint8_t *d_arena,
                                         uint64_t *d_fp_used, void *stream);
 
 /* Host batch: copies arena/descriptors to the device, runs, copies back.
- * Synchronous.  Returns bytes of fp arena used, or a negative error. */
+ * The strings come back packed in packet order (fp_arena holds exactly the
+ * sum of fp_len).  Synchronous.  Returns bytes of fp arena used, or a
+ * negative error. */
 MFP_EXPORT long long mfp_process_batch_host(mfp_context ctx, const uint8_t *arena, size_t arena_len,
                                             const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                             char *fp_arena, size_t fp_cap);
@@ -158,6 +160,19 @@ MFP_EXPORT int mfp_analyze_batch_device(mfp_context ctx, const uint8_t *d_arena,
 MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context ctx, const uint8_t *arena, size_t arena_len,
                                                const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                char *fp_arena, size_t fp_cap, mfp_analysis *analysis);
+
+/* Host batch, pipelined (the end-to-end path: capture buffer in, records
+ * out).  The batch is cut into chunks of `chunk` packets (0: 1M); two chunks
+ * are in flight on two HIP streams, so the H2D copy of one overlaps the
+ * kernels of the other and the D2H copies of both.  `analysis` may be NULL
+ * (fingerprints only).  Results are those of mfp_process_batch_host_ex on
+ * the whole batch: rec[i].fp_offset indexes fp_arena, whose strings are laid
+ * out chunk after chunk.  Host buffers should be page-locked
+ * (hipHostMalloc / hipHostRegister) for full PCIe rate.  Synchronous;
+ * returns the fp-arena bytes used or a negative error. */
+MFP_EXPORT long long mfp_process_pipelined(mfp_context ctx, const uint8_t *arena, size_t arena_len,
+                                           const mfp_pkt_desc *desc, size_t n, mfp_record *rec, char *fp_arena,
+                                           size_t fp_cap, mfp_analysis *analysis, size_t chunk);
 
 /* names behind mfp_analysis.process and the bits of mfp_analysis.attr */
 MFP_EXPORT const char *mfp_process_name(mfp_context ctx, uint32_t id);

@@ -80,6 +80,8 @@ def load_library():
     lib.mfp_normalize_server_name.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
     lib.mfp_parse_filter.restype = ctypes.c_int
     lib.mfp_parse_filter.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    lib.mfp_process_pipelined.restype = ctypes.c_longlong
+    lib.mfp_process_pipelined.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, sz]
     lib.mfp_profile_enable.restype = ctypes.c_int
     lib.mfp_profile_enable.argtypes = [vp, ctypes.c_int]
     lib.mfp_profile_read.restype = ctypes.c_int
@@ -149,6 +151,27 @@ class Context:
         if used < 0:
             raise MercuryAmdError("mfp_process_batch_host_ex failed: " + _err(self.lib))
         return rec, fp[:used].tobytes(), an
+
+    def process_pipelined(self, arena, desc, chunk=0, analysis=False, out=None):
+        """Host batch through the two-stream pipeline (mfp_process_pipelined).
+        `out`: optional preallocated (records, fp arena, analysis) host arrays
+        (page-locked for full PCIe rate).  Returns (records, fp arena bytes
+        used, analysis records or None)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        n = len(desc)
+        if out is None:
+            rec = np.zeros(n, dtype=RECORD_DTYPE)
+            fp = np.zeros(self.fp_arena_bound(desc), dtype=np.uint8)
+            an = np.zeros(n, dtype=ANALYSIS_DTYPE) if analysis else None
+        else:
+            rec, fp, an = out
+        used = self.lib.mfp_process_pipelined(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
+                                              rec.ctypes.data, fp.ctypes.data, fp.nbytes,
+                                              an.ctypes.data if an is not None else None, chunk)
+        if used < 0:
+            raise MercuryAmdError("mfp_process_pipelined failed: " + _err(self.lib))
+        return rec, int(used), an
 
     def analyze_device(self, d_arena, d_desc, n, d_rec, d_fp, d_out, stream=0):
         r = self.lib.mfp_analyze_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out, stream)

@@ -31,6 +31,9 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
                                       unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
                                       hipStream_t stream, mfp_prof *prof);
 
+extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
+                                  unsigned long long *block_sum, hipStream_t stream, mfp_prof *prof);
+
 // fp-arena reservation granule of the wave kernel and its grid (mfp_kernels.hip)
 static const uint64_t kWaveChunk = 32 * 1024;
 static const uint64_t kWaveGridWaves = 2048 * 4;
@@ -213,26 +216,52 @@ void mfp_prof_end(mfp_prof *p, hipStream_t s) {
     p->pending.back().b = b;
 }
 
+// device scratch of one batch in flight: classify bins, classifier lists and
+// counters, and for host batches the staging copies of the batch itself.
+// Slot 0 serves the synchronous calls; slots 1 and 2 alternate in
+// mfp_process_pipelined, so two batches can be in flight on two streams.
+struct Slot {
+    unsigned long long *d_used = nullptr;   // fp arena counters of host batches
+    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass
+    uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list / bin ids
+    unsigned long long *d_an_stats = nullptr;
+    uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings (bitmap)
+    uint4 *d_deferred = nullptr; size_t cap_deferred = 0;    // packets for the wave-per-packet scorer (64 B each)
+    mfp_analysis *d_an = nullptr; size_t cap_an = 0;
+    uint8_t *d_arena = nullptr; size_t cap_arena = 0;
+    mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
+    mfp_record *d_rec = nullptr; size_t cap_rec = 0;
+    char *d_fp = nullptr; size_t cap_fp = 0;
+    char *d_fp2 = nullptr; size_t cap_fp2 = 0;   // dense (compacted) fingerprints of a host batch
+    unsigned long long *h_used = nullptr;   // pinned copy of d_used
+    hipStream_t stream = nullptr;
+
+    bool init() {
+        return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
+               hipMalloc(&d_bins, 8 * sizeof(unsigned long long)) == hipSuccess &&
+               hipMalloc(&d_an_stats, 4 * sizeof(unsigned long long)) == hipSuccess &&
+               hipMemset(d_an_stats, 0, 4 * sizeof(unsigned long long)) == hipSuccess &&
+               hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
+               hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
+    }
+    void release() {
+        void *p[] = {d_used, d_bins, d_work, d_an_stats, d_pending, d_deferred, d_an, d_arena, d_desc, d_rec, d_fp, d_fp2};
+        for (void *x : p) if (x) (void)hipFree(x);
+        if (h_used) (void)hipHostFree(h_used);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|wave|lane (A/B, debugging)
     uint32_t bin_wave_mask = 0xa;        // bins fingerprinted by the wave kernel (MFP_BIN_WAVE_MASK): HTTP req + resp
     uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
-    unsigned long long *d_used = nullptr;
-    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass
-    uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
-    unsigned long long *d_an_stats = nullptr;
-    mfp_analysis *d_an = nullptr; size_t cap_an = 0;
-    uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings of a batch
-    uint4 *d_deferred = nullptr; size_t cap_deferred = 0;    // packets for the wave-per-packet scorer (64 B each)
-    // host-batch staging buffers (grown on demand)
-    uint8_t *d_arena = nullptr; size_t cap_arena = 0;
-    mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
-    mfp_record *d_rec = nullptr; size_t cap_rec = 0;
-    char *d_fp = nullptr; size_t cap_fp = 0;
-    hipStream_t stream = nullptr;
+    Slot slot[3];
+    int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
+    hipEvent_t an_done = nullptr;        // last classifier launch (pipeline: stream order across slots)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
     std::mutex mu;
 };
@@ -266,11 +295,12 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     if (bm) c->bin_wave_mask = (uint32_t)strtoul(bm, nullptr, 0);
     const char *lm = getenv("MFP_AN_LANE_MAX_P");
     if (lm) c->an_lane_max_p = (uint32_t)strtoul(lm, nullptr, 0);
-    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_used, 4 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->d_bins, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    bool ok = hipSetDevice(device) == hipSuccess &&
+              hipEventCreateWithFlags(&c->an_done, hipEventDisableTiming) == hipSuccess;
+    for (Slot &S : c->slot) ok = ok && S.init();
+    if (!ok) {
         mfp_set_error("device init failed");
-        delete c;
+        mfp_finalize(c);
         return nullptr;
     }
     if (analysis && !resources.empty()) {
@@ -283,8 +313,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
             mfp_classifier_free(clf);
         } else {
             c->tls_format = (uint32_t)mfp_classifier_tls_format(clf);
-            if (mfp_classifier_upload(clf, device) != 0 ||
-                hipMalloc(&c->d_an_stats, 4 * sizeof(unsigned long long)) != hipSuccess) {
+            if (mfp_classifier_upload(clf, device) != 0) {
                 mfp_classifier_free(clf);
                 mfp_finalize(c);
                 return nullptr;
@@ -299,10 +328,9 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->clf) mfp_classifier_free(c->clf);
-    (void)hipFree(c->d_an_stats); (void)hipFree(c->d_an); (void)hipFree(c->d_pending); (void)hipFree(c->d_deferred);
-    (void)hipFree(c->d_used); (void)hipFree(c->d_bins); (void)hipFree(c->d_work); (void)hipFree(c->d_arena); (void)hipFree(c->d_desc); (void)hipFree(c->d_rec); (void)hipFree(c->d_fp);
+    for (Slot &S : c->slot) S.release();
+    if (c->an_done) (void)hipEventDestroy(c->an_done);
     delete c->prof;
-    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -336,22 +364,43 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_work, c->cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->slot[0].d_work, c->slot[0].cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     return 0;
 }
 
-static int process_device_locked(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
+static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
                                  hipStream_t s) {
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_work, c->cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(S.d_work, S.cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(c->d_bins, 0, 8 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(S.d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
-                               fp_cap, (unsigned long long *)d_fp_used, c->d_work, c->d_bins, c->strategy, c->bin_wave_mask, s, c->prof) != 0) {
+                               fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
+                               c->bin_wave_mask, s, c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
+    return 0;
+}
+
+static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
+                          mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, hipStream_t s) {
+    Slot &S = c->slot[slot];
+    HIPCHK(hipSetDevice(c->device));
+    if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_deferred, S.cap_deferred, 4 * (n + 1))) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
+    mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
+    D->batch++;                                   // stream order across batches (fingerprint_prevalence)
+    HIPCHK(hipMemsetAsync(S.d_an_stats, 0, 4 * sizeof(unsigned long long), s));
+    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, S.d_pending,
+                            S.d_deferred, S.d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
+        mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -3;
+    }
+    c->an_slot = slot;
     return 0;
 }
 
@@ -360,35 +409,130 @@ extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t 
                                                    uint64_t *d_fp_used, void *stream) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    return process_device_locked(c, d_arena, d_desc, n, d_rec, d_fp_arena, fp_cap, d_fp_used, (hipStream_t)stream);
+    return process_device_locked(c, c->slot[0], d_arena, d_desc, n, d_rec, d_fp_arena, fp_cap, d_fp_used,
+                                 (hipStream_t)stream);
+}
+
+// copy a host batch into slot `slot` (grown as needed) and launch its kernels
+// on the slot's stream; descriptors keep their offsets: the device arena
+// pointer handed to the kernels is the staging buffer minus the (256-byte
+// aligned) start of the copied span
+static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                            size_t n, size_t fp_cap, bool analysis) {
+    Slot &S = c->slot[slot];
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (size_t i = 0; i < n; i++) {
+        lo = std::min<uint64_t>(lo, desc[i].offset);
+        hi = std::max<uint64_t>(hi, desc[i].offset + desc[i].caplen);
+    }
+    if (n == 0) lo = hi = 0;   // (a capture ring hands packets in arena order; this scan is a few ms per 1M)
+    lo &= ~(uint64_t)255;
+    if (hi > arena_len) { mfp_set_error("descriptor past the end of the arena"); return -1; }
+    const uint64_t span = hi - lo;
+    // 64 bytes of padding after the span: the kernels read the aligned block
+    // that holds a packet's last byte
+    if (grow(S.d_arena, S.cap_arena, span + 64) || grow(S.d_desc, S.cap_desc, n + 1) || grow(S.d_rec, S.cap_rec, n + 1) ||
+        grow(S.d_fp, S.cap_fp, fp_cap + 64) || grow(S.d_fp2, S.cap_fp2, fp_cap + 64) ||
+        (analysis && grow(S.d_an, S.cap_an, n + 1))) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
+    const uint64_t copy = std::min<uint64_t>(span + 16, arena_len - lo);
+    if (copy) HIPCHK(hipMemcpyAsync(S.d_arena, arena + lo, copy, hipMemcpyHostToDevice, S.stream));
+    if (n) HIPCHK(hipMemcpyAsync(S.d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, S.stream));
+    const uint8_t *d_base = S.d_arena - lo;
+    int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, fp_cap, (uint64_t *)S.d_used, S.stream);
+    if (r) return r;
+    if (analysis) {
+        if (slot != 0) HIPCHK(hipStreamWaitEvent(S.stream, c->an_done, 0));   // classifier stream order
+        r = analyze_locked(c, slot, d_base, S.d_desc, n, S.d_rec, S.d_fp, S.d_an, S.stream);
+        if (r) return r;
+        HIPCHK(hipEventRecord(c->an_done, S.stream));
+    }
+    // strings to a dense arena in packet order (d_fp2, d_used[2] bytes), records re-pointed;
+    // the bin lists in d_work are dead by now and hold the scan scratch
+    if (mfp_launch_compact(S.d_rec, n, (const uint8_t *)S.d_fp, (uint8_t *)S.d_fp2, S.d_work,
+                           (unsigned long long *)(S.d_work + ((n + 3) & ~(size_t)1)), S.stream, c->prof) != 0) {
+        mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -3;
+    }
+    return 0;
+}
+
+extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const uint8_t *arena, size_t arena_len,
+                                                          const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                                          char *fp_arena, size_t fp_cap, mfp_analysis *analysis) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    if (analysis && !c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
+    Slot &S = c->slot[0];
+    int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, analysis != nullptr);
+    if (r) return r;
+    if (analysis && n) HIPCHK(hipMemcpyAsync(analysis, S.d_an, n * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
+    if (n) HIPCHK(hipMemcpyAsync(rec, S.d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    const unsigned long long used = S.h_used[2];   // dense bytes
+    if (S.h_used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    if (used) HIPCHK(hipMemcpy(fp_arena, S.d_fp2, used, hipMemcpyDeviceToHost));
+    return (long long)used;
 }
 
 extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                        const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                        char *fp_arena, size_t fp_cap) {
+    return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, nullptr);
+}
+
+extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8_t *arena, size_t arena_len,
+                                                      const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                                      char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                                      size_t chunk) {
     if (!c) { mfp_set_error("null context"); return -1; }
+    if (analysis && !c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
-    // 16 bytes of padding after the arena: the kernel may read the aligned
-    // word that contains a packet's last byte
-    if (grow(c->d_arena, c->cap_arena, arena_len + 64) || grow(c->d_desc, c->cap_desc, n + 1) ||
-        grow(c->d_rec, c->cap_rec, n + 1) || grow(c->d_fp, c->cap_fp, fp_cap + 64)) {
-        mfp_set_error("device allocation failed");
-        return -2;
+    if (chunk == 0) chunk = (size_t)1 << 20;
+    struct Inflight { bool live; size_t lo, hi; };
+    Inflight inf[2] = {{false, 0, 0}, {false, 0, 0}};
+    uint64_t fp_base = 0;
+    // wait for the chunk in pipeline slot s, queue the copy of its packed
+    // fingerprints to the caller's arena (chunk order; the slot's next chunk
+    // queues behind it on the same stream) and rebase its records
+    auto retire = [&](int s) -> int {
+        Slot &S = c->slot[1 + s];
+        HIPCHK(hipStreamSynchronize(S.stream));
+        const unsigned long long used = S.h_used[2];   // dense bytes
+        if (S.h_used[1] || fp_base + used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+        if (used) HIPCHK(hipMemcpyAsync(fp_arena + fp_base, S.d_fp2, used, hipMemcpyDeviceToHost, S.stream));
+        for (size_t i = inf[s].lo; i < inf[s].hi; i++) rec[i].fp_offset += fp_base;
+        fp_base += used;
+        inf[s].live = false;
+        return 0;
+    };
+    const size_t nch = (n + chunk - 1) / chunk;
+    for (size_t k = 0; k < nch; k++) {
+        const int s = (int)(k & 1);
+        Slot &S = c->slot[1 + s];
+        if (inf[s].live) { int r = retire(s); if (r) return r; }
+        const size_t lo = k * chunk, hi = std::min(n, lo + chunk), m = hi - lo;
+        uint64_t bytes = 0;
+        for (size_t i = lo; i < hi; i++) bytes += desc[i].caplen;
+        const size_t cap = mfp_fp_arena_bound(m, bytes);
+        int r = stage_and_launch(c, 1 + s, arena, arena_len, desc + lo, m, cap, analysis != nullptr);
+        if (r) return r;
+        if (analysis) HIPCHK(hipMemcpyAsync(analysis + lo, S.d_an, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipMemcpyAsync(rec + lo, S.d_rec, m * sizeof(mfp_record), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
+        inf[s] = {true, lo, hi};
     }
-    HIPCHK(hipMemcpyAsync(c->d_arena, arena, arena_len, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, c->stream));
-    int r = process_device_locked(c, c->d_arena, c->d_desc, n, c->d_rec, c->d_fp, fp_cap, (uint64_t *)c->d_used,
-                                  c->stream);
-    if (r) return r;
-    unsigned long long used[4];
-    HIPCHK(hipMemcpyAsync(used, c->d_used, sizeof used, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(rec, c->d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
-    if (used[0]) HIPCHK(hipMemcpy(fp_arena, c->d_fp, used[0], hipMemcpyDeviceToHost));
-    return (long long)used[0];
+    // the older of the (up to) two chunks still in flight first
+    if (nch >= 2 && inf[nch & 1].live) { int r = retire((int)(nch & 1)); if (r) return r; }
+    for (int s = 0; s < 2; s++) if (inf[s].live) { int r = retire(s); if (r) return r; }
+    for (int s = 0; s < 2; s++) HIPCHK(hipStreamSynchronize(c->slot[1 + s].stream));   // the last string copies
+    return (long long)fp_base;
 }
 
 // ---------------------------------------------------------------------------
@@ -402,41 +546,7 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     if (!c) { mfp_set_error("null context"); return -1; }
     if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipSetDevice(c->device));
-    if (grow(c->d_pending, c->cap_pending, n + 1) || grow(c->d_deferred, c->cap_deferred, 4 * (n + 1))) {
-        mfp_set_error("device allocation failed");
-        return -2;
-    }
-    mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
-    D->batch++;                                   // stream order across batches (fingerprint_prevalence)
-    HIPCHK(hipMemsetAsync(c->d_an_stats, 0, 4 * sizeof(unsigned long long), s));
-    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, c->d_pending,
-                            c->d_deferred, c->d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
-        mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-        return -3;
-    }
-    return 0;
-}
-
-extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const uint8_t *arena, size_t arena_len,
-                                                          const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
-                                                          char *fp_arena, size_t fp_cap, mfp_analysis *analysis) {
-    long long used = mfp_process_batch_host(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap);
-    if (used < 0 || !analysis) return used;
-    if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        HIPCHK(hipSetDevice(c->device));
-        if (grow(c->d_an, c->cap_an, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
-    }
-    int r = mfp_analyze_batch_device(c, c->d_arena, c->d_desc, n, c->d_rec, c->d_fp, c->d_an, c->stream);
-    if (r) return r;
-    std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(hipMemcpyAsync(analysis, c->d_an, n * sizeof(mfp_analysis), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(rec, c->d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return used;
+    return analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, (hipStream_t)stream);
 }
 
 extern "C" MFP_EXPORT const char *mfp_process_name(mfp_context c, uint32_t id) {
@@ -451,7 +561,7 @@ extern "C" MFP_EXPORT int mfp_analysis_stats(mfp_context c, uint64_t out[4]) {
     if (!c || !c->clf) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
     unsigned long long h[4];
-    HIPCHK(hipMemcpy(h, c->d_an_stats, sizeof h, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h, c->slot[c->an_slot].d_an_stats, sizeof h, hipMemcpyDeviceToHost));
     unsigned long long seen = 0;
     HIPCHK(hipMemcpy(&seen, mfp_classifier_device(c->clf)->seen_count, sizeof seen, hipMemcpyDeviceToHost));
     out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = seen;

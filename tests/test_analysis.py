@@ -193,3 +193,38 @@ def test_analysis_stream_order_across_batches():
     names = out[0][2] + out[1][2]
     bad = compare(ref, rec, an, names)
     assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [1000, 4096, 0])
+def test_pipelined_host_path_vs_reference(chunk):
+    """mfp_process_pipelined: the batch in chunks on two streams (copies and
+    kernels overlapped) gives the reference's fingerprints and classifier
+    results, stream order of the unknown-TLS set included."""
+    a, d = synth_batch()
+    ref = load_ref_an("an_synth.tsv.gz")
+    cfg = f"select={SELECT};resources={os.path.join(GOLD, 'synth_resources.tgz')};analysis"
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        rec, used, an = ctx.process_pipelined(a, d, chunk=chunk, analysis=True)
+        names = [ctx.process_name(int(p)) for p in an["process"]]
+        ctx2 = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+        try:
+            rec1, fp1, _ = ctx2.process_host_analysis(a, d)
+        finally:
+            ctx2.close()
+    finally:
+        ctx.close()
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+    fp = np.zeros(0, np.uint8)
+    # strings: identical to the single-batch host path
+    ctx3 = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        out = (np.zeros(len(d), mercury_amd.RECORD_DTYPE), np.zeros(ctx3.fp_arena_bound(d), np.uint8), None)
+        rec3, used3, _ = ctx3.process_pipelined(a, d, chunk=chunk, out=out)
+        fp = out[1][:used3].tobytes()
+    finally:
+        ctx3.close()
+    assert mercury_amd.fingerprints(rec3, fp) == mercury_amd.fingerprints(rec1, fp1)
+    assert (rec3["fp_type"] == rec1["fp_type"]).all() and (rec3["flags"] == rec1["flags"]).all()

@@ -1,0 +1,97 @@
+"""Multi-GPU sharding logic (mercury_amd/shard.py) on the CPU: contiguous
+shards, rebased host batches, and the world_size-2 gather / max-over-ranks
+path over gloo.  Each rank fingerprints its shard with the C oracle (test
+infrastructure standing in for the GPU) and rank 0 checks that the merged
+shards equal the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from mercury_amd import shard
+from mercury_amd.api import RECORD_DTYPE
+from oracle import oracle
+from tests import synth
+
+
+def test_shard_bounds_cover_exactly():
+    for n in (0, 1, 7, 64, 1000, 1001):
+        for world in (1, 2, 3, 8):
+            spans = [shard.shard_bounds(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.shard_bounds(10, 2, 2)
+
+
+def oracle_records(arena, desc):
+    """Records + fp arena of a host batch from the C oracle (test stand-in for the GPU)."""
+    ft, fl, flags, strs = oracle.process_batch(arena, desc, oracle.config())
+    rec = np.zeros(len(desc), RECORD_DTYPE)
+    blob, off = [], 0
+    for i, s in enumerate(strs):
+        b = s.encode("latin-1")
+        rec["fp_offset"][i] = off
+        rec["fp_len"][i] = len(b)
+        rec["fp_type"][i] = ft[i]
+        rec["flags"][i] = flags[i]
+        blob.append(b)
+        off += len(b)
+    return rec, b"".join(blob)
+
+
+def test_shard_batch_rebased_equals_whole():
+    arena, desc = synth.batch(3000, seed=0x5EED0003, workload="mixed", n_templates=256)
+    want = oracle.process_batch(arena, desc, oracle.config())[3]
+    parts = []
+    for r in range(3):
+        a, d, lo = shard.shard_batch(arena, desc, r, 3)
+        assert lo == shard.shard_bounds(len(desc), r, 3)[0]
+        parts.append(oracle_records(a, d))
+    rec, fp = shard.merge_shards(parts)
+    got = [fp[int(o):int(o) + int(n)].decode("latin-1") for o, n in zip(rec["fp_offset"], rec["fp_len"])]
+    assert got == want
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        arena, desc = synth.batch(2000, seed=0x5EED0003, workload="mixed", n_templates=256)
+        a, d, _ = shard.shard_batch(arena, desc, rank, world)
+        rec, fp = oracle_records(a, d)
+        t = shard.max_over_ranks(0.5 + rank)
+        merged = shard.gather_shards(rec, fp)
+        if rank == 0:
+            want = oracle.process_batch(arena, desc, oracle.config())[3]
+            got = [merged[1][int(o):int(o) + int(n)].decode("latin-1")
+                   for o, n in zip(merged[0]["fp_offset"], merged[0]["fp_len"])]
+            q.put((got == want, t, len(merged[0])))
+        else:
+            q.put((merged is None, t, 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_and_max():
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for ok, _, _ in res)
+    assert all(t == 1.5 for _, t, _ in res)          # max over ranks
+    assert max(n for _, _, n in res) == 2000
