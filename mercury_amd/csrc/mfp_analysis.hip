@@ -419,10 +419,16 @@ constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.
 //     applied feature by feature as LDS scatters (one update per process per
 //     list, so a feature is one conflict-free scatter and each process sees
 //     the reference's addition order), max / second max, fp32 softmax, result.
-constexpr uint32_t PL = 32;       // phase L: fingerprints with at most PL processes, scored lane per packet
-constexpr int AW = 2;             // waves per k_analyze block (LDS: 16 KiB of score rows per wave)
+#ifndef MFP_AN_PL
+#define MFP_AN_PL 16
+#endif
+#ifndef MFP_AN_MINW
+#define MFP_AN_MINW 4
+#endif
+constexpr uint32_t PL = MFP_AN_PL;   // phase L: fingerprints with at most PL processes, scored lane per packet
+constexpr int AW = 2;                // waves per k_analyze block (LDS: PL * 512 bytes of score rows per wave)
 
-__global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
+__global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
     __shared__ double sc_lds[AW][64 * PL];   // per wave: phase L's lane-private score rows S[p][lane]
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
