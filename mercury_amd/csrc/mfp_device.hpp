@@ -153,6 +153,10 @@ struct Em {
         acc = 0;
     }
     DEV void flush_word(uint32_t upto) {       // write bytes [lead, upto) of word
+#ifdef MFP_PROBE_NOSTORE
+        if (acc == 0x0123456789abcdefull) *(volatile uint8_t *)word = 0;   // keep the value live
+        return;
+#endif
         if (lead == 0 && upto == 8) {
             *(uint64_t *)word = acc;
         } else {
@@ -191,6 +195,10 @@ struct Em {
         if (!p || len <= 0) return;
         last_putc = false;
         if (!EMIT) { n += (uint32_t)(2 * len); return; }
+#ifdef MFP_PROBE_NOHEXLOAD
+        for (long i = 0; i < len; i++) push(hex2((uint32_t)i), 2);
+        return;
+#endif
         long i = 0;
         for (; i + 4 <= len; i += 4) {
             uint64_t v = hex2(ld(p + i)) | (hex2(ld(p + i + 1)) << 16) | (hex2(ld(p + i + 2)) << 32) |

@@ -36,7 +36,10 @@ struct KParams {
 // packets.  Used as the fallback lane of k_wave_fp (packets larger than the
 // wave kernel's LDS staging buffer, or whose fingerprint overflows its segment
 // table); with idx == nullptr it processes the whole batch.
-__global__ __launch_bounds__(TILE) void k_fingerprint(KParams P) {
+#ifndef MFP_LANE_MINW
+#define MFP_LANE_MINW 4      // 4 waves per SIMD: measured best for the TLS CH and mixed bins
+#endif
+__global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) {
     // per-lane extension scratch for TLS formats 1/2 (dynamic: 0 bytes for
     // format 0, so the default path keeps full occupancy)
     extern __shared__ uint32_t dyn_lds[];
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, ui
 #include "mfp_internal.h"
 #define MFP_WAVE_GRID 2048   // 8 workgroups of 4 waves per CU x 256 CUs
 #ifndef MFP_WAVE_MINW
-#define MFP_WAVE_MINW 4      // min waves per SIMD (caps VGPRs at 128)
+#define MFP_WAVE_MINW 8      // min waves per SIMD (caps VGPRs at 64; measured best for the HTTP bins)
 #endif
 
 namespace mfpw {
