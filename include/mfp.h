@@ -113,9 +113,9 @@ MFP_EXPORT void mfp_finalize(mfp_context ctx);
  * [1] overflow flag (arena too small: records without strings), [2] string
  * bytes written (sum of fp_len), [3] packets handled by the fallback lane.
  * Packets are read with aligned 16-byte loads: the 16-byte block holding a
- * packet's last byte must be readable.  d_fp_arena must be 16-byte aligned
- * (every string starts on a 16-byte boundary and is written in whole 16-byte
- * blocks).  `stream` is a hipStream_t (NULL =
+ * packet's last byte must be readable.  d_fp_arena must be 256-byte aligned
+ * (as hipMalloc returns): strings start on 16- or 64-byte boundaries and are
+ * written in whole 16-byte blocks.  `stream` is a hipStream_t (NULL =
  * default stream).  Asynchronous; returns 0 or a negative error.  For no
  * overflow fp_cap must be >= mfp_fp_arena_bound(n, total caplen). */
 MFP_EXPORT int mfp_process_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,

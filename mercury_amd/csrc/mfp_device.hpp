@@ -33,6 +33,59 @@ DEV Cur cmk(const uint8_t *d, const uint8_t *e) { Cur c; c.d = d; c.e = e; retur
 
 DEV uint32_t ld(const uint8_t *p) { return *p; }
 
+// Multi-byte reads from the aligned dwords that hold the bytes: a lane reads
+// its own packet, so every load instruction touches 64 different lines and the
+// texture-address unit, not HBM, sets the pace -- fewer, wider loads.
+// Only dwords holding requested bytes are read (a packet's last aligned
+// block is readable, include/mfp.h).
+// big-endian value of n (1..4) bytes at p
+DEV uint32_t ld_be32n(const uint8_t *p, int n) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t lo = q[0];
+    const uint32_t hi = sh + (uint32_t)n > 4 ? q[1] : 0u;
+    const uint32_t le = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh)) : lo;   // p[0] in bits 0..7
+    return __builtin_bswap32(le) >> (32 - 8 * n);
+}
+DEV uint64_t ld_be(const uint8_t *p, int n) {          // n = 1..8
+    if (n <= 4) return ld_be32n(p, n);
+    return ((uint64_t)ld_be32n(p, 4) << (8 * (n - 4))) | ld_be32n(p + 4, n - 4);
+}
+// consecutive little-endian 4-byte groups of p[0, len): one aligned dword
+// load per group
+struct LeStream {
+    const uint32_t *q;
+    uint32_t sh, prev;
+    long left;
+    DEV void init(const uint8_t *p, long len) {
+        const uintptr_t a = (uintptr_t)p;
+        q = (const uint32_t *)(a & ~(uintptr_t)3);
+        sh = (uint32_t)(a & 3) * 8;
+        left = len;
+        prev = len > 0 ? q[0] : 0u;
+    }
+    DEV uint32_t next() {                      // bytes past the end read as garbage; callers mask
+        const long take = left < 4 ? left : 4;
+        const bool need_hi = left > 4 || (sh && (long)(sh / 8) + take > 4);
+        const uint32_t hi = need_hi ? q[1] : 0u;
+        const uint32_t v = sh ? (prev >> sh) | (hi << (32 - sh)) : prev;
+        prev = hi;
+        q++;
+        left -= 4;
+        return v;
+    }
+};
+// 4 bytes (b0 lowest) -> 8 lowercase hex characters, little-endian (b0's high nibble first)
+DEV uint64_t hex4(uint32_t le) {
+    uint64_t x = le;
+    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+    const uint64_t nib = ((x >> 4) & 0x000f000f000f000full) | ((x & 0x000f000f000f000full) << 8);
+    const uint64_t gt9 = ((nib + 0x7676767676767676ull) & 0x8080808080808080ull) >> 7;
+    return nib + 0x3030303030303030ull + gt9 * 0x27;
+}
+
 DEV bool cskip(Cur &c, long n) {                       // datum::skip datum.h:365
     if (!c.d) return false;
     if (n > c.e - c.d) { c.d = c.e; return false; }
@@ -52,8 +105,7 @@ DEV void cparse_soft(Cur &dst, Cur &r, long n) {       // datum::parse_soft_fail
 }
 DEV bool rd_uint(Cur &c, int n, uint64_t &out) {      // datum::read_uint datum.h:795
     if (c.d && c.d + n <= c.e) {
-        uint64_t v = 0;
-        for (int i = 0; i < n; i++) v = (v << 8) | ld(c.d + i);
+        const uint64_t v = ld_be(c.d, n);
         c.d += n; out = v; return true;
     }
     cset_null(c); out = 0; return false;
@@ -68,9 +120,7 @@ DEV uint32_t look_u8(Cur &c) {                         // datum::lookahead_uint8
 }
 DEV bool look_uint(Cur &c, int n, uint64_t &out) {    // datum::lookahead_uint datum.h:712
     if (c.d && c.d + n <= c.e) {
-        uint64_t v = 0;
-        for (int i = 0; i < n; i++) v = (v << 8) | ld(c.d + i);
-        out = v; return true;
+        out = ld_be(c.d, n); return true;
     }
     return false;
 }
@@ -137,43 +187,47 @@ struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
     static constexpr bool emit_pass() { return EMIT; }
-    // pass-2 write combining
-    uint8_t *out = nullptr;  // string start
-    uint64_t acc = 0;        // staged bytes of the current aligned word
-    uint32_t nacc = 0;       // bytes staged (including skipped lead bytes)
-    uintptr_t word = 0;      // aligned address of the staged word
-    uint32_t lead = 0;       // bytes of the first word not owned by us
+    // Pass-2 output.  The string starts 64-byte aligned and owns its slot
+    // rounded up to 64 bytes.  Bytes gather in `acc`; whole 8-byte words go
+    // to a per-lane 64-byte line in LDS, and a full line leaves as four
+    // 16-byte stores.  Lanes reach a word or line boundary at different
+    // pushes, so a store is issued for the lanes that have one; staging the
+    // line in LDS makes those (divergent) global stores 8x rarer than
+    // storing every word.
+    uint8_t *out = nullptr;  // next 64-byte line of the string
+    uint64_t *line = nullptr;   // this lane's LDS line (8 words)
+    uint64_t acc = 0;        // staged bytes of the current word
+    uint32_t nacc = 0;       // bytes in acc
+    uint32_t nw = 0;         // words in the LDS line
 
-    DEV void begin(uint8_t *o) {
+    DEV void begin(uint8_t *o, uint64_t *lds_line) {
         out = o;
-        uintptr_t a = (uintptr_t)o;
-        word = a & ~(uintptr_t)7;
-        lead = (uint32_t)(a & 7);
-        nacc = lead;
-        acc = 0;
+        line = lds_line;
+        acc = 0; nacc = 0; nw = 0;
     }
-    DEV void flush_word(uint32_t upto) {       // write bytes [lead, upto) of word
+    DEV void flush_line(uint32_t words) {       // first `words` words of the line -> out
 #ifdef MFP_PROBE_NOSTORE
-        if (acc == 0x0123456789abcdefull) *(volatile uint8_t *)word = 0;   // keep the value live
+        if (acc == 0x0123456789abcdefull) *(volatile uint8_t *)out = 0;   // keep the value live
         return;
 #endif
-        if (lead == 0 && upto == 8) {
-            *(uint64_t *)word = acc;
-        } else {
-            for (uint32_t i = lead; i < upto; i++) ((uint8_t *)word)[i] = (uint8_t)(acc >> (8 * i));
-        }
+        const uint4 *l4 = (const uint4 *)line;
+        uint4 *o4 = (uint4 *)out;
+        for (uint32_t k = 0; 2 * k < words; k++) o4[k] = l4[k];
     }
-    DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v
+    DEV void put_word() {
+        line[nw++] = acc;
+        if (nw == 8) { flush_line(8); out += 64; nw = 0; }
+    }
+    DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
         if (EMIT) {
-            uint32_t room = 8 - nacc;
+            const uint32_t room = 8 - nacc;
             if (k < room) {
                 acc |= v << (8 * nacc);
                 nacc += k;
             } else {
                 acc |= (room == 8) ? v : (v << (8 * nacc));
-                flush_word(8);
-                word += 8; lead = 0;
-                uint32_t rest = k - room;
+                put_word();
+                const uint32_t rest = k - room;
                 acc = rest ? (v >> (8 * room)) : 0;
                 nacc = rest;
             }
@@ -181,7 +235,10 @@ struct Em {
         n += k;
     }
     DEV void finish() {
-        if (EMIT && nacc > lead) flush_word(nacc);
+        if (EMIT) {
+            if (nacc) { line[nw++] = acc; nacc = 0; }
+            if (nw) flush_line(nw);
+        }
     }
     DEV void putc(uint32_t c) { push(c & 0xff, 1); last_putc = true; }
     DEV static uint64_t hex2(uint32_t b) {
@@ -199,13 +256,15 @@ struct Em {
         for (long i = 0; i < len; i++) push(hex2((uint32_t)i), 2);
         return;
 #endif
+        LeStream st;
+        st.init(p, len);
         long i = 0;
-        for (; i + 4 <= len; i += 4) {
-            uint64_t v = hex2(ld(p + i)) | (hex2(ld(p + i + 1)) << 16) | (hex2(ld(p + i + 2)) << 32) |
-                         (hex2(ld(p + i + 3)) << 48);
-            push(v, 8);
+        for (; i + 4 <= len; i += 4) push(hex4(st.next()), 8);
+        if (i < len) {
+            const uint64_t v = hex4(st.next());
+            const uint32_t k = (uint32_t)(len - i) * 2;       // 2, 4 or 6 characters
+            push(v & ((1ull << (8 * k)) - 1), k);
         }
-        for (; i < len; i++) push(hex2(ld(p + i)), 2);
     }
     DEV void hex16(uint32_t v) {                // append_uint16_hex buffer_stream.h:425
         last_putc = false;
@@ -231,7 +290,17 @@ DEV uint32_t degrease16(uint32_t x) {                   // degrease_uint16 tls.h
 template <class E>
 DEV void hex_degrease(E &b, const uint8_t *p, long len) {   // raw_as_hex_degrease tls.h:802
     if (len % 2) len--;
-    for (long i = 0; i < len; i += 2) b.hex16(degrease16((ld(p + i) << 8) | ld(p + i + 1)));
+    if (!E::emit_pass()) {                       // pass 1: lengths only
+        for (long i = 0; i < len; i += 2) b.hex16(0);
+        return;
+    }
+    LeStream st;
+    st.init(p, len);
+    for (long i = 0; i < len; i += 4) {
+        const uint32_t v = st.next();             // bytes i..i+3, little-endian
+        b.hex16(degrease16(((v & 0xff) << 8) | ((v >> 8) & 0xff)));
+        if (i + 2 < len) b.hex16(degrease16((((v >> 16) & 0xff) << 8) | (v >> 24)));
+    }
 }
 DEV bool is_static_ext(uint32_t t) {                    // static_extension_types tls.h:1000
     switch (t) {

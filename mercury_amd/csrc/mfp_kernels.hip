@@ -45,7 +45,8 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
     extern __shared__ uint32_t dyn_lds[];
     uint32_t *lds_key = dyn_lds;
     uint16_t *lds_off = (uint16_t *)(dyn_lds + MAX_LDS_EXT * TILE);
-    __shared__ uint32_t wave_tot[TILE / 64];
+    __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
+    __shared__ uint64_t out_line[TILE][8];   // pass-2 output staging, one 64-byte line per lane
     __shared__ unsigned long long tile_base;
 
     const int tid = threadIdx.x;
@@ -73,9 +74,10 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
         }
     }
 
-    // workgroup exclusive scan of len
+    // workgroup exclusive scan of the 64-byte slots (strings start 64-byte aligned)
     const int lane = tid & 63, wid = tid >> 6;
-    uint32_t incl = len;
+    const uint32_t slot = (len + 63) & ~63u;
+    uint32_t incl = slot;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         uint32_t y = __shfl_up(incl, d, 64);
@@ -90,11 +92,21 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
         if (w < wid) wbase += tt;
         total += tt;
     }
-    const uint32_t excl = wbase + incl - len;
+    const uint32_t excl = wbase + incl - slot;
+    // bytes written (fp_used[2]): the exact lengths
+    uint32_t lsum = len;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) lsum += __shfl_xor(lsum, d, 64);
+    if (lane == 0) wave_len[wid] = lsum;
+    __syncthreads();
     if (tid == 0) {
         unsigned long long b = total ? atomicAdd(&P.fp_used[0], (unsigned long long)total) : 0ull;
         if (b + total > P.fp_cap) { atomicExch(&P.fp_used[1], 1ull); b = ~0ull; }
-        else if (total) atomicAdd(&P.fp_used[2], (unsigned long long)total);
+        else if (total) {
+            uint32_t lt = 0;
+            for (int w = 0; w < TILE / 64; w++) lt += wave_len[w];
+            atomicAdd(&P.fp_used[2], (unsigned long long)lt);
+        }
         tile_base = b;
     }
     __syncthreads();
@@ -104,7 +116,7 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
     // pass 2: emit
     if (len && fits) {
         Em<true> e;
-        e.begin(P.fp_arena + base + excl);
+        e.begin(P.fp_arena + base + excl, out_line[tid]);
         Out o2;
         packet_walk(e, P.cfg, o2, data, dsc.caplen, dsc.linktype, lds_key + tid, lds_off + tid, TILE);
         e.finish();
