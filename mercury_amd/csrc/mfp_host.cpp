@@ -222,7 +222,7 @@ void mfp_prof_end(mfp_prof *p, hipStream_t s) {
 // mfp_process_pipelined, so two batches can be in flight on two streams.
 struct Slot {
     unsigned long long *d_used = nullptr;   // fp arena counters of host batches
-    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass
+    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass (8 bins)
     uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list / bin ids
     unsigned long long *d_an_stats = nullptr;
     uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings (bitmap)
@@ -364,7 +364,7 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->slot[0].d_work, c->slot[0].cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->slot[0].d_work, c->slot[0].cap_work, 10 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     return 0;
 }
 
@@ -372,7 +372,7 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
                                  hipStream_t s) {
     HIPCHK(hipSetDevice(c->device));
-    if (grow(S.d_work, S.cap_work, 7 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(S.d_work, S.cap_work, 10 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(S.d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,

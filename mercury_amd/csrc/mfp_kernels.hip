@@ -147,14 +147,17 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
 // protocol bins of the classify pass: each bin is then fingerprinted by its
 // own k_fingerprint launch over a compact index list, so the lanes of a wave
 // walk the same protocol (same parser, similar loop trip counts)
-constexpr int NBINS = 5;
+constexpr int NBINS = 8;
 DEV int msg_bin(uint32_t msg) {
     switch (msg) {
     case MFP_MSG_TLS_CH: return 0;
     case MFP_MSG_HTTP_REQ: return 1;
     case MFP_MSG_TCP_SYN: case MFP_MSG_TCP_SYNACK: return 2;
     case MFP_MSG_HTTP_RESP: return 3;
-    default: return 4;
+    case MFP_MSG_TLS_SH: case MFP_MSG_TLS_CERT: return 5;
+    case MFP_MSG_SSH_INIT: case MFP_MSG_SSH_KEX: return 6;
+    case MFP_MSG_DTLS_CH: case MFP_MSG_DTLS_SH: case MFP_MSG_DTLS_HVR: return 7;
+    default: return 4;   // no message of a selected protocol
     }
 }
 
@@ -424,15 +427,19 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
         bool any_wave = false;
         for (int b = 0; b < mfp::NBINS; b++) {
             static const char *const wave_name[mfp::NBINS] = {"k_wave_fp/tls_ch", "k_wave_fp/http_req",
-                "k_wave_fp/tcp_syn", "k_wave_fp/http_resp", "k_wave_fp/other"};
+                "k_wave_fp/tcp_syn", "k_wave_fp/http_resp", "k_wave_fp/other", "k_wave_fp/tls_sh",
+                "k_wave_fp/ssh", "k_wave_fp/dtls"};
             static const char *const lane_name[mfp::NBINS] = {"k_fingerprint/tls_ch", "k_fingerprint/http_req",
-                "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other"};
+                "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other", "k_fingerprint/tls_sh",
+                "k_fingerprint/ssh", "k_fingerprint/dtls"};
             if (bin_wave_mask & (1u << b)) {
                 W.idx = work + (uint64_t)b * n;
                 W.count = bin_count + b;
                 // the bin's protocol families only (others -> fallback lane)
-                auto kw = b == 0 ? mfpw::k_wave_fp<mfpw::SPEC_TLS>
+                auto kw = (b == 0 || b == 5) ? mfpw::k_wave_fp<mfpw::SPEC_TLS>
                         : (b == 1 || b == 3) ? mfpw::k_wave_fp<mfpw::SPEC_HTTP>
+                        : b == 6 ? mfpw::k_wave_fp<mfpw::SPEC_SSH>
+                        : b == 7 ? mfpw::k_wave_fp<mfpw::SPEC_DTLS>
                         : b == 2 ? mfpw::k_wave_fp<0u> : mfpw::k_wave_fp<mfpw::SPEC_ALL>;
                 MFP_LAUNCH(wave_name[b], kw, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
                 any_wave = true;
