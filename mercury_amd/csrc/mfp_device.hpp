@@ -136,23 +136,50 @@ DEV const uint8_t *cget_ptr(Cur &c, long n) {          // datum::get_pointer dat
 DEV void ctrim_to_length(Cur &c, long len) {           // datum::trim_to_length datum.h:383
     if (c.d && len <= (long)(c.e - c.d)) c.e = c.d + len;
 }
+// ---- SWAR byte classes: bit 7 of each byte of the result flags the byte.
+// Exact per byte (no borrow between bytes), so a masked-off byte cannot
+// raise a flag next to it.
+DEV uint64_t swar_zero(uint64_t x) {
+    return ~(((x & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | x) & 0x8080808080808080ull;
+}
+DEV uint64_t swar_eq(uint64_t w, uint32_t c) { return swar_zero(w ^ (0x0101010101010101ull * (c & 0xff))); }
+DEV uint64_t swar_upper(uint64_t w) {                  // 'A'..'Z'
+    const uint64_t x = w & 0x7f7f7f7f7f7f7f7full;
+    return (x + 0x3f3f3f3f3f3f3f3full) & ~(x + 0x2525252525252525ull) & ~w & 0x8080808080808080ull;
+}
+DEV uint64_t swar_alpha(uint64_t w) {                  // isalpha (ASCII)
+    const uint64_t x = (w | 0x2020202020202020ull) & 0x7f7f7f7f7f7f7f7full;
+    return (x + 0x1f1f1f1f1f1f1f1full) & ~(x + 0x0505050505050505ull) & ~w & 0x8080808080808080ull;
+}
+// first byte of [p, e) whose class flag is set, or e; one aligned 8-byte
+// load per 8 bytes (a lane scanning its own packet), words inside the range only
+template <class F>
+DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag) {
+    if (!p || p >= e) return e;
+    uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
+    uint64_t m = flag(*(const uint64_t *)a) & (~0ull << (8 * ((uintptr_t)p & 7)));
+    while (true) {
+        const uintptr_t in = (uintptr_t)e - a;         // bytes of this word inside the range
+        if (in < 8) m &= (1ull << (8 * in)) - 1;
+        if (m) return (const uint8_t *)(a + (__builtin_ctzll(m) >> 3));
+        a += 8;
+        if (a >= (uintptr_t)e) return e;
+        m = flag(*(const uint64_t *)a);
+    }
+}
 DEV void cparse_to_delim(Cur &dst, Cur &r, uint8_t delim) {   // datum::parse_up_to_delim datum.h:313
     if (!cnotempty(r)) { cset_null(r); cset_null(dst); return; }
     dst.d = r.d;
-    for (const uint8_t *p = r.d; p < r.e; p++) {
-        if (ld(p) == delim) { dst.e = r.d = p; return; }
-    }
+    const uint8_t *q = swar_find(r.d, r.e, [=](uint64_t w) { return swar_eq(w, delim); });
+    if (q < r.e) { dst.e = r.d = q; return; }
     dst.e = r.e;
 }
 DEV uint32_t cparse_to_delims(Cur &dst, Cur &r, uint8_t d1, uint8_t d2) {   // datum.h:328
     dst.d = r.d;
     if (r.d) {
-        while (r.d < r.e) {
-            uint32_t c = ld(r.d);
-            if (c == d1) { dst.e = r.d; return d1; }
-            if (c == d2) { dst.e = r.d; return d2; }
-            r.d++;
-        }
+        const uint8_t *q = swar_find(r.d, r.e, [=](uint64_t w) { return swar_eq(w, d1) | swar_eq(w, d2); });
+        r.d = q;
+        if (q < r.e) { dst.e = q; return ld(q); }
     }
     dst.e = r.e;
     return 0;
@@ -863,17 +890,34 @@ DEV uint64_t swar_tolower(uint64_t w) {
     return w | (upper >> 2);
 }
 
-// perfect_hash::lookup perfect_hash.h:256: exact ASCII-case-insensitive match
-DEV int name_lookup(const HdrName *tab, int ntab, Cur n) {
-    long l = clen(n);
+// perfect_hash::lookup perfect_hash.h:256: exact ASCII-case-insensitive
+// match -- the lowercased name as four packed words (aligned 8-byte loads of
+// the name's bytes) against the packed tables; returns the table index and
+// the entry's incl_value | capture << 8
+DEV int name_lookup(const HdrKey *tab, int ntab, Cur n, uint32_t &info) {
+    const long l = clen(n);
     if (l <= 0 || l > 32) return -1;
-    uint32_t c0 = c_tolower(ld(n.d));
+    const uintptr_t a = (uintptr_t)n.d & ~(uintptr_t)7;
+    const uint32_t sh = (uint32_t)((uintptr_t)n.d & 7) * 8;
+    const uintptr_t end = (uintptr_t)n.e;
+    uint64_t aw[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) aw[k] = a + 8 * k < end ? *(const uint64_t *)(a + 8 * k) : 0ull;
+    uint64_t nw[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint64_t w = sh ? (aw[k] >> sh) | (aw[k + 1] << (64 - sh)) : aw[k];
+        const long rem = l - 8 * k;
+        if (rem <= 0) w = 0;
+        else if (rem < 8) w &= (1ull << (8 * rem)) - 1;
+        nw[k] = swar_tolower(w);
+    }
     for (int i = 0; i < ntab; i++) {
-        if (tab[i].len != l || (uint8_t)tab[i].s[0] != c0) continue;
-        bool ok = true;
-        for (long j = 1; j < l; j++)
-            if (c_tolower(ld(n.d + j)) != (uint8_t)tab[i].s[j]) { ok = false; break; }
-        if (ok) return i;
+        const HdrKey &k = tab[i];
+        if (k.len == (uint32_t)l && k.w[0] == nw[0] && k.w[1] == nw[1] && k.w[2] == nw[2] && k.w[3] == nw[3]) {
+            info = k.info;
+            return i;
+        }
     }
     return -1;
 }
@@ -890,7 +934,7 @@ DEV bool http_delim(Cur &p, Cur del) {                  // delimiter(datum&, con
 template <class E>
 DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {
     Cur tmp = body;
-    const HdrName *tab = req ? k_req_names : k_resp_names;
+    const HdrKey *tab = req ? k_req_keys : k_resp_keys;
     int ntab = req ? N_REQ_NAMES : N_RESP_NAMES;
     while (true) {
         if (http_delim(tmp, delim)) break;
@@ -898,7 +942,8 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         if (!cnotempty(tmp)) { cset_null(tmp); }
         else {
             name.d = tmp.d; name.e = tmp.e;
-            for (const uint8_t *q = tmp.d; q < tmp.e; q++) if (ld(q) == ':') { name.e = q; tmp.d = q; break; }
+            const uint8_t *q = swar_find(tmp.d, tmp.e, [](uint64_t w) { return swar_eq(w, ':'); });
+            if (q < tmp.e) { name.e = q; tmp.d = q; }
         }
         if (tmp.d && tmp.e > tmp.d && ld(tmp.d) == ':') tmp.d++; else cset_null(tmp);
         while (tmp.d && tmp.d < tmp.e && (ld(tmp.d) == '\t' || ld(tmp.d) == ' ')) tmp.d++;
@@ -907,14 +952,15 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         http_delim(tmp, delim);
         hdr_body.e = value.e;
         if (cnull(tmp)) break;
-        int idx = name_lookup(tab, ntab, name);
+        uint32_t info = 0;
+        const int idx = name_lookup(tab, ntab, name, info);
         if (idx >= 0) {
             b.putc('(');
-            if (tab[idx].incl_value) b.hex(hdr_body.d, clen(hdr_body)); else b.hex(name.d, clen(name));
+            if (info & 0xff) b.hex(hdr_body.d, clen(hdr_body)); else b.hex(name.d, clen(name));
             b.putc(')');
             if (req) {
-                if (tab[idx].capture == 1 && cnull(host)) host = value;
-                if (tab[idx].capture == 2 && cnull(ua)) ua = value;
+                if ((info >> 8) == 1 && cnull(host)) host = value;
+                if ((info >> 8) == 2 && cnull(ua)) ua = value;
             }
         }
     }
@@ -991,7 +1037,7 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         cparse_to_delim(f1, p, ' ');
         long ml = clen(f1);
         if (ml < 3 || ml > 16) return false;
-        for (long i = 0; i < ml; i++) if (!c_isupper(ld(f1.d + i))) return false;
+        if (swar_find(f1.d, f1.e, [](uint64_t w) { return ~swar_upper(w) & 0x8080808080808080ull; }) < f1.e) return false;
         cskip(p, 1);
         cparse_to_delim(uri, p, ' ');
         cskip(p, 1);
@@ -1008,7 +1054,7 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         if (!cnotempty(f2)) return false;
     }
     Cur delim; delim.d = p.d;
-    while (p.d && p.d < p.e && !c_isalpha(ld(p.d))) p.d++;
+    if (p.d) p.d = swar_find(p.d, p.e, [](uint64_t w) { return swar_alpha(w); });
     delim.e = p.d;
     fp_type_prefix(b, req ? 3 : 4);
     b.putc('('); b.hex(f1.d, clen(f1)); b.putc(')');
