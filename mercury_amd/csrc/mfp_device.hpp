@@ -955,9 +955,11 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         uint32_t info = 0;
         const int idx = name_lookup(tab, ntab, name, info);
         if (idx >= 0) {
+#ifndef MFP_PROBE_LNOEMIT
             b.putc('(');
             if (info & 0xff) b.hex(hdr_body.d, clen(hdr_body)); else b.hex(name.d, clen(name));
             b.putc(')');
+#endif
             if (req) {
                 if ((info >> 8) == 1 && cnull(host)) host = value;
                 if ((info >> 8) == 2 && cnull(ua)) ua = value;

@@ -256,7 +256,7 @@ struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|wave|lane (A/B, debugging)
-    uint32_t bin_wave_mask = 0xa;        // bins fingerprinted by the wave kernel (MFP_BIN_WAVE_MASK): HTTP req + resp
+    uint32_t bin_wave_mask = 0x2;        // bins fingerprinted by the wave kernel (MFP_BIN_WAVE_MASK): HTTP requests
     uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
     Slot slot[3];
