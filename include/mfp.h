@@ -78,6 +78,10 @@ enum {
 enum {
     MFP_FLAG_EMIT      = 1,  /* the reference's write_json emits a record   */
     MFP_FLAG_TRUNCATED = 2,  /* reassembly_properties.truncated             */
+    MFP_FLAG_HASHED    = 4,  /* device arena: the string's 64-bit hash follows it
+                                at fp_offset + round_up(fp_len, 8) (the
+                                classifier's lookup key; cleared when the
+                                strings are packed for the host) */
 };
 
 enum {

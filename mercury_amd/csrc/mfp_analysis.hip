@@ -187,6 +187,13 @@ ADEV uint64_t lane_hash(const uint8_t *s, uint32_t len) {
     return hash_final(acc, len);
 }
 
+// the fingerprint's str_hash: stored after the string by the fingerprint
+// kernels (MFP_FLAG_HASHED, one 8-byte load) or computed here
+ADEV uint64_t fp_key(const mfp_record &r, const uint8_t *fp, uint32_t len) {
+    if (r.flags & MFP_FLAG_HASHED) return *(const uint64_t *)(fp + ((len + 7) & ~7u));
+    return lane_hash(fp, len);
+}
+
 ADEV bool lane_eq(const uint8_t *a, const uint8_t *b, uint32_t len) {
     for (uint32_t j0 = 0; 8 * j0 < len; j0 += LB) {
         uint64_t x[LB], y[LB];
@@ -475,7 +482,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
 #ifdef MFP_PROBE_AN_NOHASH
             fh = fl;
 #else
-            fh = lane_hash(fp, fl);
+            fh = fp_key(r, fp, fl);
 #endif
             w0 = word_at(fp, fl, 0);
             cid = cand_string_lane(D.fp_slots, D.fp_mask, fh, fl, coff);
@@ -904,7 +911,7 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
         mfp_analysis a = P.out[i];
         const mfp_record r = P.rec[i];
         const uint8_t *fp = P.fp_arena + r.fp_offset;
-        const uint64_t h = lane_hash(fp, r.fp_len);
+        const uint64_t h = fp_key(r, fp, r.fp_len);
         const mfp_classifier_dev &D = P.D;
         uint64_t k = h & (D.seen_cap - 1);
         bool first = false;

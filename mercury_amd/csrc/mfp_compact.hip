@@ -97,7 +97,10 @@ __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t 
                                 (uint32_t)__shfl((int)(uint32_t)dof, j, 64);
             for (uint32_t k = lane; k < lj; k += 64) dst[dj + k] = src[sj + k];
         }
-        if (i < n && len) rec[i].fp_offset = dof;
+        if (i < n && len) {
+            rec[i].fp_offset = dof;
+            rec[i].flags &= (uint8_t)~MFP_FLAG_HASHED;   // the hashes stay behind
+        }
     }
 }
 

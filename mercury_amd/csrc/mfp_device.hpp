@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "../../include/mfp.h"
+#include "mfp_common.hpp"
 
 namespace mfp {
 
@@ -213,6 +214,7 @@ template <bool EMIT>
 struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
+    static constexpr bool SEG = false;
     static constexpr bool emit_pass() { return EMIT; }
     // Pass-2 output.  The string starts 64-byte aligned and owns its slot
     // rounded up to 64 bytes.  Bytes gather in `acc`; whole 8-byte words go
@@ -306,6 +308,167 @@ struct Em {
     // valid iff no append truncated: end <= 8190, or 8191 reached by putc
     DEV bool valid() const { return n <= FP_MAX - 2 || (n == FP_MAX - 1 && last_putc); }
 };
+
+// ---------------------------------------------------------------------------
+// segment emitter (k_fp_seg): records an HTTP fingerprint as a list of
+// segments instead of bytes -- "(" hex(packet bytes) ")" is one segment, the
+// type prefix and bare parentheses point into a literal pool -- so that the
+// wave can expand the string afterwards with coalesced stores.  Anything an
+// HTTP fingerprint does not contain (other literals, hex16/hex8, raw pushes),
+// or a list longer than SEG_MAX, sets `ovf`: the packet goes to the fallback
+// lane kernel.  A segment is one u32: end character (13 bits), kind (2),
+// source offset in the packet or the pool (16).
+// ---------------------------------------------------------------------------
+constexpr int SEG_MAX = 24;
+enum : uint32_t { SK_POOL = 0, SK_HEX = 1, SK_HEXP = 3 };   // SK_HEXP: '(' hex ')'
+#define MFP_SEG_POOL "http_server/http/()"
+constexpr uint32_t POOL_HTTP_SERVER = 0, POOL_HTTP = 12, POOL_OPEN = 17, POOL_CLOSE = 18;
+DEV uint32_t seg_end(uint32_t s) { return s & 0x1fff; }
+DEV uint32_t seg_kind(uint32_t s) { return (s >> 13) & 3; }
+DEV uint32_t seg_src(uint32_t s) { return s >> 15; }
+
+struct SegEm {
+    static constexpr bool SEG = true;
+    static constexpr bool emit_pass() { return false; }
+    uint32_t n = 0;                     // characters produced
+    bool last_putc = false;
+    bool ovf = false;
+    const uint8_t *base;                // packet start: hex sources are offsets from it
+    uint32_t *seg;                      // this lane's list (LDS)
+    uint32_t nseg = 0;
+    bool open = false;                  // '(' produced, not yet stored
+    uint32_t sp_src = 0, sp_len = 0;    // hex bytes right after the open '(' (0 = none)
+
+    DEV SegEm(const uint8_t *b, uint32_t *s) : base(b), seg(s) {}
+    DEV void store(uint32_t kind, uint32_t src, uint32_t end) {
+        if (nseg >= (uint32_t)SEG_MAX) { ovf = true; return; }
+        seg[nseg++] = (end & 0x1fff) | (kind << 13) | (src << 15);
+    }
+    DEV void flush_open() {
+        if (!open) return;
+        if (sp_len) {
+            store(SK_POOL, POOL_OPEN, n - 2 * sp_len);
+            store(SK_HEX, sp_src, n);
+        } else {
+            store(SK_POOL, POOL_OPEN, n);
+        }
+        open = false; sp_len = 0;
+    }
+    DEV void putc(uint32_t c) {
+        c &= 0xff;
+        if (c == ')' && open) {                           // "(hex)" or "()"
+            if (sp_len) store(SK_HEXP, sp_src, n + 1);
+            else store(SK_POOL, POOL_OPEN, n + 1);
+            open = false; sp_len = 0;
+        } else {
+            flush_open();
+            if (c == '(') open = true;
+            else if (c == ')') store(SK_POOL, POOL_CLOSE, n + 1);
+            else ovf = true;
+        }
+        n += 1;
+        last_putc = true;
+    }
+    DEV void hex(const uint8_t *p, long len) {
+        if (!p || len <= 0) return;
+        last_putc = false;
+        const uint32_t src = (uint32_t)(p - base);
+        if (open && !sp_len) { sp_src = src; sp_len = (uint32_t)len; }
+        else { flush_open(); store(SK_HEX, src, n + 2 * (uint32_t)len); }
+        n += 2 * (uint32_t)len;
+    }
+    DEV void lit(const char *s) {
+        flush_open();
+        last_putc = false;
+        uint32_t k = 0;
+        while (s[k]) k++;
+        if (s[0] == 'h' && k == 5) store(SK_POOL, POOL_HTTP, n + 5);
+        else if (s[0] == 'h' && k == 12) store(SK_POOL, POOL_HTTP_SERVER, n + 12);
+        else ovf = true;
+        n += k;
+    }
+    DEV void hex16(uint32_t) { ovf = true; n += 4; last_putc = false; }
+    DEV void hex8(uint32_t) { ovf = true; n += 2; last_putc = false; }
+    DEV void push(uint64_t, uint32_t k) { ovf = true; n += k; }
+    DEV void finish() { flush_open(); }
+    DEV bool valid() const { return n <= FP_MAX - 2 || (n == FP_MAX - 1 && last_putc); }
+};
+
+DEV uint32_t hexch(uint32_t nib) { return nib + (nib < 10 ? '0' : 'a' - 10); }
+
+// XOR over the 64 lanes of a wave (every lane gets the result; all lanes active)
+DEV uint64_t wave_xor64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        lo ^= (uint32_t)__shfl_xor((int)lo, d, 64);
+        hi ^= (uint32_t)__shfl_xor((int)hi, d, 64);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave-cooperative expansion of one segment list (k_fp_seg): lane l writes
+// characters [512 r + 8 l, +8) of round r with one 8-byte store, and folds
+// its words into the string hash (mfpc::str_hash); returns this lane's part
+// of the hash accumulator (XOR over the wave gives the whole).  A lane whose
+// 8 characters are hex digits of one segment converts 4-5 source bytes with
+// one SWAR step; other lanes go character by character.
+DEV uint64_t seg_expand(const uint32_t *sg, uint32_t nseg, const uint8_t *pkt, uint32_t T, uint8_t *out,
+                        const uint8_t *pool, uint32_t lane) {
+    uint64_t h = 0;
+    for (uint32_t r0 = 0; r0 < T; r0 += 512) {
+        const uint32_t p0 = r0 + 8 * lane;
+        if (p0 >= T) continue;
+        uint32_t lo = 0, hi = nseg - 1;               // first segment ending after p0
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (seg_end(sg[mid]) > p0) hi = mid; else lo = mid + 1;
+        }
+        uint32_t s = lo, info = sg[s];
+        uint32_t s_end = seg_end(info), s_start = s ? seg_end(sg[s - 1]) : 0;
+        const uint32_t kind = seg_kind(info), q0 = p0 - s_start;
+        const uint32_t hq = kind == SK_HEXP ? q0 - 1 : q0;           // hex digit index
+        const uint32_t hend = kind == SK_HEXP ? s_end - 1 : s_end;    // end of the hex digits
+        uint64_t word = 0;
+        if (kind != SK_POOL && (kind != SK_HEXP || q0 >= 1) && p0 + 8 <= hend) {
+            const uintptr_t a = (uintptr_t)(pkt + seg_src(info) + (hq >> 1));
+            const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)(a & 3), nb = 4 + (hq & 1);
+            const uint32_t w0 = q[0];
+            const uint32_t w1 = sh + nb > 4 ? q[1] : 0u;
+            const uint64_t v = (((uint64_t)w1 << 32) | w0) >> (8 * sh);
+            const uint64_t x = hex4((uint32_t)v);
+            word = (hq & 1) ? (x >> 8) | (hex4((uint32_t)(v >> 32)) << 56) : x;
+        } else {
+            uintptr_t wa = ~(uintptr_t)0;
+            uint32_t wv = 0;
+            for (uint32_t k = 0; k < 8; k++) {
+                const uint32_t p = p0 + k;
+                if (p >= T) break;
+                if (p >= s_end) { s++; s_start = s_end; info = sg[s]; s_end = seg_end(info); }
+                const uint32_t kd = seg_kind(info), q = p - s_start;
+                uint32_t c;
+                if (kd == SK_POOL) {
+                    c = pool[seg_src(info) + q];
+                } else if (kd == SK_HEXP && q == 0) {
+                    c = '(';
+                } else if (kd == SK_HEXP && p == s_end - 1) {
+                    c = ')';
+                } else {
+                    const uint32_t hd = kd == SK_HEXP ? q - 1 : q;
+                    const uintptr_t a = (uintptr_t)(pkt + seg_src(info) + (hd >> 1));
+                    if ((a >> 2) != wa) { wa = a >> 2; wv = *(const uint32_t *)(a & ~(uintptr_t)3); }
+                    const uint32_t by = (wv >> (8 * (a & 3))) & 0xff;
+                    c = hexch((hd & 1) ? (by & 15) : (by >> 4));
+                }
+                word |= (uint64_t)c << (8 * k);
+            }
+        }
+        *(uint64_t *)(out + p0) = word;
+        h ^= mfpc::word_term(word, p0 >> 3);
+    }
+    return h;
+}
 
 // ---------------------------------------------------------------------------
 // TLS (tls.h)
@@ -1116,6 +1279,9 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
     }
     o.msg = msg;
     if (cfg.classify) return;
+    if constexpr (E::SEG) {
+        b.ovf = true;          // not an HTTP message: the fallback lane fingerprints it
+    } else {
     switch (msg) {
     case MFP_MSG_TLS_CH: {
         Cur p = pkt;
@@ -1215,6 +1381,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         return;
     }
     }
+    }
 }
 
 // set_udp_protocol pkt_proc.cc:677 (selection subset: DTLS, dtls.h)
@@ -1232,6 +1399,10 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, ui
     if (!msg) return;
     o.msg = msg;
     if (cfg.classify) return;
+    if constexpr (E::SEG) {
+        b.ovf = true;
+        return;
+    }
     Cur d = pkt, frag, body; cset_null(frag); cset_null(body);
     uint64_t t, len = 0, foff = 0, flen = 0, more = 0;
     if (clen(d) < 13) cset_null(d);
@@ -1363,6 +1534,7 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
                     o.msg = MFP_MSG_TCP_SYN;
                     if (cfg.classify) return;
                     o.flags |= MFP_FLAG_EMIT; o.fp_type = 7;
+                    if constexpr (E::SEG) { b.ovf = true; return; }
                     fp_type_prefix(b, 7);
                     tcp_syn_fp(b, ipv, iph, tcph, opts);
                 }
@@ -1373,6 +1545,7 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
                     o.msg = MFP_MSG_TCP_SYNACK;
                     if (cfg.classify) return;
                     o.flags |= MFP_FLAG_EMIT; o.fp_type = 13;
+                    if constexpr (E::SEG) { b.ovf = true; return; }
                     fp_type_prefix(b, 13);
                     tcp_syn_fp(b, ipv, iph, tcph, opts);
                 }

@@ -29,7 +29,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
-                                      hipStream_t stream, mfp_prof *prof);
+                                      uint32_t bin_seg_mask, hipStream_t stream, mfp_prof *prof);
 
 extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
                                   unsigned long long *block_sum, hipStream_t stream, mfp_prof *prof);
@@ -256,7 +256,11 @@ struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|wave|lane (A/B, debugging)
-    uint32_t bin_wave_mask = 0x2;        // bins fingerprinted by the wave kernel (MFP_BIN_WAVE_MASK): HTTP requests
+    // bin b -> kernel: k_fp_seg if bit b of bin_seg_mask (MFP_BIN_SEG_MASK; default the
+    // two HTTP bins), else k_wave_fp if bit b of bin_wave_mask (MFP_BIN_WAVE_MASK), else
+    // the lane kernel (A/B per bin: tools/gpu_masks.sh)
+    uint32_t bin_wave_mask = 0x0;
+    uint32_t bin_seg_mask = 0xa;
     uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
     Slot slot[3];
@@ -293,6 +297,8 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     else if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
     const char *bm = getenv("MFP_BIN_WAVE_MASK");
     if (bm) c->bin_wave_mask = (uint32_t)strtoul(bm, nullptr, 0);
+    const char *sm = getenv("MFP_BIN_SEG_MASK");
+    if (sm) c->bin_seg_mask = (uint32_t)strtoul(sm, nullptr, 0);
     const char *lm = getenv("MFP_AN_LANE_MAX_P");
     if (lm) c->an_lane_max_p = (uint32_t)strtoul(lm, nullptr, 0);
     bool ok = hipSetDevice(device) == hipSuccess &&
@@ -377,7 +383,7 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
     HIPCHK(hipMemsetAsync(S.d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
                                fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
-                               c->bin_wave_mask, s, c->prof) != 0) {
+                               c->bin_wave_mask, c->bin_seg_mask, s, c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
         r.fp_len = fits ? len : 0;
         r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
         r.msg = (uint8_t)o.msg;
-        r.flags = (uint8_t)o.flags;
+        r.flags = (uint8_t)o.flags;    // the lane kernel leaves hashing to the classifier
         r.status = 0;
         r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
         r.sni_len = (uint16_t)o.sni_len;
@@ -140,6 +140,138 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
         P.rec[i] = r;
     }
     __syncthreads();   // tile_base / wave_tot reuse
+    }
+}
+
+// k_fp_seg -- the HTTP bins: lane-per-packet walk (the lane walker's SWAR
+// scans and packed header-name lookup) that records the fingerprint as a
+// segment list in LDS (SegEm), one reservation per tile, then each wave
+// expands its packets' strings one after another with all 64 lanes: every
+// store instruction writes 512 consecutive bytes, where the lane kernel's
+// emission pass issues a divergent load/LDS/store stream per lane.  One walk
+// instead of two.  Packets whose fingerprint is not an HTTP one, or whose list
+// overflows SEG_MAX, go to the fallback lane kernel.
+#ifndef MFP_SEG_MINW
+#define MFP_SEG_MINW 4
+#endif
+constexpr int SEG_STRIDE = SEG_MAX + 1;   // odd word stride: lane-private lists are bank-conflict free
+__global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32_t *fallback) {
+    __shared__ uint32_t segs[TILE * SEG_STRIDE];
+    __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
+    __shared__ unsigned long long tile_base;
+    __shared__ uint8_t pool[32];
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    if (tid < 32) {
+        const char *lp = MFP_SEG_POOL;
+        pool[tid] = (uint8_t)(tid < (int)sizeof(MFP_SEG_POOL) ? lp[tid] : 0);
+    }
+    __syncthreads();
+    const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
+        const uint64_t t = tile * TILE + tid;
+        const bool live = t < count;
+        const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
+        mfp_pkt_desc dsc;
+        if (live) dsc = P.desc[i];
+        else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
+        const uint8_t *data = P.arena + dsc.offset;
+
+        Out o;
+        SegEm e(data, segs + tid * SEG_STRIDE);
+        packet_walk(e, P.cfg, o, data, dsc.caplen, dsc.linktype, nullptr, nullptr, 0);
+        e.finish();
+        const bool fb = live && e.ovf;
+        uint32_t len = 0;
+        if (!fb && o.fp_type) {
+            if (e.valid()) len = e.n;
+            else o.fp_type = 0;
+        }
+
+        // reservation: 16-byte aligned slots holding string + hash
+        const uint32_t slot = len ? (len + 8 + 15) & ~15u : 0u;
+        uint32_t incl = slot;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += y;
+        }
+        if (lane == 63) wave_tot[wid] = incl;
+        uint32_t lsum = len;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) lsum += __shfl_xor(lsum, d, 64);
+        if (lane == 0) wave_len[wid] = lsum;
+        __syncthreads();
+        uint32_t wbase = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < TILE / 64; w++) {
+            const uint32_t tt = wave_tot[w];
+            if ((uint32_t)w < wid) wbase += tt;
+            total += tt;
+        }
+        const uint32_t excl = wbase + incl - slot;
+        if (tid == 0) {
+            unsigned long long b = total ? atomicAdd(&P.fp_used[0], (unsigned long long)total) : 0ull;
+            if (b + total > P.fp_cap) { atomicExch(&P.fp_used[1], 1ull); b = ~0ull; }
+            else if (total) {
+                uint32_t lt = 0;
+                for (int w = 0; w < TILE / 64; w++) lt += wave_len[w];
+                atomicAdd(&P.fp_used[2], (unsigned long long)lt);
+            }
+            tile_base = b;
+        }
+        __syncthreads();
+        const unsigned long long base = tile_base;
+        const bool fits = base != ~0ull;
+
+        // packets for the fallback lane kernel
+        const uint64_t fbm = __ballot(fb);
+        if (fbm) {
+            uint32_t b = 0;
+            if (lane == 0) b = (uint32_t)atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(fbm));
+            b = (uint32_t)__shfl((int)b, 0, 64);
+            if (fb) fallback[b + __builtin_popcountll(fbm & ((1ull << lane) - 1))] = (uint32_t)i;
+        }
+
+        // wave-cooperative expansion, one packet at a time
+        uint64_t todo = fits ? __ballot(len != 0) : 0ull;
+#ifdef MFP_PROBE_SEG_NOEXPAND
+        todo = 0;
+#endif
+        const uint64_t dptr = (uint64_t)(uintptr_t)data;
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+            const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
+            const uint32_t ns = (uint32_t)__builtin_amdgcn_readlane((int)e.nseg, j);
+            const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dptr, j) |
+                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dptr >> 32), j) << 32);
+            uint8_t *out = P.fp_arena + base + ex;
+            uint64_t h = seg_expand(segs + (wid * 64 + j) * SEG_STRIDE, ns, (const uint8_t *)(uintptr_t)src, T, out,
+                                    pool, lane);
+            h = wave_xor64(h);
+            if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
+        }
+
+        if (live && !fb) {
+            mfp_record r;
+            r.fp_offset = fits ? base + excl : 0;
+            r.fp_len = fits ? len : 0;
+            r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
+            r.msg = (uint8_t)o.msg;
+            r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
+            r.status = 0;
+            r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
+            r.sni_len = (uint16_t)o.sni_len;
+            r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);
+            r.ua_len = (uint16_t)o.ua_len;
+            r.src_port = (uint16_t)o.src_port;
+            r.dst_port = (uint16_t)o.dst_port;
+            r.net = o.net;
+            P.rec[i] = r;
+        }
+        __syncthreads();   // tile_base / wave_tot / segs reuse
     }
 }
 
@@ -335,7 +467,7 @@ __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P
                     type = 0;                       // fingerprint::final drops truncated fingerprints
                 } else {
                     T = w.n;
-                    const uint64_t slot = (T + 15) & ~15u;
+                    const uint64_t slot = (T + 8 + 15) & ~15u;     // string + hash
                     if (!dead && cur + slot > end) {
                         uint64_t b = 0;
                         if (lane == 0) b = atomicAdd(&P.fp_used[0], (unsigned long long)CHUNK);
@@ -358,7 +490,7 @@ __global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P
             }
             if ((int)lane == j) {
                 r_off = fpo; r_len = T;
-                r_w2 = type | (w.o.msg << 8) | (w.o.flags << 16);
+                r_w2 = type | (w.o.msg << 8) | ((w.o.flags | (T ? MFP_FLAG_HASHED : 0u)) << 16);
                 r_sni = (w.o.sni_len == 0xffff ? 0 : (w.o.sni_off & 0xffff)) | (w.o.sni_len << 16);
                 r_ua = (w.o.ua_len == 0xffff ? 0 : (w.o.ua_off & 0xffff)) | (w.o.ua_len << 16);
                 r_ports = (w.o.src_port & 0xffff) | (w.o.dst_port << 16);
@@ -388,7 +520,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
-                                      hipStream_t stream, mfp_prof *prof) {
+                                      uint32_t bin_seg_mask, hipStream_t stream, mfp_prof *prof) {
 #define MFP_LAUNCH(name, ...)                                \
     do {                                                     \
         if (prof) mfp_prof_begin(prof, name, stream);        \
@@ -432,7 +564,17 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
             static const char *const lane_name[mfp::NBINS] = {"k_fingerprint/tls_ch", "k_fingerprint/http_req",
                 "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other", "k_fingerprint/tls_sh",
                 "k_fingerprint/ssh", "k_fingerprint/dtls"};
-            if (bin_wave_mask & (1u << b)) {
+            static const char *const seg_name[mfp::NBINS] = {"k_fp_seg/tls_ch", "k_fp_seg/http_req",
+                "k_fp_seg/tcp_syn", "k_fp_seg/http_resp", "k_fp_seg/other", "k_fp_seg/tls_sh",
+                "k_fp_seg/ssh", "k_fp_seg/dtls"};
+            if (bin_seg_mask & (1u << b)) {
+                // lane walk + wave expansion (HTTP; anything else -> fallback lane)
+                P.idx = work + (uint64_t)b * n;
+                P.count = bin_count + b;
+                MFP_LAUNCH(seg_name[b], mfp::k_fp_seg, dim3((uint32_t)fblocks), dim3(mfp::TILE), 0, stream, P,
+                           W.fallback);
+                any_wave = true;
+            } else if (bin_wave_mask & (1u << b)) {
                 W.idx = work + (uint64_t)b * n;
                 W.count = bin_count + b;
                 // the bin's protocol families only (others -> fallback lane)

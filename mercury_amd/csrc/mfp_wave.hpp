@@ -73,7 +73,7 @@ struct Cfg {
 };
 using mfp::SEL_TLS_CH; using mfp::SEL_TLS_SH; using mfp::SEL_TLS_CERT; using mfp::SEL_SSH_CLIENT;
 using mfp::SEL_SSH_SERVER; using mfp::SEL_HTTP_REQ; using mfp::SEL_HTTP_RESP; using mfp::SEL_TCP_SYN;
-using mfp::SEL_TCP_SYNACK; using mfp::SEL_DTLS;
+using mfp::SEL_TCP_SYNACK; using mfp::SEL_DTLS; using mfp::wave_xor64;
 
 // ---------------------------------------------------------------------------
 // the wave walker: parse state + segment emitter (buffer_stream semantics,
@@ -1593,11 +1593,14 @@ struct W {
     // cooperative expansion of the segment table into the fingerprint
     // string: lane l of round r writes characters [512 r + 8 l, +8)
     // =======================================================================
+    // ... and the string hash (mfpc::str_hash) of the words, stored after the
+    // string at round_up(T, 8) (include/mfp.h MFP_FLAG_HASHED)
     WDEV void expand(uint8_t *out) {
 #ifdef MFP_PROBE_NOEXPAND
         return;
 #endif
         const uint32_t T = n;
+        uint64_t hacc = 0;
         for (uint32_t r0 = 0; r0 < T; r0 += 512) {
             uint32_t p0 = r0 + 8 * lane;
             if (p0 < T) {
@@ -1638,8 +1641,11 @@ struct W {
                     word |= (uint64_t)c << (8 * k);
                 }
                 *(uint64_t *)(out + p0) = word;
+                hacc ^= mfpc::word_term(word, p0 >> 3);
             }
         }
+        hacc = wave_xor64(hacc);
+        if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(hacc, T);
     }
 };
 

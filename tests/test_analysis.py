@@ -143,12 +143,18 @@ def compare(ref, rec, an, names):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lane_max_p", [None, "0", "2"])
+@pytest.mark.parametrize("lane_max_p", [None, "0", "2", "seg", "lane"])
 def test_analysis_synthetic_archive_vs_reference(lane_max_p, monkeypatch):
     """lane_max_p: MFP_AN_LANE_MAX_P -- None = default split (lane-per-packet
     scoring for small P), "0" = every packet on the wave-per-packet scorer,
-    "2" = both kernels in one batch."""
-    if lane_max_p is not None:
+    "2" = both kernels in one batch.  "seg" / "lane": default scoring, HTTP
+    bins fingerprinted by k_fp_seg / every bin by the lane kernel (the
+    classifier reads the hash each fingerprint kernel stores)."""
+    if lane_max_p == "seg":
+        monkeypatch.setenv("MFP_BIN_SEG_MASK", "0xa")
+    elif lane_max_p == "lane":
+        monkeypatch.setenv("MFP_BIN_WAVE_MASK", "0x0")
+    elif lane_max_p is not None:
         monkeypatch.setenv("MFP_AN_LANE_MAX_P", lane_max_p)
     a, d = synth_batch()
     ref = load_ref_an("an_synth.tsv.gz")

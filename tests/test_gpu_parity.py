@@ -24,6 +24,26 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 CONTRACT = "tls,dtls,ssh,http,tcp,tcp.syn_ack"
 
 
+_M64 = (1 << 64) - 1
+
+
+def _mix64(x):
+    x ^= x >> 33
+    x = (x * 0xff51afd7ed558ccd) & _M64
+    x ^= x >> 33
+    x = (x * 0xc4ceb9fe1a85ec53) & _M64
+    return x ^ (x >> 33)
+
+
+def str_hash(s):
+    """mfpc::str_hash (mercury_amd/csrc/mfp_common.hpp)."""
+    acc = 0
+    for j in range(0, len(s), 8):
+        w = int.from_bytes(s[j:j + 8].ljust(8, b"\0"), "little")
+        acc ^= _mix64((w + (j // 8 + 1) * 0x9e3779b97f4a7c15) & _M64)
+    return _mix64(acc ^ ((len(s) * 0x2545f4914f6cdd1d) & _M64))
+
+
 def cfg_string(fmt):
     return CONTRACT if fmt == 0 else f"select={CONTRACT};format=tls/{fmt}"
 
@@ -119,6 +139,26 @@ def test_fuzzed_vs_oracle(fmt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wave_mask,seg_mask", [("0x0", "0x0"), ("0xff", "0x0"), ("0x0", "0xa"), ("0x0", "0xff")])
+def test_bin_kernel_choices_vs_oracle(wave_mask, seg_mask, monkeypatch):
+    """Every bin kernel (lane walker, wave walker, lane walk + wave expansion)
+    takes any packet (what it cannot fingerprint goes to the fallback lane):
+    one batch of synthetic + fuzzed packets under each assignment of kernels
+    to bins equals the oracle."""
+    from tests import pcaplib
+    monkeypatch.setenv("MFP_BIN_WAVE_MASK", wave_mask)
+    monkeypatch.setenv("MFP_BIN_SEG_MASK", seg_mask)
+    a2, d2 = synth.batch(6000, seed=0x5EED0042, workload="mixed", n_templates=1500)
+    pk = [(1, a2[int(d["offset"]):int(d["offset"]) + int(d["caplen"])].tobytes()) for d in d2]
+    pk += synth.fuzz(pk[:2000], 10000, seed=77)
+    fa, fd = pcaplib.make_batch(pk)
+    for fmt in (0, 2):
+        bad, rec = _compare(fa, fd, fmt)
+        assert not bad, f"fmt {fmt}: {len(bad)} mismatches, first {bad[:5]}"
+    assert (rec["fp_type"] == 3).sum() > 100 and (rec["fp_type"] == 4).sum() > 100
+
+
+@pytest.mark.gpu
 def test_analysis_mode_vs_oracle():
     """get_analysis_context semantics: no TCP SYN fingerprints (pkt_proc.cc:1624-1651)."""
     arena, desc = synth.batch(20000, seed=5, workload="mixed", n_templates=2000)
@@ -180,6 +220,15 @@ def test_large_device_batch_properties():
     srec = desc[sample]
     ft, fl, flags, want = oracle.process_batch(ua, ud[sample % len(ud)], oracle.config())
     assert got == want
+    # the classifier key stored after each string (MFP_FLAG_HASHED)
+    for k in sample[:300]:
+        r = rec[k]
+        o, ln = int(r["fp_offset"]), int(r["fp_len"])
+        if ln == 0:
+            continue
+        assert r["flags"] & 4
+        ho = o + ((ln + 7) & ~7)
+        assert int.from_bytes(fp_host[ho:ho + 8], "little") == str_hash(fp_host[o:o + ln])
     # replicas are identical: per-position fp_len pattern repeats
     assert np.array_equal(rec["fp_len"][:len(ud)], rec["fp_len"][-len(ud):])
     ctx.close()

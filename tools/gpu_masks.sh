@@ -1,6 +1,7 @@
 #!/bin/bash
-# parity tests, then fp-only bench per MFP_BIN_WAVE_MASK value in $MASKS
-# (bit b: bin b on the wave kernel; bins: 0 tls_ch 1 http_req 2 tcp_syn 3 http_resp 4 other)
+# parity tests, then fp-only bench per entry of $MASKS: WAVE or WAVE/SEG
+# (MFP_BIN_WAVE_MASK / MFP_BIN_SEG_MASK; bit b = bin b on that kernel; bins:
+# 0 tls_ch 1 http_req 2 tcp_syn 3 http_resp 4 other 5 tls_sh 6 ssh 7 dtls)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${TAG:-masks}
@@ -10,8 +11,10 @@ if [ -z "$NOTEST" ]; then
   tail -2 $O/pytest.log
 fi
 for m in ${MASKS:-0x2}; do
-  MFP_BIN_WAVE_MASK=$m timeout -k 10 300 python -u bench.py --packets ${PK:-10000000} --steps 5 --warmup 2 --no-cpu-baseline ${BENCH:---no-analysis} > $O/bench_$m.json 2> $O/bench_$m.err || { tail -5 $O/bench_$m.err; exit 1; }
+  wm=${m%/*}; sm=0x0; case $m in */*) sm=${m#*/};; esac
+  tag=${m//\//_}
+  MFP_BIN_WAVE_MASK=$wm MFP_BIN_SEG_MASK=$sm timeout -k 10 300 python -u bench.py --packets ${PK:-10000000} --steps 5 --warmup 2 --no-cpu-baseline ${BENCH:---no-analysis} > $O/bench_$tag.json 2> $O/bench_$tag.err || { tail -5 $O/bench_$tag.err; exit 1; }
   python -c "
-import json;d=json.load(open('$O/bench_$m.json'))
+import json;d=json.load(open('$O/bench_$tag.json'))
 print('mask $m', d['value'], 'Mpkt/s', d['ms_per_step'], 'ms', ' '.join(f'{k}={v[\"ms_per_step\"]:.2f}' for k,v in d['kernels'].items()))"
 done
