@@ -211,6 +211,38 @@ MFP_EXPORT int mfp_profile_enable(mfp_context ctx, int on);
 MFP_EXPORT int mfp_profile_read(mfp_context ctx, uint32_t i, char *name, size_t cap, uint64_t *launches,
                                 double *total_ms);
 
+/* ---- host ingest into batch arenas (host only, no device needed) ---- */
+typedef struct mfp_pcap_s *mfp_pcap;
+
+/* Replaces pcap_file_open (src/pcap_file_io.c:106-254) for reading: classic
+ * pcap only (magic a1b2c3d4 / d4c3b2a1); pcap-ng, other magics and link types
+ * outside {0, 1, 9, 101, 113, 276} fail with mfp_last_error() set (the
+ * reference exits).  A byte-swapped file's link type is the reference's
+ * htons() of the 32-bit header field (pcap_file_io.c:236). */
+MFP_EXPORT mfp_pcap mfp_pcap_open(const char *path);
+MFP_EXPORT int mfp_pcap_linktype(mfp_pcap p);
+
+/* Replaces the pcap_file_read_packet loop (pcap_file_io.c:393-468, 470-512):
+ * up to max_pkts packets back to back into arena, followed by 16 zero bytes,
+ * one descriptor each (offset, caplen, the file's link type); ts_ns
+ * (optional) gets tv_sec * 1e9 + tv_usec * 1000.  A record longer than 65536
+ * bytes yields its first 65536 (the reference's BUFLEN).  A record that does
+ * not fit the remaining arena starts the next batch.  Returns the packet count
+ * (0 at end of file) or -1 on a read error (after the packets before it have
+ * been returned); *arena_used = packet bytes written. */
+MFP_EXPORT long long mfp_pcap_read_batch(mfp_pcap p, uint8_t *arena, size_t arena_cap, mfp_pkt_desc *desc,
+                                         size_t max_pkts, uint64_t *ts_ns, size_t *arena_used);
+MFP_EXPORT void mfp_pcap_close(mfp_pcap p);
+
+/* Replaces process_all_packets_in_block (src/af_packet_v3.c:174-210):
+ * descriptors for the packets of one TPACKET_V3 ring block, offsets relative
+ * to arena_base (zero copy: the mapped ring is the arena), caplen =
+ * tp_snaplen, link type Ethernet; ts_ns (optional) = tp_sec * 1e9 + tp_nsec.
+ * Returns the packet count, or -1 when a header or packet lies outside
+ * block_len or the block holds more than max_pkts packets. */
+MFP_EXPORT long long mfp_tpacket3_block(const uint8_t *arena_base, const uint8_t *block, size_t block_len,
+                                        mfp_pkt_desc *desc, size_t max_pkts, uint64_t *ts_ns);
+
 /* last error string for this thread */
 MFP_EXPORT const char *mfp_last_error(void);
 

@@ -7,8 +7,8 @@ by tests and bench.py; it never falls back to a CPU implementation.
 """
 from .api import (ANALYSIS_DTYPE, FP_TYPE_NAMES, MSG_NAMES, NO_PROCESS, RECORD_DTYPE, DESC_DTYPE,  # noqa: F401
                   STATUS_NAMES, Context, MercuryAmdError, fingerprints, library_path, load_library,
-                  normalize_server_name, parse_filter, resource_stats)
+                  normalize_server_name, parse_filter, resource_stats, PcapReader, tpacket3_block)
 
 __all__ = ["Context", "MercuryAmdError", "fingerprints", "load_library", "library_path", "RECORD_DTYPE",
            "DESC_DTYPE", "FP_TYPE_NAMES", "MSG_NAMES", "parse_filter", "ANALYSIS_DTYPE", "NO_PROCESS",
-           "STATUS_NAMES", "normalize_server_name", "resource_stats"]
+           "STATUS_NAMES", "normalize_server_name", "resource_stats", "PcapReader", "tpacket3_block"]

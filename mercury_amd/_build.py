@@ -8,7 +8,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmercury_amd.so")
 OBJ = os.path.join(HERE, "_obj")
 
-SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_compact.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp"]
+SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_compact.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp",
+           "mfp_pcap.cpp"]
 HEADERS = ["mfp_device.hpp", "mfp_wave.hpp", "mfp_internal.h", "mfp_analysis.h", "mfp_common.hpp"]
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 

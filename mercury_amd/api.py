@@ -87,6 +87,15 @@ def load_library():
     lib.mfp_profile_read.restype = ctypes.c_int
     lib.mfp_profile_read.argtypes = [vp, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint64),
                                      ctypes.POINTER(ctypes.c_double)]
+    lib.mfp_pcap_open.restype = vp
+    lib.mfp_pcap_open.argtypes = [ctypes.c_char_p]
+    lib.mfp_pcap_linktype.restype = ctypes.c_int
+    lib.mfp_pcap_linktype.argtypes = [vp]
+    lib.mfp_pcap_read_batch.restype = ctypes.c_longlong
+    lib.mfp_pcap_read_batch.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.POINTER(ctypes.c_size_t)]
+    lib.mfp_pcap_close.argtypes = [vp]
+    lib.mfp_tpacket3_block.restype = ctypes.c_longlong
+    lib.mfp_tpacket3_block.argtypes = [vp, vp, sz, vp, sz, vp]
     _lib = lib
     return lib
 
@@ -263,3 +272,69 @@ def fingerprints(rec, fp_arena):
             o = int(r["fp_offset"])
             out.append(fp_arena[o:o + n].decode("latin-1"))
     return out
+
+
+class PcapReader:
+    """Classic pcap file -> packet batches (arena, descriptors, timestamps):
+    mfp_pcap_open / mfp_pcap_read_batch, the reference's pcap_file_open and
+    pcap_file_read_packet semantics (src/pcap_file_io.c:106-254, 393-468).
+    Host only."""
+
+    def __init__(self, path):
+        self.lib = load_library()
+        self.h = self.lib.mfp_pcap_open(os.fsencode(path))
+        if not self.h:
+            raise MercuryAmdError(_err(self.lib))
+        self.linktype = self.lib.mfp_pcap_linktype(self.h)
+
+    def read_batch(self, max_pkts=65536, arena_bytes=64 << 20):
+        """Up to max_pkts packets: (arena u8 incl. 16 zero bytes of slack,
+        desc DESC_DTYPE, ts_ns u64); empty arrays at the end of the file."""
+        arena = np.empty(max(arena_bytes, 65536 + 16), np.uint8)
+        desc = np.empty(max_pkts, DESC_DTYPE)
+        ts = np.empty(max_pkts, np.uint64)
+        used = ctypes.c_size_t(0)
+        n = self.lib.mfp_pcap_read_batch(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, max_pkts,
+                                         ts.ctypes.data, ctypes.byref(used))
+        if n < 0:
+            raise MercuryAmdError("pcap read failed: " + _err(self.lib))
+        return arena[:used.value + 16], desc[:n], ts[:n]
+
+    def __iter__(self):
+        while True:
+            a, d, t = self.read_batch()
+            if len(d) == 0:
+                return
+            yield a, d, t
+
+    def close(self):
+        if self.h:
+            self.lib.mfp_pcap_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def tpacket3_block(block, max_pkts=4096):
+    """Descriptors + ns timestamps for the packets of one TPACKET_V3 ring
+    block (a uint8 array; it is the arena, zero copy): mfp_tpacket3_block,
+    process_all_packets_in_block (src/af_packet_v3.c:174-210)."""
+    lib = load_library()
+    block = np.ascontiguousarray(block, dtype=np.uint8)
+    desc = np.empty(max_pkts, DESC_DTYPE)
+    ts = np.empty(max_pkts, np.uint64)
+    n = lib.mfp_tpacket3_block(block.ctypes.data, block.ctypes.data, block.nbytes, desc.ctypes.data, max_pkts,
+                               ts.ctypes.data)
+    if n < 0:
+        raise MercuryAmdError(_err(lib))
+    return desc[:n], ts[:n]

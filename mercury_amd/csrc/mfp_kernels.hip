@@ -155,11 +155,13 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
 #define MFP_SEG_MINW 4
 #endif
 constexpr int SEG_STRIDE = SEG_MAX + 1;   // odd word stride: lane-private lists are bank-conflict free
+constexpr uint32_t SEG_STAGE = 2048;      // packets up to this (minus alignment) are staged in LDS for expansion
 __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32_t *fallback) {
     __shared__ uint32_t segs[TILE * SEG_STRIDE];
     __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
     __shared__ unsigned long long tile_base;
     __shared__ uint8_t pool[32];
+    __shared__ uint4 stage[TILE / 64][SEG_STAGE / 16];   // per wave: the packet being expanded
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
     if (tid < 32) {
@@ -248,8 +250,21 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dptr, j) |
                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dptr >> 32), j) << 32);
             uint8_t *out = P.fp_arena + base + ex;
-            uint64_t h = seg_expand(segs + (wid * 64 + j) * SEG_STRIDE, ns, (const uint8_t *)(uintptr_t)src, T, out,
-                                    pool, lane);
+            // stage the packet in LDS (one coalesced 16-byte load per lane):
+            // the expansion's byte reads then cost an LDS round trip, not a
+            // dependent L2 round trip per character group
+            const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)dsc.caplen, j);
+            const uint8_t *pk = (const uint8_t *)(uintptr_t)src;
+            const uint32_t a16 = (uint32_t)(src & 15);
+            if (a16 + cl <= SEG_STAGE) {
+                const uint32_t nvec = (a16 + cl + 15) >> 4;
+                const uint4 *s16 = (const uint4 *)(uintptr_t)(src - a16);
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t v = lane; v < nvec; v += 64) stage[wid][v] = s16[v];
+                __builtin_amdgcn_wave_barrier();
+                pk = (const uint8_t *)&stage[wid][0] + a16;
+            }
+            uint64_t h = seg_expand(segs + (wid * 64 + j) * SEG_STRIDE, ns, pk, T, out, pool, lane);
             h = wave_xor64(h);
             if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
         }

@@ -220,16 +220,43 @@ def test_large_device_batch_properties():
     srec = desc[sample]
     ft, fl, flags, want = oracle.process_batch(ua, ud[sample % len(ud)], oracle.config())
     assert got == want
-    # the classifier key stored after each string (MFP_FLAG_HASHED)
-    for k in sample[:300]:
-        r = rec[k]
-        o, ln = int(r["fp_offset"]), int(r["fp_len"])
-        if ln == 0:
-            continue
-        assert r["flags"] & 4
-        ho = o + ((ln + 7) & ~7)
-        assert int.from_bytes(fp_host[ho:ho + 8], "little") == str_hash(fp_host[o:o + ln])
     # replicas are identical: per-position fp_len pattern repeats
     assert np.array_equal(rec["fp_len"][:len(ud)], rec["fp_len"][-len(ud):])
     ctx.close()
     del srec
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg_mask", ["0xa", "0x0"])
+def test_device_hash_keys(seg_mask, monkeypatch):
+    """Strings written by the segment and wave kernels carry their classifier
+    key (mfpc::str_hash) after the string (MFP_FLAG_HASHED); the lane kernel
+    leaves it to the classifier (flag clear)."""
+    import torch
+    monkeypatch.setenv("MFP_BIN_SEG_MASK", seg_mask)
+    monkeypatch.setenv("MFP_BIN_WAVE_MASK", "0x0" if seg_mask != "0x0" else "0xa")
+    a, d = synth.batch(30000, seed=0x5EED0077, workload="mixed", n_templates=3000)
+    n = len(d)
+    ctx = mercury_amd.Context(CONTRACT, device=0)
+    cap = ctx.fp_arena_bound(d)
+    d_arena = torch.from_numpy(a).cuda()
+    d_desc = torch.from_numpy(d.view(np.uint8)).cuda()
+    d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_fp = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(), cap,
+                       d_used.data_ptr(), 0)
+    torch.cuda.synchronize()
+    rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
+    fp_host = d_fp[:int(d_used[0])].cpu().numpy().tobytes()
+    ctx.close()
+    checked = 0
+    for r in rec:
+        o, ln = int(r["fp_offset"]), int(r["fp_len"])
+        if ln == 0 or not r["flags"] & 4:
+            continue
+        ho = o + ((ln + 7) & ~7)
+        assert int.from_bytes(fp_host[ho:ho + 8], "little") == str_hash(fp_host[o:o + ln])
+        checked += 1
+    http = int(np.isin(rec["fp_type"], [3, 4]).sum())
+    assert checked >= http > 1000
