@@ -10,6 +10,8 @@
 //   idx  emit  fp_type  truncated  fp_string
 // Output (mode "an"): analysis_context path, one TSV line per packet:
 //   idx  valid  fp_type  status  process  score  malware  p_malware  fp_string
+// Mode "json": the write_json record text, one line per packet (empty line
+// when the reference writes nothing).
 // Mode "time": run write_json with T threads (one processor per thread over
 // contiguous shards), print packets/s.
 //
@@ -124,6 +126,17 @@ int main(int argc, char **argv) {
             // reach ip_write_json and emit a record (pkt_proc.cc:1157-1158)
             int t = n > 0 ? p->analysis.fp.get_type() : 0;
             printf("%zu\t%d\t%d\t%d\t%s\n", i, n > 0, t, (int)trunc, t ? p->analysis.fp.string() : "");
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "json") {
+        // the reference's JSON record text, one line per packet ("" when none)
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        for (size_t i = 0; i < pkts.size(); i++) {
+            struct timespec ts{1700000000, 0};
+            size_t n = mercury_packet_processor_write_json_linktype(p, out.data(), out.size(),
+                                                                   (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
+            fwrite(out.data(), 1, n, stdout);
+            if (n == 0 || out[n - 1] != '\n') fputc('\n', stdout);
         }
         mercury_packet_processor_destruct(p);
     } else if (mode == "an") {
