@@ -137,11 +137,47 @@ def end_to_end(torch, ctx, ua, ud, n, analysis, steps, chunk):
     el = (time.perf_counter() - t0) / steps
     in_bytes = int(desc["caplen"].astype(np.int64).sum()) + 16 * n
     out_bytes = 32 * n + used + (24 * n if analysis else 0)
-    return {"value": round(n / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "steps": steps, "chunk": chunk,
-            "ms_per_step": round(el * 1e3, 3), "h2d_gb_per_s": round(in_bytes / el / 1e9, 3),
-            "d2h_gb_per_s": round(out_bytes / el / 1e9, 3), "pinned": True,
-            "path": "mfp_process_pipelined: pinned host arena -> 2 HIP streams (H2D | kernels | D2H) -> pinned "
-                    "records + fingerprints" + (" + classifier results" if analysis else "")}
+    res = {"value": round(n / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "steps": steps, "chunk": chunk,
+           "ms_per_step": round(el * 1e3, 3), "h2d_gb_per_s": round(in_bytes / el / 1e9, 3),
+           "d2h_gb_per_s": round(out_bytes / el / 1e9, 3), "pinned": True,
+           "path": "mfp_process_pipelined: pinned host arena -> 2 HIP streams (H2D | kernels | D2H) -> pinned "
+                   "records + fingerprints" + (" + classifier results" if analysis else "")}
+    try:
+        res["json"] = json_writer_rate(av, d, out[0], out[1], min(n, 2_000_000), 16, analysis)
+        jr = res["json"]["value"]
+        res["json"]["with_gpu_path_serial_mpkt_s"] = round(1.0 / (1.0 / res["value"] + 1.0 / jr), 3)
+    except Exception as e:
+        log(f"json leg failed: {e}")
+    return res
+
+
+def json_writer_rate(arena, desc, rec, fp, n, threads, analysis):
+    """Host JSON record assembly (mfp_write_json_batch, the text of
+    stateful_pkt_proc::write_json) over the first n results of the end-to-end
+    leg, `threads` host threads: Mpkt/s and GB/s of JSON text."""
+    import ctypes
+    from mercury_amd.api import load_library
+    lib = load_library()
+    ts = np.full(n, 1_700_000_000 * 10**9, np.uint64)
+    ends = np.zeros(n, np.uint64)
+    skipped = ctypes.c_uint64(0)
+    cap = n * 1024
+    buf = np.empty(cap, np.uint8)
+    args = (arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data, ts.ctypes.data,
+            buf.ctypes.data, cap, ends.ctypes.data, ctypes.byref(skipped), threads)
+    got = lib.mfp_write_json_batch(*args)                 # warm-up (page faults on buf)
+    if got < 0:
+        raise RuntimeError("mfp_write_json_batch failed")
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = lib.mfp_write_json_batch(*args)
+    el = (time.perf_counter() - t0) / reps
+    return {"value": round(n / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "threads": threads,
+            "json_bytes": int(got), "gb_per_s": round(got / el / 1e9, 3), "records": int((rec["flags"][:n] & 1).sum()),
+            "skipped": int(skipped.value),
+            "note": "host threads after D2H; text byte-identical to the reference's write_json" +
+                    (" minus the 'analysis' object (not built yet)" if analysis else "")}
 
 
 def find_traffic(cfg_key):

@@ -82,7 +82,13 @@ enum {
                                 at fp_offset + round_up(fp_len, 8) (the
                                 classifier's lookup key; cleared when the
                                 strings are packed for the host) */
+    MFP_FLAG_CERT_CLIENT = 8,  /* TLS certificate message: entity client (tls.h:728-744) */
+    MFP_FLAG_CERT_SERVER = 16, /* ... entity server; neither = undetermined   */
+    MFP_FLAG_ENCAP       = 32, /* reached through IP-in-IP encapsulation (pkt_proc.cc:959) */
 };
+/* For MFP_MSG_TLS_SH / MFP_MSG_TLS_CERT records sni_off/sni_len hold the
+ * certificate_list datum (tls.h:275-296), the bytes the JSON writer's
+ * "certs" array is built from; len 0xffff = no list. */
 
 enum {
     MFP_MSG_NONE = 0, MFP_MSG_TLS_CH, MFP_MSG_TLS_SH, MFP_MSG_TLS_CERT,
@@ -242,6 +248,24 @@ MFP_EXPORT void mfp_pcap_close(mfp_pcap p);
  * block_len or the block holds more than max_pkts packets. */
 MFP_EXPORT long long mfp_tpacket3_block(const uint8_t *arena_base, const uint8_t *block, size_t block_len,
                                         mfp_pkt_desc *desc, size_t max_pkts, uint64_t *ts_ns);
+
+/* ---- JSON records (host only, no device needed) ----
+ * Replaces the record text of stateful_pkt_proc::write_json
+ * (pkt_proc.cc:1157-1253, metadata_output off, no --analysis object): one
+ * line per record with MFP_FLAG_EMIT, byte-identical to the reference, built
+ * from records + packet arena + fp arena as mfp_process_batch_host /
+ * mfp_process_pipelined return them.  ts_ns (optional): per-packet time; 0 or
+ * NULL = now (pkt_proc.cc:1086-1089).  line_end[i] = end offset of packet
+ * i's line in out (its line is [line_end[i-1], line_end[i]), empty when the
+ * reference writes nothing).  *skipped (optional) = emitted records this
+ * writer cannot rebuild exactly (encapsulated packets: their
+ * "encapsulations" array); they get an empty line.  `threads` host threads.
+ * Returns the bytes written, -1 on bad arguments, -2 when out_cap is too
+ * small (nothing written; mfp_last_error() names the size needed). */
+MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+                                          const mfp_record *rec, const char *fp_arena, const uint64_t *ts_ns,
+                                          char *out, size_t out_cap, uint64_t *line_end, uint64_t *skipped,
+                                          int threads);
 
 /* last error string for this thread */
 MFP_EXPORT const char *mfp_last_error(void);

@@ -96,6 +96,9 @@ def load_library():
     lib.mfp_pcap_close.argtypes = [vp]
     lib.mfp_tpacket3_block.restype = ctypes.c_longlong
     lib.mfp_tpacket3_block.argtypes = [vp, vp, sz, vp, sz, vp]
+    lib.mfp_write_json_batch.restype = ctypes.c_longlong
+    lib.mfp_write_json_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, sz, vp, ctypes.POINTER(ctypes.c_uint64),
+                                         ctypes.c_int]
     _lib = lib
     return lib
 
@@ -338,3 +341,38 @@ def tpacket3_block(block, max_pkts=4096):
     if n < 0:
         raise MercuryAmdError(_err(lib))
     return desc[:n], ts[:n]
+
+
+def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1):
+    """JSON record lines for a fingerprinted batch (mfp_write_json_batch: the
+    text of stateful_pkt_proc::write_json, src/libmerc/pkt_proc.cc:1157-1253).
+    Returns (list of per-packet lines as bytes, b"" when the reference writes
+    nothing; count of records that could not be rebuilt). Host only."""
+    lib = load_library()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    rec = np.ascontiguousarray(rec, dtype=RECORD_DTYPE)
+    fp = np.frombuffer(bytes(fp_arena) + b"\0", dtype=np.uint8)
+    n = len(desc)
+    ts = None if ts_ns is None else np.ascontiguousarray(ts_ns, dtype=np.uint64)
+    ends = np.zeros(max(n, 1), np.uint64)
+    skipped = ctypes.c_uint64(0)
+    cap = 1 << 16
+    while True:
+        out = np.empty(cap, np.uint8)
+        got = lib.mfp_write_json_batch(arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data,
+                                       None if ts is None else ts.ctypes.data, out.ctypes.data, cap,
+                                       ends.ctypes.data, ctypes.byref(skipped), int(threads))
+        if got == -2:
+            cap *= 4
+            continue
+        if got < 0:
+            raise MercuryAmdError("mfp_write_json_batch failed: " + _err(lib))
+        break
+    buf = out[:got].tobytes()
+    lines, prev = [], 0
+    for i in range(n):
+        e = int(ends[i])
+        lines.append(buf[prev:e])
+        prev = e
+    return lines, int(skipped.value)

@@ -1140,6 +1140,11 @@ struct Out {
     uint32_t src_port, dst_port;
     uint32_t net;        // innermost IP header offset | version << 16 (flow key, flow_key.h:71)
 };
+// the certificate_list datum in the record's server-name slot (TLS server
+// messages have no server name): the JSON writer's certs array (tls.h:2183)
+DEV void cert_record(Out &o, Cur l, const uint8_t *base) {
+    if (cnotempty(l)) { o.sni_off = (uint32_t)(l.d - base); o.sni_len = (uint32_t)clen(l); }
+}
 struct Cfg {
     uint32_t select, tls_format, mode;
     uint32_t classify;   // stop after protocol identification (o.msg), emit nothing
@@ -1311,6 +1316,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         Cur frag2 = tls_record_fragment(p);
         Hs hs2 = tls_hs_parse(frag2);
         if (hs2.msg_type == 11) tls_cert_parse(cert, hs2.body);
+        cert_record(o, cert.list, base);            // tls.h:605-627 (the JSON writer's certs)
         if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
         bool hello = tls_sh_not_empty(sh);
         if (hello || cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
@@ -1322,7 +1328,14 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         Cert cert; cset_null(cert.list); cert.more = 0;
         Cur frag = tls_record_fragment(p);
         Hs hs = tls_hs_parse(frag);
-        if (hs.msg_type == 11) tls_cert_parse(cert, hs.body);
+        if (hs.msg_type == 11) {
+            tls_cert_parse(cert, hs.body);
+            uint32_t t = 0;                              // entity, tls.h:728-744
+            if (cnotempty(frag)) { Hs h = tls_hs_parse(frag); t = h.msg_type; }
+            else if (cnotempty(p)) { Cur f2 = tls_record_fragment(p); Hs h = tls_hs_parse(f2); t = h.msg_type; }
+            if (t == 16) o.flags |= MFP_FLAG_CERT_CLIENT; else if (t == 12) o.flags |= MFP_FLAG_CERT_SERVER;
+        }
+        cert_record(o, cert.list, base);
         if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
         if (cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
         return;
@@ -1517,7 +1530,10 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
                  int stride) {
     const uint8_t *iph; int ipv;
     uint32_t proto = ip_parse(pkt, iph, ipv);
-    for (int n = 0; n < 4 && (proto == 4 || proto == 41); n++) proto = ip_parse(pkt, iph, ipv);  // pkt_proc.cc:959
+    for (int n = 0; n < 4 && (proto == 4 || proto == 41); n++) {   // pkt_proc.cc:959
+        proto = ip_parse(pkt, iph, ipv);
+        o.flags |= MFP_FLAG_ENCAP;
+    }
     if (iph) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16);
     if (proto == 6) {
         const uint8_t *tcph = cget_ptr(pkt, 20);

@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <ctime>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -64,8 +65,10 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
     auto *m = new mercury;
     std::string filt = vars->packet_filter_cfg ? vars->packet_filter_cfg : "";
     // global_config.h:148-152: "key=value;..." only when the string holds ';'
-    std::string cfg = filt.find(';') != std::string::npos ? filt : (filt.empty() ? std::string("select=all") : "select=" + filt);
+    // a bare list stays bare (mfp_init parses it the same way); key=value options are added in the ';' form
+    std::string cfg = filt.empty() ? std::string("all") : filt;
     if (vars->do_analysis && vars->resources) {
+        if (cfg.find(';') == std::string::npos) cfg = "select=" + cfg;
         cfg += std::string(";resources=") + vars->resources + ";analysis";
         m->analysis = true;
     }
@@ -105,13 +108,35 @@ MFP_EXPORT mercury_packet_processor mercury_packet_processor_construct(mercury_c
 
 MFP_EXPORT void mercury_packet_processor_destruct(mercury_packet_processor mpp) { delete mpp; }
 
-MFP_EXPORT size_t mercury_packet_processor_write_json(mercury_packet_processor, void *, size_t, uint8_t *, size_t,
-                                                      struct timespec *) {
-    return 0;
+// write_json libmerc.cc:131-175 -> stateful_pkt_proc::write_json pkt_proc.cc:1256-1383: the record text
+// from a one-packet batch (device walk + mfp_write_json_batch).  Returns 0 when nothing is written, the
+// record does not fit buf_size (buffer_stream truncation, pkt_proc.cc:1249-1253), or --analysis is
+// configured (the "analysis" object is not built by the JSON writer yet).
+MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_processor p, void *buffer,
+                                                               size_t buffer_size, uint8_t *pkt, size_t len,
+                                                               struct timespec *ts, uint16_t linktype) {
+    if (!p || !buffer || !pkt || !ts) return 0;
+    if (p->mc->analysis) return 0;
+    mfp_context ctx = get_ctx(p->mc, MFP_MODE_WRITE_JSON);
+    if (!ctx) return 0;
+    if (ts->tv_sec == 0) clock_gettime(CLOCK_REALTIME, ts);   // pkt_proc.cc:1086-1089
+    p->arena.assign(pkt, pkt + len);
+    p->arena.resize(len + 16);
+    mfp_pkt_desc d{0, (uint32_t)len, linktype, 0};
+    mfp_record rec;
+    size_t cap = mfp_fp_arena_bound(1, len);
+    p->fp.resize(cap);
+    long long used = mfp_process_batch_host(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap);
+    if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
+    uint64_t t = (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec, end = 0;
+    long long n = mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
+                                       buffer_size, &end, nullptr, 1);
+    if (n <= 0 || (size_t)n >= buffer_size) return 0;    // buffer_stream keeps one byte for its NUL
+    return (size_t)n;
 }
-MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_processor, void *, size_t, uint8_t *,
-                                                               size_t, struct timespec *, uint16_t) {
-    return 0;
+MFP_EXPORT size_t mercury_packet_processor_write_json(mercury_packet_processor p, void *buffer, size_t buffer_size,
+                                                      uint8_t *pkt, size_t len, struct timespec *ts) {
+    return mercury_packet_processor_write_json_linktype(p, buffer, buffer_size, pkt, len, ts, 1);   // LINKTYPE_ETHERNET
 }
 
 static void copy_cstr(char *dst, size_t cap, const uint8_t *src, size_t len) {   // datum::strncpy
@@ -139,7 +164,8 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
     analysis_context &ac = p->ac;
     ac.fp_type = rec.fp_type;
     copy_cstr(ac.fp, sizeof ac.fp, (const uint8_t *)p->fp.data() + rec.fp_offset, rec.fp_type ? rec.fp_len : 0);
-    copy_cstr(ac.sn, sizeof ac.sn, pkt + rec.sni_off, rec.sni_len == 0xffff ? 0 : rec.sni_len);
+    bool cert_slot = rec.msg == MFP_MSG_TLS_SH || rec.msg == MFP_MSG_TLS_CERT;   // sni slot = certificate_list
+    copy_cstr(ac.sn, sizeof ac.sn, pkt + rec.sni_off, rec.sni_len == 0xffff || cert_slot ? 0 : rec.sni_len);
     copy_cstr(ac.ua, sizeof ac.ua, pkt + rec.ua_off, rec.ua_len == 0xffff ? 0 : rec.ua_len);
     if (!want_an) return nullptr;   // no classifier: analysis result never valid
     ac.status = an.status;

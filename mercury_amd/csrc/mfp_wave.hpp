@@ -859,6 +859,9 @@ struct W {
         if (!exts_par(s.extensions, 1, 0)) exts_fp0(s.extensions, 1);
     }
     struct Cert { C list; uint64_t more; };
+    WDEV void cert_record(Out &o, C l, int base) {       // see mfp_device.hpp
+        if (cnotempty(l)) { o.sni_off = (uint32_t)(l.d - base); o.sni_len = (uint32_t)clen(l); }
+    }
     WDEV void tls_cert_parse(Cert &c, C &d) {            // tls_server_certificate::parse tls.h:281
         uint64_t t = 0;
         if (!rd_uint(d, 3, t)) return;
@@ -1275,6 +1278,7 @@ struct W {
             C frag2 = tls_record_fragment(p);
             Hs hs2 = tls_hs_parse(frag2);
             if (hs2.msg_type == 11) tls_cert_parse(cert, hs2.body);
+            cert_record(o, cert.list, base);            // tls.h:605-627 (the JSON writer's certs)
             if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
             bool hello = tls_sh_not_empty(sh);
             if (hello || cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
@@ -1286,7 +1290,14 @@ struct W {
             Cert cert; cset_null(cert.list); cert.more = 0;
             C frag = tls_record_fragment(p);
             Hs hs = tls_hs_parse(frag);
-            if (hs.msg_type == 11) tls_cert_parse(cert, hs.body);
+            if (hs.msg_type == 11) {
+                tls_cert_parse(cert, hs.body);
+                uint32_t t = 0;                              // entity, tls.h:728-744
+                if (cnotempty(frag)) { Hs h = tls_hs_parse(frag); t = h.msg_type; }
+                else if (cnotempty(p)) { C f2 = tls_record_fragment(p); Hs h = tls_hs_parse(f2); t = h.msg_type; }
+                if (t == 16) o.flags |= MFP_FLAG_CERT_CLIENT; else if (t == 12) o.flags |= MFP_FLAG_CERT_SERVER;
+            }
+            cert_record(o, cert.list, base);
             if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
             if (cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
             return;
@@ -1470,7 +1481,10 @@ struct W {
     WDEV void ip_path(C pkt, int base) {
         int iph, ipv;
         uint32_t proto = ip_parse(pkt, iph, ipv);
-        for (int k = 0; k < 4 && (proto == 4 || proto == 41); k++) proto = ip_parse(pkt, iph, ipv);  // pkt_proc.cc:959
+        for (int k = 0; k < 4 && (proto == 4 || proto == 41); k++) {   // pkt_proc.cc:959
+            proto = ip_parse(pkt, iph, ipv);
+            o.flags |= MFP_FLAG_ENCAP;
+        }
         if (iph >= 0) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16);
         if (proto == 6) {
             int tcph = cget_ptr(pkt, 20);
