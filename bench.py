@@ -146,9 +146,64 @@ def end_to_end(torch, ctx, ua, ud, n, analysis, steps, chunk):
         res["json"] = json_writer_rate(av, d, out[0], out[1], min(n, 2_000_000), 16, analysis)
         jr = res["json"]["value"]
         res["json"]["with_gpu_path_serial_mpkt_s"] = round(1.0 / (1.0 / res["value"] + 1.0 / jr), 3)
+        res["json_overlapped"] = json_overlapped(torch, ctx, av, d, n, analysis, chunk, out)
     except Exception as e:
         log(f"json leg failed: {e}")
     return res
+
+
+def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_000, threads=16):
+    """Whole host path with JSON text: batches of `batch` packets go through
+    mfp_process_pipelined while the JSON writer (16 host threads, ctypes
+    releases the GIL) formats the previous batch's results; two result sets
+    alternate.  Packets in pinned host memory -> JSON text in host memory."""
+    import ctypes
+    import threading
+    from mercury_amd.api import ANALYSIS_DTYPE, RECORD_DTYPE, load_library
+    lib = load_library()
+    rec_a, fp_a, an_a = out_a
+    fp_b = torch.empty(fp_a.nbytes // max(1, n // batch), dtype=torch.uint8, pin_memory=True).numpy()
+    rec_b = torch.empty(batch * 32, dtype=torch.uint8, pin_memory=True).numpy().view(RECORD_DTYPE)
+    an_b = torch.empty(batch * 24, dtype=torch.uint8, pin_memory=True).numpy().view(ANALYSIS_DTYPE) if analysis else None
+    sets = [(rec_a[:batch], fp_a, an_a[:batch] if analysis else None), (rec_b, fp_b, an_b)]
+    ts = np.full(batch, 1_700_000_000 * 10**9, np.uint64)
+    ends = np.zeros(batch, np.uint64)
+    cap = batch * 640
+    jbuf = np.empty(cap, np.uint8)
+    skipped = ctypes.c_uint64(0)
+    total = [0]
+
+    def write(dk, o):
+        got = lib.mfp_write_json_batch(av.ctypes.data, dk.ctypes.data, len(dk), o[0].ctypes.data, o[1].ctypes.data,
+                                       ts.ctypes.data, jbuf.ctypes.data, cap, ends.ctypes.data,
+                                       ctypes.byref(skipped), threads)
+        if got < 0:
+            raise RuntimeError("mfp_write_json_batch failed")
+        total[0] += got
+
+    nb = n // batch
+    d0 = np.ascontiguousarray(d[:batch])
+    ctx.process_pipelined(av, d0, chunk=chunk, analysis=analysis, out=sets[0])
+    write(d0, sets[0])                                   # warm-up (page faults on the text buffer)
+    total[0] = 0
+    t0 = time.perf_counter()
+    prev = None
+    for k in range(nb):
+        dk = np.ascontiguousarray(d[k * batch:(k + 1) * batch])
+        o = sets[k % 2]
+        th = threading.Thread(target=write, args=prev) if prev else None
+        if th:
+            th.start()
+        ctx.process_pipelined(av, dk, chunk=chunk, analysis=analysis, out=o)
+        if th:
+            th.join()
+        prev = (dk, o)
+    write(*prev)
+    el = time.perf_counter() - t0
+    return {"value": round(nb * batch / el / 1e6, 3), "unit": "Mpkt/s", "packets": nb * batch, "batch": batch,
+            "threads": threads, "json_gb_per_s": round(total[0] / el / 1e9, 3),
+            "path": "pinned packets -> mfp_process_pipelined (batch k) || mfp_write_json_batch (batch k-1) -> "
+                    "JSON text in host memory"}
 
 
 def json_writer_rate(arena, desc, rec, fp, n, threads, analysis):
