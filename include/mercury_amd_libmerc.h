@@ -93,8 +93,9 @@ MFP_EXPORT mercury_packet_processor mercury_packet_processor_construct(mercury_c
 /* libmerc.h:253 */
 MFP_EXPORT void mercury_packet_processor_destruct(mercury_packet_processor mpp);
 /* libmerc.h:270, :293 -- the record text (mfp_write_json_batch), byte-identical to
- * the reference except: 0 for IP-in-IP packets and whenever --analysis is
- * configured (no "analysis" object yet) */
+ * the reference except: 0 for IP-in-IP packets whose outer IPv6 header has
+ * extension headers, and whenever --analysis is configured (no "analysis"
+ * object yet) */
 MFP_EXPORT size_t mercury_packet_processor_write_json(mercury_packet_processor processor, void *buffer,
                                                       size_t buffer_size, uint8_t *packet, size_t length,
                                                       struct timespec *ts);

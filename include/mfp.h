@@ -52,7 +52,10 @@ typedef struct {
     uint16_t sni_off, sni_len;
     uint16_t ua_off, ua_len;
     uint16_t src_port, dst_port;   /* host byte order */
-    uint32_t net;        /* innermost IP header: offset (bits 0-15), version (16-19) */
+    uint32_t net;        /* innermost IP header: offset (bits 0-15), version (16-19);
+                            IP-in-IP (MFP_FLAG_ENCAP): levels (20-22), outer
+                            level i is IPv6 (bit 23+i, outermost = 0), an outer
+                            header with IPv6 extension headers (27) */
 } mfp_record;
 
 /* Per-packet classifier result (analysis_result, result.h:174-300), written
@@ -251,15 +254,16 @@ MFP_EXPORT long long mfp_tpacket3_block(const uint8_t *arena_base, const uint8_t
 
 /* ---- JSON records (host only, no device needed) ----
  * Replaces the record text of stateful_pkt_proc::write_json
- * (pkt_proc.cc:1157-1253, metadata_output off, no --analysis object): one
+ * (pkt_proc.cc:1157-1253, metadata_output off, no --analysis object;
+ * IP-in-IP "encapsulations" arrays included): one
  * line per record with MFP_FLAG_EMIT, byte-identical to the reference, built
  * from records + packet arena + fp arena as mfp_process_batch_host /
  * mfp_process_pipelined return them.  ts_ns (optional): per-packet time; 0 or
  * NULL = now (pkt_proc.cc:1086-1089).  line_end[i] = end offset of packet
  * i's line in out (its line is [line_end[i-1], line_end[i]), empty when the
  * reference writes nothing).  *skipped (optional) = emitted records this
- * writer cannot rebuild exactly (encapsulated packets: their
- * "encapsulations" array); they get an empty line.  `threads` host threads.
+ * writer cannot rebuild exactly (IP-in-IP with an outer IPv6 header that
+ * has extension headers: its "encapsulations" entry); they get an empty line.  `threads` host threads.
  * Returns the bytes written, -1 on bad arguments, -2 when out_cap is too
  * small (nothing written; mfp_last_error() names the size needed). */
 MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,

@@ -1530,11 +1530,16 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
                  int stride) {
     const uint8_t *iph; int ipv;
     uint32_t proto = ip_parse(pkt, iph, ipv);
+    uint32_t enc = 0;            // net bits 20-27: levels, v6 mask, irregular (include/mfp.h)
     for (int n = 0; n < 4 && (proto == 4 || proto == 41); n++) {   // pkt_proc.cc:959
+        const uint8_t *oh = iph; const int ov = ipv;
         proto = ip_parse(pkt, iph, ipv);
         o.flags |= MFP_FLAG_ENCAP;
+        if (ov == 6) enc |= 8u << n;
+        if (!oh || !iph || iph - oh != (ov == 6 ? 40 : 20)) enc |= 128u;
+        enc = (enc & ~7u) | (uint32_t)(n + 1);
     }
-    if (iph) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16);
+    if (iph) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16) | (enc << 20);
     if (proto == 6) {
         const uint8_t *tcph = cget_ptr(pkt, 20);
         if (!tcph) return;

@@ -252,12 +252,26 @@ struct TsCache { uint64_t sec = ~0ull, usec = ~0ull; int len = 0; char text[40];
 bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const char *fp_arena,
                   uint64_t sec, uint64_t nsec) {
     if (!(r.flags & MFP_FLAG_EMIT)) return true;
-    if (r.flags & MFP_FLAG_ENCAP) return false;          // encapsulations array (pkt_proc.cc:1021-1031) not rebuilt
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
+    // IP-in-IP: outer headers sit back to back before the inner one (IPv4
+    // fixed 20 B, ip.h:124-137; IPv6 40 B when it has no extension headers)
+    const uint32_t levels = (r.net >> 20) & 7;
+    uint32_t outer[4], outer_v[4];
+    if (r.flags & MFP_FLAG_ENCAP) {
+        if (levels == 0 || levels > 4 || (r.net >> 27) & 1) return false;   // irregular: not rebuilt
+        uint32_t at = ip;
+        for (int k = (int)levels - 1; k >= 0; k--) {
+            outer_v[k] = (r.net >> (23 + k)) & 1 ? 6 : 4;
+            const uint32_t sz = outer_v[k] == 6 ? 40 : 20;
+            if (at < sz) return false;
+            at -= sz;
+            outer[k] = at;
+        }
+    }
     if ((ipv != 4 && ipv != 6) || ip + (ipv == 4 ? 20u : 40u) > caplen) return false;
-    // worst case: fixed keys/addresses/numbers < 400 B, the fp string, and at most
+    // worst case: fixed keys/addresses/numbers and 4 encapsulations < 1000 B, the fp string, and at most
     // 6 output bytes per input byte of a JSON string ("\\ufffd") or a base64 cert list
-    o.need(400 + (size_t)r.fp_len + 6 * ((r.sni_len == 0xffff ? 0 : r.sni_len) + (r.ua_len == 0xffff ? 0 : r.ua_len)));
+    o.need(1000 + (size_t)r.fp_len + 6 * ((r.sni_len == 0xffff ? 0 : r.sni_len) + (r.ua_len == 0xffff ? 0 : r.ua_len)));
     W w{o.buf.get() + o.len};
     // a readable, non-empty datum (print_key_json_string skips empty ones, json_object.h:104-108)
     auto span_ok = [&](uint32_t off, uint32_t len) { return len != 0xffff && len && (uint64_t)off + len <= caplen; };
@@ -316,6 +330,20 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
         break;
     }
     if (r.flags & MFP_FLAG_TRUNCATED) { rec.key("reassembly_properties"); w.puts("{\"truncated\":true}"); }
+    if (r.flags & MFP_FLAG_ENCAP) {                      // encapsulations::write_json pkt_proc.cc:1021-1031
+        rec.key("encapsulations");
+        w.put('[');
+        for (uint32_t k = 0; k < levels; k++) {           // ip_encapsulation::write_json ip.h:788-793
+            const uint8_t *oh = pkt + outer[k];
+            if (k) w.put(',');
+            w.puts("{\"type\":\"ip encapsulation\",\"src_ip\":\"");
+            if (outer_v[k] == 4) w.ipv4(oh + 12); else w.ipv6(oh + 8);
+            w.puts("\",\"dst_ip\":\"");
+            if (outer_v[k] == 4) w.ipv4(oh + 16); else w.ipv6(oh + 24);
+            w.puts("\"}");
+        }
+        w.put(']');
+    }
     const uint8_t *iph = pkt + ip;
     rec.key("src_ip"); w.put('"');
     if (ipv == 4) w.ipv4(iph + 12); else w.ipv6(iph + 8);

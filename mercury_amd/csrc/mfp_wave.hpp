@@ -1481,11 +1481,16 @@ struct W {
     WDEV void ip_path(C pkt, int base) {
         int iph, ipv;
         uint32_t proto = ip_parse(pkt, iph, ipv);
+        uint32_t enc = 0;        // net bits 20-27 (see mfp_device.hpp ip_path)
         for (int k = 0; k < 4 && (proto == 4 || proto == 41); k++) {   // pkt_proc.cc:959
+            const int oh = iph, ov = ipv;
             proto = ip_parse(pkt, iph, ipv);
             o.flags |= MFP_FLAG_ENCAP;
+            if (ov == 6) enc |= 8u << k;
+            if (oh < 0 || iph < 0 || iph - oh != (ov == 6 ? 40 : 20)) enc |= 128u;
+            enc = (enc & ~7u) | (uint32_t)(k + 1);
         }
-        if (iph >= 0) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16);
+        if (iph >= 0) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16) | (enc << 20);
         if (proto == 6) {
             int tcph = cget_ptr(pkt, 20);
             if (tcph < 0) return;
