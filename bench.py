@@ -1,7 +1,7 @@
 """bench.py -- device-resident fingerprint + classify throughput of the MI355X path.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mixed|tls_ch]
-                    [--packets P] [--no-analysis]
+                    [--packets P] [--no-analysis] [--e2e-total T]
 
 A step is one pass of the hot path (libmercury_amd.so) over one batch of P
 synthetic packets already resident in HBM:
@@ -13,10 +13,13 @@ synthetic packets already resident in HBM:
   --no-analysis config 3: protocol identification + fingerprint only
   --workload tls_ch --packets 10000000 --no-analysis   config 2
 
-Packets are independent, so for N > 1 every rank processes its own shard
+Multi-GPU (one process per GPU).  Under torch.distributed.run the ranks come
+from RANK/LOCAL_RANK/WORLD_SIZE; a bare `python bench.py --gpus N` starts the N
+rank processes itself (before anything touches the GPU) with the same
+arguments.  Packets are independent, so every rank processes its own shard
 (weak scaling, no data-path collective; all ranks draw from one template pool
-so the classifier's label rate is the same on every shard); the barrier and
-the max-over-ranks timing use torch.distributed only for measurement.
+so the classifier's label rate is the same on every shard).  A gloo group
+carries the barrier and the max-over-ranks time: nothing goes over RCCL.
 
 Rank 0 prints one JSON line.  `roofline` covers the kernels of one step
 (timed with HIP events on the stream they run on, mfp_profile_enable) against
@@ -25,9 +28,11 @@ comes from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the same command
 (profiles/*traffic*.json, tools/pmc_traffic.py) when one matches this
 configuration.  `cpu_baseline` is the reference libmerc compiled from
 /root/reference (oracle/_ref, travels with the snapshot) or else the C oracle
-port, timed on a bounded sample on the host cores.  `end_to_end` is the
-H2D/D2H-inclusive rate of the same configuration on --e2e-packets packets in
-page-locked host memory (mfp_process_pipelined), reported beside `value`.
+port, timed on a bounded sample on the host cores (both entry points:
+write_json and get_analysis_context).  `end_to_end` is config 5's
+H2D/D2H-inclusive rate: --e2e-total packets per job (split over the ranks)
+from page-locked host memory through mfp_process_pipelined, reported beside
+`value`, never instead of it.
 """
 import argparse
 import glob
@@ -75,25 +80,46 @@ def build_device_batch(torch, n, workload, draw_seed, unique):
     return ua, ud, d_arena, desc, d_desc
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may use (the
+    GPU box sets OMP_NUM_THREADS to its per-GPU CPU share)."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
+
+
 def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis):
-    """Reference libmerc (oracle/_ref) if present, else the C oracle port."""
+    """Reference libmerc (oracle/_ref) if present, else the C oracle port.
+    The reference is timed on both of its entry points: write_json (the CLI's
+    path, JSON text included) and get_analysis_context (the embedders' path);
+    `value` is the write_json rate."""
     from tests import pcaplib, synth
     a, d = synth.batch(sample_n, seed=TEMPLATE_SEED[workload], workload=workload, n_templates=N_TEMPLATES,
                        draw_seed=draw_seed)
     ref = os.path.join(ROOT, "oracle", "_ref", "merc_ref_drv")
+    host = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
     if os.path.exists(ref):
         with tempfile.NamedTemporaryFile(suffix=".mfpb", delete=False) as t:
             path = t.name
         pcaplib.write_mfpb(path, a, d)
         try:
-            out = subprocess.run([ref, "time", path, CONTRACT, RESOURCES if analysis else "-", str(threads),
-                                  str(seconds)],
-                                 capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
-            r = json.loads(out.decode().strip().splitlines()[-1])
-            what = "write_json with --analysis (resources loaded)" if analysis else "write_json"
+            rates = {}
+            for entry in ("json", "an"):
+                out = subprocess.run([ref, "time", path, CONTRACT, RESOURCES if analysis else "-", str(threads),
+                                      str(seconds), entry],
+                                     capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
+                rates[entry] = json.loads(out.decode().strip().splitlines()[-1])
+            r = rates["json"]
+            what = "with --analysis (resources loaded)" if analysis else "fingerprint only"
             return {"value": r["pps"] / 1e6, "unit": "Mpkt/s", "cores": threads, "kind": "reference",
-                    "sample": f"{sample_n} {workload} packets looped for {r['seconds']:.1f} s, libmerc {what}, "
-                              f"one processor per thread, {r['packets']} packets"}
+                    "entry": "write_json",
+                    "get_analysis_context_mpkt_s": round(rates["an"]["pps"] / 1e6, 4),
+                    "host": host,
+                    "sample": f"{sample_n} {workload} packets looped >= {seconds:.0f} s per entry point, "
+                              f"libmerc {what}, one processor per thread ({threads} threads); write_json "
+                              f"{r['packets']} packets in {r['seconds']:.1f} s, get_analysis_context "
+                              f"{rates['an']['packets']} packets in {rates['an']['seconds']:.1f} s"}
         finally:
             os.unlink(path)
     if analysis:
@@ -102,16 +128,19 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis):
     t, _ = oracle.time_batch(a, d, oracle.config(), threads=threads, reps=1)
     reps = max(1, int(seconds / max(t, 1e-3)))
     t, _ = oracle.time_batch(a, d, oracle.config(), threads=threads, reps=reps)
-    return {"value": sample_n * reps / t / 1e6, "unit": "Mpkt/s", "cores": threads, "kind": "port",
+    return {"value": sample_n * reps / t / 1e6, "unit": "Mpkt/s", "cores": threads, "kind": "port", "host": host,
             "sample": f"{sample_n} {workload} packets x {reps} passes, C oracle, {threads} threads"}
 
 
-def end_to_end(torch, ctx, ua, ud, n, analysis, steps, chunk):
-    """Host-resident rate: packets in page-locked host memory, records,
-    fingerprints (and classifier results) back in host memory, through
-    mfp_process_pipelined (two streams: H2D, kernels, D2H overlapped)."""
+def end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world, with_json):
+    """Config 5's host-resident rate: `per_rank` packets per rank from
+    page-locked host memory (a buffer of n_buf packets, looped), records,
+    fingerprints (and classifier results) back into page-locked host memory,
+    through mfp_process_pipelined (two HIP streams: H2D, kernels, D2H
+    overlapped).  Timed between barriers; the job time is the max over ranks."""
     from mercury_amd.api import ANALYSIS_DTYPE, DESC_DTYPE, RECORD_DTYPE
     u = len(ud)
+    n = min(n_buf, per_rank)
     span = int(ud["offset"][-1] + ud["caplen"][-1])
     stride = (span + 255) // 256 * 256
     reps = (n + u - 1) // u
@@ -131,24 +160,37 @@ def end_to_end(torch, ctx, ua, ud, n, analysis, steps, chunk):
     out = (h_rec.numpy().view(RECORD_DTYPE), h_fp.numpy(), h_an.numpy().view(ANALYSIS_DTYPE) if analysis else None)
     d = h_desc.numpy().view(DESC_DTYPE)
     ctx.process_pipelined(av, d, chunk=chunk, analysis=analysis, out=out)   # warm-up (device buffers)
+    passes = [n] * (per_rank // n) + ([per_rank % n] if per_rank % n else [])
+    if dist:
+        dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        _, used, _ = ctx.process_pipelined(av, d, chunk=chunk, analysis=analysis, out=out)
-    el = (time.perf_counter() - t0) / steps
-    in_bytes = int(desc["caplen"].astype(np.int64).sum()) + 16 * n
-    out_bytes = 32 * n + used + (24 * n if analysis else 0)
-    res = {"value": round(n / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "steps": steps, "chunk": chunk,
-           "ms_per_step": round(el * 1e3, 3), "h2d_gb_per_s": round(in_bytes / el / 1e9, 3),
-           "d2h_gb_per_s": round(out_bytes / el / 1e9, 3), "pinned": True,
+    used_tot = 0
+    for m in passes:
+        dm = d if m == n else d[:m]
+        _, used, _ = ctx.process_pipelined(av, dm, chunk=chunk, analysis=analysis, out=out)
+        used_tot += used
+    el = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        from mercury_amd import shard
+        el = shard.max_over_ranks(el)
+    in_bytes = (int(desc["caplen"].astype(np.int64).sum()) + 16 * n) * per_rank / n
+    out_bytes = 32 * per_rank + used_tot + (24 * per_rank if analysis else 0)
+    total = per_rank * world
+    res = {"value": round(total / el / 1e6, 3), "unit": "Mpkt/s", "packets": total, "n_gpus": world,
+           "packets_per_gpu": per_rank, "host_buffer_packets": n, "chunk": chunk,
+           "seconds": round(el, 4), "h2d_gb_per_s_per_gpu": round(in_bytes / el / 1e9, 3),
+           "d2h_gb_per_s_per_gpu": round(out_bytes / el / 1e9, 3), "pinned": True,
            "path": "mfp_process_pipelined: pinned host arena -> 2 HIP streams (H2D | kernels | D2H) -> pinned "
                    "records + fingerprints" + (" + classifier results" if analysis else "")}
-    try:
-        res["json"] = json_writer_rate(av, d, out[0], out[1], min(n, 2_000_000), 16, analysis)
-        jr = res["json"]["value"]
-        res["json"]["with_gpu_path_serial_mpkt_s"] = round(1.0 / (1.0 / res["value"] + 1.0 / jr), 3)
-        res["json_overlapped"] = json_overlapped(torch, ctx, av, d, n, analysis, chunk, out)
-    except Exception as e:
-        log(f"json leg failed: {e}")
+    if with_json:
+        try:
+            res["json"] = json_writer_rate(av, d, out[0], out[1], min(n, 2_000_000), 16, analysis)
+            jr = res["json"]["value"]
+            res["json"]["with_gpu_path_serial_mpkt_s"] = round(1.0 / (1.0 / res["value"] + 1.0 / jr), 3)
+            res["json_overlapped"] = json_overlapped(torch, ctx, av, d, n, analysis, chunk, out)
+        except Exception as e:
+            log(f"json leg failed: {e}")
     return res
 
 
@@ -168,18 +210,27 @@ def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_00
     sets = [(rec_a[:batch], fp_a, an_a[:batch] if analysis else None), (rec_b, fp_b, an_b)]
     ts = np.full(batch, 1_700_000_000 * 10**9, np.uint64)
     ends = np.zeros(batch, np.uint64)
-    cap = batch * 640
+    cap = batch * 1024
     jbuf = np.empty(cap, np.uint8)
     skipped = ctypes.c_uint64(0)
     total = [0]
 
+    errors = []
+
     def write(dk, o):
-        got = lib.mfp_write_json_batch(av.ctypes.data, dk.ctypes.data, len(dk), o[0].ctypes.data, o[1].ctypes.data,
-                                       ts.ctypes.data, jbuf.ctypes.data, cap, ends.ctypes.data,
-                                       ctypes.byref(skipped), threads)
-        if got < 0:
-            raise RuntimeError("mfp_write_json_batch failed")
-        total[0] += got
+        try:
+            got = lib.mfp_write_json_batch(av.ctypes.data, dk.ctypes.data, len(dk), o[0].ctypes.data,
+                                           o[1].ctypes.data, ts.ctypes.data, jbuf.ctypes.data, cap, ends.ctypes.data,
+                                           ctypes.byref(skipped), threads)
+            if got < 0:
+                raise RuntimeError("mfp_write_json_batch failed: " + lib.mfp_last_error().decode())
+            if skipped.value:
+                raise RuntimeError(f"mfp_write_json_batch skipped {skipped.value} records")
+            if got < len(dk) * 16:
+                raise RuntimeError(f"implausible JSON size {got} for {len(dk)} packets")
+            total[0] += got
+        except Exception as e:   # re-raised by the caller after join()
+            errors.append(e)
 
     nb = n // batch
     d0 = np.ascontiguousarray(d[:batch])
@@ -197,9 +248,13 @@ def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_00
         ctx.process_pipelined(av, dk, chunk=chunk, analysis=analysis, out=o)
         if th:
             th.join()
+        if errors:
+            raise errors[0]
         prev = (dk, o)
     write(*prev)
     el = time.perf_counter() - t0
+    if errors:
+        raise errors[0]
     return {"value": round(nb * batch / el / 1e6, 3), "unit": "Mpkt/s", "packets": nb * batch, "batch": batch,
             "threads": threads, "json_gb_per_s": round(total[0] / el / 1e9, 3),
             "path": "pinned packets -> mfp_process_pipelined (batch k) || mfp_write_json_batch (batch k-1) -> "
@@ -235,6 +290,37 @@ def json_writer_rate(arena, desc, rec, fp, n, threads, analysis):
                     (" minus the 'analysis' object (not built yet)" if analysis else "")}
 
 
+# protocol bin of a record's message (mfp_kernels.hip msg_bin) and its name
+BIN_NAMES = ["tls_ch", "http_req", "tcp_syn", "http_resp", "other", "tls_sh", "ssh", "dtls"]
+MSG_BIN = np.array([4, 0, 5, 5, 6, 6, 1, 3, 2, 2, 7, 7, 7] + [4] * 243, np.int64)
+
+
+def kernel_bytes(rec, desc, an):
+    """Algorithmic HBM bytes per step of each kernel:
+    what the kernel must read and write at least, from the packets' own
+    sizes.  k_classify: descriptor + the packet's first 128 bytes + the bin id
+    and index; a bin kernel: index + descriptor + the whole packet + record +
+    the fingerprint (+ its 8-byte hash); k_analyze: record + analysis record,
+    plus the fingerprint hash and the packet's address/name bytes of each
+    classified packet (table reads are L2/MALL-resident, not counted)."""
+    cap = desc["caplen"].astype(np.int64)
+    fl = rec["fp_len"].astype(np.int64)
+    hashed = np.where((rec["flags"] & 4) != 0, 8, 0)
+    b = MSG_BIN[rec["msg"].astype(np.int64)]
+    per_pkt = 4 + 16 + cap + 32 + fl + hashed
+    out = {"k_classify": int((16 + np.minimum(cap, 128) + 5).sum())}
+    sums = np.bincount(b, weights=per_pkt, minlength=8)
+    for k, nm in enumerate(BIN_NAMES):
+        for kern in ("k_fingerprint/", "k_fp_seg/", "k_wave_fp/"):
+            out[kern + nm] = int(sums[k])
+    if an is not None:
+        valid = (an["flags"] & 1) != 0
+        sn = np.where(rec["sni_len"] == 0xffff, 0, rec["sni_len"]).astype(np.int64)
+        ua = np.where(rec["ua_len"] == 0xffff, 0, rec["ua_len"]).astype(np.int64)
+        out["k_analyze"] = int(len(rec) * (32 + 24) + (valid * (8 + 16 + 32 + sn + ua)).sum())
+    return out
+
+
 def find_traffic(cfg_key):
     """Counter-derived HBM bytes per step for this configuration, if profiled."""
     best = None
@@ -248,6 +334,41 @@ def find_traffic(cfg_key):
     return best
 
 
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes
+    (this process never touches the GPU) with the torch.distributed.run
+    environment, rank 0's stdout passed through; exit with the worst status."""
+    import signal
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
+    log(f"[spawn] {n} rank processes: {[p.pid for p in procs]}")
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            r = p.poll()
+            if r is None:
+                continue
+            pending.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in pending:   # one rank failed: the others would wait at a barrier forever
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -258,13 +379,21 @@ def main():
     ap.add_argument("--unique", type=int, default=1_000_000)
     ap.add_argument("--tls-format", type=int, default=0, help="without --analysis (else the archive's)")
     ap.add_argument("--no-analysis", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--e2e-packets", type=int, default=10_000_000,
-                    help="host-resident (H2D/D2H-inclusive) leg on this many packets; 0 = skip")
+    ap.add_argument("--e2e-total", type=int, default=200_000_000,
+                    help="config 5: host-resident (H2D/D2H-inclusive) packets per job, split over the ranks; 0 = skip")
+    ap.add_argument("--e2e-buffer", type=int, default=10_000_000,
+                    help="packets in each rank's page-locked source buffer (looped up to its share)")
     ap.add_argument("--e2e-chunk", type=int, default=2_000_000)
+    ap.add_argument("--no-json-leg", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check without a GPU: ranks start, join the gloo group, report, exit")
     args = ap.parse_args()
     analysis = not args.no_analysis
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import mercury_amd
@@ -272,13 +401,31 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
+    if world != args.gpus:
+        log(f"[rank {rank}] note: WORLD_SIZE={world} overrides --gpus {args.gpus}")
+    tdist = None
+    if world > 1:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        # control only (barrier, max-over-ranks): gloo on the host, no RCCL;
+        # single node: the loopback interface (the hostname may not resolve)
+        if os.environ.get("MASTER_ADDR") in ("127.0.0.1", "localhost") and os.path.exists("/sys/class/net/lo"):
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        tdist.init_process_group("gloo")
+    if args.dry_run:
+        info = {"rank": rank, "local_rank": local, "pid": os.getpid()}
+        seen = [None] * world
+        if tdist:
+            tdist.all_gather_object(seen, info)
+            tdist.barrier()
+        else:
+            seen = [info]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": seen, "backend": "gloo" if tdist else None}),
+                  flush=True)
+        if tdist:
+            tdist.destroy_process_group()
+        return
+    torch.cuda.set_device(local)
 
     workload = args.workload
     n = args.packets or (50_000_000 if workload == "mixed" else 10_000_000)
@@ -286,20 +433,21 @@ def main():
 
     t0 = time.time()
     ua, ud, d_arena, desc, d_desc = build_device_batch(torch, n, workload, draw_seed, args.unique)
-    log(f"[rank {rank}] batch: {n} packets, {int(desc['caplen'].astype(np.int64).sum()) / 1e9:.2f} GB "
+    log(f"[rank {rank}] batch on cuda:{local}: {n} packets, {int(desc['caplen'].astype(np.int64).sum()) / 1e9:.2f} GB "
         f"({time.time() - t0:.1f} s to build)")
 
     if analysis:
         cfg = f"select={CONTRACT};resources={RESOURCES};analysis"
-        ctx = mercury_amd.Context(cfg, device=torch.cuda.current_device())
+        ctx = mercury_amd.Context(cfg, device=local)
         assert ctx.analysis_enabled
     else:
         cfg = CONTRACT if args.tls_format == 0 else f"select={CONTRACT};format=tls/{args.tls_format}"
-        ctx = mercury_amd.Context(cfg, device=torch.cuda.current_device())
+        ctx = mercury_amd.Context(cfg, device=local)
     tls_format = mercury_amd.parse_filter(cfg)[1] if not analysis else None
 
     # size the fp arena from the unique set (exact per replica)
     rec_u, fp_u = ctx.process_host(ua, ud)
+    distinct_fps = len(set(mercury_amd.fingerprints(rec_u, fp_u)) - {""})
     reps = (n + len(ud) - 1) // len(ud)
     cap = int(int(rec_u["fp_len"].astype(np.int64).sum() + 16 * len(ud)) * reps * 1.05) + (2 << 30)
     d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
@@ -323,21 +471,21 @@ def main():
         raise RuntimeError("fp arena overflow")
 
     ctx.profile(True)   # HIP events around every kernel launch, on `stream`
-    if dist:
+    if tdist:
         tdist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if dist:
+    if tdist:
         tdist.barrier()
     elapsed = time.perf_counter() - t_start
     prof = ctx.profile_read()
     ctx.profile(False)
-    if dist:
+    if tdist:
         from mercury_amd import shard
-        elapsed = shard.max_over_ranks(elapsed, device="cuda")
+        elapsed = shard.max_over_ranks(elapsed)
 
     rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
     caplen_bytes = int(desc["caplen"].astype(np.int64).sum())
@@ -361,15 +509,26 @@ def main():
     step_kern_ms = sum(kern_ms.values())
     dominant = max(kern_ms, key=kern_ms.get)
     achieved = alg_bytes / (step_kern_ms * 1e-3) / 1e9
+    kbytes = kernel_bytes(rec, desc, an if analysis else None)
 
     total_pkts = n * world
     value = total_pkts * args.steps / elapsed / 1e6
+    e2e = None
+    if args.e2e_total:
+        del d_arena, d_desc, d_fp          # room for the pipeline's staging buffers
+        torch.cuda.empty_cache()
+        try:
+            e2e = end_to_end(torch, ctx, ua, ud, args.e2e_buffer, args.e2e_total // world, analysis,
+                             args.e2e_chunk, tdist, world, world == 1 and not args.no_json_leg)
+        except Exception as e:   # reported beside the device-resident number, never instead of it
+            log(f"[rank {rank}] end-to-end leg failed: {e}")
+            if tdist:
+                raise
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, len(os.sched_getaffinity(0)))
             try:
-                cpu = cpu_baseline(workload, draw_seed, 200_000, threads, args.cpu_seconds, analysis)
+                cpu = cpu_baseline(workload, draw_seed, 200_000, cpu_threads(), args.cpu_seconds, analysis)
             except Exception as e:   # baseline is reported, never the target
                 log(f"cpu baseline failed: {e}")
         cfg_key = f"{workload}/{n}/{'analysis' if analysis else 'fp'}"
@@ -378,14 +537,6 @@ def main():
         if tr:
             traffic = tr[1]["hbm_bytes_per_step"]
         n_fp = int((rec["fp_type"] > 0).sum())
-        e2e = None
-        if world == 1 and args.e2e_packets:
-            del d_arena, d_desc, d_fp          # room for the pipeline's staging buffers
-            torch.cuda.empty_cache()
-            try:
-                e2e = end_to_end(torch, ctx, ua, ud, args.e2e_packets, analysis, 3, args.e2e_chunk)
-            except Exception as e:   # reported beside the device-resident number, never instead of it
-                log(f"end-to-end leg failed: {e}")
         if workload == "mixed":
             wl = ("config 4: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint + --analysis classifier "
                   "(synthetic resource archive)") if analysis else \
@@ -417,6 +568,7 @@ def main():
                 "resources": os.path.relpath(RESOURCES, ROOT) if analysis else None,
                 "tls_format": "archive's (tls/1)" if analysis else tls_format,
                 "parallelism": f"shard{world}",
+                "distinct_fingerprints_per_step": distinct_fps,
             },
             "gb_per_s": round(caplen_bytes * world * args.steps / elapsed / 1e9, 3),
             "fingerprints_per_step": n_fp,
@@ -424,25 +576,30 @@ def main():
             "analysis": an_info,
             "roofline": {
                 "bound": "hbm",
-                "achieved": round(achieved, 2),
+                "achieved": round(kbytes.get(dominant, 0) / (kern_ms[dominant] * 1e-3) / 1e9, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
+                "frac": round(kbytes.get(dominant, 0) / (kern_ms[dominant] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "traffic": (traffic or {}).get(dominant) if isinstance(traffic, dict) else None,
                 "traffic_source": os.path.relpath(tr[0], ROOT) if tr else None,
-                "kernel": "step pipeline (every kernel of one step, back to back on one stream)",
-                "kernel_ms": round(step_kern_ms, 4),
-                "dominant_kernel": dominant,
-                "algorithmic_bytes_per_launch": alg_bytes,
+                "kernel": dominant,
+                "kernel_ms_per_launch": round(kern_ms[dominant] / max(1.0, prof[dominant][0] / args.steps), 4),
+                "algorithmic_bytes_per_launch": kbytes.get(dominant, 0),
+                "step": {"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "kernel_ms": round(step_kern_ms, 4), "algorithmic_bytes": alg_bytes,
+                         "traffic": traffic if not isinstance(traffic, dict) else traffic.get("step"),
+                         "what": "every kernel of one step, back to back on one stream"},
             },
-            "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4)}
+            "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4),
+                            "algorithmic_bytes": kbytes.get(k),
+                            "achieved_gb_s": round(kbytes[k] / (v * 1e-3) / 1e9, 2) if kbytes.get(k) and v else None}
                         for k, v in kern_ms.items()},
             "cpu_baseline": cpu,
             "end_to_end": e2e,
         }
         print(json.dumps(out), flush=True)
     ctx.close()
-    if dist:
+    if tdist:
         tdist.destroy_process_group()
 
 

@@ -492,6 +492,10 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint
     return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, nullptr);
 }
 
+static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                                  size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                  size_t chunk);
+
 extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                       const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                       char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
@@ -499,7 +503,20 @@ extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8
     if (!c) { mfp_set_error("null context"); return -1; }
     if (analysis && !c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(hipSetDevice(c->device));
+    if (hipSetDevice(c->device) != hipSuccess) { mfp_set_error("hipSetDevice failed"); return -2; }
+    const long long r = pipelined_locked(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, chunk);
+    if (r < 0) {
+        // an error path may leave copies into the caller's buffers queued on
+        // either pipeline stream: drain both before the caller reuses them
+        // (the error string of the failure is kept)
+        for (int s = 1; s <= 2; s++) (void)hipStreamSynchronize(c->slot[s].stream);
+    }
+    return r;
+}
+
+static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                                  size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                  size_t chunk) {
     if (chunk == 0) chunk = (size_t)1 << 20;
     struct Inflight { bool live; size_t lo, hi; };
     Inflight inf[2] = {{false, 0, 0}, {false, 0, 0}};

@@ -22,6 +22,7 @@
 // utf8.hpp:200-340); IPv6 addresses through its zero-run compression
 // (append_ipv6_addr buffer_stream.h:534-690, quirks included).
 
+#include <algorithm>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -52,7 +53,9 @@ struct alignas(64) Out {
     size_t cap = 0, len = 0;
     void need(size_t n) {
         if (len + n <= cap) return;
-        size_t c = (len + n) * 2;
+        // the first reservation of a call is its estimate: exact; growth
+        // while formatting: x1.5 (ample for records longer than estimated)
+        size_t c = len == 0 ? n : std::max(len + n, cap + cap / 2);
         std::unique_ptr<char[]> b(new char[c]);
         if (len) memcpy(b.get(), buf.get(), len);
         buf.swap(b);
@@ -422,6 +425,11 @@ MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_de
     for (int t = 0; t < threads; t++) { base[(size_t)t] = total; total += part[(size_t)t].len; nbad += bad[(size_t)t]; }
     if (skipped) *skipped = nbad;
     auto give_back = [&]() {
+        // keep buffers for the next call (page faults on a fresh multi-GB
+        // buffer cost more than the formatting), but not oversized ones: a
+        // huge batch must not pin its footprint for the life of the process
+        static const size_t kKeep = (size_t)256 << 20;
+        for (auto &o : part) if (o.cap > kKeep) { o.buf.reset(); o.cap = 0; }
         std::lock_guard<std::mutex> lk(pool_mu);
         if (pool.size() < part.size()) pool.swap(part);
     };

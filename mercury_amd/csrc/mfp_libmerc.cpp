@@ -128,9 +128,16 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
     p->fp.resize(cap);
     long long used = mfp_process_batch_host(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap);
     if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
-    uint64_t t = (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec, end = 0;
+    uint64_t t = (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec, end = 0, skipped = 0;
     long long n = mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
-                                       buffer_size, &end, nullptr, 1);
+                                       buffer_size, &end, &skipped, 1);
+    if (skipped) {
+        // the reference writes a record here; the writer cannot rebuild it
+        // (IP-in-IP with an outer IPv6 extension header): say so instead of
+        // returning a silent 0
+        log_error("write_json: record not rebuilt (IP-in-IP, outer IPv6 header with extension headers)\n");
+        return 0;
+    }
     if (n <= 0 || (size_t)n >= buffer_size) return 0;    // buffer_stream keeps one byte for its NUL
     return (size_t)n;
 }

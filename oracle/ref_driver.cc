@@ -12,8 +12,9 @@
 //   idx  valid  fp_type  status  process  score  malware  p_malware  fp_string
 // Mode "json": the write_json record text, one line per packet (empty line
 // when the reference writes nothing).
-// Mode "time": run write_json with T threads (one processor per thread over
-// contiguous shards), print packets/s.
+// Mode "time": run write_json (or, with a trailing "an", the analysis_context
+// entry) with T threads (one processor per thread over contiguous shards),
+// print packets/s.
 //
 // Uses the reference's public C API (libmerc.h:211-736) plus the processor's
 // analysis context (pkt_proc.h:132), exactly as the reference's own unit-test
@@ -93,7 +94,7 @@ static int sni_mode(const char *path) {
 int main(int argc, char **argv) {
     if (argc == 3 && std::string(argv[1]) == "sni") return sni_mode(argv[2]);
     if (argc < 4) {
-        fprintf(stderr, "usage: %s fp|an|time <input> <config-string> [resources] [threads] [seconds]\n", argv[0]);
+        fprintf(stderr, "usage: %s fp|an|json|time <input> <config-string> [resources] [threads] [seconds] [json|an]\n", argv[0]);
         return 2;
     }
     std::string mode = argv[1];
@@ -163,6 +164,9 @@ int main(int argc, char **argv) {
     } else if (mode == "time") {
         int threads = argc > 5 ? atoi(argv[5]) : 1;
         double secs = argc > 6 ? atof(argv[6]) : 10.0;
+        // entry point timed: "json" = write_json_linktype (the CLI's path),
+        // "an" = get_analysis_context_linktype (the embedders' path)
+        const bool an_entry = argc > 7 && std::string(argv[7]) == "an";
         std::vector<std::thread> th;
         std::vector<unsigned long long> counts(threads, 0);
         auto t0 = std::chrono::steady_clock::now();
@@ -176,8 +180,12 @@ int main(int argc, char **argv) {
                 do {
                     for (size_t i = lo; i < hi; i++) {
                         struct timespec ts{1700000000, 0};
-                        mercury_packet_processor_write_json_linktype(p, o.data(), o.size(), (uint8_t *)pkts[i].data,
-                                                                     pkts[i].len, &ts, pkts[i].linktype);
+                        if (an_entry)
+                            mercury_packet_processor_get_analysis_context_linktype(p, (uint8_t *)pkts[i].data,
+                                                                                   pkts[i].len, &ts, pkts[i].linktype);
+                        else
+                            mercury_packet_processor_write_json_linktype(p, o.data(), o.size(), (uint8_t *)pkts[i].data,
+                                                                         pkts[i].len, &ts, pkts[i].linktype);
                     }
                     c += hi - lo;
                 } while (std::chrono::duration<double>(std::chrono::steady_clock::now() - start).count() < secs);

@@ -15,10 +15,10 @@ fi
 timeout -k 10 600 python -u bench.py ${BENCH_MAIN:-} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
 if [ -n "$BENCH_AN" ]; then
-  timeout -k 10 600 python -u bench.py --no-analysis --no-cpu-baseline --e2e-packets 0 > $O/bench_fp.json 2> $O/bench_fp.err || { tail -20 $O/bench_fp.err; exit 1; }
+  timeout -k 10 600 python -u bench.py --no-analysis --no-cpu-baseline --e2e-total 0 > $O/bench_fp.json 2> $O/bench_fp.err || { tail -20 $O/bench_fp.err; exit 1; }
   cat $O/bench_fp.json
 fi
-P="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-packets 0 ${BENCH_ARGS:-}"
+P="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-total 0 ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o kt -- $P > $O/kt.out 2>&1 || { tail -20 $O/kt.out; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o fetch -- $P > $O/fetch.out 2>&1 || { tail -20 $O/fetch.out; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write -o write -- $P > $O/write.out 2>&1 || { tail -20 $O/write.out; exit 1; }
