@@ -46,7 +46,7 @@ typedef struct {
     uint8_t  fp_type;    /* enum fingerprint_type (libmerc.h:351-373)     */
     uint8_t  msg;        /* protocol tag, MFP_MSG_*                       */
     uint8_t  flags;      /* MFP_FLAG_*                                    */
-    uint8_t  status;     /* enum fingerprint_status (libmerc.h:307-313)   */
+    uint8_t  status;     /* reserved, 0 (the classifier status is mfp_analysis.status) */
     /* classifier inputs (destination_context, result.h:346): offsets are
      * relative to the packet start, len 0xffff = absent */
     uint16_t sni_off, sni_len;
@@ -165,7 +165,7 @@ MFP_EXPORT int mfp_analysis_enabled(mfp_context ctx);
 
 /* Classify a device-resident batch already fingerprinted by
  * mfp_process_batch_device on the same stream (records and fp arena as it
- * left them).  d_out: n mfp_analysis records; rec[i].status is set too.
+ * left them).  d_out: n mfp_analysis records (the records are read only).
  * Batches must be submitted in stream order: the unknown-TLS status
  * (randomized / unlabeled) depends on earlier sightings. */
 MFP_EXPORT int mfp_analyze_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,

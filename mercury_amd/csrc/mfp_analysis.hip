@@ -356,38 +356,53 @@ ADEV uint32_t asn_v6_lane(const mfp_classifier_dev &D, uint64_t xh, uint64_t xl)
 // so the normalized name is the input itself.  *tld: offset of the top two
 // labels (get_tld_domain_name, naive_bayes.hpp:557).  Anything else takes the
 // wave path (normalize_server_name, mfp_common.hpp).
+ADEV uint64_t swar_eq8(uint64_t w, uint32_t c) {
+    const uint64_t x = w ^ (0x0101010101010101ull * (c & 0xff));
+    return ~(((x & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | x) & 0x8080808080808080ull;
+}
+ADEV uint64_t swar_range8(uint64_t w, uint32_t lo, uint32_t hi) {   // lo <= byte <= hi (ASCII, hi < 0x80)
+    const uint64_t x = w & 0x7f7f7f7f7f7f7f7full;
+    const uint64_t ge = x + 0x0101010101010101ull * (0x80 - lo);
+    const uint64_t gt = x + 0x0101010101010101ull * (0x7f - hi);
+    return ge & ~gt & ~w & 0x8080808080808080ull;
+}
 ADEV bool plain_server_name(const uint8_t *s, uint32_t n, uint32_t &tld, uint64_t &h) {
+    // word at a time (SWAR byte classes, bit 7 of each byte flags it)
     if (n == 0 || n > 256) return false;
     int last_dot = -1, prev_dot = -1;
-    bool ok = true, alpha_last = false;
-    uint32_t prevc = '.';
+    bool ok = true, alpha_last = false, prev_is_dot = true;   // a leading dot is an empty label
     uint64_t acc = 0;
     for (uint32_t j0 = 0; 8 * j0 < n; j0 += LB) {
         uint64_t w[LB];
         load_words<LB>(s, n, j0, w);
 #pragma unroll
         for (int q = 0; q < LB; q++) {
-            if (8 * (j0 + q) < n) acc ^= word_term(w[q], j0 + q);
-#pragma unroll
-            for (uint32_t b = 0; b < 8; b++) {
-                const uint32_t k = 8 * (j0 + q) + b;
-                if (k < n) {
-                    const uint32_t c = (uint32_t)(w[q] >> (8 * b)) & 0xff;
-                    if (c == '.') {
-                        ok &= prevc != '.';
-                        prev_dot = last_dot;
-                        last_dot = (int)k;
-                        alpha_last = false;
-                    } else {
-                        ok &= is_label_char(c);
-                        alpha_last |= is_alpha(c);
-                    }
-                    prevc = c;
+            const uint32_t pos = 8 * (j0 + q);
+            if (pos < n) {
+                acc ^= word_term(w[q], j0 + q);
+                const uint64_t valid = n - pos >= 8 ? 0x8080808080808080ull : (0x8080808080808080ull >> (8 * (8 - (n - pos))));
+                const uint64_t x = w[q];
+                const uint64_t dot = swar_eq8(x, '.') & valid;
+                const uint64_t alpha = (swar_range8(x, 'a', 'z') | swar_range8(x, 'A', 'Z')) & valid;
+                const uint64_t label = alpha | swar_range8(x, '0', '9') | swar_eq8(x, '-') | swar_eq8(x, '_');
+                ok &= ((label & valid) | dot) == valid;
+                // empty label: a dot right after a dot (or at the start)
+                ok &= (dot & ((dot << 8) | (prev_is_dot ? 0x80ull : 0ull))) == 0;
+                if (dot) {
+                    const int hi = 63 - __builtin_clzll(dot);
+                    const uint64_t rest = dot & ~(1ull << hi);
+                    prev_dot = rest ? (int)pos + ((63 - __builtin_clzll(rest)) >> 3) : last_dot;
+                    last_dot = (int)pos + (hi >> 3);
+                    alpha_last = (alpha >> hi) != 0;       // letters after this word's last dot
+                } else {
+                    alpha_last |= alpha != 0;
                 }
+                const uint32_t top = (n - pos >= 8 ? 8 : n - pos) * 8 - 1;   // bit 7 of the word's last byte
+                prev_is_dot = (dot >> top) & 1;
             }
         }
     }
-    ok &= prevc != '.' && last_dot >= 0 && alpha_last;
+    ok &= !prev_is_dot && last_dot >= 0 && alpha_last;
     tld = (uint32_t)(prev_dot + 1);
     h = hash_final(acc, n);
     return ok;
@@ -460,7 +475,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         if (typed && !analyzable) { a.status = 4; a.flags = MFP_AN_VALID; }   // fingerprint_status_unanalyzed
         const uint64_t am = __ballot(analyzable);
         if (!am) {
-            if (live) { P.out[i] = a; P.rec[i].status = a.status; }
+            if (live) P.out[i] = a;
             if (lane == 0) P.pend_bits[g] = 0;
             continue;
         }
@@ -719,10 +734,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             // keeps its classification (pkt_proc.cc:1716-1719)
             if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED) && !pending) a.status = 3;
         }
-        if (live) {
-            P.out[i] = a;
-            P.rec[i].status = a.status;
-        }
+        if (live) P.out[i] = a;   // the status lives in the analysis record only (no 1-byte record rewrite)
     }
     if (lane == 0 && n_an) atomicAdd(&P.stats[0], (unsigned long long)n_an);
     if (lane == 0 && n_pend) atomicAdd(&P.stats[1], (unsigned long long)n_pend);
@@ -928,7 +940,6 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
         }
         if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
         P.out[i] = a;
-        P.rec[i].status = a.status;
     }
     }
 }

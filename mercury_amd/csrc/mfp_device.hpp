@@ -18,6 +18,7 @@
 namespace mfp {
 
 #define DEV __device__ __forceinline__
+#define DEV_HD_CONSTEXPR constexpr __host__ __device__
 
 // ---------------------------------------------------------------------------
 // cursor == struct datum (datum.h:220-850); null cursor has d == nullptr
@@ -210,10 +211,15 @@ DEV uint32_t c_tolower(uint32_t c) { return c_isupper(c) ? c + 32 : c; }
 // ---------------------------------------------------------------------------
 constexpr uint32_t FP_MAX = 8192;   // fingerprint::MAX_FP_STR_LEN fingerprint.h:15
 
+struct TlsPlan;
 template <bool EMIT>
 struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
+    bool punt = false;       // the message needs a parser family this walker lacks
+    DEV void punt_pkt() { punt = true; }
+    static constexpr bool PLAN = !EMIT;   // pass 1 records a ClientHello plan (TlsPlan) in *plan
+    TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
     static constexpr bool emit_pass() { return EMIT; }
     // Pass-2 output.  The string starts 64-byte aligned and owns its slot
@@ -228,12 +234,17 @@ struct Em {
     uint64_t acc = 0;        // staged bytes of the current word
     uint32_t nacc = 0;       // bytes in acc
     uint32_t nw = 0;         // words in the LDS line
+    uint32_t wi = 0;         // words completed (string hash position)
+    uint64_t h = 0;          // mfpc::str_hash accumulator of the words so far
 
     DEV void begin(uint8_t *o, uint64_t *lds_line) {
         out = o;
         line = lds_line;
-        acc = 0; nacc = 0; nw = 0;
+        acc = 0; nacc = 0; nw = 0; wi = 0; h = 0;
     }
+    // the string's mfpc::str_hash (after finish()): the classifier's lookup
+    // key, stored behind the string so k_analyze never re-reads it
+    DEV uint64_t hash() const { return mfpc::hash_final(h, n); }
     DEV void flush_line(uint32_t words) {       // first `words` words of the line -> out
 #ifdef MFP_PROBE_NOSTORE
         if (acc == 0x0123456789abcdefull) *(volatile uint8_t *)out = 0;   // keep the value live
@@ -244,6 +255,7 @@ struct Em {
         for (uint32_t k = 0; 2 * k < words; k++) o4[k] = l4[k];
     }
     DEV void put_word() {
+        h ^= mfpc::word_term(acc, wi++);
         line[nw++] = acc;
         if (nw == 8) { flush_line(8); out += 64; nw = 0; }
     }
@@ -265,7 +277,7 @@ struct Em {
     }
     DEV void finish() {
         if (EMIT) {
-            if (nacc) { line[nw++] = acc; nacc = 0; }
+            if (nacc) { h ^= mfpc::word_term(acc, wi++); line[nw++] = acc; nacc = 0; }
             if (nw) flush_line(nw);
         }
     }
@@ -295,6 +307,7 @@ struct Em {
             push(v & ((1ull << (8 * k)) - 1), k);
         }
     }
+    DEV void hex16s(uint32_t m) { n += 4 * m; last_putc = false; }   // m hex16 appends (length only)
     DEV void hex16(uint32_t v) {                // append_uint16_hex buffer_stream.h:425
         last_putc = false;
         uint64_t w = hex2((v >> 8) & 0xff) | (hex2(v & 0xff) << 16);
@@ -329,6 +342,7 @@ DEV uint32_t seg_src(uint32_t s) { return s >> 15; }
 
 struct SegEm {
     static constexpr bool SEG = true;
+    static constexpr bool PLAN = false;
     static constexpr bool emit_pass() { return false; }
     uint32_t n = 0;                     // characters produced
     bool last_putc = false;
@@ -340,6 +354,7 @@ struct SegEm {
     uint32_t sp_src = 0, sp_len = 0;    // hex bytes right after the open '(' (0 = none)
 
     DEV SegEm(const uint8_t *b, uint32_t *s) : base(b), seg(s) {}
+    DEV void punt_pkt() { ovf = true; }
     DEV void store(uint32_t kind, uint32_t src, uint32_t end) {
         if (nseg >= (uint32_t)SEG_MAX) { ovf = true; return; }
         seg[nseg++] = (end & 0x1fff) | (kind << 13) | (src << 15);
@@ -388,6 +403,7 @@ struct SegEm {
         n += k;
     }
     DEV void hex16(uint32_t) { ovf = true; n += 4; last_putc = false; }
+    DEV void hex16s(uint32_t m) { ovf = true; n += 4 * m; last_putc = false; }
     DEV void hex8(uint32_t) { ovf = true; n += 2; last_putc = false; }
     DEV void push(uint64_t, uint32_t k) { ovf = true; n += k; }
     DEV void finish() { flush_open(); }
@@ -481,7 +497,7 @@ template <class E>
 DEV void hex_degrease(E &b, const uint8_t *p, long len) {   // raw_as_hex_degrease tls.h:802
     if (len % 2) len--;
     if (!E::emit_pass()) {                       // pass 1: lengths only
-        for (long i = 0; i < len; i += 2) b.hex16(0);
+        if (len >= 2) b.hex16s((uint32_t)(len / 2));
         return;
     }
     LeStream st;
@@ -618,6 +634,41 @@ DEV void ext_fp1(E &b, Ext &x, int role) {
     }
 }
 
+// format 0 output of one extension (the loop body of tls_extensions::fingerprint, tls.h:1553-1613)
+template <class E>
+DEV void ext_fp0(E &b, const Ext &x, int role) {
+    if (is_static_ext(x.type)) {
+        if (x.type == 0x000a || x.type == 0x002b) {
+            b.putc('(');
+            if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+            if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
+            ext_degreased_value(b, x, x.type == 0x000a ? 2 : (role == 0 ? 1 : 0));
+            b.putc(')');
+        } else if (x.type == 0x39 || x.type == 0xffa5) {
+            b.putc('('); b.putc('(');
+            if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+            b.putc(')');
+            b.putc('(');
+            Cur v = x.value;
+            while (!cnull(v)) {
+                Cur id;
+                if (qtp_parse(v, id)) { b.putc('('); qtp_write_id(b, id); b.putc(')'); }
+            }
+            b.putc(')'); b.putc(')');
+        } else {
+            b.putc('(');
+            if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+            if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
+            if (cnotempty(x.value)) b.hex(x.value.d, clen(x.value));
+            b.putc(')');
+        }
+    } else {
+        b.putc('(');
+        if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
+        b.putc(')');
+    }
+}
+
 // format 0: tls_extensions::fingerprint tls.h:1549
 template <class E>
 DEV void exts_fp0(E &b, Cur exts, int role) {
@@ -626,36 +677,7 @@ DEV void exts_fp0(E &b, Cur exts, int role) {
     while (clen(p) > 0) {
         Ext x = ext_parse(p);
         if (!x.ok) break;
-        if (is_static_ext(x.type)) {
-            if (x.type == 0x000a || x.type == 0x002b) {
-                b.putc('(');
-                if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
-                if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
-                ext_degreased_value(b, x, x.type == 0x000a ? 2 : (role == 0 ? 1 : 0));
-                b.putc(')');
-            } else if (x.type == 0x39 || x.type == 0xffa5) {
-                b.putc('('); b.putc('(');
-                if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
-                b.putc(')');
-                b.putc('(');
-                Cur v = x.value;
-                while (!cnull(v)) {
-                    Cur id;
-                    if (qtp_parse(v, id)) { b.putc('('); qtp_write_id(b, id); b.putc(')'); }
-                }
-                b.putc(')'); b.putc(')');
-            } else {
-                b.putc('(');
-                if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
-                if (x.length_ptr) hex_degrease(b, x.length_ptr, 2);
-                if (cnotempty(x.value)) b.hex(x.value.d, clen(x.value));
-                b.putc(')');
-            }
-        } else {
-            b.putc('(');
-            if (x.type_ptr) hex_degrease(b, x.type_ptr, 2);
-            b.putc(')');
-        }
+        ext_fp0(b, x, role);
     }
     b.putc(')');
 }
@@ -703,17 +725,30 @@ DEV bool ext_tie_less(const Ext &a, const Ext &b) {
     return ccmp(a.value, b.value) < 0;
 }
 
-// per-lane LDS scratch for formats 1/2 (offset of each kept extension
-// relative to the extension block, and its primary key)
-constexpr int MAX_LDS_EXT = 32;
+// Formats 1 and 2 keep the extensions they emit as a sorted list in
+// registers: (primary key << 32 | wire offset), insertion-sorted as they are
+// parsed, so equal keys stay in wire order.  No LDS scratch per lane (the
+// previous 192-byte per-lane list halved the lane kernel's occupancy).  Equal
+// non-GREASE primary keys (a repeated extension type and length) need the
+// reference's value comparison, and more than REG_EXT kept extensions do not
+// fit: both take the selection over the wire list below (same total order).
+#ifndef MFP_REG_EXT
+#define MFP_REG_EXT 24
+#endif
+constexpr int REG_EXT = MFP_REG_EXT;
+DEV bool key_is_grease(uint32_t key, int fmt) {
+    return fmt == 1 ? (key >> 16) == 0x0a0a : !(key & (1u << 23));
+}
 
 // formats 1 and 2: sort kept extensions, then emit fingerprint_format1 each
 template <class E>
-DEV void exts_fp12(E &b, Cur exts, int role, int fmt, uint32_t *lds_key, uint16_t *lds_off, int stride) {
+DEV void exts_fp12(E &b, Cur exts, int role, int fmt) {
     b.putc('[');
-    // gather
+    uint64_t V[REG_EXT];
+#pragma unroll
+    for (int k = 0; k < REG_EXT; k++) V[k] = ~0ull;
     int n = 0;
-    bool overflow = false;
+    bool rare = false;
     {
         Cur p = exts;
         while (clen(p) > 0) {
@@ -726,62 +761,46 @@ DEV void exts_fp12(E &b, Cur exts, int role, int fmt, uint32_t *lds_key, uint16_
                 if (bucket < 0) continue;
                 // keep the first three per bucket (tls.h:1695-1701)
                 int cnt = 0;
-                for (int j = 0; j < n; j++) if ((lds_key[j * stride] >> 24) == (uint32_t)bucket) cnt++;
+#pragma unroll
+                for (int k = 0; k < REG_EXT; k++) cnt += (V[k] != ~0ull && (uint32_t)(V[k] >> 56) == (uint32_t)bucket);
                 if (cnt >= 3) continue;
             }
-            if (n >= MAX_LDS_EXT) { overflow = true; break; }
-            lds_key[n * stride] = ext_key(x, fmt, bucket);
-            lds_off[n * stride] = (uint16_t)(start - exts.d);
+            if (n >= REG_EXT) { rare = true; break; }
+            const uint32_t key = ext_key(x, fmt, bucket);
+            const uint64_t v = ((uint64_t)key << 32) | (uint32_t)(start - exts.d);
+            uint32_t pos = 0;
+            bool tie = false;
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) {
+                pos += V[k] < v ? 1u : 0u;
+                tie |= (uint32_t)(V[k] >> 32) == key;
+            }
+            if (tie && !key_is_grease(key, fmt)) rare = true;
+#pragma unroll
+            for (int k = REG_EXT - 1; k > 0; k--) V[k] = (uint32_t)k > pos ? V[k - 1] : ((uint32_t)k == pos ? v : V[k]);
+            if (pos == 0) V[0] = v;
             n++;
         }
     }
-    if (!overflow) {
-        if (!E::emit_pass()) {
-            // pass 1: the length does not depend on the order
-            for (int j = 0; j < n; j++) {
-                Cur q = cmk(exts.d + lds_off[j * stride], exts.e);
-                Ext x = ext_parse(q);
-                if (fmt == 2) fmt2_bucket(x);
-                ext_fp1(b, x, role);
-            }
-        } else {
-            // insertion sort (LDS), ties broken by value bytes
-            for (int i = 1; i < n; i++) {
-                uint32_t k = lds_key[i * stride];
-                uint16_t o = lds_off[i * stride];
-                int j = i;
-                while (j > 0) {
-                    uint32_t kj = lds_key[(j - 1) * stride];
-                    bool less = k < kj;
-                    if (!less && k == kj) {
-                        Cur qa = cmk(exts.d + o, exts.e), qb = cmk(exts.d + lds_off[(j - 1) * stride], exts.e);
-                        Ext a = ext_parse(qa), bb = ext_parse(qb);
-                        less = ext_tie_less(a, bb);
-                    }
-                    if (!less) break;
-                    lds_key[j * stride] = kj;
-                    lds_off[j * stride] = lds_off[(j - 1) * stride];
-                    j--;
-                }
-                lds_key[j * stride] = k;
-                lds_off[j * stride] = o;
-            }
-            for (int j = 0; j < n; j++) {
-                Cur q = cmk(exts.d + lds_off[j * stride], exts.e);
-                Ext x = ext_parse(q);
-                if (fmt == 2) fmt2_bucket(x);
-                ext_fp1(b, x, role);
-            }
+    if (!rare) {
+        // emit in key order (pass 1 only counts; the order does not change the length)
+        for (int j = 0; j < n; j++) {
+            const uint32_t off = (uint32_t)V[0];
+#pragma unroll
+            for (int k = 0; k < REG_EXT - 1; k++) V[k] = V[k + 1];
+            Cur q = cmk(exts.d + off, exts.e);
+            Ext x = ext_parse(q);
+            if (fmt == 2) fmt2_bucket(x);
+            ext_fp1(b, x, role);
         }
     } else {
-        // rare path (> MAX_LDS_EXT kept extensions): selection over the wire
-        // list, O(n^2), same total order
+        // selection over the wire list, O(n^2), the reference's comparator
+        // (key, then value bytes, then wire position)
         uint32_t prev_key = 0; long prev_pos = -1; bool have_prev = false;
         Ext prev_x; prev_x.type = 0; prev_x.length = 0; cset_null(prev_x.value);
         while (true) {
             long best_pos = -1; uint32_t best_key = 0; Ext best_x; best_x.type = 0; cset_null(best_x.value);
             Cur p = exts; long pos = 0;
-            // for fmt 2 we must respect the first-three-per-bucket rule
             while (clen(p) > 0) {
                 Ext x = ext_parse(p);
                 if (!x.ok) break;
@@ -873,12 +892,12 @@ DEV Ch tls_ch_parse(Cur p) {                            // tls_client_hello::par
     return ch;
 }
 template <class E>
-DEV void tls_ch_fp(E &b, const Ch &ch, int fmt, uint32_t *lk, uint16_t *lo, int stride) {   // tls.h:1928
+DEV void tls_ch_fp(E &b, const Ch &ch, int fmt) {   // tls.h:1928
     if (fmt >= 1 && fmt <= 2) { b.putc('0' + fmt); b.putc('/'); }
     b.putc('('); b.hex(ch.version.d, clen(ch.version)); b.putc(')');
     b.putc('('); hex_degrease(b, ch.ciphers.d, clen(ch.ciphers)); b.putc(')');
     if (fmt == 0) exts_fp0(b, ch.extensions, 0);
-    else exts_fp12(b, ch.extensions, 0, fmt, lk, lo, stride);
+    else exts_fp12(b, ch.extensions, 0, fmt);
 }
 // tls_extensions::set_meta_data tls.h:1316 (server_name; last one wins)
 DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len) {
@@ -896,6 +915,124 @@ DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len) {
         }
     }
 }
+// ClientHello plan: pass 1 of the lane kernels records what pass 2 needs to
+// write the fingerprint -- the ClientHello's version and cipher datums and its
+// extensions in emission order (format 0: wire order; formats 1/2: the sorted
+// list, key << 32 | offset) -- so pass 2 writes the string without walking the
+// link, IP, TCP and TLS headers and the extension list again.  More than
+// REG_EXT extensions, or a tie that needs value comparison, leaves the plan
+// unset and pass 2 walks the packet as before.
+struct TlsPlan {
+    uint32_t O[REG_EXT / 2];   // extension offsets in emission order, two 16-bit offsets per word
+    Cur version, ciphers, exts;
+    uint32_t n, type, fmt;
+    bool ok;
+};
+
+// pass 1 of a TLS/DTLS ClientHello: fingerprint length (through the counting
+// emitter), the server name (tls_extensions::set_meta_data tls.h:1316, last
+// one wins) and the plan -- one walk over the extension list
+template <class E>
+DEV void tls_ch_plan(E &b, TlsPlan &pl, const Ch &ch, int fmt, uint32_t type, const uint8_t *base,
+                     uint32_t &sni_off, uint32_t &sni_len) {
+    pl.ok = false;
+    fp_type_prefix(b, type);
+    if (fmt >= 1 && fmt <= 2) { b.putc('0' + fmt); b.putc('/'); }
+    b.putc('('); b.hex(ch.version.d, clen(ch.version)); b.putc(')');
+    b.putc('('); hex_degrease(b, ch.ciphers.d, clen(ch.ciphers)); b.putc(')');
+    const uint32_t n0 = b.n;
+    b.putc(fmt == 0 ? '(' : '[');
+    uint64_t V[REG_EXT];                         // key << 32 | offset, in emission order
+#pragma unroll
+    for (int k = 0; k < REG_EXT; k++) V[k] = ~0ull;
+    int n = 0;
+    bool rare = false;
+    Cur p = ch.extensions;
+    while (clen(p) > 0) {
+        const uint8_t *start = p.d;
+        Ext x = ext_parse(p);
+        if (!x.ok) break;
+        if (x.type == 0) {                       // server_name: bytes after the 9-byte header (tls.h:1342)
+            Cur e = cmk(start, p.d);
+            cskip(e, 9);
+            sni_off = (uint32_t)(e.d - base); sni_len = (uint32_t)clen(e);
+        }
+        if (rare) continue;
+        int bucket = 0;
+        if (fmt == 2) {
+            bucket = fmt2_bucket(x);
+            if (bucket < 0) continue;
+            int cnt = 0;                         // first three per bucket (tls.h:1695-1701)
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) cnt += (V[k] != ~0ull && (uint32_t)(V[k] >> 56) == (uint32_t)bucket);
+            if (cnt >= 3) continue;
+        }
+        if (n >= REG_EXT) { rare = true; continue; }
+        const uint32_t off = (uint32_t)(start - ch.extensions.d);
+        if (fmt == 0) {
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) if (k == n) V[k] = off;
+            ext_fp0(b, x, 0);
+        } else {
+            const uint32_t key = ext_key(x, fmt, bucket);
+            const uint64_t v = ((uint64_t)key << 32) | off;
+            uint32_t pos = 0;
+            bool tie = false;
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) {
+                pos += V[k] < v ? 1u : 0u;
+                tie |= (uint32_t)(V[k] >> 32) == key;
+            }
+            if (tie && !key_is_grease(key, fmt)) rare = true;
+#pragma unroll
+            for (int k = REG_EXT - 1; k > 0; k--)
+                V[k] = (uint32_t)k > pos ? V[k - 1] : ((uint32_t)k == pos ? v : V[k]);
+            if (pos == 0) V[0] = v;
+            ext_fp1(b, x, 0);
+        }
+        n++;
+    }
+    if (rare) {                                  // length by the general walk; pass 2 re-walks
+        b.n = n0;
+        if (fmt == 0) exts_fp0(b, ch.extensions, 0);
+        else exts_fp12(b, ch.extensions, 0, fmt);
+        return;
+    }
+    b.putc(fmt == 0 ? ')' : ']');
+#pragma unroll
+    for (int k = 0; k < REG_EXT / 2; k++) pl.O[k] = ((uint32_t)V[2 * k] & 0xffff) | ((uint32_t)V[2 * k + 1] << 16);
+    pl.version = ch.version; pl.ciphers = ch.ciphers; pl.exts = ch.extensions;
+    pl.n = (uint32_t)n; pl.type = type; pl.fmt = (uint32_t)fmt;
+    pl.ok = true;
+}
+
+// pass 2 from the plan: the same bytes tls_client_hello::fingerprint writes
+// (tls.h:1928-1964)
+template <class E>
+DEV void tls_ch_emit(E &b, TlsPlan &pl) {
+    fp_type_prefix(b, pl.type);
+    const int fmt = (int)pl.fmt;
+    if (fmt >= 1) { b.putc('0' + fmt); b.putc('/'); }
+    b.putc('('); b.hex(pl.version.d, clen(pl.version)); b.putc(')');
+    b.putc('('); hex_degrease(b, pl.ciphers.d, clen(pl.ciphers)); b.putc(')');
+    b.putc(fmt == 0 ? '(' : '[');
+    for (uint32_t j = 0; j < pl.n; j++) {
+        const uint32_t off = pl.O[0] & 0xffff;
+#pragma unroll
+        for (int k = 0; k < REG_EXT / 2; k++)             // pop the front offset
+            pl.O[k] = (pl.O[k] >> 16) | (k + 1 < REG_EXT / 2 ? pl.O[k + 1] << 16 : 0u);
+        Cur q = cmk(pl.exts.d + off, pl.exts.e);
+        Ext x = ext_parse(q);
+        if (fmt == 0) {
+            ext_fp0(b, x, 0);
+        } else {
+            if (fmt == 2) fmt2_bucket(x);
+            ext_fp1(b, x, 0);
+        }
+    }
+    b.putc(fmt == 0 ? ')' : ']');
+}
+
 struct Sh { Cur version, cipher, extensions; };
 DEV Sh tls_sh_parse(Cur &rec) {                         // parse_tls_server_hello tls.h:2097
     Sh s; cset_null(s.version); cset_null(s.cipher); cset_null(s.extensions);
@@ -975,37 +1112,33 @@ DEV bool ssh_kex_fp(E *b, Cur payload) {                // ssh_kex_init::fingerp
 // ---------------------------------------------------------------------------
 // HTTP (http.h, http.cc) -- header-name tables in constant memory
 // ---------------------------------------------------------------------------
-struct HdrName { uint8_t len; uint8_t incl_value; uint8_t capture; char s[33]; };
-// http.cc:426-445 (request) and :487-536 (response); capture: 1 host, 2 user-agent
-__constant__ HdrName k_req_names[] = {
-    {6, 1, 0, "accept"}, {15, 1, 0, "accept-encoding"}, {10, 1, 0, "connection"}, {3, 1, 0, "dnt"},
-    {3, 1, 0, "dpr"}, {25, 1, 0, "upgrade-insecure-requests"}, {16, 1, 0, "x-requested-with"},
-    {14, 0, 0, "accept-charset"}, {15, 0, 0, "accept-language"}, {13, 0, 0, "authorization"},
-    {13, 0, 0, "cache-control"}, {4, 0, 1, "host"}, {17, 0, 0, "if-modified-since"}, {10, 0, 0, "keep-alive"},
-    {10, 0, 2, "user-agent"}, {15, 0, 0, "x-flash-version"}, {14, 0, 0, "x-p2p-peerdist"},
-};
-constexpr int N_REQ_NAMES = 17;
-__constant__ HdrName k_resp_names[] = {
-    {32, 1, 0, "access-control-allow-credentials"}, {28, 1, 0, "access-control-allow-headers"},
-    {28, 1, 0, "access-control-allow-methods"}, {29, 1, 0, "access-control-expose-headers"},
-    {13, 1, 0, "cache-control"}, {4, 1, 0, "code"}, {10, 1, 0, "connection"}, {16, 1, 0, "content-language"},
-    {25, 1, 0, "content-transfer-encoding"}, {3, 1, 0, "p3p"}, {6, 1, 0, "pragma"}, {6, 1, 0, "reason"},
-    {6, 1, 0, "server"}, {25, 1, 0, "strict-transport-security"}, {7, 1, 0, "version"},
-    {19, 1, 0, "x-aspnetmvc-version"}, {16, 1, 0, "x-aspnet-version"}, {5, 1, 0, "x-cid"},
-    {12, 1, 0, "x-ms-version"}, {16, 1, 0, "x-xss-protection"},
-    {17, 0, 0, "appex-activity-id"}, {7, 0, 0, "cdnuuid"}, {6, 0, 0, "cf-ray"}, {13, 0, 0, "content-range"},
-    {12, 0, 0, "content-type"}, {4, 0, 0, "date"}, {4, 0, 0, "etag"}, {7, 0, 0, "expires"},
-    {12, 0, 0, "flow_context"}, {5, 0, 0, "ms-cv"}, {8, 0, 0, "msregion"}, {12, 0, 0, "ms-requestid"},
-    {10, 0, 0, "request-id"}, {4, 0, 0, "vary"}, {12, 0, 0, "x-amz-cf-pop"}, {16, 0, 0, "x-amz-request-id"},
-    {24, 0, 0, "x-azure-ref-originshield"}, {7, 0, 0, "x-cache"}, {12, 0, 0, "x-cache-hits"},
-    {5, 0, 0, "x-ccc"}, {14, 0, 0, "x-diagnostic-s"}, {10, 0, 0, "x-feserver"}, {4, 0, 0, "x-hw"},
-    {12, 0, 0, "x-msedge-ref"}, {19, 0, 0, "x-ocsp-responder-id"}, {11, 0, 0, "x-requestid"},
-    {11, 0, 0, "x-served-by"}, {7, 0, 0, "x-timer"}, {15, 0, 0, "x-trace-context"},
-};
-constexpr int N_RESP_NAMES = 49;
+// (len, include_value, capture, name): http.cc:426-445 (request) and
+// :487-536 (response); capture: 1 host, 2 user-agent
+#define MFP_REQ_NAMES(X)                                                                                          \
+    X(6, 1, 0, "accept") X(15, 1, 0, "accept-encoding") X(10, 1, 0, "connection") X(3, 1, 0, "dnt")              \
+    X(3, 1, 0, "dpr") X(25, 1, 0, "upgrade-insecure-requests") X(16, 1, 0, "x-requested-with")                    \
+    X(14, 0, 0, "accept-charset") X(15, 0, 0, "accept-language") X(13, 0, 0, "authorization")                     \
+    X(13, 0, 0, "cache-control") X(4, 0, 1, "host") X(17, 0, 0, "if-modified-since") X(10, 0, 0, "keep-alive")    \
+    X(10, 0, 2, "user-agent") X(15, 0, 0, "x-flash-version") X(14, 0, 0, "x-p2p-peerdist")
+#define MFP_RESP_NAMES(X)                                                                                         \
+    X(32, 1, 0, "access-control-allow-credentials") X(28, 1, 0, "access-control-allow-headers")                   \
+    X(28, 1, 0, "access-control-allow-methods") X(29, 1, 0, "access-control-expose-headers")                      \
+    X(13, 1, 0, "cache-control") X(4, 1, 0, "code") X(10, 1, 0, "connection") X(16, 1, 0, "content-language")     \
+    X(25, 1, 0, "content-transfer-encoding") X(3, 1, 0, "p3p") X(6, 1, 0, "pragma") X(6, 1, 0, "reason")          \
+    X(6, 1, 0, "server") X(25, 1, 0, "strict-transport-security") X(7, 1, 0, "version")                           \
+    X(19, 1, 0, "x-aspnetmvc-version") X(16, 1, 0, "x-aspnet-version") X(5, 1, 0, "x-cid")                        \
+    X(12, 1, 0, "x-ms-version") X(16, 1, 0, "x-xss-protection")                                                   \
+    X(17, 0, 0, "appex-activity-id") X(7, 0, 0, "cdnuuid") X(6, 0, 0, "cf-ray") X(13, 0, 0, "content-range")      \
+    X(12, 0, 0, "content-type") X(4, 0, 0, "date") X(4, 0, 0, "etag") X(7, 0, 0, "expires")                       \
+    X(12, 0, 0, "flow_context") X(5, 0, 0, "ms-cv") X(8, 0, 0, "msregion") X(12, 0, 0, "ms-requestid")            \
+    X(10, 0, 0, "request-id") X(4, 0, 0, "vary") X(12, 0, 0, "x-amz-cf-pop") X(16, 0, 0, "x-amz-request-id")      \
+    X(24, 0, 0, "x-azure-ref-originshield") X(7, 0, 0, "x-cache") X(12, 0, 0, "x-cache-hits")                     \
+    X(5, 0, 0, "x-ccc") X(14, 0, 0, "x-diagnostic-s") X(10, 0, 0, "x-feserver") X(4, 0, 0, "x-hw")                \
+    X(12, 0, 0, "x-msedge-ref") X(19, 0, 0, "x-ocsp-responder-id") X(11, 0, 0, "x-requestid")                     \
+    X(11, 0, 0, "x-served-by") X(7, 0, 0, "x-timer") X(15, 0, 0, "x-trace-context")
 
-// the same tables as lowercase names packed into four little-endian words
-// (zero past the name), for word-at-a-time lookups in the wave walker
+// the names as lowercase text packed into four little-endian words (zero
+// past the name) for word-at-a-time comparison
 struct HdrKey { uint64_t w[4]; uint32_t len, info; };   // info: incl_value | capture << 8
 constexpr uint64_t pack_name(const char *s, int len, int k) {
     uint64_t w = 0;
@@ -1015,36 +1148,43 @@ constexpr uint64_t pack_name(const char *s, int len, int k) {
 }
 #define MFP_HK(len, incl, cap, str) \
     HdrKey{{pack_name(str, len, 0), pack_name(str, len, 1), pack_name(str, len, 2), pack_name(str, len, 3)}, \
-           len, (incl) | ((cap) << 8)}
-__constant__ HdrKey k_req_keys[] = {
-    MFP_HK(6, 1, 0, "accept"), MFP_HK(15, 1, 0, "accept-encoding"), MFP_HK(10, 1, 0, "connection"),
-    MFP_HK(3, 1, 0, "dnt"), MFP_HK(3, 1, 0, "dpr"), MFP_HK(25, 1, 0, "upgrade-insecure-requests"),
-    MFP_HK(16, 1, 0, "x-requested-with"), MFP_HK(14, 0, 0, "accept-charset"), MFP_HK(15, 0, 0, "accept-language"),
-    MFP_HK(13, 0, 0, "authorization"), MFP_HK(13, 0, 0, "cache-control"), MFP_HK(4, 0, 1, "host"),
-    MFP_HK(17, 0, 0, "if-modified-since"), MFP_HK(10, 0, 0, "keep-alive"), MFP_HK(10, 0, 2, "user-agent"),
-    MFP_HK(15, 0, 0, "x-flash-version"), MFP_HK(14, 0, 0, "x-p2p-peerdist"),
-};
-__constant__ HdrKey k_resp_keys[] = {
-    MFP_HK(32, 1, 0, "access-control-allow-credentials"), MFP_HK(28, 1, 0, "access-control-allow-headers"),
-    MFP_HK(28, 1, 0, "access-control-allow-methods"), MFP_HK(29, 1, 0, "access-control-expose-headers"),
-    MFP_HK(13, 1, 0, "cache-control"), MFP_HK(4, 1, 0, "code"), MFP_HK(10, 1, 0, "connection"),
-    MFP_HK(16, 1, 0, "content-language"), MFP_HK(25, 1, 0, "content-transfer-encoding"), MFP_HK(3, 1, 0, "p3p"),
-    MFP_HK(6, 1, 0, "pragma"), MFP_HK(6, 1, 0, "reason"), MFP_HK(6, 1, 0, "server"),
-    MFP_HK(25, 1, 0, "strict-transport-security"), MFP_HK(7, 1, 0, "version"),
-    MFP_HK(19, 1, 0, "x-aspnetmvc-version"), MFP_HK(16, 1, 0, "x-aspnet-version"), MFP_HK(5, 1, 0, "x-cid"),
-    MFP_HK(12, 1, 0, "x-ms-version"), MFP_HK(16, 1, 0, "x-xss-protection"),
-    MFP_HK(17, 0, 0, "appex-activity-id"), MFP_HK(7, 0, 0, "cdnuuid"), MFP_HK(6, 0, 0, "cf-ray"),
-    MFP_HK(13, 0, 0, "content-range"), MFP_HK(12, 0, 0, "content-type"), MFP_HK(4, 0, 0, "date"),
-    MFP_HK(4, 0, 0, "etag"), MFP_HK(7, 0, 0, "expires"), MFP_HK(12, 0, 0, "flow_context"), MFP_HK(5, 0, 0, "ms-cv"),
-    MFP_HK(8, 0, 0, "msregion"), MFP_HK(12, 0, 0, "ms-requestid"), MFP_HK(10, 0, 0, "request-id"),
-    MFP_HK(4, 0, 0, "vary"), MFP_HK(12, 0, 0, "x-amz-cf-pop"), MFP_HK(16, 0, 0, "x-amz-request-id"),
-    MFP_HK(24, 0, 0, "x-azure-ref-originshield"), MFP_HK(7, 0, 0, "x-cache"), MFP_HK(12, 0, 0, "x-cache-hits"),
-    MFP_HK(5, 0, 0, "x-ccc"), MFP_HK(14, 0, 0, "x-diagnostic-s"), MFP_HK(10, 0, 0, "x-feserver"),
-    MFP_HK(4, 0, 0, "x-hw"), MFP_HK(12, 0, 0, "x-msedge-ref"), MFP_HK(19, 0, 0, "x-ocsp-responder-id"),
-    MFP_HK(11, 0, 0, "x-requestid"), MFP_HK(11, 0, 0, "x-served-by"), MFP_HK(7, 0, 0, "x-timer"),
-    MFP_HK(15, 0, 0, "x-trace-context"),
-};
+           len, (incl) | ((cap) << 8)},
+__constant__ HdrKey k_req_keys[] = {MFP_REQ_NAMES(MFP_HK)};
+__constant__ HdrKey k_resp_keys[] = {MFP_RESP_NAMES(MFP_HK)};
+constexpr HdrKey kReqKeys[] = {MFP_REQ_NAMES(MFP_HK)};
+constexpr HdrKey kRespKeys[] = {MFP_RESP_NAMES(MFP_HK)};
 #undef MFP_HK
+constexpr int N_REQ_NAMES = sizeof(kReqKeys) / sizeof(kReqKeys[0]);
+constexpr int N_RESP_NAMES = sizeof(kRespKeys) / sizeof(kRespKeys[0]);
+static_assert(N_REQ_NAMES == 17 && N_RESP_NAMES == 49, "http.cc header lists");
+
+// perfect_hash::lookup (perfect_hash.h:256) as a collision-free
+// multiplicative hash of the packed lowercase name: slot -> table index + 1;
+// the candidate is then compared word for word (exact, any input)
+DEV_HD_CONSTEXPR uint64_t name_key(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint64_t len) {
+    return w0 + 3 * w1 + 5 * w2 + 7 * w3 + len;
+}
+constexpr uint64_t REQ_MUL = 0x9531985d5d9dc9f9ull, RESP_MUL = 0xad514947c1ae3f7bull;
+constexpr int REQ_BITS = 6, RESP_BITS = 7;
+template <int BITS>
+struct HdrSlots { uint8_t s[1 << BITS]; bool perfect; };
+template <int BITS, int N>
+constexpr HdrSlots<BITS> make_slots(const HdrKey (&t)[N], uint64_t mul) {
+    HdrSlots<BITS> r{};
+    r.perfect = true;
+    for (int i = 0; i < N; i++) {
+        const uint32_t h = (uint32_t)((name_key(t[i].w[0], t[i].w[1], t[i].w[2], t[i].w[3], t[i].len) * mul) >> (64 - BITS));
+        if (r.s[h]) r.perfect = false;
+        r.s[h] = (uint8_t)(i + 1);
+    }
+    return r;
+}
+constexpr HdrSlots<REQ_BITS> kReqSlots = make_slots<REQ_BITS>(kReqKeys, REQ_MUL);
+constexpr HdrSlots<RESP_BITS> kRespSlots = make_slots<RESP_BITS>(kRespKeys, RESP_MUL);
+static_assert(kReqSlots.perfect && kRespSlots.perfect, "header name hash must be collision-free");
+__constant__ HdrSlots<REQ_BITS> k_req_slots = kReqSlots;
+__constant__ HdrSlots<RESP_BITS> k_resp_slots = kRespSlots;
+
 // ASCII A-Z -> a-z in each byte of w (bytes >= 0x80 unchanged)
 DEV uint64_t swar_tolower(uint64_t w) {
     const uint64_t x = w & 0x7f7f7f7f7f7f7f7full;
@@ -1055,9 +1195,9 @@ DEV uint64_t swar_tolower(uint64_t w) {
 
 // perfect_hash::lookup perfect_hash.h:256: exact ASCII-case-insensitive
 // match -- the lowercased name as four packed words (aligned 8-byte loads of
-// the name's bytes) against the packed tables; returns the table index and
-// the entry's incl_value | capture << 8
-DEV int name_lookup(const HdrKey *tab, int ntab, Cur n, uint32_t &info) {
+// the name's bytes), one hashed slot, one word-wise comparison; returns the
+// table index and the entry's incl_value | capture << 8
+DEV int name_lookup(bool req, Cur n, uint32_t &info) {
     const long l = clen(n);
     if (l <= 0 || l > 32) return -1;
     const uintptr_t a = (uintptr_t)n.d & ~(uintptr_t)7;
@@ -1075,12 +1215,14 @@ DEV int name_lookup(const HdrKey *tab, int ntab, Cur n, uint32_t &info) {
         else if (rem < 8) w &= (1ull << (8 * rem)) - 1;
         nw[k] = swar_tolower(w);
     }
-    for (int i = 0; i < ntab; i++) {
-        const HdrKey &k = tab[i];
-        if (k.len == (uint32_t)l && k.w[0] == nw[0] && k.w[1] == nw[1] && k.w[2] == nw[2] && k.w[3] == nw[3]) {
-            info = k.info;
-            return i;
-        }
+    const uint64_t key = name_key(nw[0], nw[1], nw[2], nw[3], (uint64_t)l);
+    const int c = req ? (int)k_req_slots.s[(key * REQ_MUL) >> (64 - REQ_BITS)] - 1
+                      : (int)k_resp_slots.s[(key * RESP_MUL) >> (64 - RESP_BITS)] - 1;
+    if (c < 0) return -1;
+    const HdrKey &k = req ? k_req_keys[c] : k_resp_keys[c];
+    if (k.len == (uint32_t)l && k.w[0] == nw[0] && k.w[1] == nw[1] && k.w[2] == nw[2] && k.w[3] == nw[3]) {
+        info = k.info;
+        return c;
     }
     return -1;
 }
@@ -1097,8 +1239,6 @@ DEV bool http_delim(Cur &p, Cur del) {                  // delimiter(datum&, con
 template <class E>
 DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {
     Cur tmp = body;
-    const HdrKey *tab = req ? k_req_keys : k_resp_keys;
-    int ntab = req ? N_REQ_NAMES : N_RESP_NAMES;
     while (true) {
         if (http_delim(tmp, delim)) break;
         Cur hdr_body = tmp, name; cset_null(name);
@@ -1116,7 +1256,7 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         hdr_body.e = value.e;
         if (cnull(tmp)) break;
         uint32_t info = 0;
-        const int idx = name_lookup(tab, ntab, name, info);
+        const int idx = name_lookup(req, name, info);
         if (idx >= 0) {
 #ifndef MFP_PROBE_LNOEMIT
             b.putc('(');
@@ -1148,6 +1288,15 @@ DEV void cert_record(Out &o, Cur l, const uint8_t *base) {
 struct Cfg {
     uint32_t select, tls_format, mode;
     uint32_t classify;   // stop after protocol identification (o.msg), emit nothing
+};
+// parser families compiled into a walker instance (template argument FAM):
+// a bin kernel carries only its protocol's parser, so its code and register
+// footprint are the parser's, not the union of all of them; a packet whose
+// message needs a family that is compiled out is punted (Em::punt /
+// SegEm::ovf) to the fallback lane, which carries every family
+enum : uint32_t {
+    FAM_TLS = 1, FAM_SSH = 2, FAM_HTTP = 4, FAM_TCP = 8, FAM_DTLS = 16,
+    FAM_ALL = 31,
 };
 enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
@@ -1242,9 +1391,8 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
 }
 
 // set_tcp_protocol pkt_proc.cc:488 (selection subset)
-template <class E>
-DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, const uint8_t *base,
-                  uint32_t *lk, uint16_t *lo, int stride) {
+template <uint32_t FAM, class E>
+DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, const uint8_t *base) {
     uint32_t sel = cfg.select;
     uint32_t sport = (ld(tcph) << 8) | ld(tcph + 1), dport = (ld(tcph + 2) << 8) | ld(tcph + 3);
     uint32_t msg = 0;
@@ -1269,26 +1417,36 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
             if (hit) {
                 o.msg = MFP_MSG_HTTP_REQ;
                 if (cfg.classify) return;
-                if (http_msg(b, pkt, true, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 3; }
-                else o.msg = 0;
+                if constexpr (!(FAM & FAM_HTTP)) { b.punt_pkt(); return; }
+                else {
+                    if (http_msg(b, pkt, true, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 3; }
+                    else o.msg = 0;
+                }
                 return;
             }
         }
         if ((sel & SEL_HTTP_RESP) && kw == 0x48545450u) {
             o.msg = MFP_MSG_HTTP_RESP;
             if (cfg.classify) return;
-            if (http_msg(b, pkt, false, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 4; }
-            else o.msg = 0;
+            if constexpr (!(FAM & FAM_HTTP)) { b.punt_pkt(); return; }
+            else {
+                if (http_msg(b, pkt, false, o, base)) { o.flags |= MFP_FLAG_EMIT; o.fp_type = 4; }
+                else o.msg = 0;
+            }
         }
         return;
     }
     o.msg = msg;
     if (cfg.classify) return;
-    if constexpr (E::SEG) {
-        b.ovf = true;          // not an HTTP message: the fallback lane fingerprints it
-    } else {
+    const bool tls_msg = msg == MFP_MSG_TLS_CH || msg == MFP_MSG_TLS_SH || msg == MFP_MSG_TLS_CERT;
+    if (E::SEG || (tls_msg && !(FAM & FAM_TLS)) || (!tls_msg && !(FAM & FAM_SSH))) {
+        b.punt_pkt();          // a parser this walker lacks: the fallback lane fingerprints it
+        return;
+    }
+    if constexpr (!E::SEG) {
     switch (msg) {
     case MFP_MSG_TLS_CH: {
+        if constexpr (!(FAM & FAM_TLS)) return; else {
         Cur p = pkt;
         Cur frag = tls_record_fragment(p);
         Hs hs = tls_hs_parse(frag);
@@ -1296,12 +1454,18 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         Ch ch = tls_ch_parse(hs.body);
         if (!cnotempty(ch.compression)) return;
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 1;
-        fp_type_prefix(b, 1);
-        tls_ch_fp(b, ch, (int)cfg.tls_format, lk, lo, stride);
-        tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+        if constexpr (E::PLAN) {
+            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len);
+        } else {
+            fp_type_prefix(b, 1);
+            tls_ch_fp(b, ch, (int)cfg.tls_format);
+            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+        }
         return;
+        }
     }
     case MFP_MSG_TLS_SH: {                              // tls.h:573
+        if constexpr (!(FAM & FAM_TLS)) return; else {
         Cur p = pkt;
         Sh sh; cset_null(sh.version); cset_null(sh.cipher); cset_null(sh.extensions);
         Cert cert; cset_null(cert.list); cert.more = 0;
@@ -1322,8 +1486,10 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         if (hello || cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
         if (hello) { o.fp_type = 2; fp_type_prefix(b, 2); tls_sh_fp(b, sh); }
         return;
+        }
     }
     case MFP_MSG_TLS_CERT: {                            // tls.h:720
+        if constexpr (!(FAM & FAM_TLS)) return; else {
         Cur p = pkt;
         Cert cert; cset_null(cert.list); cert.more = 0;
         Cur frag = tls_record_fragment(p);
@@ -1339,8 +1505,10 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
         if (cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
         return;
+        }
     }
     case MFP_MSG_SSH_INIT: {                            // ssh.h:342-430
+        if constexpr (!(FAM & FAM_SSH)) return; else {
         bool server = !(dport <= sport);
         if (!(sel & (server ? SEL_SSH_SERVER : SEL_SSH_CLIENT))) { o.msg = 0; return; }
         Cur p = pkt, proto, comment; cset_null(comment);
@@ -1379,8 +1547,10 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         // analysis: user agent = protocol + comment strings (ssh.h:480)
         o.ua_off = (uint32_t)(proto.d - base); o.ua_len = (uint32_t)clen(proto);
         return;
+        }
     }
     case MFP_MSG_SSH_KEX: {                             // pkt_proc.cc:586-601
+        if constexpr (!(FAM & FAM_SSH)) return; else {
         bool server = !(dport <= sport);
         if (!(sel & (server ? SEL_SSH_SERVER : SEL_SSH_CLIENT))) { o.msg = 0; return; }
         Cur p = pkt;
@@ -1392,15 +1562,15 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         fp_type_prefix(b, o.fp_type);
         ssh_kex_fp(&b, bin.payload);
         return;
+        }
     }
     }
     }
 }
 
 // set_udp_protocol pkt_proc.cc:677 (selection subset: DTLS, dtls.h)
-template <class E>
-DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uint32_t *lk, uint16_t *lo,
-                  int stride) {
+template <uint32_t FAM, class E>
+DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
     if (!(cfg.select & SEL_DTLS) || clen(pkt) < 16) return;
     uint64_t w0 = 0, w1 = 0;
     for (int i = 0; i < 8; i++) { w0 |= (uint64_t)ld(pkt.d + i) << (8 * i); w1 |= (uint64_t)ld(pkt.d + 8 + i) << (8 * i); }
@@ -1412,10 +1582,10 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, ui
     if (!msg) return;
     o.msg = msg;
     if (cfg.classify) return;
-    if constexpr (E::SEG) {
-        b.ovf = true;
+    if constexpr (E::SEG || !(FAM & FAM_DTLS)) {
+        b.punt_pkt();
         return;
-    }
+    } else {
     Cur d = pkt, frag, body; cset_null(frag); cset_null(body);
     uint64_t t, len = 0, foff = 0, flen = 0, more = 0;
     if (clen(d) < 13) cset_null(d);
@@ -1438,9 +1608,13 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, ui
         Ch ch = tls_ch_parse(body);
         if (!cnotempty(ch.compression)) return;
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 10;
-        fp_type_prefix(b, 10);
-        tls_ch_fp(b, ch, (int)cfg.tls_format, lk, lo, stride);
-        tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+        if constexpr (E::PLAN) {
+            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len);
+        } else {
+            fp_type_prefix(b, 10);
+            tls_ch_fp(b, ch, (int)cfg.tls_format);
+            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+        }
     } else if (msg == MFP_MSG_DTLS_SH) {
         Cur b2 = body;
         Sh sh = tls_sh_parse(b2);
@@ -1453,6 +1627,7 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, ui
         rd_uint(b2, 2, t); rd_uint(b2, 1, cl);
         cparse(ck, b2, (long)cl);
         if (!cnull(b2)) o.flags |= MFP_FLAG_EMIT;
+    }
     }
 }
 
@@ -1525,9 +1700,8 @@ DEV void tcp_syn_fp(E &b, int ipv, const uint8_t *iph, const uint8_t *tcph, Cur 
 }
 
 // IP layer: ip_write_json pkt_proc.cc:1063 / analyze_ip_packet pkt_proc.cc:1597
-template <class E>
-DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uint32_t *lk, uint16_t *lo,
-                 int stride) {
+template <uint32_t FAM, class E>
+DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
     const uint8_t *iph; int ipv;
     uint32_t proto = ip_parse(pkt, iph, ipv);
     uint32_t enc = 0;            // net bits 20-27: levels, v6 mask, irregular (include/mfp.h)
@@ -1555,9 +1729,11 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
                     o.msg = MFP_MSG_TCP_SYN;
                     if (cfg.classify) return;
                     o.flags |= MFP_FLAG_EMIT; o.fp_type = 7;
-                    if constexpr (E::SEG) { b.ovf = true; return; }
-                    fp_type_prefix(b, 7);
-                    tcp_syn_fp(b, ipv, iph, tcph, opts);
+                    if constexpr (E::SEG || !(FAM & FAM_TCP)) { b.punt_pkt(); return; }
+                    else {
+                        fp_type_prefix(b, 7);
+                        tcp_syn_fp(b, ipv, iph, tcph, opts);
+                    }
                 }
                 return;
             }
@@ -1566,22 +1742,24 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base, uin
                     o.msg = MFP_MSG_TCP_SYNACK;
                     if (cfg.classify) return;
                     o.flags |= MFP_FLAG_EMIT; o.fp_type = 13;
-                    if constexpr (E::SEG) { b.ovf = true; return; }
-                    fp_type_prefix(b, 13);
-                    tcp_syn_fp(b, ipv, iph, tcph, opts);
+                    if constexpr (E::SEG || !(FAM & FAM_TCP)) { b.punt_pkt(); return; }
+                    else {
+                        fp_type_prefix(b, 13);
+                        tcp_syn_fp(b, ipv, iph, tcph, opts);
+                    }
                 }
                 return;
             }
             if (clen(pkt) == 0) return;
         }
-        tcp_data(b, cfg, o, pkt, tcph, base, lk, lo, stride);
+        tcp_data<FAM>(b, cfg, o, pkt, tcph, base);
     } else if (proto == 17) {
         const uint8_t *udph = cget_ptr(pkt, 8);
         if (udph) {
             o.src_port = (ld(udph) << 8) | ld(udph + 1);
             o.dst_port = (ld(udph + 2) << 8) | ld(udph + 3);
         }
-        udp_data(b, cfg, o, pkt, base, lk, lo, stride);
+        udp_data<FAM>(b, cfg, o, pkt, base);
     }
 }
 
@@ -1603,9 +1781,8 @@ DEV bool ppp_is_ip(Cur &p) {                            // ppp::is_ip ppp.h:76
 
 // link layer: stateful_pkt_proc::write_json(..., linktype) pkt_proc.cc:1328
 // and analyze_packet pkt_proc.cc:1814
-template <class E>
-DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t len, uint32_t linktype,
-                     uint32_t *lk, uint16_t *lo, int stride) {
+template <uint32_t FAM = FAM_ALL, class E>
+DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t len, uint32_t linktype) {
     o.fp_type = 0; o.msg = 0; o.flags = 0;
     o.sni_off = o.ua_off = 0; o.sni_len = o.ua_len = 0xffff;
     o.src_port = o.dst_port = 0;
@@ -1664,7 +1841,7 @@ DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t
         return;
     }
     if (cnull(p)) return;
-    ip_path(b, cfg, o, p, data, lk, lo, stride);
+    ip_path<FAM>(b, cfg, o, p, data);
 }
 
 }  // namespace mfp

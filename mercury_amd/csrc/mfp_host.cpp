@@ -28,15 +28,12 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *a
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
-                                      unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
-                                      uint32_t bin_seg_mask, hipStream_t stream, mfp_prof *prof);
+                                      unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
+                                      uint32_t bin_lds_mask, hipStream_t stream, mfp_prof *prof);
 
 extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
                                   unsigned long long *block_sum, hipStream_t stream, mfp_prof *prof);
 
-// fp-arena reservation granule of the wave kernel and its grid (mfp_kernels.hip)
-static const uint64_t kWaveChunk = 32 * 1024;
-static const uint64_t kWaveGridWaves = 2048 * 4;
 
 static thread_local std::string g_err;
 
@@ -255,12 +252,12 @@ struct Slot {
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
-    int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|wave|lane (A/B, debugging)
-    // bin b -> kernel: k_fp_seg if bit b of bin_seg_mask (MFP_BIN_SEG_MASK; default the
-    // two HTTP bins), else k_wave_fp if bit b of bin_wave_mask (MFP_BIN_WAVE_MASK), else
-    // the lane kernel (A/B per bin: tools/gpu_masks.sh)
-    uint32_t bin_wave_mask = 0x0;
+    int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|lane (A/B, debugging)
+    // bin b -> kernel: k_fp_lds (LDS-staged walk) if bit b of bin_lds_mask
+    // (MFP_BIN_LDS_MASK), else the HBM lane walker; the bins of bin_seg_mask
+    // (MFP_BIN_SEG_MASK; default the two HTTP bins) use segment expansion
     uint32_t bin_seg_mask = 0xa;
+    uint32_t bin_lds_mask = 0xe0;        // TLS server, SSH, DTLS: measured faster from LDS (r02c/d)
     uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
     Slot slot[3];
@@ -293,12 +290,11 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     auto *c = new mfp_context_s;
     c->device = device; c->select = sel; c->tls_format = fmt; c->mode = mode;
     const char *st = getenv("MFP_STRATEGY");
-    if (st && !strcmp(st, "wave")) c->strategy = MFP_STRATEGY_WAVE;
-    else if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
-    const char *bm = getenv("MFP_BIN_WAVE_MASK");
-    if (bm) c->bin_wave_mask = (uint32_t)strtoul(bm, nullptr, 0);
+    if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
     const char *sm = getenv("MFP_BIN_SEG_MASK");
     if (sm) c->bin_seg_mask = (uint32_t)strtoul(sm, nullptr, 0);
+    const char *dm = getenv("MFP_BIN_LDS_MASK");
+    if (dm) c->bin_lds_mask = (uint32_t)strtoul(dm, nullptr, 0);
     const char *lm = getenv("MFP_AN_LANE_MAX_P");
     if (lm) c->an_lane_max_p = (uint32_t)strtoul(lm, nullptr, 0);
     bool ok = hipSetDevice(device) == hipSuccess &&
@@ -342,12 +338,9 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
 
 extern "C" MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen) {
     // every byte of a captured frame yields at most 4 fingerprint characters
-    // (TCP NOP option "(01)"), plus the type prefix; 16-byte alignment of each
-    // string; plus one partly used reservation chunk per wave of the grid
-    // for each of the (up to 6) wave-kernel launches of a batch
-    uint64_t waves = (n + 63) / 64;
-    if (waves > kWaveGridWaves) waves = kWaveGridWaves;
-    return 4 * total_caplen + 88 * n + 6 * (waves + 1) * kWaveChunk;
+    // (TCP NOP option "(01)"), plus the type prefix; each string owns a
+    // 64-byte aligned slot that also holds its 8-byte hash
+    return 4 * total_caplen + 176 * n + 4096;
 }
 
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode) {
@@ -383,7 +376,7 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
     HIPCHK(hipMemsetAsync(S.d_bins, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
                                fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
-                               c->bin_wave_mask, c->bin_seg_mask, s, c->prof) != 0) {
+                               c->bin_seg_mask, c->bin_lds_mask, s, c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

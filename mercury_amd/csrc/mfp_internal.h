@@ -14,7 +14,7 @@ bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std:
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode);
 
 // kernel strategies of the fingerprint pass (mfp_kernels.hip)
-enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_WAVE = 1, MFP_STRATEGY_LANE = 2 };
+enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_LANE = 2 };
 
 // per-kernel HIP-event timing (mfp_profile_enable): the launchers bracket
 // every launch with begin/end when `p` is non-null

@@ -13,7 +13,6 @@
 #include <hip/hip_runtime.h>
 
 #include "mfp_device.hpp"
-#include "mfp_wave.hpp"
 
 namespace mfp {
 
@@ -32,19 +31,19 @@ struct KParams {
     const unsigned long long *count;
 };
 
-// k_fingerprint -- lane-per-packet walker, grid-stride over tiles of TILE
-// packets.  Used as the fallback lane of k_wave_fp (packets larger than the
-// wave kernel's LDS staging buffer, or whose fingerprint overflows its segment
-// table); with idx == nullptr it processes the whole batch.
+// k_fingerprint -- lane-per-packet walker straight from HBM, grid-stride
+// over tiles of TILE packets.  The fallback lane of the other bin kernels
+// (packets larger than k_fp_lds's stage, segment lists that overflow); with
+// idx == nullptr it processes the whole batch (MFP_STRATEGY=lane).
 #ifndef MFP_LANE_MINW
 #define MFP_LANE_MINW 4      // 4 waves per SIMD: measured best for the TLS CH and mixed bins
 #endif
-__global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) {
-    // per-lane extension scratch for TLS formats 1/2 (dynamic: 0 bytes for
-    // format 0, so the default path keeps full occupancy)
-    extern __shared__ uint32_t dyn_lds[];
-    uint32_t *lds_key = dyn_lds;
-    uint16_t *lds_off = (uint16_t *)(dyn_lds + MAX_LDS_EXT * TILE);
+#ifndef MFP_TLS_MINW
+#define MFP_TLS_MINW 3       // the TLS parser wants ~200 VGPRs: 3 waves/SIMD measured best (4: spills, 2: latency)
+#endif
+template <uint32_t FAM>
+__global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW) void k_fingerprint(KParams P,
+                                                                                                     uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
     __shared__ uint64_t out_line[TILE][8];   // pass-2 output staging, one 64-byte line per lane
     __shared__ unsigned long long tile_base;
@@ -62,21 +61,36 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
     else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
     const uint8_t *data = P.arena + dsc.offset;
 
-    // pass 1: walk + length
+    // pass 1: walk + length (+ the ClientHello plan pass 2 emits from)
     Out o;
     uint32_t len = 0;
+    bool punt = false;
+    TlsPlan plan;
+    plan.ok = false;
     {
         Em<false> e;
-        packet_walk(e, P.cfg, o, data, dsc.caplen, dsc.linktype, lds_key + tid, lds_off + tid, TILE);
-        if (o.fp_type) {
+        e.plan = &plan;
+        packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+        punt = live && e.punt;
+        if (o.fp_type && !punt) {
             if (e.valid()) len = e.n;
             else o.fp_type = 0;       // fingerprint::final drops truncated fingerprints
         }
     }
+    if (FAM != FAM_ALL) {             // a parser this instance lacks: the fallback lane
+        const uint64_t pm = __ballot(punt);
+        if (pm) {
+            uint32_t b = 0;
+            if ((tid & 63) == 0) b = (uint32_t)atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(pm));
+            b = (uint32_t)__shfl((int)b, 0, 64);
+            if (punt) fallback[b + __builtin_popcountll(pm & ((1ull << (tid & 63)) - 1))] = (uint32_t)i;
+        }
+    }
 
-    // workgroup exclusive scan of the 64-byte slots (strings start 64-byte aligned)
+    // workgroup exclusive scan of the 64-byte slots (strings start 64-byte
+    // aligned; each is followed by its 8-byte hash at round_up(len, 8))
     const int lane = tid & 63, wid = tid >> 6;
-    const uint32_t slot = (len + 63) & ~63u;
+    const uint32_t slot = len ? (((len + 7) & ~7u) + 8 + 63) & ~63u : 0u;
     uint32_t incl = slot;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -117,18 +131,23 @@ __global__ __launch_bounds__(TILE, MFP_LANE_MINW) void k_fingerprint(KParams P) 
     if (len && fits) {
         Em<true> e;
         e.begin(P.fp_arena + base + excl, out_line[tid]);
-        Out o2;
-        packet_walk(e, P.cfg, o2, data, dsc.caplen, dsc.linktype, lds_key + tid, lds_off + tid, TILE);
+        if (plan.ok) {
+            tls_ch_emit(e, plan);
+        } else {
+            Out o2;
+            packet_walk<FAM>(e, P.cfg, o2, data, dsc.caplen, dsc.linktype);
+        }
         e.finish();
+        *(uint64_t *)(P.fp_arena + base + excl + ((len + 7) & ~7u)) = e.hash();
     }
 
-    if (live) {
+    if (live && !punt) {
         mfp_record r;
         r.fp_offset = fits ? base + excl : 0;
         r.fp_len = fits ? len : 0;
         r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
         r.msg = (uint8_t)o.msg;
-        r.flags = (uint8_t)o.flags;    // the lane kernel leaves hashing to the classifier
+        r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
         r.status = 0;
         r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
         r.sni_len = (uint16_t)o.sni_len;
@@ -181,7 +200,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 
         Out o;
         SegEm e(data, segs + tid * SEG_STRIDE);
-        packet_walk(e, P.cfg, o, data, dsc.caplen, dsc.linktype, nullptr, nullptr, 0);
+        packet_walk<FAM_HTTP>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
         e.finish();
         const bool fb = live && e.ovf;
         uint32_t len = 0;
@@ -291,6 +310,200 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 }
 
 
+// k_fp_lds -- the lane walker over packets staged in LDS.  One wave per
+// workgroup; a wave takes 64 packets of its bin (one per lane) and copies as
+// many of them as fit its LDS stage with direct-to-LDS 16-byte loads
+// (global_load_lds_dwordx4: every wave-instruction moves 1 KiB of one packet,
+// coalesced), then every lane walks its own packet from LDS.  The walk's
+// dependent byte reads are LDS round trips instead of divergent global loads
+// that touch 64 cache lines per instruction, and each packet leaves HBM once.
+// Packets that do not fit the next sub-round wait for it; a packet larger
+// than the whole stage goes to the fallback lane kernel (global walk).
+//   SEGMODE = false: two walks (length, then emission through 64-byte LDS
+//     lines, k_fingerprint's emitter); the string hash is folded into the
+//     emission and stored behind the string.
+//   SEGMODE = true (HTTP bins): one walk recording a segment list (SegEm),
+//     then the wave expands each string with coalesced stores (seg_expand),
+//     reading the hex sources from the staged packet.
+template <bool SEGMODE, uint32_t STG, uint32_t FAM>
+__global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
+    __shared__ uint4 stage[STG / 16];
+    __shared__ uint64_t out_line[SEGMODE ? 1 : 64][8];
+    __shared__ uint32_t segs[SEGMODE ? 64 * SEG_STRIDE : 1];
+    __shared__ uint8_t pool[32];
+    const uint32_t lane = threadIdx.x;
+    uint8_t *stg = (uint8_t *)&stage[0];
+    if (SEGMODE && lane < 32) {
+        const char *lp = MFP_SEG_POOL;
+        pool[lane] = (uint8_t)(lane < sizeof(MFP_SEG_POOL) ? lp[lane] : 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t g = blockIdx.x; g * 64 < count; g += gridDim.x) {
+        const uint64_t t = g * 64 + lane;
+        const bool live = t < count;
+        const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
+        mfp_pkt_desc dsc;
+        if (live) dsc = P.desc[i];
+        else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
+        const uint32_t a16 = (uint32_t)(dsc.offset & 15);
+        const uint32_t pk_bytes = (a16 + dsc.caplen + 15) & ~15u;      // whole 16-byte blocks
+        const uint32_t need = pk_bytes;
+        const bool big = live && need > STG;
+        {   // too large for any sub-round: the fallback lane walks it from HBM
+            const uint64_t bm = __ballot(big);
+            if (bm) {
+                uint32_t b = 0;
+                if (lane == 0) b = (uint32_t)atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(bm));
+                b = (uint32_t)__shfl((int)b, 0, 64);
+                if (big) fallback[b + __builtin_popcountll(bm & ((1ull << lane) - 1))] = (uint32_t)i;
+            }
+        }
+        bool todo = live && !big;
+        while (__ballot(todo)) {
+            // this sub-round: the waiting lanes, in lane order, while they fit
+            uint32_t x = todo ? need : 0u, incl = x;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= (uint32_t)d) incl += y;
+            }
+            const bool in = todo && incl <= STG;
+            const uint32_t sbase = incl - x;
+            // stage: one packet after the other, 1 KiB per wave-instruction
+            for (uint64_t m = __ballot(in); m; m &= m - 1) {
+                const int j = __builtin_ctzll(m);
+                const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)sbase, j);
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)pk_bytes, j) >> 4;
+                const uint64_t o = dsc.offset & ~(uint64_t)15;
+                const uint64_t oj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o, j) |
+                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(o >> 32), j) << 32);
+                const uint8_t *src = P.arena + oj;
+                for (uint32_t k = 0; k * 64 < nb; k++) {
+                    const uint32_t blk = k * 64 + lane;
+                    if (blk < nb)
+                        __builtin_amdgcn_global_load_lds((const void *)(src + 16 * (uint64_t)blk),
+                                                         (void __attribute__((address_space(3))) *)(stg + bj + 1024 * k),
+                                                         16, 0, 0);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const uint8_t *data = stg + sbase + a16;
+
+            Out o;
+            uint32_t len = 0;
+            bool fb = false;
+            uint32_t nseg = 0;
+            TlsPlan plan;
+            plan.ok = false;
+            if constexpr (SEGMODE) {
+                SegEm e(data, segs + lane * SEG_STRIDE);
+                if (in) {
+                    packet_walk<FAM_HTTP>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+                    e.finish();
+                    fb = e.ovf;
+                    if (!fb && o.fp_type) {
+                        if (e.valid()) len = e.n;
+                        else o.fp_type = 0;
+                    }
+                    nseg = e.nseg;
+                }
+            } else {
+                if (in) {
+                    Em<false> e;
+                    e.plan = &plan;
+                    packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+                    fb = e.punt;
+                    if (o.fp_type && !fb) {
+                        if (e.valid()) len = e.n;
+                        else o.fp_type = 0;    // fingerprint::final drops truncated fingerprints
+                    }
+                }
+            }
+            // arena reservation for the sub-round: one atomic per wave
+            const uint32_t slot = SEGMODE ? (len ? (len + 8 + 15) & ~15u : 0u)
+                                          : (len ? (((len + 7) & ~7u) + 8 + 63) & ~63u : 0u);
+            uint32_t sincl = slot, lsum = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(sincl, d, 64);
+                if (lane >= (uint32_t)d) sincl += y;
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) lsum += __shfl_xor(lsum, d, 64);
+            const uint32_t total = (uint32_t)__shfl((int)sincl, 63, 64);
+            unsigned long long b = 0;
+            if (lane == 0 && total) {
+                b = atomicAdd(&P.fp_used[0], (unsigned long long)total);
+                if (b + total > P.fp_cap) { atomicExch(&P.fp_used[1], 1ull); b = ~0ull; }
+                else atomicAdd(&P.fp_used[2], (unsigned long long)lsum);
+            }
+            const unsigned long long base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)b, 0, 64)) |
+                                            ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(b >> 32), 0, 64) << 32);
+            const bool fits = base != ~0ull;
+            const uint32_t excl = sincl - slot;
+            {
+                const uint64_t fbm = __ballot(fb);
+                if (fbm) {
+                    uint32_t fb0 = 0;
+                    if (lane == 0) fb0 = (uint32_t)atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(fbm));
+                    fb0 = (uint32_t)__shfl((int)fb0, 0, 64);
+                    if (fb) fallback[fb0 + __builtin_popcountll(fbm & ((1ull << lane) - 1))] = (uint32_t)i;
+                }
+            }
+            if (SEGMODE) {
+                // wave-cooperative expansion, one packet at a time, from the stage
+                uint64_t todo2 = fits ? __ballot(len != 0) : 0ull;
+                while (todo2) {
+                    const int j = __builtin_ctzll(todo2);
+                    todo2 &= todo2 - 1;
+                    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+                    const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)excl, j);
+                    const uint32_t ns = (uint32_t)__builtin_amdgcn_readlane((int)nseg, j);
+                    const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)(sbase + a16), j);
+                    uint8_t *out = P.fp_arena + base + ex;
+                    uint64_t h = seg_expand(segs + j * SEG_STRIDE, ns, stg + pj, T, out, pool, lane);
+                    h = wave_xor64(h);
+                    if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
+                }
+            } else {
+                if (len && fits) {
+                    Em<true> e;
+                    e.begin(P.fp_arena + base + excl, out_line[lane]);
+                    if (plan.ok) {
+                        tls_ch_emit(e, plan);
+                    } else {
+                        Out o2;
+                        packet_walk<FAM>(e, P.cfg, o2, data, dsc.caplen, dsc.linktype);
+                    }
+                    e.finish();
+                    *(uint64_t *)(P.fp_arena + base + excl + ((len + 7) & ~7u)) = e.hash();
+                }
+            }
+            if (in && !fb) {
+                mfp_record r;
+                r.fp_offset = fits ? base + excl : 0;
+                r.fp_len = fits ? len : 0;
+                r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
+                r.msg = (uint8_t)o.msg;
+                r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
+                r.status = 0;
+                r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
+                r.sni_len = (uint16_t)o.sni_len;
+                r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);
+                r.ua_len = (uint16_t)o.ua_len;
+                r.src_port = (uint16_t)o.src_port;
+                r.dst_port = (uint16_t)o.dst_port;
+                r.net = o.net;
+                P.rec[i] = r;
+            }
+            todo = todo && !in;
+            __builtin_amdgcn_wave_barrier();   // the stage is rewritten by the next sub-round
+        }
+    }
+}
+
 // protocol bins of the classify pass: each bin is then fingerprinted by its
 // own k_fingerprint launch over a compact index list, so the lanes of a wave
 // walk the same protocol (same parser, similar loop trip counts)
@@ -351,9 +564,11 @@ __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, ui
             for (int k = 0; k <= CLS_WIN / 16; k++) win[tid][k] = v[k];
             Out o;
             Em<false> e;
+            TlsPlan plan;                 // never filled: classification stops before any parser
+            e.plan = &plan;
             Cfg c = P.cfg;
             c.classify = 1;
-            packet_walk(e, c, o, (const uint8_t *)&win[tid][0] + sh, take, dsc.linktype, nullptr, nullptr, 0);
+            packet_walk(e, c, o, (const uint8_t *)&win[tid][0] + sh, take, dsc.linktype);
             bin = msg_bin(o.msg);
             cls[i] = (uint8_t)bin;
         }
@@ -396,146 +611,19 @@ __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, ui
 }  // namespace mfp
 
 #include "mfp_internal.h"
-#define MFP_WAVE_GRID 2048   // 8 workgroups of 4 waves per CU x 256 CUs
-#ifndef MFP_WAVE_MINW
-#define MFP_WAVE_MINW 8      // min waves per SIMD (caps VGPRs at 64; measured best for the HTTP bins)
-#endif
-
-namespace mfpw {
-
-constexpr uint64_t CHUNK = 32 * 1024;    // fp-arena bytes reserved per wave at a time
-
-struct WParams {
-    Cfg cfg;
-    const uint8_t *arena;
-    const mfp_pkt_desc *desc;
-    uint64_t n;
-    mfp_record *rec;
-    uint8_t *fp_arena;
-    uint64_t fp_cap;
-    unsigned long long *fp_used;     // see KParams
-    uint32_t *fallback;              // packet indices for the lane-per-packet kernel
-    const uint32_t *idx;             // packet indices (count = *count); nullptr = all n packets
-    const unsigned long long *count;
-};
-
-WDEV uint64_t rfl64(uint64_t v) {
-    return (uint64_t)rfl((uint32_t)v) | ((uint64_t)rfl((uint32_t)(v >> 32)) << 32);
-}
-WDEV uint32_t rdl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
-
-// k_wave_fp: every wave takes groups of 64 consecutive packets (one
-// descriptor per lane, coalesced) in a grid-stride loop, then handles the
-// group's packets one at a time with the whole wave (mfp_wave.hpp).  Each
-// wave reserves fingerprint-arena space CHUNK bytes at a time (one atomic per
-// CHUNK); every string starts 16-byte aligned.  Records are gathered in the
-// lanes (lane j holds packet j's record) and stored coalesced.
-template <uint32_t SPEC>
-__global__ __launch_bounds__(64 * WAVES, MFP_WAVE_MINW) void k_wave_fp(WParams P) {
-    __shared__ WaveLds lds[WAVES];
-    // wave index made provably uniform: the compiler would otherwise treat the
-    // group loop as divergent and move all the scalar parse state to VGPRs
-    const int wid = (int)rfl(threadIdx.x >> 6);
-    WaveLds &L = lds[wid];
-    const uint32_t lane = lane_id();
-    const uint64_t n_eff = P.idx ? (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P.n;
-    const uint64_t ngroups = (n_eff + 63) / 64;
-    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
-    uint64_t cur = 0, end = 0;
-    bool dead = false;
-    unsigned long long exact = 0;
-
-    for (uint64_t g = (uint64_t)blockIdx.x * WAVES + wid; g < ngroups; g += nw) {
-        const uint64_t t = g * 64 + lane;
-        const bool live = t < n_eff;
-        const uint64_t i = live ? (P.idx ? (uint64_t)P.idx[t] : t) : 0;
-        uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_lt = 0xffff;
-        if (live) {
-            const uint4 dv = *(const uint4 *)(P.desc + i);
-            d_lo = dv.x; d_hi = dv.y; d_len = dv.z; d_lt = dv.w & 0xffff;
-        }
-        const int npk = (int)min((uint64_t)64, n_eff - g * 64);
-        // this lane's record
-        uint64_t r_off = 0;
-        uint32_t r_len = 0, r_w2 = 0, r_sni = 0xffff0000u, r_ua = 0xffff0000u, r_ports = 0, r_net = 0;
-        bool fb = false;
-
-        for (int j = 0; j < npk; j++) {
-            const uint64_t off = (uint64_t)rdl(d_lo, j) | ((uint64_t)rdl(d_hi, j) << 32);
-            const uint32_t caplen = rdl(d_len, j), lt = rdl(d_lt, j);
-            if (caplen > (uint32_t)MAX_PKT) { fb |= (int)lane == j; continue; }
-            const uint32_t a = (uint32_t)(off & 15);
-            const uint32_t nvec = (a + caplen + 15) >> 4;
-            const uint8_t *src = P.arena + (off - a);
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t v = lane; v < nvec; v += 64) *(uint4 *)(L.buf + 16 * v) = *(const uint4 *)(src + 16 * v);
-            __builtin_amdgcn_wave_barrier();
-
-            W<SPEC> w(L, P.cfg);
-            w.packet_walk((int)a, caplen, lt);
-            w.flush();
-            if (w.ovf || w.punt) { fb |= (int)lane == j; continue; }
-            uint32_t type = w.o.fp_type, T = 0;
-            uint64_t fpo = 0;
-            if (type) {
-                if (!w.valid()) {
-                    type = 0;                       // fingerprint::final drops truncated fingerprints
-                } else {
-                    T = w.n;
-                    const uint64_t slot = (T + 8 + 15) & ~15u;     // string + hash
-                    if (!dead && cur + slot > end) {
-                        uint64_t b = 0;
-                        if (lane == 0) b = atomicAdd(&P.fp_used[0], (unsigned long long)CHUNK);
-                        b = rfl64(b);
-                        if (b + CHUNK > P.fp_cap) {
-                            dead = true;
-                            if (lane == 0) atomicExch(&P.fp_used[1], 1ull);
-                        } else {
-                            cur = b; end = b + CHUNK;
-                        }
-                    }
-                    if (dead) {
-                        type = 0; T = 0;
-                    } else {
-                        fpo = cur; cur += slot;
-                        w.expand(P.fp_arena + fpo);
-                        exact += T;
-                    }
-                }
-            }
-            if ((int)lane == j) {
-                r_off = fpo; r_len = T;
-                r_w2 = type | (w.o.msg << 8) | ((w.o.flags | (T ? MFP_FLAG_HASHED : 0u)) << 16);
-                r_sni = (w.o.sni_len == 0xffff ? 0 : (w.o.sni_off & 0xffff)) | (w.o.sni_len << 16);
-                r_ua = (w.o.ua_len == 0xffff ? 0 : (w.o.ua_off & 0xffff)) | (w.o.ua_len << 16);
-                r_ports = (w.o.src_port & 0xffff) | (w.o.dst_port << 16);
-                r_net = w.o.net;
-            }
-        }
-        const uint64_t fbm = ballot(fb);
-        if (fbm) {
-            uint64_t b = 0;
-            if (lane == 0) b = atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(fbm));
-            b = rfl64(b);
-            if (fb) P.fallback[b + __builtin_popcountll(fbm & ((1ull << lane) - 1))] = (uint32_t)i;
-        }
-        if (live && !fb) {
-            uint4 *rp = (uint4 *)(P.rec + i);
-            rp[0] = make_uint4((uint32_t)r_off, (uint32_t)(r_off >> 32), r_len, r_w2);
-            rp[1] = make_uint4(r_sni, r_ua, r_ports, r_net);
-        }
-    }
-    if (lane == 0 && exact) atomicAdd(&P.fp_used[2], exact);
-}
-
-}  // namespace mfpw
 
 // launchers used by the host library (mfp_host.cpp)
+#ifndef MFP_LDS_STAGE
+#define MFP_LDS_STAGE (36 * 1024)   // per-wave stage of k_fp_lds: 40 KiB of LDS per wave, 4 waves per CU
+#endif
+#ifndef MFP_LDS_STAGE_SEG
+#define MFP_LDS_STAGE_SEG (32 * 1024)
+#endif
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
-                                      unsigned long long *bin_count, int strategy, uint32_t bin_wave_mask,
-                                      uint32_t bin_seg_mask, hipStream_t stream, mfp_prof *prof) {
+                                      unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
+                                      uint32_t bin_lds_mask, hipStream_t stream, mfp_prof *prof) {
 #define MFP_LAUNCH(name, ...)                                \
     do {                                                     \
         if (prof) mfp_prof_begin(prof, name, stream);        \
@@ -543,7 +631,6 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
         if (prof) mfp_prof_end(prof, stream);                \
     } while (0)
     if (n == 0) return 0;
-    size_t shmem = tls_format ? (size_t)mfp::MAX_LDS_EXT * mfp::TILE * 6 : 0;
     mfp::KParams P;
     P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
@@ -551,80 +638,67 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     P.idx = nullptr; P.count = nullptr;
     const uint64_t tiles = (n + mfp::TILE - 1) / mfp::TILE;
     if (strategy == MFP_STRATEGY_LANE) {
-        MFP_LAUNCH("k_fingerprint", mfp::k_fingerprint, dim3((uint32_t)tiles), dim3(mfp::TILE), shmem, stream, P);
+        MFP_LAUNCH("k_fingerprint", mfp::k_fingerprint<mfp::FAM_ALL>, dim3((uint32_t)tiles), dim3(mfp::TILE), 0, stream,
+                   P, nullptr);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    mfpw::WParams W;
-    W.cfg.select = select; W.cfg.tls_format = tls_format; W.cfg.mode = mode;
-    W.arena = arena; W.desc = desc; W.n = n; W.rec = rec; W.fp_arena = fp_arena; W.fp_cap = fp_cap;
-    W.fp_used = fp_used; W.fallback = work + (strategy == MFP_STRATEGY_BINNED ? (uint64_t)mfp::NBINS * n : 0);
-    W.idx = nullptr; W.count = nullptr;
-    uint64_t groups = (n + 63) / 64;
-    if (strategy == MFP_STRATEGY_BINNED) {
-        // classify, then one launch per protocol bin: the lane-per-packet
-        // walker or the wave-per-packet walker, whichever is faster for
-        // that protocol (bin_wave_mask bit b = wave kernel for bin b)
-        const uint64_t cblocks = tiles < 2048 ? tiles : 2048;
-        MFP_LAUNCH("k_classify", mfp::k_classify, dim3((uint32_t)cblocks), dim3(mfp::TILE), 0, stream, P, work, n, bin_count,
-                   (uint8_t *)(work + (uint64_t)(mfp::NBINS + 1) * n + 1));
-        if (hipGetLastError() != hipSuccess) return -1;
-        uint64_t fblocks = tiles < 2048 ? tiles : 2048;
-        uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
-        if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
-        bool any_wave = false;
-        for (int b = 0; b < mfp::NBINS; b++) {
-            static const char *const wave_name[mfp::NBINS] = {"k_wave_fp/tls_ch", "k_wave_fp/http_req",
-                "k_wave_fp/tcp_syn", "k_wave_fp/http_resp", "k_wave_fp/other", "k_wave_fp/tls_sh",
-                "k_wave_fp/ssh", "k_wave_fp/dtls"};
-            static const char *const lane_name[mfp::NBINS] = {"k_fingerprint/tls_ch", "k_fingerprint/http_req",
-                "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other", "k_fingerprint/tls_sh",
-                "k_fingerprint/ssh", "k_fingerprint/dtls"};
-            static const char *const seg_name[mfp::NBINS] = {"k_fp_seg/tls_ch", "k_fp_seg/http_req",
-                "k_fp_seg/tcp_syn", "k_fp_seg/http_resp", "k_fp_seg/other", "k_fp_seg/tls_sh",
-                "k_fp_seg/ssh", "k_fp_seg/dtls"};
-            if (bin_seg_mask & (1u << b)) {
-                // lane walk + wave expansion (HTTP; anything else -> fallback lane)
-                P.idx = work + (uint64_t)b * n;
-                P.count = bin_count + b;
-                MFP_LAUNCH(seg_name[b], mfp::k_fp_seg, dim3((uint32_t)fblocks), dim3(mfp::TILE), 0, stream, P,
-                           W.fallback);
-                any_wave = true;
-            } else if (bin_wave_mask & (1u << b)) {
-                W.idx = work + (uint64_t)b * n;
-                W.count = bin_count + b;
-                // the bin's protocol families only (others -> fallback lane)
-                auto kw = (b == 0 || b == 5) ? mfpw::k_wave_fp<mfpw::SPEC_TLS>
-                        : (b == 1 || b == 3) ? mfpw::k_wave_fp<mfpw::SPEC_HTTP>
-                        : b == 6 ? mfpw::k_wave_fp<mfpw::SPEC_SSH>
-                        : b == 7 ? mfpw::k_wave_fp<mfpw::SPEC_DTLS>
-                        : b == 2 ? mfpw::k_wave_fp<0u> : mfpw::k_wave_fp<mfpw::SPEC_ALL>;
-                MFP_LAUNCH(wave_name[b], kw, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
-                any_wave = true;
-            } else {
-                P.idx = work + (uint64_t)b * n;
-                P.count = bin_count + b;
-                MFP_LAUNCH(lane_name[b], mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
-            }
-            if (hipGetLastError() != hipSuccess) return -1;
-        }
-        if (any_wave) {
-            // fallback lane for packets the wave kernel handed back
-            P.idx = W.fallback;
-            P.count = fp_used + 3;
-            uint64_t fb = tiles < 1024 ? tiles : 1024;
-            MFP_LAUNCH("k_fingerprint/fallback", mfp::k_fingerprint, dim3((uint32_t)fb), dim3(mfp::TILE), shmem, stream, P);
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    uint64_t wblocks = (groups + mfpw::WAVES - 1) / mfpw::WAVES;
-    if (wblocks > (uint64_t)MFP_WAVE_GRID) wblocks = MFP_WAVE_GRID;
-    MFP_LAUNCH("k_wave_fp", mfpw::k_wave_fp<mfpw::SPEC_ALL>, dim3((uint32_t)wblocks), dim3(64 * mfpw::WAVES), 0, stream, W);
+    // classify, then one launch per protocol bin over its index list: the
+    // LDS-staged walker (bin_lds_mask), the HBM lane walker, or for the HTTP
+    // bins (bin_seg_mask) the segment-expansion variant of either
+    uint32_t *fallback = work + (uint64_t)mfp::NBINS * n;
+    const uint64_t cblocks = tiles < 2048 ? tiles : 2048;
+    MFP_LAUNCH("k_classify", mfp::k_classify, dim3((uint32_t)cblocks), dim3(mfp::TILE), 0, stream, P, work, n, bin_count,
+               (uint8_t *)(work + (uint64_t)(mfp::NBINS + 1) * n + 1));
     if (hipGetLastError() != hipSuccess) return -1;
-    // fallback lane over the packets the wave kernel handed back
-    P.idx = work;
-    P.count = fp_used + 3;
-    uint64_t fblocks = tiles < 1024 ? tiles : 1024;
-    MFP_LAUNCH("k_fingerprint/fallback", mfp::k_fingerprint, dim3((uint32_t)fblocks), dim3(mfp::TILE), shmem, stream, P);
+    const uint64_t fblocks = tiles < 2048 ? tiles : 2048;
+    const uint64_t lblocks = ((n + 63) / 64) < 2048 ? (n + 63) / 64 : 2048;
+    static const char *const lane_name[mfp::NBINS] = {"k_fingerprint/tls_ch", "k_fingerprint/http_req",
+        "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other", "k_fingerprint/tls_sh",
+        "k_fingerprint/ssh", "k_fingerprint/dtls"};
+    static const char *const seg_name[mfp::NBINS] = {"k_fp_seg/tls_ch", "k_fp_seg/http_req",
+        "k_fp_seg/tcp_syn", "k_fp_seg/http_resp", "k_fp_seg/other", "k_fp_seg/tls_sh",
+        "k_fp_seg/ssh", "k_fp_seg/dtls"};
+    static const char *const lds_name[mfp::NBINS] = {"k_fp_lds/tls_ch", "k_fp_lds/http_req",
+        "k_fp_lds/tcp_syn", "k_fp_lds/http_resp", "k_fp_lds/other", "k_fp_lds/tls_sh",
+        "k_fp_lds/ssh", "k_fp_lds/dtls"};
+    // each bin's kernel carries its protocol's parser family only (bin 4,
+    // "other", all of them); misbinned packets are punted to the fallback lane
+    using namespace mfp;
+    for (int b = 0; b < NBINS; b++) {
+        P.idx = work + (uint64_t)b * n;
+        P.count = bin_count + b;
+        const bool seg = bin_seg_mask & (1u << b);
+        const bool lds = bin_lds_mask & (1u << b);
+        const dim3 lg((uint32_t)lblocks), fg((uint32_t)fblocks);
+#define MFP_BIN(FAMILY)                                                                                          \
+        do {                                                                                                     \
+            if (lds && seg) MFP_LAUNCH(lds_name[b], (k_fp_lds<true, MFP_LDS_STAGE_SEG, FAM_HTTP>), lg, dim3(64), 0, \
+                                       stream, P, fallback);                                                     \
+            else if (lds) MFP_LAUNCH(lds_name[b], (k_fp_lds<false, MFP_LDS_STAGE, FAMILY>), lg, dim3(64), 0,     \
+                                     stream, P, fallback);                                                       \
+            else if (seg) MFP_LAUNCH(seg_name[b], k_fp_seg, fg, dim3(TILE), 0, stream, P, fallback);             \
+            else MFP_LAUNCH(lane_name[b], k_fingerprint<FAMILY>, fg, dim3(TILE), 0, stream, P, fallback);       \
+        } while (0)
+        switch (b) {
+        case 0: case 5: MFP_BIN(FAM_TLS); break;      // TLS ClientHello, ServerHello/Certificate
+        case 1: case 3: MFP_BIN(FAM_HTTP); break;     // HTTP request, response
+        case 2: MFP_BIN(FAM_TCP); break;              // SYN, SYN-ACK
+        case 6: MFP_BIN(FAM_SSH); break;
+        case 7: MFP_BIN(FAM_DTLS); break;
+        default: MFP_BIN(FAM_ALL); break;             // no message of a selected protocol (or misbinned)
+        }
+#undef MFP_BIN
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    {
+        // the fallback lane: every parser family, straight from HBM, over the
+        // packets the bin kernels handed back (fp_used[3] of them)
+        P.idx = fallback;
+        P.count = fp_used + 3;
+        const uint64_t fb = tiles < 1024 ? tiles : 1024;
+        MFP_LAUNCH("k_fingerprint/fallback", k_fingerprint<FAM_ALL>, dim3((uint32_t)fb), dim3(TILE), 0, stream, P,
+                   nullptr);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #undef MFP_LAUNCH

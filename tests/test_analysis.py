@@ -153,7 +153,7 @@ def test_analysis_synthetic_archive_vs_reference(lane_max_p, monkeypatch):
     if lane_max_p == "seg":
         monkeypatch.setenv("MFP_BIN_SEG_MASK", "0xa")
     elif lane_max_p == "lane":
-        monkeypatch.setenv("MFP_BIN_WAVE_MASK", "0x0")
+        monkeypatch.setenv("MFP_BIN_SEG_MASK", "0x0")
     elif lane_max_p is not None:
         monkeypatch.setenv("MFP_AN_LANE_MAX_P", lane_max_p)
     a, d = synth_batch()

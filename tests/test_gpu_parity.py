@@ -139,15 +139,18 @@ def test_fuzzed_vs_oracle(fmt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wave_mask,seg_mask", [("0x0", "0x0"), ("0xff", "0x0"), ("0x0", "0xa"), ("0x0", "0xff")])
-def test_bin_kernel_choices_vs_oracle(wave_mask, seg_mask, monkeypatch):
-    """Every bin kernel (lane walker, wave walker, lane walk + wave expansion)
-    takes any packet (what it cannot fingerprint goes to the fallback lane):
-    one batch of synthetic + fuzzed packets under each assignment of kernels
-    to bins equals the oracle."""
+@pytest.mark.parametrize("seg_mask,lds_mask", [
+    ("0x0", "0x0"), ("0xa", "0x0"), ("0xff", "0x0"), ("0xa", "0xff"), ("0x0", "0xff"), ("0xff", "0xff"),
+    ("0xa", "0x5a")])
+def test_bin_kernel_choices_vs_oracle(seg_mask, lds_mask, monkeypatch):
+    """Every bin kernel (HBM lane walker, lane walk + wave expansion, and the
+    LDS-staged walker in both emission modes, each carrying only its bin's
+    parser family) takes any packet (what it cannot fingerprint goes to the
+    fallback lane): one batch of synthetic + fuzzed packets under each
+    assignment of kernels to bins equals the oracle."""
     from tests import pcaplib
-    monkeypatch.setenv("MFP_BIN_WAVE_MASK", wave_mask)
     monkeypatch.setenv("MFP_BIN_SEG_MASK", seg_mask)
+    monkeypatch.setenv("MFP_BIN_LDS_MASK", lds_mask)
     a2, d2 = synth.batch(6000, seed=0x5EED0042, workload="mixed", n_templates=1500)
     pk = [(1, a2[int(d["offset"]):int(d["offset"]) + int(d["caplen"])].tobytes()) for d in d2]
     pk += synth.fuzz(pk[:2000], 10000, seed=77)
@@ -227,14 +230,14 @@ def test_large_device_batch_properties():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seg_mask", ["0xa", "0x0"])
-def test_device_hash_keys(seg_mask, monkeypatch):
-    """Strings written by the segment and wave kernels carry their classifier
-    key (mfpc::str_hash) after the string (MFP_FLAG_HASHED); the lane kernel
-    leaves it to the classifier (flag clear)."""
+@pytest.mark.parametrize("seg_mask,lds_mask", [("0xa", "0xff"), ("0xa", "0x0"), ("0x0", "0x0")])
+def test_device_hash_keys(seg_mask, lds_mask, monkeypatch):
+    """Every fingerprint kernel stores its string's classifier key
+    (mfpc::str_hash) right after the string (MFP_FLAG_HASHED), so k_analyze
+    never re-reads the string to hash it."""
     import torch
     monkeypatch.setenv("MFP_BIN_SEG_MASK", seg_mask)
-    monkeypatch.setenv("MFP_BIN_WAVE_MASK", "0x0" if seg_mask != "0x0" else "0xa")
+    monkeypatch.setenv("MFP_BIN_LDS_MASK", lds_mask)
     a, d = synth.batch(30000, seed=0x5EED0077, workload="mixed", n_templates=3000)
     n = len(d)
     ctx = mercury_amd.Context(CONTRACT, device=0)
@@ -260,3 +263,4 @@ def test_device_hash_keys(seg_mask, monkeypatch):
         checked += 1
     http = int(np.isin(rec["fp_type"], [3, 4]).sum())
     assert checked >= http > 1000
+    assert checked == int(((rec["fp_len"] > 0) & (rec["fp_type"] > 0)).sum())   # every string hashed
