@@ -455,6 +455,14 @@ def main():
     d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
     d_an = torch.empty(n * 24 if analysis else 1, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
+    prev = None
+    if analysis and tdist:
+        # the shards of one stream: unknown-TLS statuses decided in shard order
+        # (shard.ordered_prevalence_merge), every rank on its own copy of the LRU
+        from mercury_amd import shard
+        prev = mercury_amd.Prevalence(100000)
+        ctx.set_prevalence(prev)
+        ctx.defer(True)
 
     def step():
         ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(), cap,
@@ -462,6 +470,8 @@ def main():
         if analysis:
             ctx.analyze_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(),
                                d_an.data_ptr(), stream.cuda_stream)
+            if prev is not None:
+                shard.ordered_prevalence_merge(ctx, prev, rank * n)
 
     for _ in range(args.warmup):
         step()

@@ -189,14 +189,76 @@ MFP_EXPORT long long mfp_process_pipelined(mfp_context ctx, const uint8_t *arena
                                            const mfp_pkt_desc *desc, size_t n, mfp_record *rec, char *fp_arena,
                                            size_t fp_cap, mfp_analysis *analysis, size_t chunk);
 
+/* ---- the unknown-TLS prevalence set (fingerprint_prevalence, analysis.h:362-421) ----
+ * A TLS fingerprint the archive does not label, and not in its known
+ * prevalence list, is "randomized" when it is not in an LRU of the 100000 most
+ * recently seen such fingerprints (analysis.h:433) and "unlabeled" when it is;
+ * the LRU is updated on every sighting, in stream order
+ * (perform_analysis_common analysis.h:1043-1083).  The device finds each
+ * batch's sightings; the decisions are made on the host, in stream order, by
+ * an mfp_prevalence object (identity: the string's 64-bit hash).  By default
+ * every analysis call decides its own batch (the call waits for its kernels);
+ * shards of one stream (several contexts) defer the decision and resolve their
+ * batches in shard order against one shared object. */
+typedef struct mfp_prevalence_s *mfp_prevalence;
+
+/* one distinct fingerprint of a batch's sightings */
+typedef struct {
+    uint64_t hash;        /* the fingerprint string's hash                         */
+    uint64_t first, last; /* stream positions of its first and last sighting (the
+                             batch's packet indices; add a shard's base to order
+                             the shards of one stream)                             */
+    uint32_t count;       /* sightings                                             */
+    uint32_t first_seen;  /* decision: 1 = in the LRU at the first sighting
+                             (unlabeled), 0 = randomized; later sightings are all
+                             unlabeled                                             */
+} mfp_sighting;
+
+MFP_EXPORT mfp_prevalence mfp_prevalence_create(uint32_t capacity);   /* the reference: 100000 */
+MFP_EXPORT void mfp_prevalence_destroy(mfp_prevalence p);
+MFP_EXPORT uint64_t mfp_prevalence_size(mfp_prevalence p);
+MFP_EXPORT int mfp_prevalence_contains(mfp_prevalence p, uint64_t hash);
+/* the set from least to most recently used (hashes); returns its size */
+MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t cap);
+/* 1 when the distinct form is exact for these entries (no eviction possible) */
+MFP_EXPORT int mfp_prevalence_distinct_exact(mfp_prevalence p, const mfp_sighting *d, size_t u);
+/* decide first_seen of every entry (entries of several shards together, in
+ * any order: `first`/`last` order them) and apply them; -2 when the entries
+ * could evict (nothing applied: resolve the sighting sequence instead) */
+MFP_EXPORT int mfp_prevalence_resolve_distinct(mfp_prevalence p, mfp_sighting *d, size_t u);
+/* every sighting in stream order: seen[j] = 1 when hash[j] was in the LRU */
+MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen);
+
+/* the context's own LRU (created with the classifier) */
+MFP_EXPORT mfp_prevalence mfp_analysis_prevalence(mfp_context ctx);
+/* decide this context's sightings against p (shared by the shards of one
+ * stream; the caller keeps ownership), or against its own again (p = NULL) */
+MFP_EXPORT int mfp_analysis_set_prevalence(mfp_context ctx, mfp_prevalence p);
+/* on != 0: analysis calls leave the unknown-TLS statuses of their batch
+ * provisional (randomized, MFP_AN_PENDING) until mfp_analysis_resolve[_sequence] */
+MFP_EXPORT int mfp_analysis_defer(mfp_context ctx, int on);
+/* the last deferred batch's distinct unknown-TLS fingerprints (first/last =
+ * batch indices); returns their count, or -3 when the batch has more distinct
+ * fingerprints than its table holds (use the sequence) */
+MFP_EXPORT long long mfp_analysis_distinct(mfp_context ctx, mfp_sighting *out, size_t cap);
+/* its sightings' hashes in stream order; returns their count */
+MFP_EXPORT long long mfp_analysis_sequence(mfp_context ctx, uint64_t *hash, size_t cap);
+/* apply the decisions (entries in mfp_analysis_distinct's order / one byte
+ * per sighting in stream order) to the last deferred batch's records */
+MFP_EXPORT int mfp_analysis_resolve(mfp_context ctx, const mfp_sighting *d, size_t u);
+MFP_EXPORT int mfp_analysis_resolve_sequence(mfp_context ctx, const uint8_t *seen, size_t m);
+/* the last analysed batch's analysis records as they are now on the device
+ * (for host batches analysed deferred, after the decision); returns the
+ * batch's packet count */
+MFP_EXPORT long long mfp_analysis_last(mfp_context ctx, mfp_analysis *out, size_t cap);
+
 /* names behind mfp_analysis.process and the bits of mfp_analysis.attr */
 MFP_EXPORT const char *mfp_process_name(mfp_context ctx, uint32_t id);
 MFP_EXPORT const char *mfp_attribute_name(mfp_context ctx, uint32_t bit);
 
 /* last analysis batch: [0] packets classified, [1] unknown-TLS sightings,
  * [2] fingerprints with more processes than the kernel handles (512),
- * [3] distinct unknown TLS fingerprints seen so far (the reference's LRU
- * holds 100000; beyond that its evictions are not reproduced) */
+ * [3] fingerprints in the context's prevalence LRU */
 MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
 
 /* host only (tests): load an archive; out = {fingerprints, entries,

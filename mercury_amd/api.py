@@ -13,7 +13,10 @@ RECORD_DTYPE = np.dtype([("fp_offset", "<u8"), ("fp_len", "<u4"), ("fp_type", "u
                          ("net", "<u4")])
 ANALYSIS_DTYPE = np.dtype([("score", "<f8"), ("malware_prob", "<f8"), ("process", "<u4"), ("attr", "<u2"),
                            ("status", "u1"), ("flags", "u1")])
+SIGHTING_DTYPE = np.dtype([("hash", "<u8"), ("first", "<u8"), ("last", "<u8"), ("count", "<u4"),
+                           ("first_seen", "<u4")])
 assert DESC_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 32 and ANALYSIS_DTYPE.itemsize == 24
+assert SIGHTING_DTYPE.itemsize == 32
 NO_PROCESS = 0xFFFFFFFF
 STATUS_NAMES = ["no_info_available", "labeled", "randomized", "unlabeled", "unanalyzed"]
 
@@ -99,6 +102,38 @@ def load_library():
     lib.mfp_write_json_batch.restype = ctypes.c_longlong
     lib.mfp_write_json_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, sz, vp, ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.c_int]
+    u64 = ctypes.c_uint64
+    lib.mfp_prevalence_create.restype = vp
+    lib.mfp_prevalence_create.argtypes = [ctypes.c_uint32]
+    lib.mfp_prevalence_destroy.argtypes = [vp]
+    lib.mfp_prevalence_size.restype = u64
+    lib.mfp_prevalence_size.argtypes = [vp]
+    lib.mfp_prevalence_contains.restype = ctypes.c_int
+    lib.mfp_prevalence_contains.argtypes = [vp, u64]
+    lib.mfp_prevalence_keys.restype = ctypes.c_longlong
+    lib.mfp_prevalence_keys.argtypes = [vp, vp, sz]
+    lib.mfp_prevalence_distinct_exact.restype = ctypes.c_int
+    lib.mfp_prevalence_distinct_exact.argtypes = [vp, vp, sz]
+    lib.mfp_prevalence_resolve_distinct.restype = ctypes.c_int
+    lib.mfp_prevalence_resolve_distinct.argtypes = [vp, vp, sz]
+    lib.mfp_prevalence_resolve_sequence.restype = ctypes.c_int
+    lib.mfp_prevalence_resolve_sequence.argtypes = [vp, vp, sz, vp]
+    lib.mfp_analysis_prevalence.restype = vp
+    lib.mfp_analysis_prevalence.argtypes = [vp]
+    lib.mfp_analysis_set_prevalence.restype = ctypes.c_int
+    lib.mfp_analysis_set_prevalence.argtypes = [vp, vp]
+    lib.mfp_analysis_defer.restype = ctypes.c_int
+    lib.mfp_analysis_defer.argtypes = [vp, ctypes.c_int]
+    lib.mfp_analysis_distinct.restype = ctypes.c_longlong
+    lib.mfp_analysis_distinct.argtypes = [vp, vp, sz]
+    lib.mfp_analysis_sequence.restype = ctypes.c_longlong
+    lib.mfp_analysis_sequence.argtypes = [vp, vp, sz]
+    lib.mfp_analysis_resolve.restype = ctypes.c_int
+    lib.mfp_analysis_resolve.argtypes = [vp, vp, sz]
+    lib.mfp_analysis_last.restype = ctypes.c_longlong
+    lib.mfp_analysis_last.argtypes = [vp, vp, sz]
+    lib.mfp_analysis_resolve_sequence.restype = ctypes.c_int
+    lib.mfp_analysis_resolve_sequence.argtypes = [vp, vp, sz]
     _lib = lib
     return lib
 
@@ -226,11 +261,122 @@ class Context:
             out[name.value.decode()] = (int(cnt.value), float(ms.value))
             i += 1
 
+    # ---- the unknown-TLS prevalence LRU (see include/mfp.h) ----
+    def prevalence(self):
+        return Prevalence(handle=self.lib.mfp_analysis_prevalence(self.h))
+
+    def set_prevalence(self, prev):
+        if self.lib.mfp_analysis_set_prevalence(self.h, prev.h if prev is not None else None) != 0:
+            raise MercuryAmdError(_err(self.lib))
+
+    def defer(self, on=True):
+        if self.lib.mfp_analysis_defer(self.h, 1 if on else 0) != 0:
+            raise MercuryAmdError(_err(self.lib))
+
+    def analysis_distinct(self):
+        """The last deferred batch's distinct unknown-TLS fingerprints
+        (SIGHTING_DTYPE), or None when the batch has too many for its table."""
+        n = self.lib.mfp_analysis_distinct(self.h, None, 0)
+        if n == -3:
+            return None
+        if n < 0:
+            raise MercuryAmdError(_err(self.lib))
+        out = np.zeros(max(n, 1), SIGHTING_DTYPE)
+        self.lib.mfp_analysis_distinct(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def analysis_sequence(self):
+        n = self.lib.mfp_analysis_sequence(self.h, None, 0)
+        if n < 0:
+            raise MercuryAmdError(_err(self.lib))
+        out = np.zeros(max(n, 1), np.uint64)
+        self.lib.mfp_analysis_sequence(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def analysis_resolve(self, sightings):
+        d = np.ascontiguousarray(sightings, SIGHTING_DTYPE)
+        if self.lib.mfp_analysis_resolve(self.h, d.ctypes.data, len(d)) != 0:
+            raise MercuryAmdError(_err(self.lib))
+
+    def last_analysis(self):
+        """The last analysed batch's analysis records as they are on the device now."""
+        n = self.lib.mfp_analysis_last(self.h, None, 0)
+        if n < 0:
+            raise MercuryAmdError(_err(self.lib))
+        out = np.zeros(max(n, 1), ANALYSIS_DTYPE)
+        self.lib.mfp_analysis_last(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def analysis_resolve_sequence(self, seen):
+        b = np.ascontiguousarray(seen, np.uint8)
+        if self.lib.mfp_analysis_resolve_sequence(self.h, b.ctypes.data, len(b)) != 0:
+            raise MercuryAmdError(_err(self.lib))
+
     def process_device(self, d_arena, d_desc, n, d_rec, d_fp, fp_cap, d_used, stream=0):
         """All arguments are device pointers (ints, e.g. torch data_ptr())."""
         r = self.lib.mfp_process_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, fp_cap, d_used, stream)
         if r != 0:
             raise MercuryAmdError("mfp_process_batch_device failed: " + _err(self.lib))
+
+
+class Prevalence:
+    """The unknown-TLS prevalence LRU (fingerprint_prevalence, analysis.h:362-421):
+    mfp_prevalence_* on the host.  `owned=False` wraps a context's own object."""
+
+    def __init__(self, capacity=100000, handle=None):
+        self.lib = load_library()
+        self.owned = handle is None
+        self.h = handle if handle is not None else self.lib.mfp_prevalence_create(capacity)
+        if not self.h:
+            raise MercuryAmdError(_err(self.lib))
+
+    def close(self):
+        if self.h and self.owned:
+            self.lib.mfp_prevalence_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(self.lib.mfp_prevalence_size(self.h))
+
+    def __contains__(self, h):
+        return bool(self.lib.mfp_prevalence_contains(self.h, int(h)))
+
+    def keys(self):
+        """Hashes from least to most recently used."""
+        n = self.lib.mfp_prevalence_keys(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.uint64)
+        self.lib.mfp_prevalence_keys(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def resolve_sequence(self, hashes):
+        """seen[j] = 1 when hashes[j] was in the set at sighting j (unlabeled)."""
+        h = np.ascontiguousarray(hashes, np.uint64)
+        seen = np.zeros(max(len(h), 1), np.uint8)
+        if self.lib.mfp_prevalence_resolve_sequence(self.h, h.ctypes.data, len(h), seen.ctypes.data) != 0:
+            raise MercuryAmdError(_err(self.lib))
+        return seen[:len(h)]
+
+    def distinct_exact(self, sightings):
+        d = np.ascontiguousarray(sightings, SIGHTING_DTYPE)
+        return self.lib.mfp_prevalence_distinct_exact(self.h, d.ctypes.data, len(d)) == 1
+
+    def resolve_distinct(self, sightings):
+        """Decide first_seen of each entry in place; False (nothing applied)
+        when the entries could evict."""
+        if len(sightings) and not sightings.flags["C_CONTIGUOUS"]:
+            raise ValueError("sightings must be contiguous (decided in place)")
+        r = self.lib.mfp_prevalence_resolve_distinct(self.h, sightings.ctypes.data, len(sightings))
+        if r == -2:
+            return False
+        if r != 0:
+            raise MercuryAmdError(_err(self.lib))
+        return True
 
 
 def resource_stats(path):

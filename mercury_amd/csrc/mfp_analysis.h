@@ -46,9 +46,22 @@ struct mfp_update {     // class update (naive_bayes.hpp:21-41)
 struct mfp_asn4 { uint32_t lo, hi, asn, pad; };             // host-order address interval
 struct mfp_asn6 { uint64_t lo_hi, lo_lo, hi_hi, hi_lo; uint32_t asn, pad; };   // 128-bit host-order interval
 
-struct mfp_seen_slot {  // fingerprint_prevalence, adaptive part
-    unsigned long long hash;
-    unsigned long long first;   // (batch << 32) | packet index of the first sighting
+// one batch's unknown-TLS sightings, per distinct fingerprint hash (the
+// adaptive part of fingerprint_prevalence is decided on the host,
+// mfp_prevalence.cpp, from this table)
+struct mfp_seen_slot {          // the table is reset to all-ones bytes per batch
+    unsigned long long hash;    // ~0 = empty
+    unsigned int first;         // packet index of the first sighting (atomicMin)
+    unsigned int nlast;         // ~(packet index of the last sighting) (atomicMin)
+    unsigned int count_m1;      // sightings - 1 (atomicAdd from ~0)
+    unsigned int pos;           // position in the distinct list (k_seen_export)
+};
+struct mfp_seen_tab {
+    mfp_seen_slot *slots = nullptr;
+    uint32_t mask = 0;          // slots - 1 (power of two)
+    uint32_t *list = nullptr;   // distinct list: slot index per position
+    uint32_t list_cap = 0;      // more distinct fingerprints than this: overflow
+    unsigned int *counters = nullptr;   // [0] distinct, [1] overflow
 };
 
 struct mfp_classifier_dev {
@@ -67,9 +80,6 @@ struct mfp_classifier_dev {
     uint32_t types_mask = 0;           // analyzable fingerprint types (fp_types)
     uint32_t enc_channel_idx = 7, faketls_idx = 9;
     uint32_t randomized_entry[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};   // "tls/", "tls/1/", "tls/2/" + "randomized"
-    mfp_seen_slot *seen = nullptr; uint32_t seen_cap = 0;
-    unsigned long long *seen_count = nullptr;
-    uint32_t batch = 0;
 };
 
 typedef struct mfp_classifier_s mfp_classifier;

@@ -22,10 +22,10 @@
 //      (compute_score_and_probability / get_analysis_result analysis.h:222-358),
 //      encrypted_channel attribute (analysis.h:1161-1163).
 // Unknown TLS fingerprints follow fingerprint_prevalence (analysis.h:362-421):
-// the known set is a device table; the adaptive set is a device hash set
-// whose per-fingerprint word is min((batch << 32) | packet index), so the
-// first sighting in stream order is "randomized" and every later one
-// "unlabeled" (k_analyze_status).
+// the known set is a device table; the adaptive set, an LRU of 100000
+// fingerprints, is decided on the host in stream order (mfp_prevalence.cpp)
+// from this batch's sightings per distinct fingerprint (a batch-local device
+// table), and k_analyze_resolve applies the decisions.
 #include <hip/hip_runtime.h>
 
 #include "mfp_analysis.h"
@@ -422,7 +422,8 @@ struct AParams {
     mfp_record *rec;
     const uint8_t *fp_arena;
     mfp_analysis *out;
-    uint64_t *pend_bits;         // per group of 64 packets: unknown-TLS sightings (k_analyze_status)
+    uint64_t *pend_bits;         // per group of 64 packets: unknown-TLS sightings (k_analyze_resolve)
+    mfp_seen_tab seen;           // this batch's sightings per distinct fingerprint
     struct Deferred *deferred;   // packets scored by k_analyze_wave
     uint32_t mode;
     uint32_t lane_max_p;         // phase L takes fingerprints with P <= min(lane_max_p, PL)
@@ -521,18 +522,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 if (pid != 0xffffffffu) {
                     status = 3;                    // unlabeled (known set; no LRU update)
                 } else {
-                    // adaptive set: record the sighting; k_analyze_status decides
+                    // adaptive set (fingerprint_prevalence LRU): the host
+                    // decides the sighting in stream order (mfp_prevalence.cpp);
+                    // meanwhile it is classified as a first sighting would be
                     pending = true;
                     status = 2;
-                    uint64_t k = fh & (D.seen_cap - 1);
-                    for (uint32_t t = 0; t < D.seen_cap; t++, k = (k + 1) & (D.seen_cap - 1)) {
-                        const unsigned long long prev = atomicCAS(&D.seen[k].hash, ~0ull, (unsigned long long)fh);
-                        if (prev == ~0ull) atomicAdd(D.seen_count, 1ull);
-                        if (prev == ~0ull || prev == fh) {
-                            atomicMin(&D.seen[k].first, ((unsigned long long)D.batch << 32) | (uint32_t)i);
-                            break;
-                        }
-                    }
                     // classify with "<prefix>randomized" when the DB has it
                     const uint32_t c4 = (uint32_t)(w0 >> 32) & 0xff, c5 = (uint32_t)(w0 >> 40) & 0xff;
                     const uint32_t pre = fl > 5 && c5 == '/' ? (c4 == '1' ? 1u : c4 == '2' ? 2u : 0u) : 0u;
@@ -542,10 +536,40 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 status = 3;                                                   // unlabeled
             }
         }
-        {   // unknown-TLS sightings of this group, for k_analyze_status
+        {   // unknown-TLS sightings of this group: the per-group bitmap, and the
+            // batch table per distinct fingerprint (first / last sighting, count),
+            // one set of atomics per distinct hash per wave
             const uint64_t pm = __ballot(pending);
             if (lane == 0) P.pend_bits[g] = pm;
             n_pend += (uint32_t)__builtin_popcountll(pm);
+            uint64_t left = pm;
+            while (left) {
+                const int l0 = __builtin_ctzll(left);
+                const uint64_t h0 = rl64(fh, l0);
+                const uint64_t same = __ballot(pending && fh == h0) & left;
+                left &= ~same;
+                if ((int)lane == l0) {
+                    const uint32_t i_first = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(same));
+                    const uint32_t i_last = (uint32_t)(g * 64 + 63 - (uint64_t)__builtin_clzll(same));
+                    const mfp_seen_tab &T = P.seen;
+                    uint64_t k = h0 & T.mask;
+                    for (uint32_t t = 0; t <= T.mask; t++, k = (k + 1) & T.mask) {
+                        const unsigned long long prev = atomicCAS(&T.slots[k].hash, ~0ull, (unsigned long long)h0);
+                        if (prev == ~0ull) {             // new in this batch: a position in the distinct list
+                            const unsigned int pos = atomicAdd(&T.counters[0], 1u);
+                            if (pos < T.list_cap) T.list[pos] = (uint32_t)k;
+                            else atomicExch(&T.counters[1], 1u);
+                        }
+                        if (prev == ~0ull || prev == h0) {      // (slots start all-ones: min, min of ~last, count - 1)
+                            atomicMin(&T.slots[k].first, i_first);
+                            atomicMin(&T.slots[k].nlast, ~i_last);
+                            atomicAdd(&T.slots[k].count_m1, (unsigned int)__builtin_popcountll(same));
+                            break;
+                        }
+                        if (t == T.mask) atomicExch(&T.counters[1], 1u);   // table full
+                    }
+                }
+            }
         }
         bool scored = analyzable && entry != 0xffffffffu;
         if (scored) {
@@ -912,33 +936,69 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
     }
 }
 
-// k_analyze_status: unknown TLS fingerprints (the sightings k_analyze queued)
-// -- the first sighting in stream order is "randomized" (classified with the
-// randomized entry, if any), every later one "unlabeled" (no process)
-__global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
+// k_seen_export: the batch's distinct unknown-TLS fingerprints, in the order
+// they were first inserted (the host sorts them by first sighting)
+__global__ __launch_bounds__(256) void k_seen_export(mfp_seen_tab T, mfp_sighting *out) {
+    const uint32_t u = T.counters[0] < T.list_cap ? T.counters[0] : T.list_cap;
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < u; p += gridDim.x * 256) {
+        mfp_seen_slot &sl = T.slots[T.list[p]];
+        sl.pos = p;
+        mfp_sighting o;
+        o.hash = sl.hash; o.first = sl.first; o.last = ~sl.nlast; o.count = sl.count_m1 + 1u; o.first_seen = 0;
+        out[p] = o;
+    }
+}
+
+// k_seen_sequence: every sighting's fingerprint hash in stream order (the
+// host's exact LRU simulation when the distinct form cannot be exact);
+// group_off[g] = sightings before group g
+__global__ __launch_bounds__(256) void k_seen_sequence(AParams P, const uint32_t *group_off, uint64_t *seq) {
     const uint64_t ngroups = (P.n + 63) / 64;
     for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += (uint64_t)gridDim.x * 256) {
+        uint32_t r = group_off[g];
+        for (uint64_t w = P.pend_bits[g]; w; w &= w - 1) {
+            const uint32_t i = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(w));
+            const mfp_record rc = P.rec[i];
+            seq[r++] = fp_key(rc, P.fp_arena + rc.fp_offset, rc.fp_len);
+        }
+    }
+}
+
+// k_analyze_resolve: the unknown-TLS statuses the host decided.  A sighting
+// stays "randomized" (classified with the randomized entry, if any) when it
+// was not in the LRU; every other one becomes "unlabeled" (no process).
+//   seen_pos != nullptr: per distinct fingerprint (distinct form): randomized
+//     iff it is the fingerprint's first sighting and seen_pos[pos] == 0;
+//   else per sighting in stream order: seen_seq[group_off[g] + rank] == 0.
+__global__ __launch_bounds__(256) void k_analyze_resolve(AParams P, const uint8_t *seen_pos, const uint32_t *group_off,
+                                                         const uint8_t *seen_seq) {
+    const uint64_t ngroups = (P.n + 63) / 64;
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += (uint64_t)gridDim.x * 256) {
+    uint32_t r = seen_pos ? 0u : group_off[g];
     for (uint64_t w = P.pend_bits[g]; w; w &= w - 1) {
         const uint32_t i = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(w));
         mfp_analysis a = P.out[i];
-        const mfp_record r = P.rec[i];
-        const uint8_t *fp = P.fp_arena + r.fp_offset;
-        const uint64_t h = fp_key(r, fp, r.fp_len);
-        const mfp_classifier_dev &D = P.D;
-        uint64_t k = h & (D.seen_cap - 1);
-        bool first = false;
-        for (uint32_t t = 0; t < D.seen_cap; t++, k = (k + 1) & (D.seen_cap - 1)) {
-            const unsigned long long sh = D.seen[k].hash;
-            if (sh == h) { first = D.seen[k].first == (((unsigned long long)D.batch << 32) | i); break; }
-            if (sh == ~0ull) break;
+        const mfp_record rc = P.rec[i];
+        bool seen;
+        if (seen_pos) {
+            const uint64_t h = fp_key(rc, P.fp_arena + rc.fp_offset, rc.fp_len);
+            uint64_t k = h & P.seen.mask;
+            seen = true;
+            for (uint32_t t = 0; t <= P.seen.mask; t++, k = (k + 1) & P.seen.mask) {
+                const mfp_seen_slot &sl = P.seen.slots[k];
+                if (sl.hash == h) { seen = !(sl.first == i && seen_pos[sl.pos] == 0); break; }
+                if (sl.hash == ~0ull) break;
+            }
+        } else {
+            seen = seen_seq[r++] != 0;
         }
         a.flags &= (uint8_t)~MFP_AN_PENDING;
-        if (!first) {
+        if (seen) {
             a.status = 3;
             a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0;
             a.flags = MFP_AN_VALID;
         }
-        if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
+        if (P.mode == MFP_MODE_ANALYSIS && (rc.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
         P.out[i] = a;
     }
     }
@@ -946,18 +1006,27 @@ __global__ __launch_bounds__(256) void k_analyze_status(AParams P) {
 
 }  // namespace mfpa
 
-extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
-                                   uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   uint32_t *pending, void *deferred, unsigned long long *stats, uint32_t mode,
-                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof) {
-    if (n == 0) return 0;
+static mfpa::AParams make_params(const mfp_classifier_dev *D, const mfp_seen_tab &T, const uint8_t *arena,
+                                 const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
+                                 mfp_analysis *out, uint32_t *pending, void *deferred, unsigned long long *stats,
+                                 uint32_t mode, uint32_t lane_max_p) {
     mfpa::AParams P;
     P.D = *D;
+    P.seen = T;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = mode;
     P.pend_bits = (uint64_t *)pending;
     P.deferred = (mfpa::Deferred *)deferred;
     P.lane_max_p = lane_max_p;
     P.stats = stats;
+    return P;
+}
+
+extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
+                                   const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
+                                   mfp_analysis *out, uint32_t *pending, void *deferred, unsigned long long *stats,
+                                   uint32_t mode, uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof) {
+    if (n == 0) return 0;
+    mfpa::AParams P = make_params(D, *T, arena, desc, n, rec, fp_arena, out, pending, deferred, stats, mode, lane_max_p);
     uint64_t groups = (n + 63) / 64, blocks = (groups + mfpa::AW - 1) / mfpa::AW;
     if (blocks > 4096) blocks = 4096;
     if (prof) mfp_prof_begin(prof, "k_analyze", stream);
@@ -967,11 +1036,41 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *a
     if (prof) mfp_prof_begin(prof, "k_analyze_wave", stream);
     hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(1024), dim3(256), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
-    if (hipGetLastError() != hipSuccess) return -1;
-    uint64_t sblocks = (groups + 255) / 256;
-    if (sblocks > 1024) sblocks = 1024;
-    if (prof) mfp_prof_begin(prof, "k_analyze_status", stream);
-    hipLaunchKernelGGL(mfpa::k_analyze_status, dim3((uint32_t)sblocks), dim3(256), 0, stream, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mfp_launch_seen_export(const mfp_seen_tab *T, uint32_t u, mfp_sighting *out, hipStream_t stream) {
+    if (u == 0) return 0;
+    const uint32_t blocks = (u + 255) / 256 < 1024 ? (u + 255) / 256 : 1024;
+    hipLaunchKernelGGL(mfpa::k_seen_export, dim3(blocks), dim3(256), 0, stream, *T, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mfp_launch_seen_sequence(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
+                                        const mfp_record *rec, const uint8_t *fp_arena, uint32_t *pending,
+                                        const uint32_t *group_off, uint64_t *seq, hipStream_t stream) {
+    if (n == 0) return 0;
+    mfpa::AParams P = make_params(D, *T, nullptr, nullptr, n, (mfp_record *)rec, fp_arena, nullptr, pending, nullptr,
+                                  nullptr, 0, 0);
+    uint64_t groups = (n + 63) / 64, blocks = (groups + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(mfpa::k_seen_sequence, dim3((uint32_t)blocks), dim3(256), 0, stream, P, group_off, seq);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mfp_launch_analysis_resolve(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
+                                           const mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
+                                           uint32_t *pending, uint32_t mode, const uint8_t *seen_pos,
+                                           const uint32_t *group_off, const uint8_t *seen_seq, hipStream_t stream,
+                                           mfp_prof *prof) {
+    if (n == 0) return 0;
+    mfpa::AParams P = make_params(D, *T, nullptr, nullptr, n, (mfp_record *)rec, fp_arena, out, pending, nullptr,
+                                  nullptr, mode, 0);
+    uint64_t groups = (n + 63) / 64, blocks = (groups + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    if (prof) mfp_prof_begin(prof, "k_analyze_resolve", stream);
+    hipLaunchKernelGGL(mfpa::k_analyze_resolve, dim3((uint32_t)blocks), dim3(256), 0, stream, P, seen_pos, group_off,
+                       seen_seq);
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -819,19 +819,12 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     for (uint32_t ty : c->fp_types) d.types_mask |= 1u << ty;
     d.enc_channel_idx = 7;
     d.faketls_idx = 9;
-    // adaptive "seen" set of unknown TLS fingerprints (fingerprint_prevalence LRU)
-    d.seen_cap = 1u << 18;
-    if (hipMalloc((void **)&d.seen, (size_t)d.seen_cap * sizeof(mfp_seen_slot)) != hipSuccess) return -2;
-    if (hipMemset(d.seen, 0xff, (size_t)d.seen_cap * sizeof(mfp_seen_slot)) != hipSuccess) return -2;
-    if (hipMalloc((void **)&d.seen_count, sizeof(unsigned long long)) != hipSuccess) return -2;
-    if (hipMemset(d.seen_count, 0, sizeof(unsigned long long)) != hipSuccess) return -2;
-    d.batch = 0;
     return 0;
 }
 
 void mfp_classifier_free_device(mfp_classifier_dev &d) {
     void *ptrs[] = {d.fp_slots, d.prev_slots, d.entry, d.prior, d.proc_id, d.proc_mal, d.proc_attr,
-                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn6, d.seen, d.seen_count};
+                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn6};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = mfp_classifier_dev{};
 }

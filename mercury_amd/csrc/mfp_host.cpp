@@ -20,10 +20,19 @@
 #include "mfp_analysis.h"
 #include "mfp_internal.h"
 
-extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const uint8_t *arena, const mfp_pkt_desc *desc,
-                                   uint64_t n, mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
-                                   uint32_t *pending, void *deferred, unsigned long long *stats, uint32_t mode,
-                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof);
+extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
+                                   const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
+                                   mfp_analysis *out, uint32_t *pending, void *deferred, unsigned long long *stats,
+                                   uint32_t mode, uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof);
+extern "C" int mfp_launch_seen_export(const mfp_seen_tab *T, uint32_t u, mfp_sighting *out, hipStream_t stream);
+extern "C" int mfp_launch_seen_sequence(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
+                                        const mfp_record *rec, const uint8_t *fp_arena, uint32_t *pending,
+                                        const uint32_t *group_off, uint64_t *seq, hipStream_t stream);
+extern "C" int mfp_launch_analysis_resolve(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
+                                           const mfp_record *rec, const uint8_t *fp_arena, mfp_analysis *out,
+                                           uint32_t *pending, uint32_t mode, const uint8_t *seen_pos,
+                                           const uint32_t *group_off, const uint8_t *seen_seq, hipStream_t stream,
+                                           mfp_prof *prof);
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
@@ -225,6 +234,19 @@ struct Slot {
     uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings (bitmap)
     uint4 *d_deferred = nullptr; size_t cap_deferred = 0;    // packets for the wave-per-packet scorer (64 B each)
     mfp_analysis *d_an = nullptr; size_t cap_an = 0;
+    // the unknown-TLS sightings of the batch analysed in this slot (mfp_prevalence)
+    mfp_seen_tab seen;
+    mfp_sighting *d_sight = nullptr;                          // distinct list export
+    uint8_t *d_seen_bits = nullptr; size_t cap_seen_bits = 0; // decisions per distinct / per sighting
+    uint32_t *d_group_off = nullptr; size_t cap_group_off = 0;
+    uint64_t *d_seq = nullptr; size_t cap_seq = 0;
+    // the batch whose statuses wait for a decision (deferred, or pipelined until retire)
+    struct Pending {
+        bool live = false;
+        uint64_t n = 0;
+        const mfp_record *rec = nullptr; const char *fp = nullptr; mfp_analysis *out = nullptr;
+        hipStream_t stream = nullptr;
+    } pend;
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
     mfp_record *d_rec = nullptr; size_t cap_rec = 0;
@@ -242,7 +264,8 @@ struct Slot {
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
-        void *p[] = {d_used, d_bins, d_work, d_an_stats, d_pending, d_deferred, d_an, d_arena, d_desc, d_rec, d_fp, d_fp2};
+        void *p[] = {d_used, d_bins, d_work, d_an_stats, d_pending, d_deferred, d_an, d_arena, d_desc, d_rec, d_fp, d_fp2,
+                     seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         if (h_used) (void)hipHostFree(h_used);
         if (stream) (void)hipStreamDestroy(stream);
@@ -260,9 +283,11 @@ struct mfp_context_s {
     uint32_t bin_lds_mask = 0xe0;        // TLS server, SSH, DTLS: measured faster from LDS (r02c/d)
     uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
+    mfp_prevalence own_prev = nullptr;   // the context's fingerprint_prevalence LRU
+    mfp_prevalence prev = nullptr;       // the one its sightings are decided against (own or shared)
+    bool defer = false;                  // mfp_analysis_defer
     Slot slot[3];
     int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
-    hipEvent_t an_done = nullptr;        // last classifier launch (pipeline: stream order across slots)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
     std::mutex mu;
 };
@@ -297,8 +322,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     if (dm) c->bin_lds_mask = (uint32_t)strtoul(dm, nullptr, 0);
     const char *lm = getenv("MFP_AN_LANE_MAX_P");
     if (lm) c->an_lane_max_p = (uint32_t)strtoul(lm, nullptr, 0);
-    bool ok = hipSetDevice(device) == hipSuccess &&
-              hipEventCreateWithFlags(&c->an_done, hipEventDisableTiming) == hipSuccess;
+    bool ok = hipSetDevice(device) == hipSuccess;
     for (Slot &S : c->slot) ok = ok && S.init();
     if (!ok) {
         mfp_set_error("device init failed");
@@ -321,6 +345,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
                 return nullptr;
             }
             c->clf = clf;
+            c->own_prev = c->prev = mfp_prevalence_create(100000);   // analysis.h:433
         }
     }
     return c;
@@ -330,8 +355,8 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->clf) mfp_classifier_free(c->clf);
+    if (c->own_prev) mfp_prevalence_destroy(c->own_prev);
     for (Slot &S : c->slot) S.release();
-    if (c->an_done) (void)hipEventDestroy(c->an_done);
     delete c->prof;
     delete c;
 }
@@ -383,24 +408,138 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
     return 0;
 }
 
+// the slot's sighting table, sized for a batch of n packets (reset per batch)
+static int seen_reserve(Slot &S, size_t n, hipStream_t s) {
+    uint64_t want = 4096;
+    const uint64_t target = 2 * std::min<uint64_t>(n, (uint64_t)1 << 21);
+    while (want < target) want <<= 1;
+    if (S.seen.slots == nullptr || S.seen.mask + 1 < want) {
+        if (S.seen.slots) (void)hipFree(S.seen.slots);
+        if (S.seen.list) (void)hipFree(S.seen.list);
+        if (S.d_sight) (void)hipFree(S.d_sight);
+        S.seen.slots = nullptr; S.seen.list = nullptr; S.d_sight = nullptr;
+        if (hipMalloc(&S.seen.slots, want * sizeof(mfp_seen_slot)) != hipSuccess ||
+            hipMalloc(&S.seen.list, want / 2 * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&S.d_sight, want / 2 * sizeof(mfp_sighting)) != hipSuccess)
+            return -2;
+        S.seen.mask = (uint32_t)(want - 1);
+        S.seen.list_cap = (uint32_t)(want / 2);
+    }
+    if (!S.seen.counters && hipMalloc(&S.seen.counters, 4 * sizeof(unsigned int)) != hipSuccess) return -2;
+    if (hipMemsetAsync(S.seen.slots, 0xff, (S.seen.mask + 1ull) * sizeof(mfp_seen_slot), s) != hipSuccess ||
+        hipMemsetAsync(S.seen.counters, 0, 4 * sizeof(unsigned int), s) != hipSuccess)
+        return -2;
+    return 0;
+}
+
 static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
                           mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, hipStream_t s) {
     Slot &S = c->slot[slot];
     HIPCHK(hipSetDevice(c->device));
-    if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_deferred, S.cap_deferred, 4 * (n + 1))) {
+    if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_deferred, S.cap_deferred, 4 * (n + 1)) ||
+        seen_reserve(S, n, s)) {
         mfp_set_error("device allocation failed");
         return -2;
     }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
-    D->batch++;                                   // stream order across batches (fingerprint_prevalence)
     HIPCHK(hipMemsetAsync(S.d_an_stats, 0, 4 * sizeof(unsigned long long), s));
-    if (mfp_launch_analysis(D, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, S.d_pending,
+    if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, S.d_pending,
                             S.d_deferred, S.d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
     c->an_slot = slot;
+    S.pend.live = true;
+    S.pend.n = n; S.pend.rec = d_rec; S.pend.fp = d_fp_arena; S.pend.out = d_out; S.pend.stream = s;
     return 0;
+}
+
+// ---- deciding a batch's unknown-TLS sightings (mfp_prevalence) ----
+// the distinct list of the slot's pending batch; -3 when its table overflowed
+static long long slot_distinct(mfp_context c, Slot &S, std::vector<mfp_sighting> &d) {
+    hipStream_t s = S.pend.stream;
+    unsigned int cnt[4];
+    HIPCHK(hipMemcpyAsync(cnt, S.seen.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (cnt[1] || cnt[0] > S.seen.list_cap) return -3;
+    d.resize(cnt[0]);
+    if (cnt[0]) {
+        if (mfp_launch_seen_export(&S.seen, cnt[0], S.d_sight, s) != 0) { mfp_set_error("export launch failed"); return -3; }
+        HIPCHK(hipMemcpyAsync(d.data(), S.d_sight, cnt[0] * sizeof(mfp_sighting), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    (void)c;
+    return (long long)cnt[0];
+}
+
+// the slot's pending sightings in stream order (hashes), and the per-group
+// offsets the resolve kernel indexes them with (left in S.d_group_off)
+static long long slot_sequence(mfp_context c, Slot &S, std::vector<uint64_t> &seq) {
+    hipStream_t s = S.pend.stream;
+    const uint64_t groups = (S.pend.n + 63) / 64;
+    std::vector<uint64_t> bits(groups);
+    if (groups) HIPCHK(hipMemcpyAsync(bits.data(), S.d_pending, groups * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<uint32_t> off(groups + 1, 0);
+    for (uint64_t g = 0; g < groups; g++) off[g + 1] = off[g] + (uint32_t)__builtin_popcountll(bits[g]);
+    const uint64_t m = off[groups];
+    if (grow(S.d_group_off, S.cap_group_off, groups + 1) || grow(S.d_seq, S.cap_seq, m + 1)) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
+    if (groups) HIPCHK(hipMemcpyAsync(S.d_group_off, off.data(), (groups + 1) * 4, hipMemcpyHostToDevice, s));
+    if (mfp_launch_seen_sequence(mfp_classifier_device(c->clf), &S.seen, S.pend.n, S.pend.rec,
+                                 (const uint8_t *)S.pend.fp, S.d_pending, S.d_group_off, S.d_seq, s) != 0) {
+        mfp_set_error("sequence launch failed");
+        return -3;
+    }
+    seq.resize(m);
+    if (m) HIPCHK(hipMemcpyAsync(seq.data(), S.d_seq, m * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return (long long)m;
+}
+
+// apply decisions to the slot's pending batch: per distinct entry (pos order)
+// or per sighting (seq), on the device records
+static int slot_apply(mfp_context c, Slot &S, const uint8_t *bits, size_t nbits, bool per_sighting) {
+    hipStream_t s = S.pend.stream;
+    if (grow(S.d_seen_bits, S.cap_seen_bits, nbits + 1)) { mfp_set_error("device allocation failed"); return -2; }
+    if (nbits) HIPCHK(hipMemcpyAsync(S.d_seen_bits, bits, nbits, hipMemcpyHostToDevice, s));
+    if (mfp_launch_analysis_resolve(mfp_classifier_device(c->clf), &S.seen, S.pend.n, S.pend.rec,
+                                    (const uint8_t *)S.pend.fp, S.pend.out, S.d_pending, c->mode,
+                                    per_sighting ? nullptr : S.d_seen_bits, S.d_group_off,
+                                    per_sighting ? S.d_seen_bits : nullptr, s, c->prof) != 0) {
+        mfp_set_error("resolve launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -3;
+    }
+    S.pend.live = false;
+    return 0;
+}
+
+// decide the slot's pending batch against c->prev and apply: the distinct
+// form when it is exact, else the sighting sequence
+static int slot_resolve(mfp_context c, Slot &S) {
+    if (!S.pend.live) return 0;
+    std::vector<mfp_sighting> d;
+    const long long u = slot_distinct(c, S, d);
+    if (u == -2) return -2;
+    if (u >= 0) {
+        // the device's distinct list is in insertion order: positions are
+        // what k_seen_export stored in the slots (index = pos)
+        const int r = mfp_prevalence_resolve_distinct(c->prev, d.data(), d.size());
+        if (r == 0) {
+            std::vector<uint8_t> bits(d.size());
+            for (size_t i = 0; i < d.size(); i++) bits[i] = (uint8_t)d[i].first_seen;
+            return slot_apply(c, S, bits.data(), bits.size(), false);
+        }
+        if (r != -2) return r;
+    }
+    std::vector<uint64_t> seq;
+    const long long m = slot_sequence(c, S, seq);
+    if (m < 0) return (int)m;
+    std::vector<uint8_t> seen(seq.size());
+    if (mfp_prevalence_resolve_sequence(c->prev, seq.data(), seq.size(), seen.data()) != 0) return -1;
+    return slot_apply(c, S, seen.data(), seen.size(), true);
 }
 
 extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
@@ -410,6 +549,45 @@ extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t 
     std::lock_guard<std::mutex> lk(c->mu);
     return process_device_locked(c, c->slot[0], d_arena, d_desc, n, d_rec, d_fp_arena, fp_cap, d_fp_used,
                                  (hipStream_t)stream);
+}
+
+// decide the slot's pending batch against c->prev and patch the host copies
+// of its records (the pipeline retires chunks in order, after their D2H)
+static void host_patch(mfp_context c, mfp_analysis &a, const mfp_record &r, bool seen) {
+    a.flags &= (uint8_t)~MFP_AN_PENDING;
+    if (seen) {
+        a.status = 3;
+        a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.flags = MFP_AN_VALID;
+    }
+    if (c->mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
+}
+static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp_record *rec) {
+    if (!S.pend.live) return 0;
+    S.pend.live = false;
+    const size_t m = S.pend.n;
+    std::vector<mfp_sighting> d;
+    const long long u = slot_distinct(c, S, d);
+    if (u == -2) return -2;
+    if (u >= 0) {
+        const int r = mfp_prevalence_resolve_distinct(c->prev, d.data(), d.size());
+        if (r == 0) {
+            std::vector<uint8_t> randomized(m, 0);
+            for (const auto &x : d) if (!x.first_seen && x.first < m) randomized[x.first] = 1;
+            for (size_t i = 0; i < m; i++)
+                if (an[i].flags & MFP_AN_PENDING) host_patch(c, an[i], rec[i], !randomized[i]);
+            return 0;
+        }
+        if (r != -2) return r;
+    }
+    std::vector<uint64_t> seq;
+    const long long ms = slot_sequence(c, S, seq);
+    if (ms < 0) return (int)ms;
+    std::vector<uint8_t> seen(seq.size());
+    if (mfp_prevalence_resolve_sequence(c->prev, seq.data(), seq.size(), seen.data()) != 0) return -1;
+    size_t k = 0;
+    for (size_t i = 0; i < m && k < seen.size(); i++)
+        if (an[i].flags & MFP_AN_PENDING) host_patch(c, an[i], rec[i], seen[k++] != 0);
+    return 0;
 }
 
 // copy a host batch into slot `slot` (grown as needed) and launch its kernels
@@ -443,10 +621,11 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, fp_cap, (uint64_t *)S.d_used, S.stream);
     if (r) return r;
     if (analysis) {
-        if (slot != 0) HIPCHK(hipStreamWaitEvent(S.stream, c->an_done, 0));   // classifier stream order
         r = analyze_locked(c, slot, d_base, S.d_desc, n, S.d_rec, S.d_fp, S.d_an, S.stream);
         if (r) return r;
-        HIPCHK(hipEventRecord(c->an_done, S.stream));
+        // the synchronous host batch decides its unknown-TLS sightings now;
+        // pipeline slots when they retire (chunk order), on the host copies
+        if (slot == 0 && !c->defer) { r = slot_resolve(c, S); if (r) return r; }
     }
     // strings to a dense arena in packet order (d_fp2, d_used[2] bytes), records re-pointed;
     // the bin lists in d_work are dead by now and hold the scan scratch
@@ -455,6 +634,7 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
         mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
+    S.pend.fp = S.d_fp2;   // the records now point into the dense arena
     return 0;
 }
 
@@ -520,6 +700,10 @@ static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t ar
     auto retire = [&](int s) -> int {
         Slot &S = c->slot[1 + s];
         HIPCHK(hipStreamSynchronize(S.stream));
+        if (analysis) {   // (the pipeline always decides its chunks itself, in order)
+            const int r = slot_resolve_host(c, S, analysis + inf[s].lo, rec + inf[s].lo);
+            if (r) return r;
+        }
         const unsigned long long used = S.h_used[2];   // dense bytes
         if (S.h_used[1] || fp_base + used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
         if (used) HIPCHK(hipMemcpyAsync(fp_arena + fp_base, S.d_fp2, used, hipMemcpyDeviceToHost, S.stream));
@@ -562,7 +746,101 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     if (!c) { mfp_set_error("null context"); return -1; }
     if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    return analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, (hipStream_t)stream);
+    const int r = analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, (hipStream_t)stream);
+    if (r || c->defer) return r;
+    // the batch's unknown-TLS sightings are decided now, in stream order: the
+    // call waits for its kernels (a few microseconds of host time per batch)
+    return slot_resolve(c, c->slot[0]);
+}
+
+// ---- the prevalence LRU: sharing across the shards of one stream ----
+extern "C" MFP_EXPORT mfp_prevalence mfp_analysis_prevalence(mfp_context c) { return c ? c->prev : nullptr; }
+
+extern "C" MFP_EXPORT int mfp_analysis_set_prevalence(mfp_context c, mfp_prevalence p) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->prev = p ? p : c->own_prev;
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_analysis_defer(mfp_context c, int on) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->defer = on != 0;
+    return 0;
+}
+
+static Slot *deferred_slot(mfp_context c) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return nullptr; }
+    Slot &S = c->slot[c->an_slot];
+    if (!S.pend.live) { mfp_set_error("no analysed batch waits for its prevalence decisions"); return nullptr; }
+    return &S;
+}
+
+extern "C" MFP_EXPORT long long mfp_analysis_distinct(mfp_context c, mfp_sighting *out, size_t cap) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot *S = deferred_slot(c);
+    if (!S) return -1;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<mfp_sighting> d;
+    const long long u = slot_distinct(c, *S, d);
+    if (u < 0) return u;
+    if (out) memcpy(out, d.data(), std::min<size_t>(cap, d.size()) * sizeof(mfp_sighting));
+    return u;
+}
+
+extern "C" MFP_EXPORT long long mfp_analysis_sequence(mfp_context c, uint64_t *hash, size_t cap) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot *S = deferred_slot(c);
+    if (!S) return -1;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> seq;
+    const long long m = slot_sequence(c, *S, seq);
+    if (m < 0) return m;
+    if (hash) memcpy(hash, seq.data(), std::min<size_t>(cap, seq.size()) * 8);
+    return m;
+}
+
+extern "C" MFP_EXPORT int mfp_analysis_resolve(mfp_context c, const mfp_sighting *d, size_t u) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot *S = deferred_slot(c);
+    if (!S) return -1;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint8_t> bits(u);
+    for (size_t i = 0; i < u; i++) bits[i] = (uint8_t)d[i].first_seen;
+    const int r = slot_apply(c, *S, bits.data(), u, false);
+    if (r == 0) HIPCHK(hipStreamSynchronize(S->pend.stream));
+    return r;
+}
+
+extern "C" MFP_EXPORT long long mfp_analysis_last(mfp_context c, mfp_analysis *out, size_t cap) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot &S = c->slot[c->an_slot];
+    if (!S.pend.out) { mfp_set_error("no analysed batch"); return -1; }
+    HIPCHK(hipSetDevice(c->device));
+    const size_t m = std::min<size_t>(cap, S.pend.n);
+    if (m) HIPCHK(hipMemcpyAsync(out, S.pend.out, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.pend.stream));
+    HIPCHK(hipStreamSynchronize(S.pend.stream));
+    return (long long)S.pend.n;
+}
+
+extern "C" MFP_EXPORT int mfp_analysis_resolve_sequence(mfp_context c, const uint8_t *seen, size_t m) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot *S = deferred_slot(c);
+    if (!S) return -1;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> seq;
+    const long long ms = slot_sequence(c, *S, seq);   // leaves the group offsets on the device
+    if (ms < 0) return (int)ms;
+    if ((size_t)ms != m) { mfp_set_error("sequence length %zu, batch has %lld sightings", m, ms); return -1; }
+    const int r = slot_apply(c, *S, seen, m, true);
+    if (r == 0) HIPCHK(hipStreamSynchronize(S->pend.stream));
+    return r;
 }
 
 extern "C" MFP_EXPORT const char *mfp_process_name(mfp_context c, uint32_t id) {
@@ -578,9 +856,7 @@ extern "C" MFP_EXPORT int mfp_analysis_stats(mfp_context c, uint64_t out[4]) {
     std::lock_guard<std::mutex> lk(c->mu);
     unsigned long long h[4];
     HIPCHK(hipMemcpy(h, c->slot[c->an_slot].d_an_stats, sizeof h, hipMemcpyDeviceToHost));
-    unsigned long long seen = 0;
-    HIPCHK(hipMemcpy(&seen, mfp_classifier_device(c->clf)->seen_count, sizeof seen, hipMemcpyDeviceToHost));
-    out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = seen;
+    out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = mfp_prevalence_size(c->prev);
     return 0;
 }
 

@@ -1,0 +1,198 @@
+// mfp_prevalence.cpp -- the adaptive part of the classifier's
+// fingerprint_prevalence (analysis.h:362-421): an LRU of at most `capacity`
+// unknown TLS fingerprints (the reference: 100000, analysis.h:433), updated on
+// every sighting, in stream order (perform_analysis_common analysis.h:1043-
+// 1083):
+//   in the set      -> status unlabeled, moved to the front;
+//   not in the set  -> status randomized, inserted at the front, the least
+//                      recently used one evicted when the set is full.
+// Identity is the fingerprint string's 64-bit hash (mfpc::str_hash).
+//
+// The device finds a batch's sightings; this host object decides them, in
+// order, for one context or for the shards of one stream (shard order), so the
+// decision is the single-thread reference's.  Two ways in:
+//   * distinct: the batch's distinct fingerprints with their first and last
+//     sighting; exact whenever no eviction can happen inside the batch (the set
+//     plus the batch's new fingerprints fit the capacity): the first sighting
+//     of a fingerprint not in the set is randomized, everything else unlabeled,
+//     and the recency order afterwards is the order of the last sightings;
+//   * sequence: every sighting in stream order, simulated one by one (used
+//     when the distinct form cannot be exact).
+#include <algorithm>
+#include <cstdint>
+#include <unordered_set>
+#include <cstring>
+#include <vector>
+
+#include "../../include/mfp.h"
+#include "mfp_internal.h"
+
+namespace {
+
+// LRU over 64-bit keys: open-addressing index + intrusive doubly linked list
+// in arrays (node 0 is the list head sentinel)
+struct Lru {
+    uint32_t cap;
+    std::vector<uint64_t> key;
+    std::vector<uint32_t> prev, next;
+    std::vector<uint32_t> free_nodes;
+    std::vector<uint32_t> slot;     // index: node id + 1, 0 empty, ~0u tombstone
+    uint64_t mask;
+    uint32_t size = 0, used_slots = 0;
+
+    explicit Lru(uint32_t c) : cap(c ? c : 1) {
+        key.assign((size_t)cap + 1, 0);
+        prev.assign((size_t)cap + 1, 0);
+        next.assign((size_t)cap + 1, 0);
+        for (uint32_t i = cap; i >= 1; i--) free_nodes.push_back(i);
+        uint64_t s = 16;
+        while (s < 2ull * cap + 16) s <<= 1;
+        slot.assign(s, 0);
+        mask = s - 1;
+    }
+    static uint64_t mix(uint64_t x) {
+        x ^= x >> 31; x *= 0x7fb5d329728ea185ull; x ^= x >> 27; x *= 0x81dadef4bc2dd44dull; x ^= x >> 33;
+        return x;
+    }
+    // index slot of k: its node, or (found = false) the first reusable slot
+    uint64_t find(uint64_t k, bool &found) const {
+        uint64_t i = mix(k) & mask, tomb = ~0ull;
+        while (true) {
+            const uint32_t s = slot[i];
+            if (s == 0) { found = false; return tomb != ~0ull ? tomb : i; }
+            if (s == ~0u) { if (tomb == ~0ull) tomb = i; }
+            else if (key[s] == k) { found = true; return i; }
+            i = (i + 1) & mask;
+        }
+    }
+    void unlink(uint32_t n) { next[prev[n]] = next[n]; prev[next[n]] = prev[n]; }
+    void push_front(uint32_t n) { next[n] = next[0]; prev[n] = 0; prev[next[0]] = n; next[0] = n; }
+    void rehash() {   // drop tombstones
+        std::vector<uint32_t> old;
+        old.swap(slot);
+        slot.assign(old.size(), 0);
+        used_slots = 0;
+        for (uint32_t s : old)
+            if (s != 0 && s != ~0u) {
+                uint64_t i = mix(key[s]) & mask;
+                while (slot[i]) i = (i + 1) & mask;
+                slot[i] = s;
+                used_slots++;
+            }
+    }
+    bool contains(uint64_t k) const { bool f; find(k, f); return f; }
+    // fingerprint_prevalence::update (analysis.h:386-408); returns whether k
+    // was in the set (the caller's contains() before the update)
+    bool access(uint64_t k) {
+        bool found;
+        const uint64_t i = find(k, found);
+        if (found) {
+            const uint32_t n = slot[i];
+            unlink(n);
+            push_front(n);
+            return true;
+        }
+        if (size == cap) {                         // evict the least recently used
+            const uint32_t t = prev[0];
+            unlink(t);
+            bool f2;
+            const uint64_t j = find(key[t], f2);
+            slot[j] = ~0u;
+            free_nodes.push_back(t);
+            size--;
+        }
+        const uint32_t n = free_nodes.back();
+        free_nodes.pop_back();
+        key[n] = k;
+        push_front(n);
+        bool f3;
+        const uint64_t j = find(k, f3);              // the slot may have moved past a new tombstone
+        if (slot[j] == 0) used_slots++;
+        slot[j] = n;
+        size++;
+        if (used_slots > (mask + 1) / 2) rehash();
+        return false;
+    }
+    // the keys from least to most recently used
+    void export_keys(std::vector<uint64_t> &out) const {
+        out.clear();
+        for (uint32_t n = prev[0]; n != 0; n = prev[n]) out.push_back(key[n]);
+    }
+};
+
+}  // namespace
+
+struct mfp_prevalence_s {
+    Lru lru;
+    explicit mfp_prevalence_s(uint32_t c) : lru(c) {}
+};
+
+extern "C" {
+
+MFP_EXPORT mfp_prevalence mfp_prevalence_create(uint32_t capacity) {
+    if (capacity == 0) { mfp_set_error("prevalence capacity must be > 0"); return nullptr; }
+    return new mfp_prevalence_s(capacity);
+}
+
+MFP_EXPORT void mfp_prevalence_destroy(mfp_prevalence p) { delete p; }
+
+MFP_EXPORT uint64_t mfp_prevalence_size(mfp_prevalence p) { return p ? p->lru.size : 0; }
+
+MFP_EXPORT int mfp_prevalence_contains(mfp_prevalence p, uint64_t hash) {
+    return p && p->lru.contains(hash) ? 1 : 0;
+}
+
+MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t cap) {
+    if (!p) return -1;
+    std::vector<uint64_t> k;
+    p->lru.export_keys(k);
+    const size_t m = k.size() < cap ? k.size() : cap;
+    if (out && m) memcpy(out, k.data(), m * sizeof(uint64_t));
+    return (long long)k.size();
+}
+
+MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen) {
+    if (!p || (m && (!hash || !seen))) { mfp_set_error("mfp_prevalence_resolve_sequence: bad arguments"); return -1; }
+    for (size_t j = 0; j < m; j++) seen[j] = p->lru.access(hash[j]) ? 1 : 0;
+    return 0;
+}
+
+// Whether the distinct form is exact for these entries: no eviction can
+// happen while they are applied (the set plus the fingerprints new to it fit).
+// Entries may repeat a hash (the same fingerprint in several shards).
+MFP_EXPORT int mfp_prevalence_distinct_exact(mfp_prevalence p, const mfp_sighting *d, size_t u) {
+    if (!p || (u && !d)) return -1;
+    std::unordered_set<uint64_t> fresh;
+    for (size_t i = 0; i < u; i++)
+        if (!p->lru.contains(d[i].hash)) fresh.insert(d[i].hash);
+    return (uint64_t)p->lru.size + fresh.size() <= p->lru.cap ? 1 : 0;
+}
+
+// Decide the first sighting of every entry and apply the entries to the set.
+// `first`/`last` are positions in one stream order (for shards: the shard's
+// base plus the batch index).  first_seen = 1: at that first sighting the
+// fingerprint was in the set (status unlabeled); 0: randomized.  Every later
+// sighting of an entry is unlabeled.  Fails with -2 (nothing applied) when
+// the batch could evict: resolve the sighting sequence then.
+MFP_EXPORT int mfp_prevalence_resolve_distinct(mfp_prevalence p, mfp_sighting *d, size_t u) {
+    if (!p || (u && !d)) { mfp_set_error("mfp_prevalence_resolve_distinct: bad arguments"); return -1; }
+    if (mfp_prevalence_distinct_exact(p, d, u) != 1) {
+        mfp_set_error("mfp_prevalence_resolve_distinct: the batch can evict (set %u + new fingerprints > capacity %u); "
+                      "resolve the sighting sequence instead", p->lru.size, p->lru.cap);
+        return -2;
+    }
+    std::vector<size_t> ord(u);
+    for (size_t i = 0; i < u; i++) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return d[a].first < d[b].first; });
+    std::unordered_set<uint64_t> earlier;   // seen by an earlier entry of these (no eviction: stays in the set)
+    for (size_t i : ord) {
+        d[i].first_seen = (p->lru.contains(d[i].hash) || earlier.count(d[i].hash)) ? 1 : 0;
+        earlier.insert(d[i].hash);
+    }
+    // recency afterwards: the order of the last sightings
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return d[a].last < d[b].last; });
+    for (size_t i : ord) p->lru.access(d[i].hash);
+    return 0;
+}
+
+}  // extern "C"

@@ -6,13 +6,20 @@ classifies packets [lo_r, hi_r) on its own GPU and the shards concatenate in
 rank order (packet order is preserved).  torch.distributed is used only for
 control: the barrier and the max-over-ranks time of bench.py, and -- for
 host pipelines that want one output stream -- gathering the per-shard records
-to one rank.  The one cross-packet dependency, the classifier's unknown-TLS
-prevalence set, is per context (per GPU); the reference itself is not
-deterministic across threads there (analysis.h:390-394).
+to one rank.
+
+The one cross-packet dependency is the classifier's unknown-TLS prevalence
+LRU (fingerprint_prevalence, analysis.h:362-421): a sighting's status depends
+on every earlier sighting of the stream.  ordered_prevalence_merge is the
+host-side ordered merge of SURVEY 8(e): every rank analyses its shard with the
+decision deferred, the ranks exchange their batch's distinct unknown-TLS
+fingerprints (a few hundred entries, gloo all_gather), and every rank applies
+the same decisions, in shard order, to an identical copy of the LRU -- so the
+sharded output equals one context over the concatenated stream.
 """
 import numpy as np
 
-from .api import DESC_DTYPE, RECORD_DTYPE
+from .api import DESC_DTYPE, RECORD_DTYPE, SIGHTING_DTYPE
 
 
 def shard_bounds(n, rank, world):
@@ -74,3 +81,40 @@ def max_over_ranks(value, device=None, group=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
+    """Decide the unknown-TLS sightings of this rank's last analysed batch
+    (ctx deferred, see Context.defer) in stream order across the ranks of
+    `group`: rank order is stream order, `shard_base` is the stream position of
+    this rank's first packet.  `prev` is this rank's copy of the LRU (every
+    rank applies the same decisions to its own copy).  Returns the number of
+    distinct fingerprints exchanged (or sightings, on the sequence path)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dl = ctx.analysis_distinct()
+    mine = (None if dl is None else dl.tobytes(), int(shard_base))
+    allp = [None] * world
+    dist.all_gather_object(allp, mine, group=group)
+    if all(p[0] is not None for p in allp):
+        lists = []
+        for b, base in allp:
+            x = np.frombuffer(b, SIGHTING_DTYPE).copy()
+            x["first"] += np.uint64(base)
+            x["last"] += np.uint64(base)
+            lists.append(x)
+        allv = np.concatenate(lists) if lists else np.zeros(0, SIGHTING_DTYPE)
+        if prev.resolve_distinct(allv):
+            k = sum(len(x) for x in lists[:rank])
+            ctx.analysis_resolve(allv[k:k + len(lists[rank])])
+            return len(allv)
+    # the sequence form: every rank's sightings in shard order
+    seq = ctx.analysis_sequence()
+    alls = [None] * world
+    dist.all_gather_object(alls, seq.tobytes(), group=group)
+    seqs = [np.frombuffer(b, np.uint64) for b in alls]
+    seen = prev.resolve_sequence(np.concatenate(seqs) if seqs else np.zeros(0, np.uint64))
+    k = sum(len(x) for x in seqs[:rank])
+    ctx.analysis_resolve_sequence(seen[k:k + len(seqs[rank])])
+    return len(seen)

@@ -469,3 +469,49 @@ def fuzz(pkts, n, seed):
                 b.insert(j, int(rng.integers(0, 256)))
         out.append((lt, bytes(b)))
     return out
+
+
+# ---------------------------------------------------------------------------
+# unknown-TLS prevalence stream (fingerprint_prevalence LRU, analysis.h:362-421)
+# ---------------------------------------------------------------------------
+def lru_keys(capacity=100000, seed=0x5EED1234):
+    """The key sequence of a stream that crosses the reference's LRU capacity:
+    1.2 x capacity distinct fingerprints once each (the oldest fifth is
+    evicted), the first tenth again (evicted: randomized again, evicting more),
+    a tenth near the recent end (still in the set: unlabeled), then 0.3 x
+    capacity draws around the eviction boundary, where each status depends on
+    the exact recency order."""
+    rng = np.random.default_rng(seed)
+    c = capacity
+    first = np.arange(int(1.2 * c))
+    again_old = np.arange(int(0.1 * c))
+    again_new = np.arange(int(1.0 * c), int(1.1 * c))
+    mix = rng.integers(0, int(1.3 * c), int(0.3 * c))
+    return np.concatenate([first, again_old, again_new, mix]).astype(np.int64)
+
+
+def lru_batch(keys, seed=0x5EED1235):
+    """One TLS ClientHello per key whose fingerprint is unique to the key (two
+    cipher suites encode it; no other field varies), Ethernet/IPv4/TCP 443."""
+    rng = np.random.default_rng(seed)
+    base = bytearray(frame(tcp(client_hello(rng, "openssl", "lru.example.com"), sport=50000, dport=443), 6))
+    # the cipher list: the openssl profile's first two suites are patched
+    cs = struct.pack(">HH", OPENSSL_CIPHERS[0], OPENSSL_CIPHERS[1])
+    at = bytes(base).index(cs)
+    n = len(keys)
+    L = len(base)
+    arena = np.zeros(n * L + 64, np.uint8)
+    arena[:n * L] = np.tile(np.frombuffer(bytes(base), np.uint8), n)
+    k = np.asarray(keys, np.int64)
+    c1 = 0x3000 + ((k >> 12) & 0xfff)
+    c2 = 0x4000 + (k & 0xfff)
+    offs = np.arange(n, dtype=np.int64) * L + at
+    arena[offs] = (c1 >> 8) & 0xff
+    arena[offs + 1] = c1 & 0xff
+    arena[offs + 2] = (c2 >> 8) & 0xff
+    arena[offs + 3] = c2 & 0xff
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    desc["offset"] = np.arange(n, dtype=np.uint64) * L
+    desc["caplen"] = L
+    desc["linktype"] = 1
+    return arena, desc

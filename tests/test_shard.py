@@ -95,3 +95,79 @@ def test_gloo_world2_gather_and_max():
     assert all(ok for ok, _, _ in res)
     assert all(t == 1.5 for _, t, _ in res)          # max over ranks
     assert max(n for _, _, n in res) == 2000
+
+
+class _ShardCtx:
+    """Stands in for a deferred analysis context (CPU): one shard's unknown-TLS
+    sightings as keys; records the decisions it is given."""
+
+    def __init__(self, keys):
+        from tests.test_prevalence import distinct_of, key_hash
+        self.keys = keys
+        self.dl = distinct_of(keys)
+        self.seq = key_hash(keys)
+        self.seen = None
+
+    def analysis_distinct(self):
+        return self.dl.copy()
+
+    def analysis_sequence(self):
+        return self.seq
+
+    def analysis_resolve(self, d):
+        self.seen = np.ones(len(self.keys), np.uint8)
+        for e in d:
+            self.seen[int(e["first"]) - self.base] = e["first_seen"]
+
+    def analysis_resolve_sequence(self, seen):
+        self.seen = np.asarray(seen, np.uint8)
+
+
+def _merge_worker(rank, world, port, q, cap, span, seed):
+    import torch.distributed as dist
+    import mercury_amd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(seed)
+    prev = mercury_amd.Prevalence(cap)
+    out = []
+    for step in range(6):
+        shards = [rng.integers(0, span, 50).tolist() for _ in range(world)]
+        c = _ShardCtx(shards[rank])
+        c.base = step * 50 * world + rank * 50
+        shard.ordered_prevalence_merge(c, prev, c.base)
+        out.append(c.seen.tolist())
+    q.put((rank, out, prev.keys().tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cap,span", [(400, 150), (60, 150)])
+def test_ordered_prevalence_merge_world2(cap, span):
+    """Two gloo ranks, each with its own shard of one stream: the ordered merge
+    gives every sighting the status of one LRU over the concatenated stream
+    (distinct form when exact, else the sequence form: cap 60 < the distinct
+    fingerprints in flight), and both ranks end with the same LRU."""
+    import multiprocessing as mp
+    from tests.test_prevalence import key_hash, lru_model
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ps = [ctxm.Process(target=_merge_worker, args=(r, 2, port, q, cap, span, 11)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (o, k)) for r, o, k in [q.get(timeout=120) for _ in ps])
+    for p in ps:
+        p.join(timeout=60)
+    rng = np.random.default_rng(11)
+    stream = []
+    for step in range(6):
+        shards = [rng.integers(0, span, 50).tolist() for _ in range(2)]
+        stream += shards[0] + shards[1]
+    want, order = lru_model(stream, cap)
+    got = []
+    for step in range(6):
+        got += res[0][0][step] + res[1][0][step]
+    assert np.array_equal(np.array(got, np.uint8), want)
+    assert res[0][1] == res[1][1] == key_hash(order).tolist()
