@@ -82,9 +82,20 @@ static std::string trim(const std::string &s) {
 // protocols of this path; the reference's traffic_selector turns the map
 // into matchers (proto_identify.h:620-895)
 static bool parse_select(const std::string &list, uint32_t &sel) {
-    std::string s = list.empty() ? "all" : list;
+    // "all" (and the empty selection, which the reference reads as "all",
+    // global_config.h:248) selects ~45 protocols this path does not parse
+    // (DNS, QUIC, SMTP, ...) and the GRE/VXLAN/Geneve decapsulations: the
+    // reference would write records the device cannot, so it is refused
+    // rather than silently diverging
+    if (strip(list).empty() || strip(list) == "all") {
+        mfp_set_error("protocol selection \"%s\" includes protocols outside the device path; select from: tls, "
+                      "tls.client_hello, tls.server_hello, tls.server_certificate, ssh, ssh.client, ssh.server, "
+                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, none", list.empty() ? "" : list.c_str());
+        return false;
+    }
+    const std::string &s = list;
     std::map<std::string, uint32_t> known = {
-        {"all", SEL_ALL}, {"none", 0},
+        {"none", 0},
         {"tls", SEL_TLS_CH | SEL_TLS_SH | SEL_TLS_CERT}, {"tls.client_hello", SEL_TLS_CH},
         {"tls.server_hello", SEL_TLS_SH}, {"tls.server_certificate", SEL_TLS_CERT},
         {"ssh", SEL_SSH_CLIENT | SEL_SSH_SERVER}, {"ssh.client", SEL_SSH_CLIENT}, {"ssh.server", SEL_SSH_SERVER},

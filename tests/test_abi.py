@@ -51,9 +51,6 @@ def test_only_declared_symbols_are_exported():
 
 
 @pytest.mark.parametrize("cfg,sel,fmt", [
-    (None, oracle.SEL_ALL, 0),
-    ("", oracle.SEL_ALL, 0),
-    ("all", oracle.SEL_ALL, 0),
     ("tls", oracle.SEL["tls"], 0),
     ("tls,dtls,ssh,http,tcp,tcp.syn_ack", oracle.SEL_ALL, 0),
     ("select=tls,http;format=tls/1", oracle.SEL["tls"] | oracle.SEL["http"], 1),
@@ -66,7 +63,8 @@ def test_parse_filter(cfg, sel, fmt):
     assert mercury_amd.parse_filter(cfg) == (sel, fmt)
 
 
-@pytest.mark.parametrize("cfg", ["select=tls", "quic", "tls,dns", "select=tls;format=tls/9", "select=tls;reassembly"])
+@pytest.mark.parametrize("cfg", ["select=tls", "quic", "tls,dns", "select=tls;format=tls/9", "select=tls;reassembly",
+                                 None, "", "all", " all ", "select=all;format=tls/1", "tls,all"])
 def test_parse_filter_rejects(cfg):
     with pytest.raises(mercury_amd.MercuryAmdError):
         mercury_amd.parse_filter(cfg)

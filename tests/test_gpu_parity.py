@@ -1,14 +1,20 @@
 """Parity of the HIP path (libmercury_amd.so, called through the C-ABI) with
-the reference.
+the REFERENCE: every expected value below is the reference's own output
+(libmerc 2.18.0 compiled from /root/reference by oracle/Makefile.ref, run by
+tests/golden/make_golden*.py; committed under tests/golden/):
 
-* golden: packets from the reference's own test pcaps, compared with the
-  reference's output committed under tests/golden/ (fmt 0/1/2);
-* oracle: seeded synthetic and fuzzed batches, compared with the C oracle;
-* large: BASELINE-sized device-resident batches checked through
-  size-independent properties (every fingerprint string of a sample equals the
-  oracle's; arena accounting; record/type consistency).
+* golden: packets from the reference's own test pcaps (fmt 0/1/2) and its
+  top_100_fingerprints.fp file;
+* cases (tests/cases.py, tests/golden/cases/): 40 000 fuzzed packets per
+  format, truncation/oversize edge cases, synthetic mixed and ClientHello
+  batches, the reference's own fuzzing seeds, the analysis_context path, and
+  every assignment of bin kernels;
+* large: a BASELINE-sized device-resident batch (config 2, 10 M TLS
+  ClientHellos): a seeded sample against the reference, plus size-independent
+  properties (arena accounting, replica consistency).
 Bar: byte-identical fingerprint strings, identical fp types, emit and
-truncation flags.
+truncation flags.  (The C oracle, oracle/mfp_oracle.c, is a debugging twin,
+pinned to the same reference outputs by tests/test_oracle.py.)
 """
 import gzip
 import os
@@ -17,8 +23,7 @@ import numpy as np
 import pytest
 
 import mercury_amd
-from oracle import oracle
-from tests import synth
+from tests import cases, synth
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 CONTRACT = "tls,dtls,ssh,http,tcp,tcp.syn_ack"
@@ -99,42 +104,50 @@ def test_golden_top100_file():
     assert tls == want
 
 
-def _compare(arena, desc, fmt, mode=0):
-    cfg = oracle.config(tls_format=fmt, mode=mode)
-    ft, fl, flags, want = oracle.process_batch(arena, desc, cfg)
-    ctx = mercury_amd.Context(cfg_string(fmt), device=0, mode=mode)
+def _vs_reference(name, fmt, mode="fp"):
+    """The HIP path on case `name` against the reference's output."""
+    pk = cases.CASES[name][0]()
+    arena, desc = cases.batch(pk)
+    want = cases.load_golden(name, fmt, mode)
+    ctx = mercury_amd.Context(cfg_string(fmt), device=0, mode=0 if mode == "fp" else 1)
     try:
         rec, fp = ctx.process_host(arena, desc)
     finally:
         ctx.close()
     got = mercury_amd.fingerprints(rec, fp)
-    bad = [i for i in range(len(desc))
-           if got[i] != want[i] or int(rec["fp_type"][i]) != int(ft[i])
-           or int(rec["flags"][i] & 3) != int(flags[i] & 3) and (flags[i] & 1)]
+    bad = []
+    for i, (emit, t, trunc, s) in enumerate(want):
+        if mode == "fp":
+            g_emit = int(rec["flags"][i] & 1)
+            g = (g_emit, int(rec["fp_type"][i]), int((rec["flags"][i] >> 1) & 1) & g_emit, got[i])
+            if g != (emit, t, trunc, s):
+                bad.append(i)
+        elif (int(rec["fp_type"][i]), got[i]) != (t, s):
+            bad.append(i)
     return bad, rec
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", [0, 1, 2])
 @pytest.mark.parametrize("workload", ["mixed", "tls_ch"])
-def test_synthetic_vs_oracle(fmt, workload):
-    arena, desc = synth.batch(30000, seed=0x5EED0003 + fmt, workload=workload, n_templates=3000)
-    bad, rec = _compare(arena, desc, fmt)
+def test_synthetic_vs_reference(fmt, workload):
+    bad, rec = _vs_reference(f"synth_{workload}{fmt}", fmt)
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
     assert (rec["fp_type"] > 0).sum() > 10000
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", [0, 1, 2])
-def test_fuzzed_vs_oracle(fmt):
-    arena, desc, _ = load_golden()
-    pk = [(int(d["linktype"]), arena[int(d["offset"]):int(d["offset"]) + int(d["caplen"])].tobytes()) for d in desc]
-    a2, d2 = synth.batch(3000, seed=99, workload="mixed", n_templates=1000)
-    pk += [(1, a2[int(d["offset"]):int(d["offset"]) + int(d["caplen"])].tobytes()) for d in d2]
-    from tests import pcaplib
-    fz = synth.fuzz(pk, 40000, seed=1000 + fmt)
-    fa, fd = pcaplib.make_batch(fz)
-    bad, _ = _compare(fa, fd, fmt)
+def test_fuzzed_vs_reference(fmt):
+    bad, _ = _vs_reference(f"fuzz{fmt}", fmt)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_reference_fuzz_corpus(fmt):
+    """The reference's own fuzzing seeds (test/fuzz/*/corpus) in frames, and all their prefixes."""
+    bad, _ = _vs_reference("corpus", fmt)
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
 
 
@@ -142,54 +155,49 @@ def test_fuzzed_vs_oracle(fmt):
 @pytest.mark.parametrize("seg_mask,lds_mask", [
     ("0x0", "0x0"), ("0xa", "0x0"), ("0xff", "0x0"), ("0xa", "0xff"), ("0x0", "0xff"), ("0xff", "0xff"),
     ("0xa", "0x5a")])
-def test_bin_kernel_choices_vs_oracle(seg_mask, lds_mask, monkeypatch):
+def test_bin_kernel_choices_vs_reference(seg_mask, lds_mask, monkeypatch):
     """Every bin kernel (HBM lane walker, lane walk + wave expansion, and the
     LDS-staged walker in both emission modes, each carrying only its bin's
     parser family) takes any packet (what it cannot fingerprint goes to the
     fallback lane): one batch of synthetic + fuzzed packets under each
-    assignment of kernels to bins equals the oracle."""
-    from tests import pcaplib
+    assignment of kernels to bins equals the reference."""
     monkeypatch.setenv("MFP_BIN_SEG_MASK", seg_mask)
     monkeypatch.setenv("MFP_BIN_LDS_MASK", lds_mask)
-    a2, d2 = synth.batch(6000, seed=0x5EED0042, workload="mixed", n_templates=1500)
-    pk = [(1, a2[int(d["offset"]):int(d["offset"]) + int(d["caplen"])].tobytes()) for d in d2]
-    pk += synth.fuzz(pk[:2000], 10000, seed=77)
-    fa, fd = pcaplib.make_batch(pk)
     for fmt in (0, 2):
-        bad, rec = _compare(fa, fd, fmt)
+        bad, rec = _vs_reference("binmix", fmt)
         assert not bad, f"fmt {fmt}: {len(bad)} mismatches, first {bad[:5]}"
     assert (rec["fp_type"] == 3).sum() > 100 and (rec["fp_type"] == 4).sum() > 100
 
 
 @pytest.mark.gpu
-def test_analysis_mode_vs_oracle():
+def test_lane_strategy_vs_reference(monkeypatch):
+    """MFP_STRATEGY=lane: one lane walker over the whole batch (no binning)."""
+    monkeypatch.setenv("MFP_STRATEGY", "lane")
+    bad, _ = _vs_reference("binmix", 0)
+    assert not bad
+
+
+@pytest.mark.gpu
+def test_analysis_mode_vs_reference():
     """get_analysis_context semantics: no TCP SYN fingerprints (pkt_proc.cc:1624-1651)."""
-    arena, desc = synth.batch(20000, seed=5, workload="mixed", n_templates=2000)
-    bad, rec = _compare(arena, desc, 1, mode=1)
+    bad, rec = _vs_reference("analysis_mode", 1, "an")
     assert not bad
     assert int((rec["fp_type"] == 7).sum()) == 0
 
 
 @pytest.mark.gpu
-def test_edge_cases():
-    """empty packets, zero-length batch members, ragged sizes, max-size frames."""
-    from tests import pcaplib
-    pk = [(1, b""), (1, b"\x00"), (101, b"\x45"), (1, bytes(14)), (1, bytes(65535))]
-    a, d = synth.batch(200, seed=3, workload="mixed", n_templates=100)
-    for x in d[:50]:
-        b = a[int(x["offset"]):int(x["offset"]) + int(x["caplen"])].tobytes()
-        pk.append((1, b + bytes(70000 - len(b))))   # giant trailing data
-        for cut in (0, 13, 14, 33, 34, 53, 54, len(b) // 2, len(b) - 1):
-            pk.append((1, b[:cut]))
-    fa, fd = pcaplib.make_batch(pk)
-    bad, _ = _compare(fa, fd, 0)
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_edge_cases(fmt):
+    """empty packets, 1-byte frames, truncation at every header boundary,
+    65 535-byte frames and giant trailing data (the fallback lane)."""
+    bad, _ = _vs_reference("edge", fmt)
     assert not bad
 
 
 @pytest.mark.gpu
 def test_large_device_batch_properties():
     """BASELINE-size batch (config 2 shape, 10 M TLS ClientHellos) device-resident;
-    a seeded 20 000-packet sample must equal the oracle byte for byte and the
+    a seeded 20 000-packet sample must equal the reference byte for byte and the
     arena accounting must be exact."""
     import torch
     n = 10_000_000
@@ -216,17 +224,18 @@ def test_large_device_batch_properties():
     # every string lies inside the reserved part of the arena
     assert int((rec["fp_offset"] + rec["fp_len"]).max()) <= reserved
     used = reserved
+    # a seeded sample of packets whose unique original is in the reference's
+    # golden head (the first 20 000 unique packets)
     rng = np.random.default_rng(1)
-    sample = rng.choice(n, 20000, replace=False)
+    sample = rng.choice(reps, 20000) * len(ud) + rng.integers(0, 20000, 20000)
     fp_host = d_fp[:used].cpu().numpy().tobytes()
     got = mercury_amd.fingerprints(rec[sample], fp_host)
-    srec = desc[sample]
-    ft, fl, flags, want = oracle.process_batch(ua, ud[sample % len(ud)], oracle.config())
-    assert got == want
+    want = cases.load_golden("tls_ch_head", 0, "fp")
+    assert got == [want[int(i) % len(ud)][3] for i in sample]
+    assert [int(t) for t in rec["fp_type"][sample]] == [want[int(i) % len(ud)][1] for i in sample]
     # replicas are identical: per-position fp_len pattern repeats
     assert np.array_equal(rec["fp_len"][:len(ud)], rec["fp_len"][-len(ud):])
     ctx.close()
-    del srec
 
 
 @pytest.mark.gpu

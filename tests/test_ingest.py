@@ -178,12 +178,12 @@ def test_tpacket3_block_walk():
 
 @pytest.mark.gpu
 def test_pcap_ingest_to_device(tmp_path):
-    """pcap file -> mfp_pcap batches -> device fingerprints == oracle."""
-    from oracle import oracle
-    a, d = synth.batch(5000, seed=0x5EED0099, workload="mixed", n_templates=1000)
-    pk = [a[int(x["offset"]):int(x["offset"]) + int(x["caplen"])].tobytes() for x in d]
+    """pcap file -> mfp_pcap batches -> device fingerprints == the reference's
+    (tests/golden/cases/binmix.fp0: synthetic + fuzzed packets)."""
+    from tests import cases
+    pk = cases.binmix_case()
     p = tmp_path / "m.pcap"
-    write_pcap(p, pk)
+    write_pcap(p, [b for _, b in pk])
     ctx = mercury_amd.Context("tls,dtls,ssh,http,tcp,tcp.syn_ack", device=0)
     got = []
     with mercury_amd.PcapReader(p) as r:
@@ -191,5 +191,5 @@ def test_pcap_ingest_to_device(tmp_path):
             rec, fp = ctx.process_host(arena, desc)
             got += mercury_amd.fingerprints(rec, fp)
     ctx.close()
-    _, _, _, want = oracle.process_batch(a, d, oracle.config())
-    assert got == want and sum(1 for s in got if s) > 2000
+    want = [row[3] for row in cases.load_golden("binmix", 0, "fp")]
+    assert got == want and sum(1 for s in got if s) > 5000

@@ -153,3 +153,23 @@ def test_synthetic_generator_deterministic():
     # every family of the contract mix shows up, and "no output" packets exist
     assert set(np.unique(ft)) >= {0, 1, 2, 3, 7}
     assert (flags & 1).sum() < len(d1)
+
+
+@pytest.mark.parametrize("name,fmt,mode", [("fuzz0", 0, "fp"), ("fuzz2", 2, "fp"), ("edge", 1, "fp"),
+                                           ("corpus", 0, "fp"), ("analysis_mode", 1, "an")])
+def test_oracle_vs_reference_cases(name, fmt, mode):
+    """The C oracle (the debugging twin) equals the reference on the GPU
+    parity cases too (tests/golden/cases, from oracle/_ref)."""
+    from tests import cases
+    pk = cases.CASES[name][0]()
+    a, d = cases.batch(pk)
+    ref = cases.load_golden(name, fmt, mode)
+    ft, fl, flags, strs = oracle.process_batch(a, d, oracle.config(tls_format=fmt, mode=0 if mode == "fp" else 1))
+    bad = 0
+    for i, (emit, t, tr, s) in enumerate(ref):
+        if mode == "fp":
+            o = (int(flags[i] & 1), int(ft[i]), int((flags[i] >> 1) & 1) & int(flags[i] & 1), strs[i])
+            bad += o != (emit, t, tr, s)
+        else:
+            bad += (int(ft[i]), strs[i]) != (t, s)
+    assert bad == 0
