@@ -156,7 +156,7 @@ def end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world
     fp_cap = int((int(rec_u["fp_len"].astype(np.int64).sum()) + 16 * u) * reps * 1.05) + (64 << 20)
     h_rec = torch.empty(n * 32, dtype=torch.uint8, pin_memory=True)
     h_fp = torch.empty(fp_cap, dtype=torch.uint8, pin_memory=True)
-    h_an = torch.empty(n * 24 if analysis else 8, dtype=torch.uint8, pin_memory=True)
+    h_an = torch.empty(n * ANALYSIS_DTYPE.itemsize if analysis else 8, dtype=torch.uint8, pin_memory=True)
     out = (h_rec.numpy().view(RECORD_DTYPE), h_fp.numpy(), h_an.numpy().view(ANALYSIS_DTYPE) if analysis else None)
     d = h_desc.numpy().view(DESC_DTYPE)
     ctx.process_pipelined(av, d, chunk=chunk, analysis=analysis, out=out)   # warm-up (device buffers)
@@ -175,7 +175,7 @@ def end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world
         from mercury_amd import shard
         el = shard.max_over_ranks(el)
     in_bytes = (int(desc["caplen"].astype(np.int64).sum()) + 16 * n) * per_rank / n
-    out_bytes = 32 * per_rank + used_tot + (24 * per_rank if analysis else 0)
+    out_bytes = 32 * per_rank + used_tot + (ANALYSIS_DTYPE.itemsize * per_rank if analysis else 0)
     total = per_rank * world
     res = {"value": round(total / el / 1e6, 3), "unit": "Mpkt/s", "packets": total, "n_gpus": world,
            "packets_per_gpu": per_rank, "host_buffer_packets": n, "chunk": chunk,
@@ -206,7 +206,7 @@ def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_00
     rec_a, fp_a, an_a = out_a
     fp_b = torch.empty(fp_a.nbytes // max(1, n // batch), dtype=torch.uint8, pin_memory=True).numpy()
     rec_b = torch.empty(batch * 32, dtype=torch.uint8, pin_memory=True).numpy().view(RECORD_DTYPE)
-    an_b = torch.empty(batch * 24, dtype=torch.uint8, pin_memory=True).numpy().view(ANALYSIS_DTYPE) if analysis else None
+    an_b = torch.empty(batch * ANALYSIS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True).numpy().view(ANALYSIS_DTYPE) if analysis else None
     sets = [(rec_a[:batch], fp_a, an_a[:batch] if analysis else None), (rec_b, fp_b, an_b)]
     ts = np.full(batch, 1_700_000_000 * 10**9, np.uint64)
     ends = np.zeros(batch, np.uint64)
@@ -453,7 +453,7 @@ def main():
     d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_fp = torch.empty(cap, dtype=torch.uint8, device="cuda")
     d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
-    d_an = torch.empty(n * 24 if analysis else 1, dtype=torch.uint8, device="cuda")
+    d_an = torch.empty(n * mercury_amd.ANALYSIS_DTYPE.itemsize if analysis else 1, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
     prev = None
     if analysis and tdist:
@@ -510,7 +510,7 @@ def main():
     if analysis:
         an = d_an.cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)
         valid = (an["flags"] & 1) != 0
-        alg_bytes += 32 * n + 24 * n + int(rec["fp_len"][valid].astype(np.int64).sum())
+        alg_bytes += 32 * n + mercury_amd.ANALYSIS_DTYPE.itemsize * n + int(rec["fp_len"][valid].astype(np.int64).sum())
         st = np.bincount(an["status"][valid], minlength=5)
         an_info = {"classified": int(valid.sum()),
                    "status": {mercury_amd.api.STATUS_NAMES[i]: int(st[i]) for i in range(5)},

@@ -11,8 +11,7 @@
  *   - the returned analysis_context points into the processor and is
  *     overwritten by the next call on it (libmerc.cc:173-175);
  *   - errors return 0 / NULL, never abort (libmerc.cc:138-240).
- * Not provided on this path: JSON record output (write_json returns 0: the
- * JSON writer is the next component), stats, FDC/CBOR.
+ * Not provided on this path: stats, FDC/CBOR, encrypted resource archives.
  */
 #ifndef MERCURY_AMD_LIBMERC_H
 #define MERCURY_AMD_LIBMERC_H
@@ -78,6 +77,19 @@ enum fingerprint_type {
     fingerprint_type_ssh_server = 18, fingerprint_type_ssh_kex_server = 19, fingerprint_type_ssh_init_server = 20,
 };
 
+/* libmerc.h:164-180 */
+struct attribute_context {
+    const char *const *tag_names;      /* attribute names                         */
+    const long double *prob_scores;    /* probability per name (0 when not set)   */
+    size_t attributes_len;             /* length of both arrays                   */
+};
+
+/* libmerc.h:481-484 */
+struct os_information {
+    char *os_name;
+    uint64_t os_prevalence;
+};
+
 typedef struct mercury *mercury_context;
 typedef struct mercury_packet_processor_s *mercury_packet_processor;
 struct analysis_context;
@@ -92,10 +104,9 @@ MFP_EXPORT int mercury_finalize(mercury_context mc);
 MFP_EXPORT mercury_packet_processor mercury_packet_processor_construct(mercury_context mc);
 /* libmerc.h:253 */
 MFP_EXPORT void mercury_packet_processor_destruct(mercury_packet_processor mpp);
-/* libmerc.h:270, :293 -- the record text (mfp_write_json_batch), byte-identical to
- * the reference except: 0 for IP-in-IP packets whose outer IPv6 header has
- * extension headers, and whenever --analysis is configured (no "analysis"
- * object yet) */
+/* libmerc.h:270, :293 -- the record text (mfp_write_json_batch[_analysis]), with the
+ * "analysis" object under do_analysis; byte-identical to the reference except
+ * 0 for IP-in-IP packets whose outer IPv6 header has extension headers */
 MFP_EXPORT size_t mercury_packet_processor_write_json(mercury_packet_processor processor, void *buffer,
                                                       size_t buffer_size, uint8_t *packet, size_t length,
                                                       struct timespec *ts);
@@ -127,6 +138,16 @@ MFP_EXPORT bool analysis_context_get_process_info(const struct analysis_context 
 /* libmerc.h:471 */
 MFP_EXPORT bool analysis_context_get_malware_info(const struct analysis_context *ac,
                                                   bool *probable_process_is_malware, double *probability_malware);
+/* libmerc.h:505 -- os_info of the selected process (report_os) */
+MFP_EXPORT bool analysis_context_get_os_info(const struct analysis_context *ac, const struct os_information **os_info,
+                                             size_t *os_info_len);
+/* libmerc.h:733 -- the ClientHello's ALPN protocol_name_list */
+MFP_EXPORT bool analysis_context_get_alpns(const struct analysis_context *ac, const uint8_t **alpn_data,
+                                           size_t *alpn_length);
+/* libmerc.h:790 -- the attributes of the processor's last result */
+MFP_EXPORT const struct attribute_context *mercury_packet_processor_get_attributes(mercury_packet_processor processor);
+/* libmerc.h:647 -- opaque classifier handle (the analysis context), NULL without one */
+MFP_EXPORT void *mercury_get_classifier(mercury_context mc);
 /* libmerc.h:754 -- reassembly is off on this path */
 MFP_EXPORT bool mercury_packet_processor_more_pkts_needed(mercury_packet_processor processor);
 /* libmerc.h:603, :617, :556, :638 */

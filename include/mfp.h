@@ -59,24 +59,44 @@ typedef struct {
 } mfp_record;
 
 /* Per-packet classifier result (analysis_result, result.h:174-300), written
- * by the --analysis pass for packets whose fingerprint type the resource
- * archive covers. */
+ * by the --analysis pass for packets whose message the classifier sees
+ * (TLS ClientHello, HTTP request, SSH client KEXINIT: MFP_AN_VALID). */
 typedef struct {
     double   score;          /* analysis_result::max_score                      */
     double   malware_prob;   /* analysis_result::malware_prob (-1 if none)      */
     uint32_t process;        /* process-name id (mfp_process_name), or ~0u     */
-    uint16_t attr;           /* attribute_result tags (mfp_attribute_name bits) */
+    uint16_t attr;           /* attribute_result tags (mfp_attribute_name bits):
+                                the selected process's tags (bits >=
+                                MFP_ATTR_DB_FIRST) plus encrypted_dns,
+                                encrypted_channel, domain_faking, faketls     */
     uint8_t  status;         /* enum fingerprint_status (libmerc.h:307-313)     */
     uint8_t  flags;          /* MFP_AN_*                                        */
+    uint32_t proc_slot;      /* the selected process of its fingerprint entry
+                                (os_info: mfp_process_os_info), or ~0u          */
+    uint32_t reserved;       /* 0 */
 } mfp_analysis;
 
 enum {
-    MFP_AN_VALID     = 1,    /* analysis_result::is_valid() (result.h:254)  */
+    MFP_AN_VALID     = 1,    /* the message was classified: the reference writes
+                                an "analysis" object (pkt_proc.cc:1211-1213)  */
     MFP_AN_MALWARE   = 2,    /* max_mal                                      */
     MFP_AN_CLASSIFY_MALWARE = 4,   /* malware fields meaningful (malware db) */
     MFP_AN_PENDING   = 8,    /* internal: unknown TLS, status resolved later */
 };
 #define MFP_NO_PROCESS 0xffffffffu
+
+/* Attribute probabilities (attribute_result::prob_score, result.h:38).  Tags
+ * 0-9 are the reserved names (residential_proxy ... faketls, pkt_proc.h:72,
+ * analysis.h:830); the archive's own tags take 10-15 (attribute_names,
+ * result.h:133-172).  A reserved tag's probability follows from the record:
+ * encrypted_channel = malware_prob, encrypted_dns / domain_faking / faketls =
+ * 1.0 (analysis.h:555-577).  The archive tags' probabilities (the softmax
+ * mass of the processes carrying the tag, analysis.h:268-277,335-341) come in
+ * an optional per-packet array of MFP_ATTR_DB_TAGS doubles: attr_prob[i *
+ * MFP_ATTR_DB_TAGS + (bit - MFP_ATTR_DB_FIRST)], written for the set bits. */
+#define MFP_ATTR_DB_FIRST 10
+#define MFP_ATTR_DB_TAGS  6
+#define MFP_ATTR_MAX_TAGS 16
 
 enum {
     MFP_FLAG_EMIT      = 1,  /* the reference's write_json emits a record   */
@@ -88,10 +108,14 @@ enum {
     MFP_FLAG_CERT_CLIENT = 8,  /* TLS certificate message: entity client (tls.h:728-744) */
     MFP_FLAG_CERT_SERVER = 16, /* ... entity server; neither = undetermined   */
     MFP_FLAG_ENCAP       = 32, /* reached through IP-in-IP encapsulation (pkt_proc.cc:959) */
+    MFP_FLAG_NO_CIPHERS  = 64, /* (D)TLS ClientHello with an empty cipher-suite list: the
+                                  reference writes no "tls"/"dtls" object for it (tls.h:1882-1885) */
 };
 /* For MFP_MSG_TLS_SH / MFP_MSG_TLS_CERT records sni_off/sni_len hold the
  * certificate_list datum (tls.h:275-296), the bytes the JSON writer's
- * "certs" array is built from; len 0xffff = no list. */
+ * "certs" array is built from; len 0xffff = no list.  For MFP_MSG_TLS_CH and
+ * MFP_MSG_DTLS_CH records ua_off/ua_len hold the ALPN protocol_name_list
+ * (destination_context::alpn_array, analysis_context_get_alpns). */
 
 enum {
     MFP_MSG_NONE = 0, MFP_MSG_TLS_CH, MFP_MSG_TLS_SH, MFP_MSG_TLS_CERT,
@@ -165,16 +189,20 @@ MFP_EXPORT int mfp_analysis_enabled(mfp_context ctx);
 
 /* Classify a device-resident batch already fingerprinted by
  * mfp_process_batch_device on the same stream (records and fp arena as it
- * left them).  d_out: n mfp_analysis records (the records are read only).
- * Batches must be submitted in stream order: the unknown-TLS status
- * (randomized / unlabeled) depends on earlier sightings. */
+ * left them).  d_out: n mfp_analysis records (the records are read only);
+ * d_attr_prob: NULL, or n * MFP_ATTR_DB_TAGS doubles for the archive tags'
+ * probabilities.  Batches must be submitted in stream order: the unknown-TLS
+ * status (randomized / unlabeled) depends on earlier sightings. */
 MFP_EXPORT int mfp_analyze_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
-                                        mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, void *stream);
+                                        mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out,
+                                        double *d_attr_prob, void *stream);
 
-/* mfp_process_batch_host plus classification into analysis[n] (NULL: none). */
+/* mfp_process_batch_host plus classification into analysis[n] (NULL: none)
+ * and attr_prob[n * MFP_ATTR_DB_TAGS] (NULL: not wanted). */
 MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context ctx, const uint8_t *arena, size_t arena_len,
                                                const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
-                                               char *fp_arena, size_t fp_cap, mfp_analysis *analysis);
+                                               char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                               double *attr_prob);
 
 /* Host batch, pipelined (the end-to-end path: capture buffer in, records
  * out).  The batch is cut into chunks of `chunk` packets (0: 1M); two chunks
@@ -182,12 +210,13 @@ MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context ctx, const uint8_t *a
  * kernels of the other and the D2H copies of both.  `analysis` may be NULL
  * (fingerprints only).  Results are those of mfp_process_batch_host_ex on
  * the whole batch: rec[i].fp_offset indexes fp_arena, whose strings are laid
- * out chunk after chunk.  Host buffers should be page-locked
+ * out chunk after chunk.  attr_prob as for mfp_process_batch_host_ex (NULL:
+ * not copied back).  Host buffers should be page-locked
  * (hipHostMalloc / hipHostRegister) for full PCIe rate.  Synchronous;
  * returns the fp-arena bytes used or a negative error. */
 MFP_EXPORT long long mfp_process_pipelined(mfp_context ctx, const uint8_t *arena, size_t arena_len,
                                            const mfp_pkt_desc *desc, size_t n, mfp_record *rec, char *fp_arena,
-                                           size_t fp_cap, mfp_analysis *analysis, size_t chunk);
+                                           size_t fp_cap, mfp_analysis *analysis, double *attr_prob, size_t chunk);
 
 /* ---- the unknown-TLS prevalence set (fingerprint_prevalence, analysis.h:362-421) ----
  * A TLS fingerprint the archive does not label, and not in its known
@@ -255,6 +284,21 @@ MFP_EXPORT long long mfp_analysis_last(mfp_context ctx, mfp_analysis *out, size_
 /* names behind mfp_analysis.process and the bits of mfp_analysis.attr */
 MFP_EXPORT const char *mfp_process_name(mfp_context ctx, uint32_t id);
 MFP_EXPORT const char *mfp_attribute_name(mfp_context ctx, uint32_t bit);
+/* the archive's VERSION text (classifier::get_resource_version analysis.h:1174) */
+MFP_EXPORT const char *mfp_resource_version(mfp_context ctx);
+/* number of attribute names (attribute_names::value().size(), <= 16) */
+MFP_EXPORT int mfp_attribute_count(mfp_context ctx);
+
+/* libmerc_config.report_os (libmerc.h:118): os_info of the selected process
+ * in analysis results (fingerprint_data ctor analysis.h:195-205).  Off by
+ * default, as in the reference. */
+MFP_EXPORT int mfp_analysis_report_os(mfp_context ctx, int on);
+/* os_info entry k of a process slot (mfp_analysis.proc_slot): *name and
+ * *prevalence (os_information, libmerc.h:481-484; archive order).  Returns the
+ * entry count (0 when report_os is off or the process has none), -1 on a bad
+ * slot. */
+MFP_EXPORT int mfp_process_os_info(mfp_context ctx, uint32_t proc_slot, uint32_t k, const char **name,
+                                   uint64_t *prevalence);
 
 /* last analysis batch: [0] packets classified, [1] unknown-TLS sightings,
  * [2] fingerprints with more processes than the kernel handles (512),
@@ -332,6 +376,19 @@ MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_de
                                           const mfp_record *rec, const char *fp_arena, const uint64_t *ts_ns,
                                           char *out, size_t out_cap, uint64_t *line_end, uint64_t *skipped,
                                           int threads);
+
+/* mfp_write_json_batch with --analysis: records whose analysis has
+ * MFP_AN_VALID get the "analysis" object (analysis_result::write_json
+ * result.h:207-252, placed as pkt_proc.cc:1211-1213 places it), with names,
+ * os_info and attribute names from ctx (the context that classified the
+ * batch; mfp_analysis_enabled).  analysis: the batch's n results; attr_prob:
+ * as mfp_process_batch_host_ex returned it (NULL only when no record carries
+ * an archive tag). */
+MFP_EXPORT long long mfp_write_json_batch_analysis(mfp_context ctx, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                                   size_t n, const mfp_record *rec, const char *fp_arena,
+                                                   const mfp_analysis *analysis, const double *attr_prob,
+                                                   const uint64_t *ts_ns, char *out, size_t out_cap,
+                                                   uint64_t *line_end, uint64_t *skipped, int threads);
 
 /* last error string for this thread */
 MFP_EXPORT const char *mfp_last_error(void);

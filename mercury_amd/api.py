@@ -12,12 +12,17 @@ RECORD_DTYPE = np.dtype([("fp_offset", "<u8"), ("fp_len", "<u4"), ("fp_type", "u
                          ("ua_off", "<u2"), ("ua_len", "<u2"), ("src_port", "<u2"), ("dst_port", "<u2"),
                          ("net", "<u4")])
 ANALYSIS_DTYPE = np.dtype([("score", "<f8"), ("malware_prob", "<f8"), ("process", "<u4"), ("attr", "<u2"),
-                           ("status", "u1"), ("flags", "u1")])
+                           ("status", "u1"), ("flags", "u1"), ("proc_slot", "<u4"), ("reserved", "<u4")])
 SIGHTING_DTYPE = np.dtype([("hash", "<u8"), ("first", "<u8"), ("last", "<u8"), ("count", "<u4"),
                            ("first_seen", "<u4")])
-assert DESC_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 32 and ANALYSIS_DTYPE.itemsize == 24
+assert DESC_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 32 and ANALYSIS_DTYPE.itemsize == 32
 assert SIGHTING_DTYPE.itemsize == 32
 NO_PROCESS = 0xFFFFFFFF
+# attribute tags (include/mfp.h): the archive's own tags take bits 10..15 and
+# their probabilities come in MFP_ATTR_DB_TAGS doubles per packet
+ATTR_DB_FIRST = 10
+ATTR_DB_TAGS = 6
+AN_VALID, AN_MALWARE, AN_CLASSIFY_MALWARE = 1, 2, 4
 STATUS_NAMES = ["no_info_available", "labeled", "randomized", "unlabeled", "unanalyzed"]
 
 # fingerprint::get_type_name (src/libmerc/fingerprint.h:159-192)
@@ -68,9 +73,18 @@ def load_library():
     lib.mfp_analysis_enabled.restype = ctypes.c_int
     lib.mfp_analysis_enabled.argtypes = [vp]
     lib.mfp_analyze_batch_device.restype = ctypes.c_int
-    lib.mfp_analyze_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
+    lib.mfp_analyze_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     lib.mfp_process_batch_host_ex.restype = ctypes.c_longlong
-    lib.mfp_process_batch_host_ex.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp]
+    lib.mfp_process_batch_host_ex.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, vp]
+    lib.mfp_attribute_count.restype = ctypes.c_int
+    lib.mfp_attribute_count.argtypes = [vp]
+    lib.mfp_resource_version.restype = ctypes.c_char_p
+    lib.mfp_resource_version.argtypes = [vp]
+    lib.mfp_analysis_report_os.restype = ctypes.c_int
+    lib.mfp_analysis_report_os.argtypes = [vp, ctypes.c_int]
+    lib.mfp_process_os_info.restype = ctypes.c_int
+    lib.mfp_process_os_info.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
+                                        ctypes.POINTER(ctypes.c_uint64)]
     lib.mfp_process_name.restype = ctypes.c_char_p
     lib.mfp_process_name.argtypes = [vp, ctypes.c_uint32]
     lib.mfp_attribute_name.restype = ctypes.c_char_p
@@ -84,7 +98,7 @@ def load_library():
     lib.mfp_parse_filter.restype = ctypes.c_int
     lib.mfp_parse_filter.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     lib.mfp_process_pipelined.restype = ctypes.c_longlong
-    lib.mfp_process_pipelined.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, sz]
+    lib.mfp_process_pipelined.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, vp, sz]
     lib.mfp_profile_enable.restype = ctypes.c_int
     lib.mfp_profile_enable.argtypes = [vp, ctypes.c_int]
     lib.mfp_profile_read.restype = ctypes.c_int
@@ -102,6 +116,9 @@ def load_library():
     lib.mfp_write_json_batch.restype = ctypes.c_longlong
     lib.mfp_write_json_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, sz, vp, ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.c_int]
+    lib.mfp_write_json_batch_analysis.restype = ctypes.c_longlong
+    lib.mfp_write_json_batch_analysis.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, sz, vp,
+                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     u64 = ctypes.c_uint64
     lib.mfp_prevalence_create.restype = vp
     lib.mfp_prevalence_create.argtypes = [ctypes.c_uint32]
@@ -184,26 +201,32 @@ class Context:
     def analysis_enabled(self):
         return bool(self.lib.mfp_analysis_enabled(self.h))
 
-    def process_host_analysis(self, arena, desc):
-        """Fingerprint + classify a host batch -> (records, fp arena bytes, analysis records)."""
+    def process_host_analysis(self, arena, desc, attr_prob=False):
+        """Fingerprint + classify a host batch -> (records, fp arena bytes, analysis
+        records), plus the (n, ATTR_DB_TAGS) attribute probabilities when attr_prob."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
         n = len(desc)
         rec = np.zeros(n, dtype=RECORD_DTYPE)
         an = np.zeros(n, dtype=ANALYSIS_DTYPE)
+        ap = np.zeros((max(n, 1), ATTR_DB_TAGS), np.float64) if attr_prob else None
         cap = self.fp_arena_bound(desc)
         fp = np.zeros(cap, dtype=np.uint8)
         used = self.lib.mfp_process_batch_host_ex(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
-                                                  rec.ctypes.data, fp.ctypes.data, cap, an.ctypes.data)
+                                                  rec.ctypes.data, fp.ctypes.data, cap, an.ctypes.data,
+                                                  ap.ctypes.data if ap is not None else None)
         if used < 0:
             raise MercuryAmdError("mfp_process_batch_host_ex failed: " + _err(self.lib))
+        if attr_prob:
+            return rec, fp[:used].tobytes(), an, ap[:n]
         return rec, fp[:used].tobytes(), an
 
-    def process_pipelined(self, arena, desc, chunk=0, analysis=False, out=None):
+    def process_pipelined(self, arena, desc, chunk=0, analysis=False, out=None, attr_prob=None):
         """Host batch through the two-stream pipeline (mfp_process_pipelined).
         `out`: optional preallocated (records, fp arena, analysis) host arrays
-        (page-locked for full PCIe rate).  Returns (records, fp arena bytes
-        used, analysis records or None)."""
+        (page-locked for full PCIe rate); attr_prob: None, or a float64 array
+        of n * ATTR_DB_TAGS for the attribute probabilities.  Returns (records,
+        fp arena bytes used, analysis records or None)."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
         n = len(desc)
@@ -213,15 +236,18 @@ class Context:
             an = np.zeros(n, dtype=ANALYSIS_DTYPE) if analysis else None
         else:
             rec, fp, an = out
+        if attr_prob is not None and attr_prob.size < n * ATTR_DB_TAGS:
+            raise ValueError("attr_prob needs n * ATTR_DB_TAGS doubles")
         used = self.lib.mfp_process_pipelined(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
                                               rec.ctypes.data, fp.ctypes.data, fp.nbytes,
-                                              an.ctypes.data if an is not None else None, chunk)
+                                              an.ctypes.data if an is not None else None,
+                                              attr_prob.ctypes.data if attr_prob is not None else None, chunk)
         if used < 0:
             raise MercuryAmdError("mfp_process_pipelined failed: " + _err(self.lib))
         return rec, int(used), an
 
-    def analyze_device(self, d_arena, d_desc, n, d_rec, d_fp, d_out, stream=0):
-        r = self.lib.mfp_analyze_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out, stream)
+    def analyze_device(self, d_arena, d_desc, n, d_rec, d_fp, d_out, stream=0, d_attr_prob=None):
+        r = self.lib.mfp_analyze_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out, d_attr_prob, stream)
         if r != 0:
             raise MercuryAmdError("mfp_analyze_batch_device failed: " + _err(self.lib))
 
@@ -234,6 +260,32 @@ class Context:
     def attribute_name(self, bit):
         s = self.lib.mfp_attribute_name(self.h, int(bit))
         return s.decode() if s else None
+
+    def attribute_count(self):
+        return int(self.lib.mfp_attribute_count(self.h))
+
+    def resource_version(self):
+        s = self.lib.mfp_resource_version(self.h)
+        return s.decode() if s is not None else None
+
+    def report_os(self, on=True):
+        """libmerc_config.report_os: os_info of the selected process in results."""
+        if self.lib.mfp_analysis_report_os(self.h, 1 if on else 0) != 0:
+            raise MercuryAmdError(_err(self.lib))
+
+    def os_info(self, proc_slot):
+        """[(os name, prevalence)] of a process slot (empty unless report_os)."""
+        if proc_slot == NO_PROCESS:
+            return []
+        nm, pv = ctypes.c_char_p(), ctypes.c_uint64(0)
+        cnt = self.lib.mfp_process_os_info(self.h, int(proc_slot), 0, None, None)
+        if cnt < 0:
+            raise MercuryAmdError(_err(self.lib))
+        out = []
+        for k in range(cnt):
+            self.lib.mfp_process_os_info(self.h, int(proc_slot), k, ctypes.byref(nm), ctypes.byref(pv))
+            out.append((nm.value.decode("latin-1"), int(pv.value)))
+        return out
 
     def analysis_stats(self):
         out = (ctypes.c_uint64 * 4)()
@@ -489,12 +541,16 @@ def tpacket3_block(block, max_pkts=4096):
     return desc[:n], ts[:n]
 
 
-def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1):
+def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1, ctx=None, analysis=None, attr_prob=None):
     """JSON record lines for a fingerprinted batch (mfp_write_json_batch: the
-    text of stateful_pkt_proc::write_json, src/libmerc/pkt_proc.cc:1157-1253).
-    Returns (list of per-packet lines as bytes, b"" when the reference writes
-    nothing; count of records that could not be rebuilt). Host only."""
+    text of stateful_pkt_proc::write_json, src/libmerc/pkt_proc.cc:1157-1253);
+    with ctx + analysis (+ attr_prob), the --analysis "analysis" objects
+    (mfp_write_json_batch_analysis).  Returns (list of per-packet lines as
+    bytes, b"" when the reference writes nothing; count of records that could
+    not be rebuilt). Host only."""
     lib = load_library()
+    an = None if analysis is None else np.ascontiguousarray(analysis, dtype=ANALYSIS_DTYPE)
+    ap = None if attr_prob is None else np.ascontiguousarray(attr_prob, dtype=np.float64)
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
     rec = np.ascontiguousarray(rec, dtype=RECORD_DTYPE)
@@ -506,9 +562,16 @@ def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1):
     cap = 1 << 16
     while True:
         out = np.empty(cap, np.uint8)
-        got = lib.mfp_write_json_batch(arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data,
-                                       None if ts is None else ts.ctypes.data, out.ctypes.data, cap,
-                                       ends.ctypes.data, ctypes.byref(skipped), int(threads))
+        if an is not None:
+            got = lib.mfp_write_json_batch_analysis(ctx.h, arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data,
+                                                    fp.ctypes.data, an.ctypes.data,
+                                                    None if ap is None else ap.ctypes.data,
+                                                    None if ts is None else ts.ctypes.data, out.ctypes.data, cap,
+                                                    ends.ctypes.data, ctypes.byref(skipped), int(threads))
+        else:
+            got = lib.mfp_write_json_batch(arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data,
+                                           None if ts is None else ts.ctypes.data, out.ctypes.data, cap,
+                                           ends.ctypes.data, ctypes.byref(skipped), int(threads))
         if got == -2:
             cap *= 4
             continue

@@ -78,9 +78,24 @@ struct mfp_classifier_dev {
     mfp_asn4 *asn4 = nullptr; uint32_t n_asn4 = 0;
     mfp_asn6 *asn6 = nullptr; uint32_t n_asn6 = 0;
     uint32_t types_mask = 0;           // analyzable fingerprint types (fp_types)
-    uint32_t enc_channel_idx = 7, faketls_idx = 9;
+    uint32_t enc_channel_idx = 7, faketls_idx = 9, doh_idx = 6, domain_faking_idx = 8;
     uint32_t randomized_entry[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};   // "tls/", "tls/1/", "tls/2/" + "randomized"
+    uint32_t db_tags = 0;              // bits of the archive's own attribute tags (>= MFP_ATTR_DB_FIRST)
+    // classifier-agnostic attributes (check_additional_attributes_util,
+    // analysis.h:555-570): encrypted_dns from doh-watchlist.txt, domain_faking
+    // from domain-mappings.db (subnet_data::is_domain_faking addr.cc:707-792)
+    uint32_t doh_enabled = 0, faking_enabled = 0;
+    mfp_fp_slot *doh_names = nullptr; uint64_t doh_names_mask = 0;   // watchlist DNS names
+    uint32_t *doh_v4 = nullptr; uint32_t n_doh_v4 = 0;               // sorted IPv4 (parse_ipv4 values)
+    uint64_t *doh_v6 = nullptr; uint32_t n_doh_v6 = 0;               // sorted (hi, lo) pairs
+    mfp_fp_slot *dom_slots = nullptr; uint64_t dom_mask = 0;         // mapped domain -> domain index (id)
+    mfp_asn4 *dom4 = nullptr; uint32_t n_dom4 = 0;                   // prefix intervals, asn = info + 1
+    mfp_asn6 *dom6 = nullptr; uint32_t n_dom6 = 0;                   // 0: no IPv6 mappings
+    uint32_t *dom_info = nullptr;      // per prefix: [type (1 mapping, 2 exception) | count << 8, byte offset]
+    uint8_t *dom_bytes = nullptr;      // mapped domain indices (uint8_t, as the reference stores them)
 };
+#define MFP_DOM_MAPPING 1u
+#define MFP_DOM_EXCEPTION 2u
 
 typedef struct mfp_classifier_s mfp_classifier;
 
@@ -92,6 +107,10 @@ int mfp_classifier_tls_format(const mfp_classifier *c);
 bool mfp_classifier_disabled(const mfp_classifier *c);
 const char *mfp_classifier_process_name(const mfp_classifier *c, uint32_t id);
 const char *mfp_classifier_attr_name(const mfp_classifier *c, uint32_t i);
+int mfp_classifier_attr_count(const mfp_classifier *c);
+const char *mfp_classifier_version(const mfp_classifier *c);
+// os_info entry k of process slot `slot` (proc_off + index); returns the count, -1 bad slot
+int mfp_classifier_os_info(const mfp_classifier *c, uint32_t slot, uint32_t k, const char **name, uint64_t *prev);
 void mfp_classifier_stats(const mfp_classifier *c, uint64_t out[8]);
 const mfp_classifier_dev *mfp_classifier_device(const mfp_classifier *c);
 mfp_classifier_dev *mfp_classifier_device_mut(mfp_classifier *c);

@@ -348,6 +348,123 @@ ADEV uint32_t asn_v6_lane(const mfp_classifier_dev &D, uint64_t xh, uint64_t xl)
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// classifier-agnostic attributes (check_additional_attributes_util
+// analysis.h:555-570, tls_client_hello::do_analysis tls.h:1977-1996)
+// ---------------------------------------------------------------------------
+// the destination as the reference reads it back from dst_ip_str
+struct Dst {
+    uint32_t ipv;        // 4, 6, or 0
+    uint32_t v4;         // address bytes in packet order (ipv4_address_string value)
+    uint64_t hi, lo;     // IPv6 as big-endian halves, after the text round trip
+};
+
+ADEV Dst dst_of(const uint8_t *pkt, uint32_t net) {
+    Dst d;
+    d.ipv = (net >> 16) & 15;
+    d.v4 = 0; d.hi = 0; d.lo = 0;
+    const uint32_t ipo = net & 0xffff;
+    if (d.ipv == 4) {
+        d.v4 = (uint32_t)word_at(pkt + ipo + 16, 4, 0);
+    } else if (d.ipv == 6) {
+        d.hi = __builtin_bswap64(word_at(pkt + ipo + 24, 16, 0));
+        d.lo = __builtin_bswap64(word_at(pkt + ipo + 24, 16, 1));
+        v6_text_roundtrip(d.hi, d.lo);
+    }
+    return d;
+}
+
+// watchlist::contains (dns name) || watchlist::contains_addr (watchlist.hpp:574-599)
+ADEV bool doh_hit(const mfp_classifier_dev &D, const uint8_t *sn, uint32_t cl, uint64_t ch, const Dst &d) {
+    if (probe_string_lane(D.doh_names, D.doh_names_mask, D.pool, sn, cl, ch) != 0xffffffffu) return true;
+    if (d.ipv == 4) {
+        int lo = 0, hi = (int)D.n_doh_v4 - 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            const uint32_t v = D.doh_v4[mid];
+            if (v == d.v4) return true;
+            if (v < d.v4) lo = mid + 1; else hi = mid - 1;
+        }
+    } else if (d.ipv == 6) {
+        int lo = 0, hi = (int)D.n_doh_v6 - 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            const uint64_t a = D.doh_v6[2 * mid], b = D.doh_v6[2 * mid + 1];
+            if (a == d.hi && b == d.lo) return true;
+            if (a < d.hi || (a == d.hi && b < d.lo)) lo = mid + 1; else hi = mid - 1;
+        }
+    }
+    return false;
+}
+
+// subnet_data::is_domain_faking (addr.cc:707-792): a mapped domain (a leading
+// "www." dropped) whose public destination is not in one of its prefixes nor
+// in an exception prefix
+ADEV bool domain_faking(const mfp_classifier_dev &D, const uint8_t *sn, uint32_t cl, const Dst &d) {
+    const bool www = cl >= 4 && sn[0] == 'w' && sn[1] == 'w' && sn[2] == 'w' && sn[3] == '.';
+    const uint8_t *nm = www ? sn + 4 : sn;
+    const uint32_t nl = www ? cl - 4 : cl;
+    const uint32_t didx = probe_string_lane(D.dom_slots, D.dom_mask, D.pool, nm, nl, lane_hash(nm, nl));
+    if (didx == 0xffffffffu) return false;
+    uint32_t info = 0;
+    if (d.ipv == 4) {
+        const uint32_t v = d.v4;   // ipv4_address::get_addr_type private_use (ip_address.hpp:119-123)
+        if ((v & 0xff) == 0x0a || (v & 0xf0ff) == 0x10ac || (v & 0xffff) == 0xa8c0) return false;
+        const uint32_t h = __builtin_bswap32(v);
+        int lo = 0, hi = (int)D.n_dom4 - 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            const mfp_asn4 r = D.dom4[mid];
+            if (h < r.lo) hi = mid - 1;
+            else if (h > r.hi) lo = mid + 1;
+            else { info = r.asn; break; }
+        }
+    } else if (d.ipv == 6 && D.n_dom6) {
+        // is_private_address (ipv6_lctrie.h:255): the first byte in memory of
+        // the host-order high half, i.e. address byte 7
+        if ((d.hi & 0xff) == 0xfc || (d.hi & 0xff) == 0xfd) return false;
+        int lo = 0, hi = (int)D.n_dom6 - 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            const mfp_asn6 r = D.dom6[mid];
+            if (!le128(r.lo_hi, r.lo_lo, d.hi, d.lo)) hi = mid - 1;
+            else if (!le128(d.hi, d.lo, r.hi_hi, r.hi_lo)) lo = mid + 1;
+            else { info = r.asn; break; }
+        }
+    } else {
+        return false;
+    }
+    if (info == 0) return true;                    // no prefix holds the destination
+    const uint32_t ty = D.dom_info[2 * (info - 1)], off = D.dom_info[2 * (info - 1) + 1];
+    if ((ty & 0xff) == MFP_DOM_EXCEPTION) return false;
+    for (uint32_t k = 0; k < (ty >> 8); k++)
+        if ((uint32_t)D.dom_bytes[off + k] == didx) return false;   // uint8_t entry vs uint32_t index
+    return true;
+}
+
+// is_faketls_util (tls.h:923-949) on the fingerprint string: its second
+// parenthesised group is the ClientHello's cipher suites, degreased, as hex
+// (raw_as_hex_degrease tls.h:802-813); faketls when none is in the IANA list
+// or the exception list (no suites at all included)
+__constant__ uint16_t kCipherRanges[][2] = {
+#include "mfp_cipher_ranges.inc"
+};
+ADEV bool faketls_fp(const uint8_t *fp, uint32_t len) {
+    uint32_t p = 0;
+    while (p < len && fp[p] != ')') p++;
+    p += 2;                                        // ")("
+    for (; p + 4 <= len && fp[p] != ')'; p += 4) {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; k++) {
+            const uint32_t c = fp[p + k];
+            v = v << 4 | (c <= '9' ? c - '0' : c - 'a' + 10);
+        }
+        for (uint32_t r = 0; r < sizeof(kCipherRanges) / sizeof(kCipherRanges[0]); r++)
+            if (v >= kCipherRanges[r][0] && v <= kCipherRanges[r][1]) return false;
+    }
+    return true;
+}
+
 // A server name that server_identifier::get_normalized_domain_name leaves
 // unchanged (watchlist.hpp:326-390): 1..256 bytes of label characters and
 // dots, no empty label, at least two labels, the last one with a letter.
@@ -408,6 +525,55 @@ ADEV bool plain_server_name(const uint8_t *s, uint32_t n, uint32_t &tld, uint64_
     return ok;
 }
 
+// ---------------------------------------------------------------------------
+// expf as the reference computes it: the softmax calls the C library's expf
+// (softmax.hpp:252); on x86-64 glibc resolves it to its FMA build of the
+// table method -- x*32/ln2 = k + r, 2^(k/32) from a 32-entry table of
+// 2^(i/32), a cubic in r, all in double, one rounding to float at the end.
+// Restated here with the same operations and the same fused multiply-adds
+// (the table holds round-to-nearest 2^(i/32), minus i << 47), so the
+// probabilities are bit-identical to the reference's; checked against the
+// host's expf on every float in [-110, 0] (the softmax only takes x <= 0).
+// ---------------------------------------------------------------------------
+__constant__ uint64_t kExp2Tab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull,
+};
+ADEV float expf_ref(float x) {
+#pragma clang fp contract(off)
+    const uint32_t ux = __float_as_uint(x);
+    const uint32_t abstop = (ux >> 20) & 0x7ff;
+    if (abstop >= 0x42b) {                              // |x| >= 88 or NaN
+        if (ux == 0xff800000u) return 0.0f;             // -inf
+        if (abstop >= 0x7f8) return x + x;              // +inf, NaN
+        if (x > 0x1.62e42ep6f) return __uint_as_float(0x7f800000u);   // overflow
+        if (x < -0x1.9fe368p6f) return 0.0f;            // underflow
+    }
+    const double inv_ln2_n = 0x1.71547652b82fep+0 * 32, shift = 0x1.8p+52;
+    const double c0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, c1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+                 c2 = 0x1.62e42ff0c52d6p-1 / 32;
+    const double xd = (double)x;
+    const double z = inv_ln2_n * xd;
+    double kd = z + shift;
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd -= shift;
+    const double r = __builtin_fma(inv_ln2_n, xd, -kd);
+    const uint64_t t = kExp2Tab[ki & 31] + (ki << 47);
+    const double s = __longlong_as_double((long long)t);
+    const double zz = __builtin_fma(c0, r, c1);
+    const double r2 = r * r;
+    double y = __builtin_fma(c2, r, 1.0);
+    y = __builtin_fma(zz, r2, y);
+    y = y * s;
+    return (float)y;
+}
+
 // a packet k_analyze hands to k_analyze_wave, with its feature lookups done
 struct Deferred {
     uint32_t i, entry, slow_sni, pad;   // slow_sni: domain / SNI lookups still to do
@@ -422,6 +588,7 @@ struct AParams {
     mfp_record *rec;
     const uint8_t *fp_arena;
     mfp_analysis *out;
+    double *attr_prob;           // optional: archive-tag probabilities, MFP_ATTR_DB_TAGS per packet
     uint64_t *pend_bits;         // per group of 64 packets: unknown-TLS sightings (k_analyze_resolve)
     mfp_seen_tab seen;           // this batch's sightings per distinct fingerprint
     struct Deferred *deferred;   // packets scored by k_analyze_wave
@@ -468,6 +635,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; }
         mfp_analysis a;   // default: no information (analysis_result())
         a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.status = 0; a.flags = 0;
+        a.proc_slot = MFP_NO_PROCESS; a.reserved = 0;
         // messages whose do_analysis calls the classifier: TLS ClientHello
         // (tls.h:1977), HTTP request (http.cc:571), SSH client KEXINIT
         // (ssh.h:480); their type must also be in the archive (fp_types)
@@ -587,20 +755,34 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         uint64_t vk[3] = {0, 0, 0};
         Hit vh[3] = {Hit{0, 0}, Hit{0, 0}, Hit{0, 0}};
         bool has[3] = {false, false, false};
+        // ---- destination context (destination_context::init, result.h:346)
+        // and the classifier-agnostic attributes of a ClientHello
+        const bool xcheck = analyzable && r.fp_type == 1 && (D.doh_enabled | D.faking_enabled);
+        const uint8_t *pkt = P.arena + (scored || xcheck ? P.desc[i].offset : 0);
+        Dst dd;
+        dd.ipv = 0; dd.v4 = 0; dd.hi = 0; dd.lo = 0;
+        if (scored || xcheck) dd = dst_of(pkt, r.net);
+        uint32_t xattr = 0;   // encrypted_dns, domain_faking, faketls
+        if (xcheck) {
+            // sn_str: the server name as a C string (strncpy MAX_SNI_LEN, result.h:348)
+            const uint32_t sl0 = r.sni_len == 0xffff ? 0u : r.sni_len;
+            uint64_t ch = 0;
+            const uint32_t cl = cstr_hash(pkt + r.sni_off, sl0 < 256 ? sl0 : 256u, ch);
+            if (D.doh_enabled && doh_hit(D, pkt + r.sni_off, cl, ch, dd)) xattr |= 1u << D.doh_idx;
+            if (D.faking_enabled && domain_faking(D, pkt + r.sni_off, cl, dd)) xattr |= 1u << D.domain_faking_idx;
+        }
+        if (pending && faketls_fp(fp, fl)) xattr |= 1u << D.faketls_idx;   // randomized ClientHellos only
         if (scored) {
-            // ---- 2. destination context (destination_context::init, result.h:346)
-            const uint8_t *pkt = P.arena + P.desc[i].offset;
-            const uint32_t ipv = (r.net >> 16) & 15, ipo = r.net & 0xffff;
+            const uint32_t ipv = dd.ipv;
             uint32_t asn = 0;
             uint64_t ipkey = 0, v6w0 = 0, v6w1 = 0;
             if (ipv == 4) {
-                const uint32_t v4 = (uint32_t)word_at(pkt + ipo + 16, 4, 0);   // network order, as bytes
-                asn = asn_v4_lane(D, __builtin_bswap32(v4));
-                ipkey = normalize_ipv4(v4);
+                asn = asn_v4_lane(D, __builtin_bswap32(dd.v4));
+                ipkey = normalize_ipv4(dd.v4);
             } else if (ipv == 6) {
-                v6w0 = word_at(pkt + ipo + 24, 16, 0);
-                v6w1 = word_at(pkt + ipo + 24, 16, 1);
-                if (D.n_asn6) asn = asn_v6_lane(D, __builtin_bswap64(v6w0), __builtin_bswap64(v6w1));
+                v6w0 = __builtin_bswap64(dd.hi);
+                v6w1 = __builtin_bswap64(dd.lo);
+                if (D.n_asn6) asn = asn_v6_lane(D, dd.hi, dd.lo);
                 // normalize_ipv6 (mfp_common.hpp) on the two words
                 const bool gu = (v6w0 & 0xe0) == 0x20;
                 const bool mapped = v6w0 == 0 && (v6w1 & 0xffffffffull) == 0xffff0000ull;
@@ -614,7 +796,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             uint64_t nh = 0;
             plain = plain_server_name(sp, sl, tld, nh);   // no NUL in a plain name
             // user agent (strncpy 511, NUL stops); TLS has none
-            uint32_t ul = r.ua_len == 0xffff ? 0u : r.ua_len;
+            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH ? 0u : r.ua_len;   // (ClientHello: the ALPN slot)
             if (ul > 511) ul = 511;
             const uint8_t *up = pkt + r.ua_off;
             uint64_t uh = 0;
@@ -699,27 +881,48 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 if (v > mx) { sx = mx; isx = imx; mx = v; imx = p; }
                 else if (v > sx) { sx = v; isx = p; }
             }
+            // the "generic dmz process" swap is decided by the ranks alone
+            const bool swap = mdb && dmz == imx && !((mbits >> isx) & 1u);
+            const uint32_t ibest = swap ? isx : imx;
+            // archive tags of the selected process: their probability is the
+            // softmax mass of the processes carrying them (analysis.h:268-277;
+            // the swapped-out maximum counts 0)
+            const uint32_t tags = D.proc_attr[po + ibest] & D.db_tags;
+            double ap[MFP_ATTR_DB_TAGS];
+#pragma unroll
+            for (int k = 0; k < MFP_ATTR_DB_TAGS; k++) ap[k] = 0.0;
             double ssum = 0.0, swo = 0.0, mal = 0.0, p_imx = 0.0, p_isx = 0.0;
             for (uint32_t p = 0; p < np; p++) {
-                const double e = (double)expf((float)(S[p * 64] - mx));
+                const double e = (double)expf_ref((float)(S[p * 64] - mx));
                 ssum += e;
                 if (p != imx) swo += e;
                 if ((mbits >> p) & 1u) mal += e;
                 if (p == imx) p_imx = e;
                 if (p == isx) p_isx = e;
+                if (tags && !(swap && p == imx)) {
+                    const uint32_t pa = D.proc_attr[po + p] & tags;
+#pragma unroll
+                    for (int k = 0; k < MFP_ATTR_DB_TAGS; k++)
+                        if ((pa >> (MFP_ATTR_DB_FIRST + k)) & 1u) ap[k] += e;
+                }
             }
             double max_score = p_imx;
             if (ssum > 0.0 && mdb) mal /= ssum;
-            uint32_t ibest = imx;
-            if (mdb && dmz == imx && !((mbits >> isx) & 1u)) {
-                ibest = isx;
+            if (swap) {
                 ssum = swo;
                 max_score = p_isx;
             }
             if (ssum > 0.0) max_score /= ssum;
+            if (tags && P.attr_prob) {
+                double *o = P.attr_prob + i * MFP_ATTR_DB_TAGS;
+#pragma unroll
+                for (int k = 0; k < MFP_ATTR_DB_TAGS; k++)
+                    if ((tags >> (MFP_ATTR_DB_FIRST + k)) & 1u) o[k] = ssum > 0.0 ? ap[k] / ssum : ap[k];
+            }
             a.score = max_score;
             a.process = D.proc_id[po + ibest];
-            a.attr = (uint16_t)D.proc_attr[po + ibest];
+            a.proc_slot = po + ibest;
+            a.attr = (uint16_t)(D.proc_attr[po + ibest] | xattr);
             a.malware_prob = -1.0;
             a.flags = MFP_AN_VALID;
             if (mdb) {
@@ -750,7 +953,8 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         }
         if (analyzable) {
             if (!lanep) {   // no process distribution (yet: k_analyze_wave scores the deferred ones)
-                a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.flags = MFP_AN_VALID;
+                a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = (uint16_t)xattr;
+                a.flags = MFP_AN_VALID; a.proc_slot = MFP_NO_PROCESS;
             }
             a.status = (uint8_t)status;
             if (pending) a.flags |= MFP_AN_PENDING;
@@ -774,6 +978,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
 __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
     __shared__ char sni_buf[4][336];
     __shared__ double sc_lds[4][64 * MAXP_CHUNKS];
+    __shared__ uint8_t fl_lds[4][64 * MAXP_CHUNKS];   // per process: malware (bit 0), archive tags (1-6), swapped out (7)
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
     char *nbuf = sni_buf[wid];
@@ -891,36 +1096,72 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
         isx = rfl(isx);
         if (isx == 0xffffffffu) isx = 0;   // P == 1: index_sec stays 0
 
-        // ---- softmax (expf in fp32, stored as double), sums
-        double ssum = 0.0, swo = 0.0, mal = 0.0, p_imx = 0.0, p_isx = 0.0;
+        // ---- the dmz swap (decided by the ranks alone) and the selected
+        // process's archive tags (analysis.h:258-277)
+        const bool swap = mdb && dmz == imx && !D.proc_mal[po + isx];
+        const uint32_t ibest = swap ? isx : imx;
+        const uint32_t tags = rfl(D.proc_attr[po + ibest] & D.db_tags);
+        // ---- softmax (expf in fp32, stored as double) into LDS; then the
+        // sums in process order, as the reference adds them (softmax.hpp:
+        // 250-263, analysis.h:268-277), one sum per lane: 0 score_sum, 1
+        // score_sum_without_max, 2 malware_prob, 3.. the archive tags
+        uint8_t *fl = fl_lds[wid];
 #pragma unroll
         for (int c = 0; c < MAXP_CHUNKS; c++) {
             const uint32_t pi = (uint32_t)c * 64 + lane;
             if (pi < np) {
-                const double p = (double)expf((float)(sc[c] - mx));
-                ssum += p;
-                if (pi != imx) swo += p;
-                if (malbits & (1u << c)) mal += p;
-                if (pi == imx) p_imx = p;
-                if (pi == isx) p_isx = p;
+                scl[pi] = (double)expf_ref((float)(sc[c] - mx));
+                uint32_t f = (malbits >> c) & 1u;
+                if (tags) f |= ((D.proc_attr[po + pi] & tags) >> MFP_ATTR_DB_FIRST) << 1;
+                if (swap && pi == imx) f |= 0x80u;   // process_score[index_max] = 0 (analysis.h:264)
+                fl[pi] = (uint8_t)f;
             }
         }
-        ssum = sum_all(ssum); swo = sum_all(swo); mal = sum_all(mal);
-        p_imx = sum_all(p_imx); p_isx = sum_all(p_isx);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        double acc = 0.0;
+        const uint32_t nsum = tags ? 3u + MFP_ATTR_DB_TAGS : 3u;
+        if (lane < nsum) {
+            for (uint32_t p = 0; p < np; p++) {
+                const double e = scl[p];
+                const uint32_t f = fl[p];
+                const bool take = lane == 0 ? true
+                                : lane == 1 ? p != imx
+                                : lane == 2 ? (f & 1u) != 0
+                                : ((f >> (lane - 2)) & 1u) && !(f & 0x80u);
+                if (take) acc += e;
+            }
+        }
+        auto lane_d = [&](uint32_t l) {
+            return __hiloint2double(__builtin_amdgcn_readlane((int)(__double_as_longlong(acc) >> 32), (int)l),
+                                    __builtin_amdgcn_readlane((int)__double_as_longlong(acc), (int)l));
+        };
+        double ssum = lane_d(0), swo = lane_d(1), mal = lane_d(2);
+        const double p_imx = scl[imx], p_isx = scl[isx];
+        double ap = 0.0;   // lane k < MFP_ATTR_DB_TAGS: tag k's sum
+        if (tags) {
+#pragma unroll
+            for (int k = 0; k < MFP_ATTR_DB_TAGS; k++) {
+                const double v = lane_d(3 + k);
+                if ((int)lane == k) ap = v;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
         double max_score = p_imx;
         if (ssum > 0.0 && mdb) mal /= ssum;
-        uint32_t ibest = imx;
-        if (mdb && dmz == imx && !D.proc_mal[po + isx]) {
-            ibest = isx;
+        if (swap) {
             ssum = swo;
             max_score = p_isx;
         }
         if (ssum > 0.0) max_score /= ssum;
+        if (tags && P.attr_prob && lane < MFP_ATTR_DB_TAGS && ((tags >> (MFP_ATTR_DB_FIRST + lane)) & 1u))
+            P.attr_prob[(uint64_t)i * MFP_ATTR_DB_TAGS + lane] = ssum > 0.0 ? ap / ssum : ap;
         if (lane == 0) {
-            mfp_analysis a = P.out[i];   // status and pending flag from k_analyze
+            mfp_analysis a = P.out[i];   // status, pending flag and the additional attributes from k_analyze
             a.score = max_score;
             a.process = D.proc_id[po + ibest];
-            a.attr = (uint16_t)D.proc_attr[po + ibest];
+            a.proc_slot = po + ibest;
+            a.attr = (uint16_t)(D.proc_attr[po + ibest] | a.attr);
             a.malware_prob = -1.0;
             a.flags = (uint8_t)(MFP_AN_VALID | (a.flags & MFP_AN_PENDING));
             if (mdb) {
@@ -993,9 +1234,10 @@ __global__ __launch_bounds__(256) void k_analyze_resolve(AParams P, const uint8_
             seen = seen_seq[r++] != 0;
         }
         a.flags &= (uint8_t)~MFP_AN_PENDING;
-        if (seen) {
+        if (seen) {   // unlabeled: no process, no faketls; encrypted_dns / domain_faking stay
             a.status = 3;
-            a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0;
+            a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.proc_slot = MFP_NO_PROCESS;
+            a.attr &= (uint16_t)((1u << P.D.doh_idx) | (1u << P.D.domain_faking_idx));
             a.flags = MFP_AN_VALID;
         }
         if (P.mode == MFP_MODE_ANALYSIS && (rc.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
@@ -1014,6 +1256,7 @@ static mfpa::AParams make_params(const mfp_classifier_dev *D, const mfp_seen_tab
     P.D = *D;
     P.seen = T;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = mode;
+    P.attr_prob = nullptr;
     P.pend_bits = (uint64_t *)pending;
     P.deferred = (mfpa::Deferred *)deferred;
     P.lane_max_p = lane_max_p;
@@ -1023,10 +1266,12 @@ static mfpa::AParams make_params(const mfp_classifier_dev *D, const mfp_seen_tab
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
-                                   mfp_analysis *out, uint32_t *pending, void *deferred, unsigned long long *stats,
-                                   uint32_t mode, uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof) {
+                                   mfp_analysis *out, double *attr_prob, uint32_t *pending, void *deferred,
+                                   unsigned long long *stats, uint32_t mode, uint32_t lane_max_p, hipStream_t stream,
+                                   mfp_prof *prof) {
     if (n == 0) return 0;
     mfpa::AParams P = make_params(D, *T, arena, desc, n, rec, fp_arena, out, pending, deferred, stats, mode, lane_max_p);
+    P.attr_prob = attr_prob;
     uint64_t groups = (n + 63) / 64, blocks = (groups + mfpa::AW - 1) / mfpa::AW;
     if (blocks > 4096) blocks = 4096;
     if (prof) mfp_prof_begin(prof, "k_analyze", stream);

@@ -194,12 +194,16 @@ bool read_tgz(const char *path, F f) {
     return true;
 }
 
+// the lines of an archive member as the reference's loader sees them:
+// `while (archive.getline(line))` (analysis.h:859-930) strips the newline and
+// stops at the first empty line (getline returns the length, archive.h:247-270)
 template <class F>
 void for_lines(const std::string &s, F f) {
     size_t a = 0;
     while (a < s.size()) {
         size_t b = s.find('\n', a);
         if (b == std::string::npos) b = s.size();
+        if (b == a) break;
         std::string line = s.substr(a, b - a);
         f(line);
         a = b + 1;
@@ -220,8 +224,19 @@ struct Entry {
     std::vector<uint8_t> malware;
     std::vector<uint32_t> attr;
     std::vector<double> prior;
+    std::vector<std::vector<std::pair<std::string, uint64_t>>> os;   // per process: os_info (archive order)
     bool malware_db = false;
     FeatMap f[7];
+};
+
+typedef unsigned __int128 u128;
+
+// one domain-mappings.db prefix (subnet_data::domains_prefix, addr.cc:256-309)
+struct DomPrefix {
+    u128 addr;                  // host order, unmasked until process_domain_mappings_final
+    int len;
+    uint32_t type;              // MFP_DOM_MAPPING / MFP_DOM_EXCEPTION
+    std::vector<uint8_t> idx;   // mapped domain indices, uint8_t as the reference stores them
 };
 
 struct Weights { double as, domain, port, ip, sni, ua; double sum() const { return as + domain + port + ip + sni + ua; } };
@@ -252,6 +267,19 @@ struct mfp_classifier_s {
     std::vector<std::pair<std::string, uint32_t>> asn6;        // (16 bytes + len byte, asn)
     std::vector<std::string> proc_names;                       // global process-name table
     std::unordered_map<std::string, uint32_t> proc_name_id;
+    // encrypted_dns: doh-watchlist.txt (watchlist::process_line watchlist.hpp:624-652)
+    bool doh_enabled = false;
+    std::unordered_set<std::string> doh_names;
+    std::vector<uint32_t> doh_v4;
+    std::vector<std::pair<uint64_t, uint64_t>> doh_v6;
+    // domain_faking: domain-mappings.db (analysis.h:765-819, addr.cc:256-458)
+    bool faking_enabled = false;
+    std::unordered_map<std::string, uint32_t> dom_idx;         // subnet_data::domains_watchlist
+    std::vector<std::pair<std::string, std::string>> dom_lines4, dom_lines6;   // (subnet, tag) per family
+    std::vector<DomPrefix> dom4, dom6;
+    // os_info per process slot (flattened like the device's prior array)
+    std::vector<std::pair<uint32_t, uint32_t>> os_span;         // (first, count) into os_flat
+    std::vector<std::pair<std::string, uint64_t>> os_flat;
     mfp_classifier_dev dev;                                    // device tables (mfp_analysis.h)
     int device = -1;
 };
@@ -406,6 +434,11 @@ void process_fp_db_line(mfp_classifier_s &c, const std::string &line) {
             c.accept_attr = false;
         }
         e->attr.push_back(bits);
+        // os_info (analysis.h:195-205; loaded whatever report_os says, reported only when it is on)
+        e->os.emplace_back();
+        if (const JV *oi = x.get("os_info"); oi && oi->t == JV::OBJ)
+            for (auto &kv : oi->o)
+                if (!kv.first.empty()) e->os.back().push_back({kv.first, kv.second.is_uint ? kv.second.u : 0});
         if (x.t == JV::OBJ) {
             // domain_name_model: sni (normalized keys) then domains
             const JV *sni = x.get("classes_hostname_sni");
@@ -509,6 +542,121 @@ void process_asn_line(mfp_classifier_s &c, const std::string &line) {
     }
 }
 
+// dns_string (watchlist.hpp:54-83): the host name at the start of s (labels
+// of [A-Za-z0-9_-] separated by dots, an optional leading "*.", the last
+// label holding a letter); trailing bytes are left unparsed
+bool dns_prefix(const std::string &s, std::string &out) {
+    size_t p = 0;
+    const size_t n = s.size();
+    if (p < n && s[p] == '*') {
+        p++;
+        if (p < n && s[p] == '.') p++;
+        else return false;
+    }
+    long ls = -1, le = -1;
+    while (p < n) {
+        const size_t a = p;
+        while (p < n && mfpc::is_label_char((uint8_t)s[p])) p++;
+        if (p == a) break;
+        ls = (long)a; le = (long)p;
+        if (p < n && s[p] == '.') p++;
+        else break;
+    }
+    bool alpha = false;
+    for (long k = ls; k >= 0 && k < le; k++) alpha |= mfpc::is_alpha((uint8_t)s[k]);
+    if (!alpha) return false;
+    out = s.substr(0, (size_t)le);
+    return true;
+}
+
+// watchlist::process_line (watchlist.hpp:624-652): an IPv4 address, else a
+// DNS name, else an IPv6 address; '#' comments and empty lines are skipped,
+// anything else is ignored (the loader drops process_line's false)
+void process_doh_line(mfp_classifier_s &c, const std::string &line) {
+    if (line.empty() || line[0] == '#') return;
+    const uint8_t *s = (const uint8_t *)line.data();
+    int pos = 0;
+    uint32_t v4;
+    if (mfpc::parse_ipv4(s, (int)line.size(), pos, v4)) { c.doh_v4.push_back(v4); return; }
+    std::string name;
+    if (dns_prefix(line, name)) { c.doh_names.insert(name); return; }
+    pos = 0;
+    uint8_t a[16];
+    if (mfpc::parse_ipv6(s, (int)line.size(), pos, a)) {
+        uint64_t hi = 0, lo = 0;
+        for (int k = 0; k < 8; k++) { hi = hi << 8 | a[k]; lo = lo << 8 | a[8 + k]; }
+        c.doh_v6.push_back({hi, lo});
+    }
+}
+
+// classifier::process_domain_mapping_line (analysis.h:765-819): the subnet
+// and its tag ("proxy"/"sinkhole" entries carry their type as the tag); a
+// '.' in the subnet makes it IPv4
+void process_domain_line(mfp_classifier_s &c, const std::string &line) {
+    JV o;
+    if (!parse_json(line, o) || o.t != JV::OBJ) return;
+    const JV *sub = o.get("subnet"), *type = o.get("type"), *tag = o.get("tag");
+    if (!sub || sub->t != JV::STR || !type || type->t != JV::STR || !tag || tag->t != JV::STR) return;
+    std::string t;
+    if (type->s == "domain_mapping") t = tag->s;
+    else if (type->s == "proxy" || type->s == "sinkhole") t = type->s;
+    else return;
+    (sub->s.find('.') != std::string::npos ? c.dom_lines4 : c.dom_lines6).push_back({sub->s, t});
+}
+
+// subnet_data::lct_add_domain_mapping / lct_add_domain_exception (addr.cc:256-309,
+// 350-403): a mapping whose exact (address, length) was seen before gains the
+// domain index (its length differing: dropped); an exception is always a new
+// prefix; indices are stored as uint8_t
+template <class Map>
+void add_domain_prefix(mfp_classifier_s &c, std::vector<DomPrefix> &v, Map &seen, u128 addr, int len,
+                       const std::string &tag) {
+    if (tag == "proxy" || tag == "sinkhole") {
+        v.push_back(DomPrefix{addr, len, MFP_DOM_EXCEPTION, {}});
+        return;
+    }
+    uint32_t idx;
+    auto it = c.dom_idx.find(tag);
+    if (it == c.dom_idx.end()) { idx = (uint32_t)c.dom_idx.size(); c.dom_idx[tag] = idx; }
+    else idx = it->second;
+    auto s = seen.find(addr);
+    if (s != seen.end()) {
+        DomPrefix &p = v[s->second];
+        if (p.type == MFP_DOM_MAPPING && p.addr == addr && p.len == len) p.idx.push_back((uint8_t)idx);
+        return;
+    }
+    seen[addr] = v.size();
+    v.push_back(DomPrefix{addr, len, MFP_DOM_MAPPING, {(uint8_t)idx}});
+}
+
+struct U128Hash { size_t operator()(u128 x) const { return std::hash<uint64_t>()((uint64_t)x ^ (uint64_t)(x >> 64) * 31); } };
+
+// process_domain_mapping_subnets[_v6] (addr.cc:311-348, 405-458): IPv4 lines
+// first (their domains get the first indices), then IPv6
+void build_domain_prefixes(mfp_classifier_s &c) {
+    std::unordered_map<u128, size_t, U128Hash> seen4, seen6;
+    for (auto &e : c.dom_lines4) {
+        uint32_t addr = 0;
+        unsigned char *dq = (unsigned char *)&addr;   // host order, as the reference fills it
+        uint8_t len = 0;
+        if (sscanf(e.first.c_str(), "%hhu.%hhu.%hhu.%hhu/%hhu", dq + 3, dq + 2, dq + 1, dq, &len) != 5) continue;
+        if (len == 0 || len > 32) continue;
+        add_domain_prefix(c, c.dom4, seen4, (u128)addr, len, e.second);
+    }
+    for (auto &e : c.dom_lines6) {
+        char a[46];
+        uint8_t len = 0;
+        if (sscanf(e.first.c_str(), "%45[^/]/%hhu", a, &len) != 2) continue;
+        if (len == 0 || len > 128) break;   // the reference abandons the rest of the IPv6 list
+        int pos = 0;
+        uint8_t b[16];
+        if (!mfpc::parse_ipv6((const uint8_t *)a, (int)strlen(a), pos, b)) continue;
+        u128 v = 0;
+        for (int k = 0; k < 16; k++) v = v << 8 | b[k];
+        add_domain_prefix(c, c.dom6, seen6, v, len, e.second);
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -538,6 +686,12 @@ mfp_classifier *mfp_classifier_load(const char *path) {
             } else if (name == "pyasn.db") {
                 for_lines(data, [&](const std::string &l) { process_asn_line(*c, l); });
                 got_asn = true;
+            } else if (name == "doh-watchlist.txt") {
+                for_lines(data, [&](const std::string &l) { process_doh_line(*c, l); });
+                c->doh_enabled = true;
+            } else if (name == "domain-mappings.db") {
+                for_lines(data, [&](const std::string &l) { process_domain_line(*c, l); });
+                c->faking_enabled = true;
             }
         });
         if (!ok) { mfp_set_error("cannot read resource archive %s", path); return nullptr; }
@@ -553,14 +707,34 @@ mfp_classifier *mfp_classifier_load(const char *path) {
     if (std::count(c->version.begin(), c->version.end(), ';') != 1) c->disabled = true;
     if (!got_db || !got_prev || !got_ver || !got_asn) c->disabled = true;
     c->accept_attr = false;
-    // global process-name table
-    for (auto &e : c->entries)
+    build_domain_prefixes(*c);
+    // global process-name table; os_info per process slot
+    for (auto &e : c->entries) {
         for (auto &n : e->proc_name)
             if (!c->proc_name_id.count(n)) {
                 c->proc_name_id[n] = (uint32_t)c->proc_names.size();
                 c->proc_names.push_back(n);
             }
+        for (size_t i = 0; i < e->prior.size(); i++) {
+            const auto &os = i < e->os.size() ? e->os[i] : std::vector<std::pair<std::string, uint64_t>>{};
+            c->os_span.push_back({(uint32_t)c->os_flat.size(), (uint32_t)os.size()});
+            c->os_flat.insert(c->os_flat.end(), os.begin(), os.end());
+        }
+    }
     return c.release();
+}
+
+int mfp_classifier_attr_count(const mfp_classifier *c) { return (int)c->attr_names.size(); }
+const char *mfp_classifier_version(const mfp_classifier *c) { return c->version.c_str(); }
+
+int mfp_classifier_os_info(const mfp_classifier *c, uint32_t slot, uint32_t k, const char **name, uint64_t *prev) {
+    if (slot >= c->os_span.size()) return -1;
+    const auto &sp = c->os_span[slot];
+    if (k < sp.second) {
+        if (name) *name = c->os_flat[sp.first + k].first.c_str();
+        if (prev) *prev = c->os_flat[sp.first + k].second;
+    }
+    return (int)sp.second;
 }
 
 void mfp_classifier_free(mfp_classifier *c) {
@@ -619,7 +793,75 @@ struct HostTables {
     std::vector<mfp_fp_slot> prev_slots;   // known prevalence set
     std::vector<mfp_asn4> asn4;
     std::vector<mfp_asn6> asn6;
+    // additional attributes
+    std::vector<mfp_fp_slot> doh_names, dom_slots;
+    std::vector<uint32_t> doh_v4;
+    std::vector<uint64_t> doh_v6;
+    std::vector<mfp_asn4> dom4;
+    std::vector<mfp_asn6> dom6;
+    std::vector<uint32_t> dom_info;
+    std::vector<uint8_t> dom_bytes;
 };
+
+// a prefix for the longest-match sweep: [lo, hi], its value, its length
+struct Pfx { u128 lo, hi; uint32_t val; int len; };
+struct Iv { u128 lo, hi; uint32_t val; };
+
+// lctrie preparation (addr.cc:460-518 / 584-705): masked prefixes sorted by
+// (address, length) -- glibc's qsort is a stable merge sort -- then
+// subnet_dedup (lctrie_ip.hpp:383-420), kept literally: of two adjacent equal
+// prefixes the first stays, and the loop steps past the survivor, so a third
+// copy is compared with the one after it
+void sort_dedup(std::vector<Pfx> &v) {
+    std::stable_sort(v.begin(), v.end(), [](const Pfx &a, const Pfx &b) { return a.lo != b.lo ? a.lo < b.lo : a.len < b.len; });
+    size_t size = v.size();
+    for (size_t i = 0, j = 1; j < size; ++i, ++j)
+        if (v[i].lo == v[j].lo && v[i].len == v[j].len) {
+            v.erase(v.begin() + (long)j);
+            --size;
+        }
+}
+
+// lct_find (lctrie.hpp:348) as disjoint intervals: the prefixes are nested
+// or disjoint, so one sweep in (start, length) order with a stack of open
+// prefixes gives every address range its innermost (longest) prefix
+std::vector<Iv> lpm_intervals(const std::vector<Pfx> &ps) {
+    std::vector<Iv> out;
+    std::vector<Pfx> st;
+    u128 cursor = 0;
+    bool wrapped = false;   // the cursor passed the top of the space
+    auto emit = [&](u128 lo, u128 hi, uint32_t v) { if (!wrapped && lo <= hi) out.push_back(Iv{lo, hi, v}); };
+    auto close_top = [&]() {
+        const Pfx b = st.back();
+        emit(std::max(cursor, b.lo), b.hi, b.val);
+        if (b.hi == ~(u128)0) wrapped = true;
+        else cursor = std::max(cursor, b.hi + 1);
+        st.pop_back();
+    };
+    for (auto &p : ps) {
+        while (!st.empty() && st.back().hi < p.lo) close_top();
+        if (!st.empty() && p.lo > 0) emit(std::max(cursor, st.back().lo), p.lo - 1, st.back().val);
+        cursor = std::max(cursor, p.lo);
+        st.push_back(p);
+    }
+    while (!st.empty()) close_top();
+    return out;
+}
+
+Pfx pfx(u128 addr, int len, int bits, uint32_t val) {
+    const u128 span = len == 0 ? (bits == 128 ? ~(u128)0 : (((u128)1 << bits) - 1)) : (((u128)1 << (bits - len)) - 1);
+    const u128 lo = addr & ~span;
+    return Pfx{lo, lo + span, val, len};
+}
+
+mfp_asn4 iv4(const Iv &v) { mfp_asn4 r; r.lo = (uint32_t)v.lo; r.hi = (uint32_t)v.hi; r.asn = v.val; r.pad = 0; return r; }
+mfp_asn6 iv6(const Iv &v) {
+    mfp_asn6 r;
+    r.lo_hi = (uint64_t)(v.lo >> 64); r.lo_lo = (uint64_t)v.lo;
+    r.hi_hi = (uint64_t)(v.hi >> 64); r.hi_lo = (uint64_t)v.hi;
+    r.asn = v.val; r.pad = 0;
+    return r;
+}
 
 uint32_t pool_add(HostTables &t, const std::string &s) {
     uint32_t off = (uint32_t)t.pool.size();
@@ -708,81 +950,58 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
                 put_feat(eid, k, mfpc::str_hash((const uint8_t *)kv.first.data(), 16), kv.second, &kv.first);
         }
     }
-    // ASN: disjoint intervals of the IPv4 prefixes, longest prefix wins
-    // (lct_find semantics); prefixes are nested or disjoint, so one sweep
-    // with a stack of open prefixes emits the elementary intervals
+    // ASN (subnet_data::get_asn_info addr.cc:172-208): longest-prefix match
+    // over the deduplicated prefixes, as disjoint intervals
     {
-        struct P { uint64_t lo, hi; uint32_t asn; int len; };
-        std::vector<P> ps;
-        for (auto &p : c->asn4) {
-            int len = (int)(p.first & 0xff);
-            uint64_t lo = p.first >> 8, hi = lo + (len == 0 ? (1ULL << 32) : (1ULL << (32 - len))) - 1;
-            ps.push_back({lo, hi, p.second, len});
-        }
-        std::stable_sort(ps.begin(), ps.end(), [](const P &a, const P &b) {
-            return a.lo != b.lo ? a.lo < b.lo : a.len < b.len;
-        });
-        std::vector<P> st;
-        uint64_t cursor = 0;
-        auto emit = [&](uint64_t lo, uint64_t hi, uint32_t asn) {
-            if (lo <= hi) t.asn4.push_back(mk4((uint32_t)lo, (uint32_t)hi, asn));
-        };
-        for (auto &p : ps) {
-            while (!st.empty() && st.back().hi < p.lo) {
-                emit(std::max(cursor, st.back().lo), st.back().hi, st.back().asn);
-                cursor = std::max(cursor, st.back().hi + 1);
-                st.pop_back();
-            }
-            if (!st.empty() && p.lo > 0) emit(std::max(cursor, st.back().lo), p.lo - 1, st.back().asn);
-            cursor = std::max(cursor, p.lo);
-            st.push_back(p);
-        }
-        while (!st.empty()) {
-            emit(std::max(cursor, st.back().lo), st.back().hi, st.back().asn);
-            cursor = std::max(cursor, st.back().hi + 1);
-            st.pop_back();
-        }
-    }
-    // IPv6: the same sweep on 128-bit keys
-    {
-        typedef unsigned __int128 u128;
-        struct P { u128 lo, hi; uint32_t asn; int len; };
-        std::vector<P> ps;
+        std::vector<Pfx> ps;
+        for (auto &p : c->asn4) ps.push_back(pfx((u128)(p.first >> 8), (int)(p.first & 0xff), 32, p.second));
+        sort_dedup(ps);
+        for (auto &v : lpm_intervals(ps)) t.asn4.push_back(iv4(v));
+        ps.clear();
         for (auto &p : c->asn6) {
             u128 lo = 0;
             for (int k = 0; k < 16; k++) lo = lo << 8 | (uint8_t)p.first[k];
-            int len = (uint8_t)p.first[16];
-            u128 span = len == 0 ? ~(u128)0 : (((u128)1 << (128 - len)) - 1);
-            ps.push_back({lo, lo + span, p.second, len});
+            ps.push_back(pfx(lo, (uint8_t)p.first[16], 128, p.second));
         }
-        std::stable_sort(ps.begin(), ps.end(), [](const P &a, const P &b) {
-            return a.lo != b.lo ? a.lo < b.lo : a.len < b.len;
-        });
-        std::vector<P> st;
-        u128 cursor = 0;
-        bool wrapped = false;   // cursor passed the top of the space
-        auto emit = [&](u128 lo, u128 hi, uint32_t asn) {
-            if (lo > hi) return;
-            mfp_asn6 r;
-            r.lo_hi = (uint64_t)(lo >> 64); r.lo_lo = (uint64_t)lo;
-            r.hi_hi = (uint64_t)(hi >> 64); r.hi_lo = (uint64_t)hi;
-            r.asn = asn; r.pad = 0;
-            t.asn6.push_back(r);
-        };
-        auto close_top = [&]() {
-            P &b = st.back();
-            if (!wrapped) emit(std::max(cursor, b.lo), b.hi, b.asn);
-            if (b.hi == ~(u128)0) wrapped = true;
-            else cursor = std::max(cursor, b.hi + 1);
-            st.pop_back();
-        };
-        for (auto &p : ps) {
-            while (!st.empty() && st.back().hi < p.lo) close_top();
-            if (!st.empty() && p.lo > 0 && !wrapped) emit(std::max(cursor, st.back().lo), p.lo - 1, st.back().asn);
-            cursor = std::max(cursor, p.lo);
-            st.push_back(p);
+        sort_dedup(ps);
+        for (auto &v : lpm_intervals(ps)) t.asn6.push_back(iv6(v));
+    }
+    // encrypted_dns watchlist: names (hash table), addresses (sorted sets)
+    t.doh_names.assign(pow2_at_least(2 * c->doh_names.size() + 2), mfp_fp_slot{0, 0xffffffffu, 0, 0});
+    for (auto &nm : c->doh_names)
+        insert_string_slot(t.doh_names, mfpc::str_hash((const uint8_t *)nm.data(), (uint32_t)nm.size()), 0,
+                           pool_add(t, nm), (uint32_t)nm.size());
+    t.doh_v4 = c->doh_v4;
+    std::sort(t.doh_v4.begin(), t.doh_v4.end());
+    t.doh_v4.erase(std::unique(t.doh_v4.begin(), t.doh_v4.end()), t.doh_v4.end());
+    {
+        auto v6 = c->doh_v6;
+        std::sort(v6.begin(), v6.end());
+        v6.erase(std::unique(v6.begin(), v6.end()), v6.end());
+        for (auto &x : v6) { t.doh_v6.push_back(x.first); t.doh_v6.push_back(x.second); }
+    }
+    // domain_faking: mapped domains (hash table -> domain index) and the
+    // mapping / exception prefixes (process_domain_mappings_final[_v6]
+    // addr.cc:584-705: masked, sorted, deduplicated, longest match)
+    t.dom_slots.assign(pow2_at_least(2 * c->dom_idx.size() + 2), mfp_fp_slot{0, 0xffffffffu, 0, 0});
+    for (auto &kv : c->dom_idx)
+        insert_string_slot(t.dom_slots, mfpc::str_hash((const uint8_t *)kv.first.data(), (uint32_t)kv.first.size()),
+                           kv.second, pool_add(t, kv.first), (uint32_t)kv.first.size());
+    for (int fam = 0; fam < 2; fam++) {
+        const std::vector<DomPrefix> &src = fam == 0 ? c->dom4 : c->dom6;
+        std::vector<Pfx> ps;
+        for (size_t k = 0; k < src.size(); k++) ps.push_back(pfx(src[k].addr, src[k].len, fam == 0 ? 32 : 128, (uint32_t)k));
+        sort_dedup(ps);
+        for (auto &v : lpm_intervals(ps)) {
+            const DomPrefix &dp = src[v.val];
+            const uint32_t info = (uint32_t)t.dom_info.size() / 2;
+            t.dom_info.push_back(dp.type | (uint32_t)dp.idx.size() << 8);
+            t.dom_info.push_back((uint32_t)t.dom_bytes.size());
+            t.dom_bytes.insert(t.dom_bytes.end(), dp.idx.begin(), dp.idx.end());
+            Iv w = v;
+            w.val = info + 1;
+            if (fam == 0) t.dom4.push_back(iv4(w)); else t.dom6.push_back(iv6(w));
         }
-        while (!st.empty()) close_top();
     }
     if (t.pool.empty()) t.pool.push_back(0);
     if (t.upd.empty()) t.upd.push_back(mfp_update{0, 0, 0});
@@ -790,6 +1009,12 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0, 0, {0, 0, 0}});
     if (t.asn4.empty()) t.asn4.push_back(mk4(1, 0, 0));
     if (t.asn6.empty()) { mfp_asn6 r{}; r.lo_lo = 1; t.asn6.push_back(r); }
+    if (t.doh_v4.empty()) t.doh_v4.push_back(0);
+    if (t.doh_v6.empty()) { t.doh_v6.push_back(0); t.doh_v6.push_back(0); }
+    if (t.dom4.empty()) t.dom4.push_back(mk4(1, 0, 0));
+    if (t.dom6.empty()) { mfp_asn6 r{}; r.lo_lo = 1; t.dom6.push_back(r); }
+    if (t.dom_info.empty()) { t.dom_info.push_back(0); t.dom_info.push_back(0); }
+    if (t.dom_bytes.empty()) t.dom_bytes.push_back(0);
 
     mfp_classifier_dev &d = c->dev;
     mfp_classifier_free_device(d);
@@ -803,7 +1028,9 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     bool ok = up(d.fp_slots, t.fp_slots) && up(d.prev_slots, t.prev_slots) && up(d.entry, t.entry) &&
               up(d.prior, t.prior) && up(d.proc_id, t.proc_id) && up(d.proc_mal, t.proc_mal) &&
               up(d.proc_attr, t.proc_attr) && up(d.feat_slots, t.feat_slots) && up(d.upd, t.upd) && up(d.pool, t.pool) &&
-              up(d.asn4, t.asn4) && up(d.asn6, t.asn6);
+              up(d.asn4, t.asn4) && up(d.asn6, t.asn6) && up(d.doh_names, t.doh_names) &&
+              up(d.doh_v4, t.doh_v4) && up(d.doh_v6, t.doh_v6) && up(d.dom_slots, t.dom_slots) &&
+              up(d.dom4, t.dom4) && up(d.dom6, t.dom6) && up(d.dom_info, t.dom_info) && up(d.dom_bytes, t.dom_bytes);
     if (!ok) { mfp_set_error("classifier device upload failed"); return -2; }
     d.fp_mask = t.fp_slots.size() - 1;
     d.prev_mask = t.prev_slots.size() - 1;
@@ -819,12 +1046,25 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     for (uint32_t ty : c->fp_types) d.types_mask |= 1u << ty;
     d.enc_channel_idx = 7;
     d.faketls_idx = 9;
+    d.doh_idx = 6;
+    d.domain_faking_idx = 8;
+    d.db_tags = 0;
+    for (size_t k = MFP_ATTR_DB_FIRST; k < c->attr_names.size() && k < MFP_ATTR_MAX_TAGS; k++) d.db_tags |= 1u << k;
+    d.doh_enabled = c->doh_enabled;
+    d.doh_names_mask = t.doh_names.size() - 1;
+    d.n_doh_v4 = (uint32_t)c->doh_v4.size() ? (uint32_t)t.doh_v4.size() : 0;
+    d.n_doh_v6 = (uint32_t)(c->doh_v6.empty() ? 0 : t.doh_v6.size() / 2);
+    d.faking_enabled = c->faking_enabled;
+    d.dom_mask = t.dom_slots.size() - 1;
+    d.n_dom4 = (uint32_t)t.dom4.size();
+    d.n_dom6 = c->dom6.empty() ? 0 : (uint32_t)t.dom6.size();
     return 0;
 }
 
 void mfp_classifier_free_device(mfp_classifier_dev &d) {
     void *ptrs[] = {d.fp_slots, d.prev_slots, d.entry, d.prior, d.proc_id, d.proc_mal, d.proc_attr,
-                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn6};
+                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn6, d.doh_names, d.doh_v4, d.doh_v6,
+                    d.dom_slots, d.dom4, d.dom6, d.dom_info, d.dom_bytes};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = mfp_classifier_dev{};
 }

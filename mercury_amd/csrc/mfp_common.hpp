@@ -210,6 +210,35 @@ MFP_HD int put_ipv6(char *out, int o, const uint8_t a[16]) {
     return o;
 }
 
+// The classifier sees a flow's destination as text (key::sprintf_dst_addr
+// flow_key.h:206-231, i.e. append_ipv6_addr above) parsed back
+// (ipv6_address_string ip_address.hpp:643-880).  With the printer's run
+// bookkeeping the "::" can stand for pieces that are not zero, so the
+// address it classifies is the packet's with pieces [lr, lr + lr_len) zeroed.
+// hi/lo: the address as two big-endian halves.
+MFP_HD void v6_text_roundtrip(uint64_t &hi, uint64_t &lo) {
+    uint32_t pc[8];
+    for (int i = 0; i < 4; i++) {
+        pc[i] = (uint32_t)(hi >> (48 - 16 * i)) & 0xffff;
+        pc[4 + i] = (uint32_t)(lo >> (48 - 16 * i)) & 0xffff;
+    }
+    int run = -1, run_len = 0, lr = -1, lr_len = 0;
+    for (int i = 0; i < 8; i++) {
+        if (pc[i] == 0) {
+            if (run_len == 0) run = i;
+            run_len++;
+        } else if (run_len != 0 && lr_len < run_len) {
+            lr_len = run_len; lr = run; run_len = 0;
+        }
+    }
+    if (lr_len < run_len) { lr_len = run_len; lr = run; }
+    if (lr_len < 2) return;   // no "::": all eight pieces printed
+    for (int i = lr; i < lr + lr_len && i < 8; i++) {
+        if (i < 4) hi &= ~((uint64_t)0xffff << (48 - 16 * i));
+        else lo &= ~((uint64_t)0xffff << (48 - 16 * (i - 4)));
+    }
+}
+
 // returns the normalized length; out must hold >= 330 bytes
 MFP_HD int normalize_server_name(const uint8_t *s, int len, char *out) {
     int o = 0;

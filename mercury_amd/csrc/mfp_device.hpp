@@ -900,7 +900,18 @@ DEV void tls_ch_fp(E &b, const Ch &ch, int fmt) {   // tls.h:1928
     else exts_fp12(b, ch.extensions, 0, fmt);
 }
 // tls_extensions::set_meta_data tls.h:1316 (server_name; last one wins)
-DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len) {
+// the ALPN extension's protocol_name_list (tls.h:1357-1362, protocol_name_list
+// tls.h:1172-1176: a 16-bit length, then that many bytes; short: none)
+DEV void tls_alpn(const uint8_t *start, const uint8_t *end, const uint8_t *base, uint32_t &off, uint32_t &len) {
+    Cur e = cmk(start, end);
+    cskip(e, 4);
+    uint64_t l;
+    if (rd_uint(e, 2, l) && (uint64_t)clen(e) >= l) { off = (uint32_t)(e.d - base); len = (uint32_t)l; }
+    else { off = 0; len = 0xffff; }
+}
+// server name (tls_extensions::set_meta_data tls.h:1316-1366; the last one
+// wins) and ALPN list of a ClientHello's extensions
+DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len, uint32_t &aoff, uint32_t &alen) {
     Cur p = exts;
     while (clen(p) > 0) {
         const uint8_t *start = p.d;
@@ -913,6 +924,7 @@ DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len) {
             cskip(e, 9);
             off = (uint32_t)(e.d - base); len = (uint32_t)clen(e);
         }
+        if (t == 16) tls_alpn(start, p.d, base, aoff, alen);
     }
 }
 // ClientHello plan: pass 1 of the lane kernels records what pass 2 needs to
@@ -934,7 +946,7 @@ struct TlsPlan {
 // one wins) and the plan -- one walk over the extension list
 template <class E>
 DEV void tls_ch_plan(E &b, TlsPlan &pl, const Ch &ch, int fmt, uint32_t type, const uint8_t *base,
-                     uint32_t &sni_off, uint32_t &sni_len) {
+                     uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len) {
     pl.ok = false;
     fp_type_prefix(b, type);
     if (fmt >= 1 && fmt <= 2) { b.putc('0' + fmt); b.putc('/'); }
@@ -957,6 +969,7 @@ DEV void tls_ch_plan(E &b, TlsPlan &pl, const Ch &ch, int fmt, uint32_t type, co
             cskip(e, 9);
             sni_off = (uint32_t)(e.d - base); sni_len = (uint32_t)clen(e);
         }
+        if (x.type == 16) tls_alpn(start, p.d, base, alpn_off, alpn_len);
         if (rare) continue;
         int bucket = 0;
         if (fmt == 2) {
@@ -1454,12 +1467,13 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         Ch ch = tls_ch_parse(hs.body);
         if (!cnotempty(ch.compression)) return;
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 1;
+        if (clen(ch.ciphers) <= 0) o.flags |= MFP_FLAG_NO_CIPHERS;   // no "tls" object (tls.h:1882-1885)
         if constexpr (E::PLAN) {
-            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len);
+            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
         } else {
             fp_type_prefix(b, 1);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
-            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
         }
         return;
         }
@@ -1608,12 +1622,13 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         Ch ch = tls_ch_parse(body);
         if (!cnotempty(ch.compression)) return;
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 10;
+        if (clen(ch.ciphers) <= 0) o.flags |= MFP_FLAG_NO_CIPHERS;   // no "dtls" object (tls.h:1882-1885)
         if constexpr (E::PLAN) {
-            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len);
+            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
         } else {
             fp_type_prefix(b, 10);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
-            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len);
+            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
         }
     } else if (msg == MFP_MSG_DTLS_SH) {
         Cur b2 = body;

@@ -22,8 +22,9 @@
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
-                                   mfp_analysis *out, uint32_t *pending, void *deferred, unsigned long long *stats,
-                                   uint32_t mode, uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof);
+                                   mfp_analysis *out, double *attr_prob, uint32_t *pending, void *deferred,
+                                   unsigned long long *stats, uint32_t mode, uint32_t lane_max_p, hipStream_t stream,
+                                   mfp_prof *prof);
 extern "C" int mfp_launch_seen_export(const mfp_seen_tab *T, uint32_t u, mfp_sighting *out, hipStream_t stream);
 extern "C" int mfp_launch_seen_sequence(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
                                         const mfp_record *rec, const uint8_t *fp_arena, uint32_t *pending,
@@ -245,6 +246,7 @@ struct Slot {
     uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings (bitmap)
     uint4 *d_deferred = nullptr; size_t cap_deferred = 0;    // packets for the wave-per-packet scorer (64 B each)
     mfp_analysis *d_an = nullptr; size_t cap_an = 0;
+    double *d_ap = nullptr; size_t cap_ap = 0;               // archive-tag probabilities of host batches
     // the unknown-TLS sightings of the batch analysed in this slot (mfp_prevalence)
     mfp_seen_tab seen;
     mfp_sighting *d_sight = nullptr;                          // distinct list export
@@ -275,7 +277,7 @@ struct Slot {
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
-        void *p[] = {d_used, d_bins, d_work, d_an_stats, d_pending, d_deferred, d_an, d_arena, d_desc, d_rec, d_fp, d_fp2,
+        void *p[] = {d_used, d_bins, d_work, d_an_stats, d_pending, d_deferred, d_an, d_ap, d_arena, d_desc, d_rec, d_fp, d_fp2,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         if (h_used) (void)hipHostFree(h_used);
@@ -297,6 +299,7 @@ struct mfp_context_s {
     mfp_prevalence own_prev = nullptr;   // the context's fingerprint_prevalence LRU
     mfp_prevalence prev = nullptr;       // the one its sightings are decided against (own or shared)
     bool defer = false;                  // mfp_analysis_defer
+    bool report_os = false;              // libmerc_config.report_os (mfp_analysis_report_os)
     Slot slot[3];
     int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
@@ -444,7 +447,8 @@ static int seen_reserve(Slot &S, size_t n, hipStream_t s) {
 }
 
 static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
-                          mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, hipStream_t s) {
+                          mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, double *d_attr_prob,
+                          hipStream_t s) {
     Slot &S = c->slot[slot];
     HIPCHK(hipSetDevice(c->device));
     if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_deferred, S.cap_deferred, 4 * (n + 1)) ||
@@ -454,8 +458,8 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
     }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
     HIPCHK(hipMemsetAsync(S.d_an_stats, 0, 4 * sizeof(unsigned long long), s));
-    if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, S.d_pending,
-                            S.d_deferred, S.d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
+    if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, d_attr_prob,
+                            S.d_pending, S.d_deferred, S.d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
@@ -566,9 +570,12 @@ extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t 
 // of its records (the pipeline retires chunks in order, after their D2H)
 static void host_patch(mfp_context c, mfp_analysis &a, const mfp_record &r, bool seen) {
     a.flags &= (uint8_t)~MFP_AN_PENDING;
-    if (seen) {
+    if (seen) {   // as k_analyze_resolve: unlabeled keeps encrypted_dns / domain_faking only
+        const mfp_classifier_dev *D = mfp_classifier_device(c->clf);
         a.status = 3;
-        a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.flags = MFP_AN_VALID;
+        a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.proc_slot = MFP_NO_PROCESS;
+        a.attr &= (uint16_t)((1u << D->doh_idx) | (1u << D->domain_faking_idx));
+        a.flags = MFP_AN_VALID;
     }
     if (c->mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
 }
@@ -606,7 +613,7 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
 // pointer handed to the kernels is the staging buffer minus the (256-byte
 // aligned) start of the copied span
 static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
-                            size_t n, size_t fp_cap, bool analysis) {
+                            size_t n, size_t fp_cap, bool analysis, bool attr_prob) {
     Slot &S = c->slot[slot];
     uint64_t lo = UINT64_MAX, hi = 0;
     for (size_t i = 0; i < n; i++) {
@@ -621,7 +628,8 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     // that holds a packet's last byte
     if (grow(S.d_arena, S.cap_arena, span + 64) || grow(S.d_desc, S.cap_desc, n + 1) || grow(S.d_rec, S.cap_rec, n + 1) ||
         grow(S.d_fp, S.cap_fp, fp_cap + 64) || grow(S.d_fp2, S.cap_fp2, fp_cap + 64) ||
-        (analysis && grow(S.d_an, S.cap_an, n + 1))) {
+        (analysis && grow(S.d_an, S.cap_an, n + 1)) ||
+        (analysis && attr_prob && grow(S.d_ap, S.cap_ap, MFP_ATTR_DB_TAGS * (n + 1)))) {
         mfp_set_error("device allocation failed");
         return -2;
     }
@@ -632,7 +640,7 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, fp_cap, (uint64_t *)S.d_used, S.stream);
     if (r) return r;
     if (analysis) {
-        r = analyze_locked(c, slot, d_base, S.d_desc, n, S.d_rec, S.d_fp, S.d_an, S.stream);
+        r = analyze_locked(c, slot, d_base, S.d_desc, n, S.d_rec, S.d_fp, S.d_an, attr_prob ? S.d_ap : nullptr, S.stream);
         if (r) return r;
         // the synchronous host batch decides its unknown-TLS sightings now;
         // pipeline slots when they retire (chunk order), on the host copies
@@ -651,16 +659,19 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
 
 extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                           const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
-                                                          char *fp_arena, size_t fp_cap, mfp_analysis *analysis) {
+                                                          char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                                          double *attr_prob) {
     if (!c) { mfp_set_error("null context"); return -1; }
     if (analysis && !c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
     if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
     Slot &S = c->slot[0];
-    int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, analysis != nullptr);
+    int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, analysis != nullptr, attr_prob != nullptr);
     if (r) return r;
     if (analysis && n) HIPCHK(hipMemcpyAsync(analysis, S.d_an, n * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
+    if (analysis && attr_prob && n)
+        HIPCHK(hipMemcpyAsync(attr_prob, S.d_ap, n * MFP_ATTR_DB_TAGS * sizeof(double), hipMemcpyDeviceToHost, S.stream));
     if (n) HIPCHK(hipMemcpyAsync(rec, S.d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
@@ -673,22 +684,22 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
 extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                        const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                        char *fp_arena, size_t fp_cap) {
-    return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, nullptr);
+    return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, nullptr, nullptr);
 }
 
 static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                                   size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
-                                  size_t chunk);
+                                  double *attr_prob, size_t chunk);
 
 extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                       const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                       char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
-                                                      size_t chunk) {
+                                                      double *attr_prob, size_t chunk) {
     if (!c) { mfp_set_error("null context"); return -1; }
     if (analysis && !c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     if (hipSetDevice(c->device) != hipSuccess) { mfp_set_error("hipSetDevice failed"); return -2; }
-    const long long r = pipelined_locked(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, chunk);
+    const long long r = pipelined_locked(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, attr_prob, chunk);
     if (r < 0) {
         // an error path may leave copies into the caller's buffers queued on
         // either pipeline stream: drain both before the caller reuses them
@@ -700,7 +711,7 @@ extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8
 
 static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                                   size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
-                                  size_t chunk) {
+                                  double *attr_prob, size_t chunk) {
     if (chunk == 0) chunk = (size_t)1 << 20;
     struct Inflight { bool live; size_t lo, hi; };
     Inflight inf[2] = {{false, 0, 0}, {false, 0, 0}};
@@ -732,9 +743,12 @@ static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t ar
         uint64_t bytes = 0;
         for (size_t i = lo; i < hi; i++) bytes += desc[i].caplen;
         const size_t cap = mfp_fp_arena_bound(m, bytes);
-        int r = stage_and_launch(c, 1 + s, arena, arena_len, desc + lo, m, cap, analysis != nullptr);
+        int r = stage_and_launch(c, 1 + s, arena, arena_len, desc + lo, m, cap, analysis != nullptr, attr_prob != nullptr);
         if (r) return r;
         if (analysis) HIPCHK(hipMemcpyAsync(analysis + lo, S.d_an, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
+        if (analysis && attr_prob && m)
+            HIPCHK(hipMemcpyAsync(attr_prob + lo * MFP_ATTR_DB_TAGS, S.d_ap, m * MFP_ATTR_DB_TAGS * sizeof(double),
+                                  hipMemcpyDeviceToHost, S.stream));
         HIPCHK(hipMemcpyAsync(rec + lo, S.d_rec, m * sizeof(mfp_record), hipMemcpyDeviceToHost, S.stream));
         HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
         inf[s] = {true, lo, hi};
@@ -753,11 +767,11 @@ extern "C" MFP_EXPORT int mfp_analysis_enabled(mfp_context c) { return c && c->c
 
 extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
                                                    size_t n, mfp_record *d_rec, const char *d_fp_arena,
-                                                   mfp_analysis *d_out, void *stream) {
+                                                   mfp_analysis *d_out, double *d_attr_prob, void *stream) {
     if (!c) { mfp_set_error("null context"); return -1; }
     if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    const int r = analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, (hipStream_t)stream);
+    const int r = analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, (hipStream_t)stream);
     if (r || c->defer) return r;
     // the batch's unknown-TLS sightings are decided now, in stream order: the
     // call waits for its kernels (a few microseconds of host time per batch)
@@ -860,6 +874,28 @@ extern "C" MFP_EXPORT const char *mfp_process_name(mfp_context c, uint32_t id) {
 
 extern "C" MFP_EXPORT const char *mfp_attribute_name(mfp_context c, uint32_t bit) {
     return c && c->clf ? mfp_classifier_attr_name(c->clf, bit) : nullptr;
+}
+
+extern "C" MFP_EXPORT const char *mfp_resource_version(mfp_context c) {
+    return c && c->clf ? mfp_classifier_version(c->clf) : nullptr;
+}
+
+extern "C" MFP_EXPORT int mfp_attribute_count(mfp_context c) {
+    return c && c->clf ? mfp_classifier_attr_count(c->clf) : 0;
+}
+
+extern "C" MFP_EXPORT int mfp_analysis_report_os(mfp_context c, int on) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return -1; }
+    c->report_os = on != 0;
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_process_os_info(mfp_context c, uint32_t proc_slot, uint32_t k, const char **name,
+                                              uint64_t *prevalence) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return -1; }
+    const int cnt = mfp_classifier_os_info(c->clf, proc_slot, k, name, prevalence);
+    if (cnt < 0) { mfp_set_error("bad process slot %u", proc_slot); return -1; }
+    return c->report_os ? cnt : 0;
 }
 
 extern "C" MFP_EXPORT int mfp_analysis_stats(mfp_context c, uint64_t out[4]) {

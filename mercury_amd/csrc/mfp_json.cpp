@@ -249,11 +249,96 @@ struct Obj {
 
 bool is_tcp_msg(unsigned m) { return m != MFP_MSG_DTLS_CH && m != MFP_MSG_DTLS_SH && m != MFP_MSG_DTLS_HVR; }
 
+// "%f" (json_object::print_key_float json_object.h:174-177)
+void put_float(W &w, double d) {
+    char t[352];   // %f of the largest double is 316 digits + sign, dot, 6 decimals
+    const int n = snprintf(t, sizeof t, "%f", d);
+    w.mem(t, n > 0 ? (size_t)n : 0);
+}
+
+// worst-case text of a record's "analysis" object
+size_t analysis_bound(mfp_context ctx, const mfp_analysis &a) {
+    size_t b = 400 + 16 * 64;                       // keys, numbers, 16 attribute entries
+    const int na = mfp_attribute_count(ctx);
+    for (int k = 0; k < na; k++) { const char *nm = mfp_attribute_name(ctx, (uint32_t)k); b += nm ? strlen(nm) : 0; }
+    if (a.process != MFP_NO_PROCESS) b += 256;      // max_proc holds at most 255 bytes (result.h:198)
+    if (a.proc_slot != MFP_NO_PROCESS) {
+        const int cnt = mfp_process_os_info(ctx, a.proc_slot, 0, nullptr, nullptr);
+        for (int k = 0; k < cnt; k++) {
+            const char *nm = nullptr;
+            mfp_process_os_info(ctx, a.proc_slot, (uint32_t)k, &nm, nullptr);
+            b += (nm ? strlen(nm) : 0) + 32;
+        }
+    }
+    return b;
+}
+
+// analysis_result::write_json (result.h:207-252) with attribute_result::write_json (result.h:62-77)
+void write_analysis(W &w, mfp_context ctx, const mfp_analysis &a, const double *ap) {
+    w.puts("{");
+    Obj o{w};
+    auto process_part = [&]() {
+        o.key("process"); w.put('"');
+        const char *nm = mfp_process_name(ctx, a.process);
+        if (nm) w.mem(nm, strnlen(nm, 255));        // strncpy(max_proc, proc, max_proc_len - 1)
+        w.put('"');
+        o.key("score"); put_float(w, a.score);
+        if (a.flags & MFP_AN_CLASSIFY_MALWARE) {
+            o.key("malware"); w.put((a.flags & MFP_AN_MALWARE) ? '1' : '0');
+            o.key("p_malware"); put_float(w, a.malware_prob);
+        }
+        const int cnt = a.proc_slot == MFP_NO_PROCESS ? 0 : mfp_process_os_info(ctx, a.proc_slot, 0, nullptr, nullptr);
+        if (cnt > 0) {
+            o.key("os_info"); w.put('{');
+            for (int k = 0; k < cnt; k++) {
+                const char *nm2 = nullptr;
+                uint64_t prev = 0;
+                mfp_process_os_info(ctx, a.proc_slot, (uint32_t)k, &nm2, &prev);
+                if (k) w.put(',');
+                w.put('"'); w.putz(nm2 ? nm2 : ""); w.puts("\":"); w.udec(prev);
+            }
+            w.put('}');
+        }
+    };
+    const bool named = a.process != MFP_NO_PROCESS && mfp_process_name(ctx, a.process) &&
+                       mfp_process_name(ctx, a.process)[0] != 0;
+    switch (a.status) {
+    case 1:                                          // fingerprint_status_labeled
+        process_part();
+        break;
+    case 2:                                          // fingerprint_status_randomized
+        if (named) process_part();
+        o.key("status"); w.puts("\"randomized_fingerprint\"");
+        break;
+    case 3:                                          // fingerprint_status_unlabled
+        o.key("status"); w.puts("\"unlabeled_fingerprint\"");
+        break;
+    default:
+        o.key("status"); w.puts("\"unknown\"");
+        break;
+    }
+    o.key("attributes"); w.put('[');
+    const int na = mfp_attribute_count(ctx);
+    bool first = true;
+    for (int k = 0; k < na && k < MFP_ATTR_MAX_TAGS; k++) {
+        if (!((a.attr >> k) & 1u)) continue;
+        if (!first) w.put(',');
+        first = false;
+        w.puts("{\"name\":\""); w.putz(mfp_attribute_name(ctx, (uint32_t)k)); w.puts("\",\"probability_score\":");
+        double p = 1.0;                               // encrypted_dns, domain_faking, faketls (analysis.h:555-573)
+        if (k >= MFP_ATTR_DB_FIRST) p = ap ? ap[k - MFP_ATTR_DB_FIRST] : 0.0;
+        else if (k == 7) p = a.malware_prob;          // encrypted_channel (analysis.h:1161-1163)
+        put_float(w, p);
+        w.put('}');
+    }
+    w.puts("]}");
+}
+
 // one record; returns false when the record cannot be written exactly here
 struct TsCache { uint64_t sec = ~0ull, usec = ~0ull; int len = 0; char text[40]; };
 
 bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const char *fp_arena,
-                  uint64_t sec, uint64_t nsec) {
+                  uint64_t sec, uint64_t nsec, mfp_context ctx, const mfp_analysis *an, const double *ap) {
     if (!(r.flags & MFP_FLAG_EMIT)) return true;
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
     // IP-in-IP: outer headers sit back to back before the inner one (IPv4
@@ -274,7 +359,9 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     if ((ipv != 4 && ipv != 6) || ip + (ipv == 4 ? 20u : 40u) > caplen) return false;
     // worst case: fixed keys/addresses/numbers and 4 encapsulations < 1000 B, the fp string, and at most
     // 6 output bytes per input byte of a JSON string ("\\ufffd") or a base64 cert list
-    o.need(1000 + (size_t)r.fp_len + 6 * ((r.sni_len == 0xffff ? 0 : r.sni_len) + (r.ua_len == 0xffff ? 0 : r.ua_len)));
+    const bool with_an = ctx && an && (an->flags & MFP_AN_VALID);
+    o.need(1000 + (size_t)r.fp_len + 6 * ((r.sni_len == 0xffff ? 0 : r.sni_len) + (r.ua_len == 0xffff ? 0 : r.ua_len)) +
+           (with_an ? analysis_bound(ctx, *an) : 0));
     W w{o.buf.get() + o.len};
     // a readable, non-empty datum (print_key_json_string skips empty ones, json_object.h:104-108)
     auto span_ok = [&](uint32_t off, uint32_t len) { return len != 0xffff && len && (uint64_t)off + len <= caplen; };
@@ -289,6 +376,7 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     switch (r.msg) {
     case MFP_MSG_TLS_CH:
     case MFP_MSG_DTLS_CH:
+        if (r.flags & MFP_FLAG_NO_CIPHERS) break;      // tls_client_hello::write_json tls.h:1882-1885
         if (r.msg == MFP_MSG_TLS_CH) rec.key("tls"); else rec.key("dtls");
         w.puts("{\"client\":{");
         if (span_ok(r.sni_off, r.sni_len)) { w.puts("\"server_name\":\""); w.utf8(pkt + r.sni_off, r.sni_len); w.put('"'); }
@@ -332,6 +420,7 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     default:
         break;
     }
+    if (with_an) { rec.key("analysis"); write_analysis(w, ctx, *an, ap); }   // pkt_proc.cc:1211-1213
     if (r.flags & MFP_FLAG_TRUNCATED) { rec.key("reassembly_properties"); w.puts("{\"truncated\":true}"); }
     if (r.flags & MFP_FLAG_ENCAP) {                      // encapsulations::write_json pkt_proc.cc:1021-1031
         rec.key("encapsulations");
@@ -371,10 +460,10 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
 
 }  // namespace
 
-MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
-                                          const mfp_record *rec, const char *fp_arena, const uint64_t *ts_ns,
-                                          char *out, size_t out_cap, uint64_t *line_end, uint64_t *skipped,
-                                          int threads) {
+static long long write_json_batch(mfp_context ctx, const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+                                   const mfp_record *rec, const char *fp_arena, const mfp_analysis *an, const double *ap,
+                                   const uint64_t *ts_ns, char *out, size_t out_cap, uint64_t *line_end,
+                                   uint64_t *skipped, int threads) {
     if ((n && (!arena || !desc || !rec || !fp_arena || !line_end)) || (out_cap && !out)) {
         mfp_set_error("mfp_write_json_batch: null argument");
         return -1;
@@ -412,7 +501,8 @@ MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_de
             if (ts_ns) { sec = ts_ns[i] / 1000000000ull; nsec = ts_ns[i] % 1000000000ull; }
             if (sec == 0) { sec = (uint64_t)now.tv_sec; nsec = (uint64_t)now.tv_nsec; }
             size_t mark = o.len;
-            if (!write_record(o, tc, arena + desc[i].offset, desc[i].caplen, rec[i], fp_arena, sec, nsec)) {
+            if (!write_record(o, tc, arena + desc[i].offset, desc[i].caplen, rec[i], fp_arena, sec, nsec, ctx,
+                              an ? an + i : nullptr, ap ? ap + i * MFP_ATTR_DB_TAGS : nullptr)) {
                 o.len = mark;
                 bad[(size_t)t]++;
             }
@@ -445,4 +535,32 @@ MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_de
     });
     give_back();
     return (long long)total;
+}
+
+MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+                                          const mfp_record *rec, const char *fp_arena, const uint64_t *ts_ns,
+                                          char *out, size_t out_cap, uint64_t *line_end, uint64_t *skipped,
+                                          int threads) {
+    return write_json_batch(nullptr, arena, desc, n, rec, fp_arena, nullptr, nullptr, ts_ns, out, out_cap, line_end,
+                            skipped, threads);
+}
+
+MFP_EXPORT long long mfp_write_json_batch_analysis(mfp_context ctx, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                                   size_t n, const mfp_record *rec, const char *fp_arena,
+                                                   const mfp_analysis *analysis, const double *attr_prob,
+                                                   const uint64_t *ts_ns, char *out, size_t out_cap,
+                                                   uint64_t *line_end, uint64_t *skipped, int threads) {
+    if (!ctx || !mfp_analysis_enabled(ctx)) {
+        mfp_set_error("mfp_write_json_batch_analysis: the context has no classifier");
+        return -1;
+    }
+    if (n && !analysis) { mfp_set_error("mfp_write_json_batch_analysis: null analysis"); return -1; }
+    if (!attr_prob)   // an archive tag on any record needs its probability
+        for (size_t i = 0; i < n; i++)
+            if ((analysis[i].flags & MFP_AN_VALID) && (analysis[i].attr >> MFP_ATTR_DB_FIRST)) {
+                mfp_set_error("mfp_write_json_batch_analysis: record %zu carries archive tags but attr_prob is NULL", i);
+                return -1;
+            }
+    return write_json_batch(ctx, arena, desc, n, rec, fp_arena, analysis, attr_prob, ts_ns, out, out_cap, line_end,
+                            skipped, threads);
 }

@@ -3,6 +3,7 @@
 // Every call is a one-packet batch on the GPU; the high-throughput
 // interface is the batch API.  File:line cites are relative to
 // /root/reference/src/libmerc/.
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -17,21 +18,32 @@
 
 struct mercury {
     std::string cfg;              // packet_filter_cfg as mfp_init takes it
-    std::string resource_version;
     bool analysis = false;
+    bool report_os = false;
     std::mutex mu;
     mfp_context ctx[2] = {nullptr, nullptr};   // per reference entry point (write_json / analysis)
+    // one fingerprint_prevalence for the mercury context (the reference's
+    // classifier owns one, shared by every processor and entry point)
+    mfp_prevalence prev = nullptr;
 };
 
-struct analysis_context {       // the fields libmerc's accessors read (result.h:383-420)
+struct analysis_context {       // the fields libmerc's accessors read (result.h:174-420)
     char fp[8193];
     uint32_t fp_type = 0;
     uint32_t status = 0;
     char sn[257];               // destination_context::sn_str (MAX_SNI_LEN)
     char ua[512];               // destination_context::ua_str (MAX_USER_AGENT_LEN)
+    uint8_t alpn[128];          // destination_context::alpn_array (MAX_ALPN_STR_LEN)
+    size_t alpn_len = 0;
     std::string process;
     double score = 0, malware_prob = -1;
     bool malware = false, classify_malware = false, has_process = false;
+    std::vector<os_information> os;             // analysis_result::os_info
+    uint32_t attr = 0;                          // attribute_result tags
+    long double prob[MFP_ATTR_MAX_TAGS];        // attribute_result::prob_score
+    const char *tag_names[MFP_ATTR_MAX_TAGS];
+    size_t n_tags = 0;
+    attribute_context actx;
 };
 
 struct mercury_packet_processor_s {
@@ -72,6 +84,7 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
         cfg += std::string(";resources=") + vars->resources + ";analysis";
         m->analysis = true;
     }
+    m->report_os = vars->report_os;
     m->cfg = cfg;
     // validate now, so a bad configuration fails at init as in the reference
     uint32_t sel, fmt;
@@ -86,6 +99,7 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
 MFP_EXPORT int mercury_finalize(mercury_context mc) {
     if (!mc) return -1;
     for (auto &c : mc->ctx) if (c) mfp_finalize(c);
+    if (mc->prev) mfp_prevalence_destroy(mc->prev);
     delete mc;
     return 0;
 }
@@ -93,8 +107,14 @@ MFP_EXPORT int mercury_finalize(mercury_context mc) {
 static mfp_context get_ctx(mercury *m, int mode) {
     std::lock_guard<std::mutex> lk(m->mu);
     if (!m->ctx[mode]) {
-        m->ctx[mode] = mfp_init(m->cfg.c_str(), 0, mode);
-        if (!m->ctx[mode]) log_error("%s\n", mfp_last_error());
+        mfp_context c = mfp_init(m->cfg.c_str(), 0, mode);
+        if (!c) { log_error("%s\n", mfp_last_error()); return nullptr; }
+        if (mfp_analysis_enabled(c)) {
+            if (!m->prev) m->prev = mfp_prevalence_create(100000);   // analysis.h:433
+            mfp_analysis_set_prevalence(c, m->prev);
+            mfp_analysis_report_os(c, m->report_os ? 1 : 0);
+        }
+        m->ctx[mode] = c;
     }
     return m->ctx[mode];
 }
@@ -108,15 +128,71 @@ MFP_EXPORT mercury_packet_processor mercury_packet_processor_construct(mercury_c
 
 MFP_EXPORT void mercury_packet_processor_destruct(mercury_packet_processor mpp) { delete mpp; }
 
+static void copy_cstr(char *dst, size_t cap, const uint8_t *src, size_t len) {   // datum::strncpy
+    size_t n = len < cap - 1 ? len : cap - 1;
+    size_t k = 0;
+    for (; k < n && src[k]; k++) dst[k] = (char)src[k];
+    dst[k] = 0;
+}
+
+// the processor's analysis_context from one classified packet (the state the
+// reference's accessors read after write_json or get_analysis_context)
+static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *pkt, const mfp_record &rec,
+                         const char *fp, const mfp_analysis *an, const double *ap) {
+    ac.fp_type = rec.fp_type;
+    copy_cstr(ac.fp, sizeof ac.fp, (const uint8_t *)fp + rec.fp_offset, rec.fp_type ? rec.fp_len : 0);
+    const bool cert_slot = rec.msg == MFP_MSG_TLS_SH || rec.msg == MFP_MSG_TLS_CERT;   // sni slot = certificate_list
+    const bool hello = rec.msg == MFP_MSG_TLS_CH || rec.msg == MFP_MSG_DTLS_CH;        // ua slot = ALPN list
+    copy_cstr(ac.sn, sizeof ac.sn, pkt + rec.sni_off, rec.sni_len == 0xffff || cert_slot ? 0 : rec.sni_len);
+    copy_cstr(ac.ua, sizeof ac.ua, pkt + rec.ua_off, rec.ua_len == 0xffff || hello ? 0 : rec.ua_len);
+    ac.alpn_len = 0;
+    ac.alpn[0] = 0;
+    if (hello && rec.ua_len != 0xffff) {   // alpn.write_to_buffer(alpn_array, 128) (result.h:352-353)
+        ac.alpn_len = rec.ua_len;
+        memcpy(ac.alpn, pkt + rec.ua_off, std::min<size_t>(rec.ua_len, sizeof ac.alpn));
+    }
+    ac.status = 0; ac.has_process = false; ac.process.clear(); ac.score = 0; ac.malware = false;
+    ac.classify_malware = false; ac.malware_prob = -1; ac.os.clear(); ac.attr = 0; ac.n_tags = 0;
+    if (!an) return;
+    ac.status = an->status;
+    ac.has_process = an->process != MFP_NO_PROCESS;
+    ac.process = ac.has_process ? mfp_process_name(ctx, an->process) : "";
+    if (ac.process.size() > 255) ac.process.resize(255);   // max_proc (result.h:176,198)
+    ac.score = an->score;
+    ac.malware = an->flags & MFP_AN_MALWARE;
+    ac.classify_malware = an->flags & MFP_AN_CLASSIFY_MALWARE;
+    ac.malware_prob = an->malware_prob;
+    if (an->proc_slot != MFP_NO_PROCESS) {
+        const int cnt = mfp_process_os_info(ctx, an->proc_slot, 0, nullptr, nullptr);
+        for (int k = 0; k < cnt; k++) {
+            const char *nm = nullptr;
+            uint64_t prev = 0;
+            mfp_process_os_info(ctx, an->proc_slot, (uint32_t)k, &nm, &prev);
+            ac.os.push_back(os_information{(char *)nm, prev});
+        }
+    }
+    ac.attr = an->attr;
+    ac.n_tags = (size_t)mfp_attribute_count(ctx);
+    for (size_t k = 0; k < MFP_ATTR_MAX_TAGS; k++) {
+        ac.tag_names[k] = k < ac.n_tags ? mfp_attribute_name(ctx, (uint32_t)k) : nullptr;
+        long double p = 0;
+        if ((ac.attr >> k) & 1u) {
+            if (k >= MFP_ATTR_DB_FIRST) p = ap ? ap[k - MFP_ATTR_DB_FIRST] : 0;
+            else if (k == 7) p = an->malware_prob;   // encrypted_channel
+            else p = 1.0;                            // encrypted_dns, domain_faking, faketls
+        }
+        ac.prob[k] = p;
+    }
+}
+
 // write_json libmerc.cc:131-175 -> stateful_pkt_proc::write_json pkt_proc.cc:1256-1383: the record text
-// from a one-packet batch (device walk + mfp_write_json_batch).  Returns 0 when nothing is written, the
-// record does not fit buf_size (buffer_stream truncation, pkt_proc.cc:1249-1253), or --analysis is
-// configured (the "analysis" object is not built by the JSON writer yet).
+// from a one-packet batch (device walk, --analysis classification, mfp_write_json_batch[_analysis]).
+// Returns 0 when nothing is written or the record does not fit buf_size (buffer_stream truncation,
+// pkt_proc.cc:1249-1253).
 MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_processor p, void *buffer,
                                                                size_t buffer_size, uint8_t *pkt, size_t len,
                                                                struct timespec *ts, uint16_t linktype) {
     if (!p || !buffer || !pkt || !ts) return 0;
-    if (p->mc->analysis) return 0;
     mfp_context ctx = get_ctx(p->mc, MFP_MODE_WRITE_JSON);
     if (!ctx) return 0;
     if (ts->tv_sec == 0) clock_gettime(CLOCK_REALTIME, ts);   // pkt_proc.cc:1086-1089
@@ -124,13 +200,20 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
     p->arena.resize(len + 16);
     mfp_pkt_desc d{0, (uint32_t)len, linktype, 0};
     mfp_record rec;
+    mfp_analysis an;
+    double ap[MFP_ATTR_DB_TAGS] = {0, 0, 0, 0, 0, 0};
     size_t cap = mfp_fp_arena_bound(1, len);
     p->fp.resize(cap);
-    long long used = mfp_process_batch_host(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap);
+    const bool want_an = mfp_analysis_enabled(ctx);
+    long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap,
+                                               want_an ? &an : nullptr, want_an ? ap : nullptr);
     if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
+    fill_context(ctx, p->ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
     uint64_t t = (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec, end = 0, skipped = 0;
-    long long n = mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
-                                       buffer_size, &end, &skipped, 1);
+    long long n = want_an ? mfp_write_json_batch_analysis(ctx, p->arena.data(), &d, 1, &rec, p->fp.data(), &an, ap, &t,
+                                                          (char *)buffer, buffer_size, &end, &skipped, 1)
+                          : mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
+                                                 buffer_size, &end, &skipped, 1);
     if (skipped) {
         // the reference writes a record here; the writer cannot rebuild it
         // (IP-in-IP with an outer IPv6 extension header): say so instead of
@@ -146,13 +229,6 @@ MFP_EXPORT size_t mercury_packet_processor_write_json(mercury_packet_processor p
     return mercury_packet_processor_write_json_linktype(p, buffer, buffer_size, pkt, len, ts, 1);   // LINKTYPE_ETHERNET
 }
 
-static void copy_cstr(char *dst, size_t cap, const uint8_t *src, size_t len) {   // datum::strncpy
-    size_t n = len < cap - 1 ? len : cap - 1;
-    size_t k = 0;
-    for (; k < n && src[k]; k++) dst[k] = (char)src[k];
-    dst[k] = 0;
-}
-
 static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt, size_t len, uint16_t linktype) {
     if (!p || !pkt) return nullptr;
     mfp_context ctx = get_ctx(p->mc, MFP_MODE_ANALYSIS);
@@ -162,26 +238,16 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
     mfp_pkt_desc d{0, (uint32_t)len, linktype, 0};
     mfp_record rec;
     mfp_analysis an;
+    double ap[MFP_ATTR_DB_TAGS] = {0, 0, 0, 0, 0, 0};
     size_t cap = mfp_fp_arena_bound(1, len);
     p->fp.resize(cap);
     bool want_an = mfp_analysis_enabled(ctx);
     long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap,
-                                               want_an ? &an : nullptr);
+                                               want_an ? &an : nullptr, want_an ? ap : nullptr);
     if (used < 0) { log_error("%s\n", mfp_last_error()); return nullptr; }
     analysis_context &ac = p->ac;
-    ac.fp_type = rec.fp_type;
-    copy_cstr(ac.fp, sizeof ac.fp, (const uint8_t *)p->fp.data() + rec.fp_offset, rec.fp_type ? rec.fp_len : 0);
-    bool cert_slot = rec.msg == MFP_MSG_TLS_SH || rec.msg == MFP_MSG_TLS_CERT;   // sni slot = certificate_list
-    copy_cstr(ac.sn, sizeof ac.sn, pkt + rec.sni_off, rec.sni_len == 0xffff || cert_slot ? 0 : rec.sni_len);
-    copy_cstr(ac.ua, sizeof ac.ua, pkt + rec.ua_off, rec.ua_len == 0xffff ? 0 : rec.ua_len);
+    fill_context(ctx, ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
     if (!want_an) return nullptr;   // no classifier: analysis result never valid
-    ac.status = an.status;
-    ac.has_process = an.process != MFP_NO_PROCESS;
-    ac.process = ac.has_process ? mfp_process_name(ctx, an.process) : "";
-    ac.score = an.score;
-    ac.malware = an.flags & MFP_AN_MALWARE;
-    ac.classify_malware = an.flags & MFP_AN_CLASSIFY_MALWARE;
-    ac.malware_prob = an.malware_prob;
     return (an.flags & MFP_AN_VALID) ? &ac : nullptr;
 }
 
@@ -230,6 +296,41 @@ MFP_EXPORT bool analysis_context_get_malware_info(const struct analysis_context 
     return true;
 }
 
+// analysis_result::get_os_info result.h:290-299 (the array holds os_information {name, prevalence})
+MFP_EXPORT bool analysis_context_get_os_info(const struct analysis_context *ac, const struct os_information **os_info,
+                                             size_t *os_info_len) {
+    if (!ac || ac->os.empty()) return false;
+    if (os_info) *os_info = ac->os.data();
+    if (os_info_len) *os_info_len = ac->os.size();
+    return true;
+}
+
+// analysis_context::get_alpns result.h:401-408
+MFP_EXPORT bool analysis_context_get_alpns(const struct analysis_context *ac, const uint8_t **alpn_data,
+                                           size_t *alpn_length) {
+    if (!ac || ac->alpn[0] == 0) return false;
+    if (alpn_data) *alpn_data = ac->alpn;
+    if (alpn_length) *alpn_length = ac->alpn_len;
+    return true;
+}
+
+// mercury_packet_processor_get_attributes libmerc.cc:398-411 / attribute_result::get_attributes result.h:102-116
+MFP_EXPORT const struct attribute_context *mercury_packet_processor_get_attributes(mercury_packet_processor p) {
+    if (!p || p->ac.attr == 0 || p->ac.n_tags == 0) return nullptr;
+    analysis_context &ac = p->ac;
+    ac.actx.tag_names = ac.tag_names;
+    ac.actx.prob_scores = ac.prob;
+    ac.actx.attributes_len = ac.n_tags;
+    return &ac.actx;
+}
+
+// mercury_get_classifier libmerc.cc:85-90: an opaque handle, NULL without a classifier
+MFP_EXPORT void *mercury_get_classifier(mercury_context mc) {
+    if (!mc || !mc->analysis) return nullptr;
+    mfp_context c = get_ctx(mc, MFP_MODE_ANALYSIS);
+    return c && mfp_analysis_enabled(c) ? (void *)c : nullptr;
+}
+
 MFP_EXPORT bool mercury_packet_processor_more_pkts_needed(mercury_packet_processor) { return false; }
 
 MFP_EXPORT uint32_t mercury_get_version_number(void) { return mfp_reference_version(); }
@@ -240,8 +341,10 @@ MFP_EXPORT void mercury_get_version_string(char *buf, size_t size) {
 MFP_EXPORT const char *mercury_get_license_string(void) {
     return "libmercury_amd: MI355X fingerprint/classify path for the libmerc API";
 }
+// mercury_get_resource_version libmerc.cc:78-83: the archive's VERSION, NULL without a classifier
 MFP_EXPORT const char *mercury_get_resource_version(mercury_context mc) {
-    return mc ? mc->resource_version.c_str() : nullptr;
+    void *c = mercury_get_classifier(mc);
+    return c ? mfp_resource_version((mfp_context)c) : nullptr;
 }
 
 }  // extern "C"

@@ -527,8 +527,9 @@ static void tls_ch_fp(sb *b, const tls_ch *ch, unsigned fmt) {
     else if (fmt == 1) exts_fp1(b, ch->extensions, 0);
     else exts_fp2(b, ch->extensions, 0);
 }
-/* tls_extensions::set_meta_data tls.h:1316 (server_name only on this path) */
-static void tls_sni(cur exts, int32_t *off, int32_t *len, const uint8_t *base) {
+/* tls_extensions::set_meta_data tls.h:1316: server_name and the ALPN
+ * protocol_name_list (tls.h:1172-1176; a short list is none) */
+static void tls_sni(cur exts, int32_t *off, int32_t *len, int32_t *aoff, int32_t *alen, const uint8_t *base) {
     cur p = exts;
     while (clen(p) > 0) {
         const uint8_t *start = p.d;
@@ -540,6 +541,13 @@ static void tls_sni(cur exts, int32_t *off, int32_t *len, const uint8_t *base) {
             cur e = { start, p.d };
             cskip(&e, 9);
             *off = (int32_t)(e.d - base); *len = (int32_t)clen(e);
+        }
+        if (t == 16) {
+            cur e = { start, p.d };
+            uint64_t al;
+            cskip(&e, 4);
+            if (rd_uint(&e, 2, &al) && (uint64_t)clen(e) >= al) { *aoff = (int32_t)(e.d - base); *alen = (int32_t)al; }
+            else { *aoff = 0; *alen = -1; }
         }
     }
 }
@@ -938,7 +946,7 @@ static void tcp_data(ctx *c, cur pkt, const uint8_t *tcph) {
         r->emit = 1;
         fp_set_type(&c->b, &c->type, MFPO_FP_TLS);
         tls_ch_fp(&c->b, &ch, cfg->tls_format);
-        tls_sni(ch.extensions, &r->sni_off, &r->sni_len, c->base);
+        tls_sni(ch.extensions, &r->sni_off, &r->sni_len, &r->ua_off, &r->ua_len, c->base);
         finish_fp(c);
         return;
     }
@@ -1055,7 +1063,7 @@ static void udp_data(ctx *c, cur pkt) {
         r->emit = 1;
         fp_set_type(&c->b, &c->type, MFPO_FP_DTLS);
         tls_ch_fp(&c->b, &ch, c->cfg->tls_format);
-        tls_sni(ch.extensions, &r->sni_off, &r->sni_len, c->base);
+        tls_sni(ch.extensions, &r->sni_off, &r->sni_len, &r->ua_off, &r->ua_len, c->base);
         finish_fp(c);
     } else if (msg == MFPO_MSG_DTLS_SH) {
         tls_sh sh; memset(&sh, 0, sizeof sh);

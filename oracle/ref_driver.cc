@@ -12,6 +12,14 @@
 //   idx  valid  fp_type  status  process  score  malware  p_malware  fp_string
 // Mode "json": the write_json record text, one line per packet (empty line
 // when the reference writes nothing).
+// Mode "attr": analysis_context path, the accessors the embedders read, one
+// TSV line per packet:
+//   idx  valid  status  attributes  os_info  alpn
+// attributes: name=prob;... from mercury_packet_processor_get_attributes
+// (prob %.17Lg, set tags only), os_info: name=prevalence;... from
+// analysis_context_get_os_info, alpn: hex of analysis_context_get_alpns
+// (first min(len, 128) bytes) and ":len".
+// Environment: MERC_REPORT_OS=1 sets libmerc_config.report_os.
 // Mode "time": run write_json (or, with a trailing "an", the analysis_context
 // entry) with T threads (one processor per thread over contiguous shards),
 // print packets/s.
@@ -27,6 +35,8 @@
 #include <vector>
 #include <thread>
 #include <chrono>
+#include <fcntl.h>
+#include <unistd.h>
 #include "libmerc.h"
 #include "pkt_proc.h"
 
@@ -111,7 +121,17 @@ int main(int argc, char **argv) {
         cfg.resources = (char *)res.c_str();
         cfg.do_analysis = true;
     }
+    const char *ros = getenv("MERC_REPORT_OS");
+    cfg.report_os = ros && ros[0] == '1';
+    // lctrie's subnet_dedup prints to stdout while the archive loads
+    // (lctrie_ip.hpp:399-410): keep that out of the record stream
+    fflush(stdout);
+    int saved = dup(1), devnull = open("/dev/null", O_WRONLY);
+    if (devnull >= 0) dup2(devnull, 1);
     mercury_context mc = mercury_init(&cfg, 0);
+    fflush(stdout);
+    if (saved >= 0) { dup2(saved, 1); close(saved); }
+    if (devnull >= 0) close(devnull);
     if (!mc) { fprintf(stderr, "mercury_init failed\n"); return 1; }
 
     std::vector<char> out(1 << 16);
@@ -159,6 +179,39 @@ int main(int argc, char **argv) {
                    (int)analysis_context_get_fingerprint_status(ac),
                    proc ? proc : "", score, (int)mal, pm,
                    analysis_context_get_fingerprint_string(ac));
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "attr") {
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        for (size_t i = 0; i < pkts.size(); i++) {
+            struct timespec ts{1700000000, 0};
+            const analysis_context *ac = mercury_packet_processor_get_analysis_context_linktype(
+                p, (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
+            std::string attrs, os, alpn;
+            const attribute_context *at = mercury_packet_processor_get_attributes(p);
+            if (at) {
+                for (size_t k = 0; k < at->attributes_len; k++) {
+                    if (at->prob_scores[k] == 0) continue;
+                    char t[96];
+                    snprintf(t, sizeof t, "=%.17Lg;", at->prob_scores[k]);
+                    attrs += std::string(at->tag_names[k]) + t;
+                }
+            }
+            if (ac) {
+                const os_information *oi = nullptr;
+                size_t ol = 0;
+                if (analysis_context_get_os_info(ac, &oi, &ol))
+                    for (size_t k = 0; k < ol; k++) os += std::string(oi[k].os_name) + "=" + std::to_string(oi[k].os_prevalence) + ";";
+                const uint8_t *ad = nullptr;
+                size_t al = 0;
+                if (analysis_context_get_alpns(ac, &ad, &al)) {
+                    char h[3];
+                    for (size_t k = 0; k < al && k < 128; k++) { snprintf(h, sizeof h, "%02x", ad[k]); alpn += h; }
+                    alpn += ":" + std::to_string(al);
+                }
+            }
+            printf("%zu\t%d\t%d\t%s\t%s\t%s\n", i, ac != nullptr, ac ? (int)analysis_context_get_fingerprint_status(ac) : 0,
+                   attrs.c_str(), os.c_str(), alpn.c_str());
         }
         mercury_packet_processor_destruct(p);
     } else if (mode == "time") {

@@ -20,7 +20,10 @@ from tests import synth
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 SELECT = "tls,dtls,ssh,http,tcp,tcp.syn_ack"
-TOL = 1e-6
+# the scores are bit-identical to the reference's: same fp64 addition order,
+# glibc's expf restated on the device (mfp_analysis.hip expf_ref) and the sums
+# in process order; the goldens print %.17g, which round-trips a double
+TOL = 0.0
 
 
 def load_ref_an(name):
