@@ -8,8 +8,12 @@ synthetic packets already resident in HBM:
 
   default       BASELINE config 4: 50 M mixed TLS/HTTP/SSH/TCP packets,
                 protocol identification + fingerprint + the --analysis
-                process classifier (synthetic resource archive
-                tests/golden/synth_resources.tgz, built for this traffic)
+                process classifier on a SURVEY-sized synthetic resource
+                archive (tests/synth_db.py build_survey: ~20 000
+                fingerprints, P ~ Zipf on 1..256, ~100 000 pyasn prefixes,
+                encrypted-DNS watchlist, domain mappings; regenerated into
+                tests/golden/_gen/ when absent); --resources test: the
+                small test archive tests/golden/synth_resources.tgz
   --no-analysis config 3: protocol identification + fingerprint only
   --workload tls_ch --packets 10000000 --no-analysis   config 2
 
@@ -50,7 +54,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 CONTRACT = "tls,dtls,ssh,http,tcp,tcp.syn_ack"
-RESOURCES = os.path.join(ROOT, "tests", "golden", "synth_resources.tgz")
+TEST_RESOURCES = os.path.join(ROOT, "tests", "golden", "synth_resources.tgz")
 TEMPLATE_SEED = {"mixed": 0x5EED0003, "tls_ch": 0x5EED0001}
 N_TEMPLATES = 4096
 METRIC = "device-resident Mpkt/s + GB/s, fingerprint+classify, mixed-protocol batch"
@@ -88,7 +92,7 @@ def cpu_threads():
     return max(1, min(aff, int(env))) if env and env.isdigit() else aff
 
 
-def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis):
+def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis, resources):
     """Reference libmerc (oracle/_ref) if present, else the C oracle port.
     The reference is timed on both of its entry points: write_json (the CLI's
     path, JSON text included) and get_analysis_context (the embedders' path);
@@ -106,7 +110,7 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis):
         try:
             rates = {}
             for entry in ("json", "an"):
-                out = subprocess.run([ref, "time", path, CONTRACT, RESOURCES if analysis else "-", str(threads),
+                out = subprocess.run([ref, "time", path, CONTRACT, resources if analysis else "-", str(threads),
                                       str(seconds), entry],
                                      capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
                 rates[entry] = json.loads(out.decode().strip().splitlines()[-1])
@@ -138,7 +142,7 @@ def end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world
     fingerprints (and classifier results) back into page-locked host memory,
     through mfp_process_pipelined (two HIP streams: H2D, kernels, D2H
     overlapped).  Timed between barriers; the job time is the max over ranks."""
-    from mercury_amd.api import ANALYSIS_DTYPE, DESC_DTYPE, RECORD_DTYPE
+    from mercury_amd.api import ANALYSIS_DTYPE, ATTR_DB_TAGS, DESC_DTYPE, RECORD_DTYPE
     u = len(ud)
     n = min(n_buf, per_rank)
     span = int(ud["offset"][-1] + ud["caplen"][-1])
@@ -185,7 +189,13 @@ def end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world
                    "records + fingerprints" + (" + classifier results" if analysis else "")}
     if with_json:
         try:
-            res["json"] = json_writer_rate(av, d, out[0], out[1], min(n, 2_000_000), 16, analysis)
+            m = min(n, 2_000_000)
+            ap = None
+            if analysis:   # the archive tags' probabilities for the writer (not part of the timed leg above)
+                ap = np.zeros(m * ATTR_DB_TAGS, np.float64)
+                ctx.process_pipelined(av, d[:m], chunk=chunk, analysis=True, out=(out[0], out[1], out[2]),
+                                      attr_prob=ap)
+            res["json"] = json_writer_rate(av, d, out[0], out[1], m, 16, ctx if analysis else None, out[2], ap)
             jr = res["json"]["value"]
             res["json"]["with_gpu_path_serial_mpkt_s"] = round(1.0 / (1.0 / res["value"] + 1.0 / jr), 3)
             res["json_overlapped"] = json_overlapped(torch, ctx, av, d, n, analysis, chunk, out)
@@ -203,7 +213,10 @@ def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_00
     import threading
     from mercury_amd.api import ANALYSIS_DTYPE, RECORD_DTYPE, load_library
     lib = load_library()
+    from mercury_amd.api import ATTR_DB_TAGS
     rec_a, fp_a, an_a = out_a
+    ap_sets = [torch.empty(batch * ATTR_DB_TAGS * 8, dtype=torch.uint8, pin_memory=True).numpy().view(np.float64)
+               for _ in range(2)] if analysis else [None, None]
     fp_b = torch.empty(fp_a.nbytes // max(1, n // batch), dtype=torch.uint8, pin_memory=True).numpy()
     rec_b = torch.empty(batch * 32, dtype=torch.uint8, pin_memory=True).numpy().view(RECORD_DTYPE)
     an_b = torch.empty(batch * ANALYSIS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True).numpy().view(ANALYSIS_DTYPE) if analysis else None
@@ -217,11 +230,17 @@ def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_00
 
     errors = []
 
-    def write(dk, o):
+    def write(dk, o, ap):
         try:
-            got = lib.mfp_write_json_batch(av.ctypes.data, dk.ctypes.data, len(dk), o[0].ctypes.data,
-                                           o[1].ctypes.data, ts.ctypes.data, jbuf.ctypes.data, cap, ends.ctypes.data,
-                                           ctypes.byref(skipped), threads)
+            if analysis:
+                got = lib.mfp_write_json_batch_analysis(ctx.h, av.ctypes.data, dk.ctypes.data, len(dk),
+                                                        o[0].ctypes.data, o[1].ctypes.data, o[2].ctypes.data,
+                                                        ap.ctypes.data, ts.ctypes.data, jbuf.ctypes.data, cap,
+                                                        ends.ctypes.data, ctypes.byref(skipped), threads)
+            else:
+                got = lib.mfp_write_json_batch(av.ctypes.data, dk.ctypes.data, len(dk), o[0].ctypes.data,
+                                               o[1].ctypes.data, ts.ctypes.data, jbuf.ctypes.data, cap,
+                                               ends.ctypes.data, ctypes.byref(skipped), threads)
             if got < 0:
                 raise RuntimeError("mfp_write_json_batch failed: " + lib.mfp_last_error().decode())
             if skipped.value:
@@ -234,37 +253,39 @@ def json_overlapped(torch, ctx, av, d, n, analysis, chunk, out_a, batch=2_000_00
 
     nb = n // batch
     d0 = np.ascontiguousarray(d[:batch])
-    ctx.process_pipelined(av, d0, chunk=chunk, analysis=analysis, out=sets[0])
-    write(d0, sets[0])                                   # warm-up (page faults on the text buffer)
+    ctx.process_pipelined(av, d0, chunk=chunk, analysis=analysis, out=sets[0], attr_prob=ap_sets[0])
+    write(d0, sets[0], ap_sets[0])                       # warm-up (page faults on the text buffer)
     total[0] = 0
     t0 = time.perf_counter()
     prev = None
     for k in range(nb):
         dk = np.ascontiguousarray(d[k * batch:(k + 1) * batch])
-        o = sets[k % 2]
+        o, ap = sets[k % 2], ap_sets[k % 2]
         th = threading.Thread(target=write, args=prev) if prev else None
         if th:
             th.start()
-        ctx.process_pipelined(av, dk, chunk=chunk, analysis=analysis, out=o)
+        ctx.process_pipelined(av, dk, chunk=chunk, analysis=analysis, out=o, attr_prob=ap)
         if th:
             th.join()
         if errors:
             raise errors[0]
-        prev = (dk, o)
+        prev = (dk, o, ap)
     write(*prev)
     el = time.perf_counter() - t0
     if errors:
         raise errors[0]
     return {"value": round(nb * batch / el / 1e6, 3), "unit": "Mpkt/s", "packets": nb * batch, "batch": batch,
             "threads": threads, "json_gb_per_s": round(total[0] / el / 1e9, 3),
-            "path": "pinned packets -> mfp_process_pipelined (batch k) || mfp_write_json_batch (batch k-1) -> "
-                    "JSON text in host memory"}
+            "path": "pinned packets -> mfp_process_pipelined (batch k) || mfp_write_json_batch" +
+                    ("_analysis" if analysis else "") + " (batch k-1) -> JSON text in host memory" +
+                    (" (records with their 'analysis' objects)" if analysis else "")}
 
 
-def json_writer_rate(arena, desc, rec, fp, n, threads, analysis):
-    """Host JSON record assembly (mfp_write_json_batch, the text of
-    stateful_pkt_proc::write_json) over the first n results of the end-to-end
-    leg, `threads` host threads: Mpkt/s and GB/s of JSON text."""
+def json_writer_rate(arena, desc, rec, fp, n, threads, ctx=None, an=None, ap=None):
+    """Host JSON record assembly (mfp_write_json_batch[_analysis], the text of
+    stateful_pkt_proc::write_json, with the "analysis" objects under
+    --analysis) over the first n results of the end-to-end leg, `threads` host
+    threads: Mpkt/s and GB/s of JSON text."""
     import ctypes
     from mercury_amd.api import load_library
     lib = load_library()
@@ -273,21 +294,28 @@ def json_writer_rate(arena, desc, rec, fp, n, threads, analysis):
     skipped = ctypes.c_uint64(0)
     cap = n * 1024
     buf = np.empty(cap, np.uint8)
-    args = (arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data, ts.ctypes.data,
-            buf.ctypes.data, cap, ends.ctypes.data, ctypes.byref(skipped), threads)
-    got = lib.mfp_write_json_batch(*args)                 # warm-up (page faults on buf)
+    if ctx is not None:
+        fn = lib.mfp_write_json_batch_analysis
+        args = (ctx.h, arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data, an.ctypes.data,
+                ap.ctypes.data, ts.ctypes.data, buf.ctypes.data, cap, ends.ctypes.data, ctypes.byref(skipped), threads)
+    else:
+        fn = lib.mfp_write_json_batch
+        args = (arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data, ts.ctypes.data,
+                buf.ctypes.data, cap, ends.ctypes.data, ctypes.byref(skipped), threads)
+    got = fn(*args)                                       # warm-up (page faults on buf)
     if got < 0:
-        raise RuntimeError("mfp_write_json_batch failed")
+        raise RuntimeError("mfp_write_json_batch failed: " + lib.mfp_last_error().decode())
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        got = lib.mfp_write_json_batch(*args)
+        got = fn(*args)
     el = (time.perf_counter() - t0) / reps
     return {"value": round(n / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "threads": threads,
             "json_bytes": int(got), "gb_per_s": round(got / el / 1e9, 3), "records": int((rec["flags"][:n] & 1).sum()),
             "skipped": int(skipped.value),
+            "analysis_objects": int(((an["flags"][:n] & 1) != 0).sum()) if an is not None else 0,
             "note": "host threads after D2H; text byte-identical to the reference's write_json" +
-                    (" minus the 'analysis' object (not built yet)" if analysis else "")}
+                    (" (with its 'analysis' objects)" if ctx is not None else "")}
 
 
 # protocol bin of a record's message (mfp_kernels.hip msg_bin) and its name
@@ -317,7 +345,7 @@ def kernel_bytes(rec, desc, an):
         valid = (an["flags"] & 1) != 0
         sn = np.where(rec["sni_len"] == 0xffff, 0, rec["sni_len"]).astype(np.int64)
         ua = np.where(rec["ua_len"] == 0xffff, 0, rec["ua_len"]).astype(np.int64)
-        out["k_analyze"] = int(len(rec) * (32 + 24) + (valid * (8 + 16 + 32 + sn + ua)).sum())
+        out["k_analyze"] = int(len(rec) * (32 + an.dtype.itemsize) + (valid * (8 + 16 + 32 + sn + ua)).sum())
     return out
 
 
@@ -379,6 +407,8 @@ def main():
     ap.add_argument("--unique", type=int, default=1_000_000)
     ap.add_argument("--tls-format", type=int, default=0, help="without --analysis (else the archive's)")
     ap.add_argument("--no-analysis", action="store_true")
+    ap.add_argument("--resources", default="survey", choices=["survey", "test"],
+                    help="survey: the SURVEY-sized synthetic archive (config 4); test: tests/golden/synth_resources.tgz")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-total", type=int, default=200_000_000,
@@ -436,10 +466,24 @@ def main():
     log(f"[rank {rank}] batch on cuda:{local}: {n} packets, {int(desc['caplen'].astype(np.int64).sum()) / 1e9:.2f} GB "
         f"({time.time() - t0:.1f} s to build)")
 
+    resources, db = None, None
     if analysis:
-        cfg = f"select={CONTRACT};resources={RESOURCES};analysis"
+        if args.resources == "survey":
+            from tests import synth_db
+            t1 = time.time()
+            resources = synth_db.build_survey()      # every rank builds the same file; the write is atomic
+            log(f"[rank {rank}] survey archive {os.path.getsize(resources) / 1e6:.1f} MB ({time.time() - t1:.1f} s)")
+        else:
+            resources = TEST_RESOURCES
+        cfg = f"select={CONTRACT};resources={resources};analysis"
+        t1 = time.time()
         ctx = mercury_amd.Context(cfg, device=local)
         assert ctx.analysis_enabled
+        db = dict(mercury_amd.resource_stats(resources))
+        db.pop("disabled", None)
+        db["archive_bytes"] = os.path.getsize(resources)
+        db["device_table_bytes"] = ctx.device_table_bytes()
+        db["load_seconds"] = round(time.time() - t1, 2)
     else:
         cfg = CONTRACT if args.tls_format == 0 else f"select={CONTRACT};format=tls/{args.tls_format}"
         ctx = mercury_amd.Context(cfg, device=local)
@@ -504,7 +548,7 @@ def main():
     # algorithmic bytes per step: every packet
     # read once, its descriptor, its 32-B record and its fingerprint written;
     # the classifier re-reads the record and the fingerprint of each
-    # classified packet and writes a 24-B analysis record per packet
+    # classified packet and writes a 32-B analysis record per packet
     alg_bytes = caplen_bytes + 16 * n + 32 * n + fp_bytes
     an_info = None
     if analysis:
@@ -538,7 +582,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(workload, draw_seed, 200_000, cpu_threads(), args.cpu_seconds, analysis)
+                cpu = cpu_baseline(workload, draw_seed, 200_000, cpu_threads(), args.cpu_seconds, analysis, resources)
             except Exception as e:   # baseline is reported, never the target
                 log(f"cpu baseline failed: {e}")
         cfg_key = f"{workload}/{n}/{'analysis' if analysis else 'fp'}"
@@ -549,7 +593,8 @@ def main():
         n_fp = int((rec["fp_type"] > 0).sum())
         if workload == "mixed":
             wl = ("config 4: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint + --analysis classifier "
-                  "(synthetic resource archive)") if analysis else \
+                  f"({'SURVEY-sized' if args.resources == 'survey' else 'test'} synthetic resource archive)") \
+                if analysis else \
                  "config 3: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint"
         else:
             wl = "config 2: 10M TLS ClientHello, fingerprint" + (" + classifier" if analysis else "")
@@ -575,7 +620,8 @@ def main():
                 "packet_bytes_per_gpu": caplen_bytes,
                 "select": CONTRACT,
                 "analysis": analysis,
-                "resources": os.path.relpath(RESOURCES, ROOT) if analysis else None,
+                "resources": os.path.relpath(resources, ROOT) if analysis else None,
+                "resource_db": db,
                 "tls_format": "archive's (tls/1)" if analysis else tls_format,
                 "parallelism": f"shard{world}",
                 "distinct_fingerprints_per_step": distinct_fps,

@@ -305,6 +305,9 @@ MFP_EXPORT int mfp_process_os_info(mfp_context ctx, uint32_t proc_slot, uint32_t
  * [3] fingerprints in the context's prevalence LRU */
 MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
 
+/* bytes of the classifier's device tables in HBM */
+MFP_EXPORT uint64_t mfp_analysis_device_bytes(mfp_context ctx);
+
 /* host only (tests): load an archive; out = {fingerprints, entries,
  * processes, feature updates, known-prevalence, asn prefixes, disabled,
  * distinct process names} */

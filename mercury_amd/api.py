@@ -76,6 +76,8 @@ def load_library():
     lib.mfp_analyze_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     lib.mfp_process_batch_host_ex.restype = ctypes.c_longlong
     lib.mfp_process_batch_host_ex.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, vp]
+    lib.mfp_analysis_device_bytes.restype = ctypes.c_uint64
+    lib.mfp_analysis_device_bytes.argtypes = [vp]
     lib.mfp_attribute_count.restype = ctypes.c_int
     lib.mfp_attribute_count.argtypes = [vp]
     lib.mfp_resource_version.restype = ctypes.c_char_p
@@ -260,6 +262,10 @@ class Context:
     def attribute_name(self, bit):
         s = self.lib.mfp_attribute_name(self.h, int(bit))
         return s.decode() if s else None
+
+    def device_table_bytes(self):
+        """Bytes of the classifier's tables in HBM."""
+        return int(self.lib.mfp_analysis_device_bytes(self.h))
 
     def attribute_count(self):
         return int(self.lib.mfp_attribute_count(self.h))

@@ -109,6 +109,7 @@ const char *mfp_classifier_process_name(const mfp_classifier *c, uint32_t id);
 const char *mfp_classifier_attr_name(const mfp_classifier *c, uint32_t i);
 int mfp_classifier_attr_count(const mfp_classifier *c);
 const char *mfp_classifier_version(const mfp_classifier *c);
+uint64_t mfp_classifier_device_bytes(const mfp_classifier *c);
 // os_info entry k of process slot `slot` (proc_off + index); returns the count, -1 bad slot
 int mfp_classifier_os_info(const mfp_classifier *c, uint32_t slot, uint32_t k, const char **name, uint64_t *prev);
 void mfp_classifier_stats(const mfp_classifier *c, uint64_t out[8]);

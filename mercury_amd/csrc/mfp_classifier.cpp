@@ -281,6 +281,7 @@ struct mfp_classifier_s {
     std::vector<std::pair<uint32_t, uint32_t>> os_span;         // (first, count) into os_flat
     std::vector<std::pair<std::string, uint64_t>> os_flat;
     mfp_classifier_dev dev;                                    // device tables (mfp_analysis.h)
+    uint64_t device_bytes = 0;                                 // their size in HBM
     int device = -1;
 };
 
@@ -726,6 +727,7 @@ mfp_classifier *mfp_classifier_load(const char *path) {
 
 int mfp_classifier_attr_count(const mfp_classifier *c) { return (int)c->attr_names.size(); }
 const char *mfp_classifier_version(const mfp_classifier *c) { return c->version.c_str(); }
+uint64_t mfp_classifier_device_bytes(const mfp_classifier *c) { return c->device_bytes; }
 
 int mfp_classifier_os_info(const mfp_classifier *c, uint32_t slot, uint32_t k, const char **name, uint64_t *prev) {
     if (slot >= c->os_span.size()) return -1;
@@ -1032,6 +1034,13 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
               up(d.doh_v4, t.doh_v4) && up(d.doh_v6, t.doh_v6) && up(d.dom_slots, t.dom_slots) &&
               up(d.dom4, t.dom4) && up(d.dom6, t.dom6) && up(d.dom_info, t.dom_info) && up(d.dom_bytes, t.dom_bytes);
     if (!ok) { mfp_set_error("classifier device upload failed"); return -2; }
+    {
+        auto nb = [](const auto &v) { return (uint64_t)(v.size() * sizeof(v[0])); };
+        c->device_bytes = nb(t.fp_slots) + nb(t.prev_slots) + nb(t.entry) + nb(t.prior) + nb(t.proc_id) +
+                          nb(t.proc_mal) + nb(t.proc_attr) + nb(t.feat_slots) + nb(t.upd) + nb(t.pool) + nb(t.asn4) +
+                          nb(t.asn6) + nb(t.doh_names) + nb(t.doh_v4) + nb(t.doh_v6) + nb(t.dom_slots) + nb(t.dom4) +
+                          nb(t.dom6) + nb(t.dom_info) + nb(t.dom_bytes);
+    }
     d.fp_mask = t.fp_slots.size() - 1;
     d.prev_mask = t.prev_slots.size() - 1;
     d.feat_mask = t.feat_slots.size() - 1;

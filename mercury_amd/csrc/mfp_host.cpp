@@ -907,6 +907,10 @@ extern "C" MFP_EXPORT int mfp_analysis_stats(mfp_context c, uint64_t out[4]) {
     return 0;
 }
 
+extern "C" MFP_EXPORT uint64_t mfp_analysis_device_bytes(mfp_context c) {
+    return c && c->clf ? mfp_classifier_device_bytes(c->clf) : 0;
+}
+
 // host-only: load a resource archive and report its size (no device needed)
 extern "C" MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]) {
     mfp_classifier *clf = mfp_classifier_load(path);

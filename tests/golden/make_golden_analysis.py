@@ -9,6 +9,10 @@ Outputs (committed):
   resources-test.tgz    the reference's own test archive (test/data/resources-test.tgz, a data file)
   an_synth.tsv.gz       reference results for synth.batch(N_SYNTH, seed=SEED_SYNTH) with synth_resources.tgz
   an_ref.tsv.gz         reference results for ref_packets.npz with resources-test.tgz
+  an_survey.tsv.gz      reference results for the same synthetic batch with the SURVEY-sized
+                        archive (tests/synth_db.py build_survey(): ~20k fingerprints, P up to
+                        256, ~100k pyasn prefixes; regenerated, not committed -- its sha256 is
+                        in the manifest)
   an_manifest.json      what produced them (plus a checksum of the regenerated batch)
 Columns: idx  valid  fp_type  status  process  score  malware  p_malware
 """
@@ -61,6 +65,10 @@ def main():
     with gzip.open(os.path.join(HERE, "an_synth.tsv.gz"), "wt", encoding="latin-1") as f:
         f.write(run_ref(tmp, os.path.join(HERE, "synth_resources.tgz")))
 
+    survey = synth_db.build_survey()
+    with gzip.open(os.path.join(HERE, "an_survey.tsv.gz"), "wt", encoding="latin-1") as f:
+        f.write(run_ref(tmp, survey))
+
     z = np.load(os.path.join(HERE, "ref_packets.npz"))
     pcaplib.write_mfpb(tmp, z["arena"], z["desc"])
     with gzip.open(os.path.join(HERE, "an_ref.tsv.gz"), "wt", encoding="latin-1") as f:
@@ -73,6 +81,9 @@ def main():
         "synth": {"n": N_SYNTH, "seed": SEED_SYNTH, "workload": "mixed", "n_templates": 4096,
                   "sha256": batch_digest(a, d), "db": info},
         "ref": {"packets": "ref_packets.npz", "resources": "resources-test.tgz (test/data of the reference)"},
+        "survey": {"archive": "tests/golden/_gen/survey_resources.tgz (tests/synth_db.py build_survey)",
+                   "params": {k: v for k, v in synth_db.SURVEY.items()},
+                   "sha256": hashlib.sha256(open(survey, "rb").read()).hexdigest()},
         "columns": ["idx", "valid", "fp_type", "status", "process", "score", "malware", "p_malware"],
     }
     with open(os.path.join(HERE, "an_manifest.json"), "w") as f:

@@ -171,6 +171,33 @@ def test_analysis_synthetic_archive_vs_reference(lane_max_p, monkeypatch):
     assert stats[0] > 5000
 
 
+def survey_archive():
+    """The SURVEY-sized archive (tests/synth_db.py build_survey), regenerated
+    when absent and checked against the golden's sha256."""
+    from tests import synth_db
+    path = synth_db.build_survey()
+    want = json.load(open(os.path.join(GOLD, "an_manifest.json")))["survey"]["sha256"]
+    assert hashlib.sha256(open(path, "rb").read()).hexdigest() == want, "survey archive differs from the golden's"
+    return path
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lane_max_p", [None, "0"])
+def test_analysis_survey_archive_vs_reference(lane_max_p, monkeypatch):
+    """SURVEY 8(d) config-4 archive: ~20 000 fingerprints, P ~ Zipf on 1..256,
+    ~100 000 pyasn prefixes -- the wave scorer's sizes (P up to 256) and a
+    table set far beyond the L2."""
+    if lane_max_p is not None:
+        monkeypatch.setenv("MFP_AN_LANE_MAX_P", lane_max_p)
+    path = survey_archive()
+    a, d = synth_batch()
+    ref = load_ref_an("an_survey.tsv.gz")
+    rec, fp, an, names, stats = run_analysis(a, d, path)
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+    assert sum(1 for r in ref if r["status"] == 1) > 3000
+
+
 @pytest.mark.gpu
 def test_analysis_reference_archive_and_pcaps():
     z = np.load(os.path.join(GOLD, "ref_packets.npz"))

@@ -49,4 +49,4 @@ def test_kernel_bytes_accounting():
     assert kb["k_fp_seg/http_req"] == 4 + 16 + 200 + 32 + 100 + 8
     assert kb["k_fingerprint/tcp_syn"] == 4 + 16 + 60 + 32 + 40
     assert kb["k_classify"] == 3 * (16 + 5) + 128 + 128 + 60
-    assert kb["k_analyze"] == 3 * 56 + (8 + 16 + 32 + 20)
+    assert kb["k_analyze"] == 3 * (32 + 32) + (8 + 16 + 32 + 20)   # record + 32-B analysis record
