@@ -280,6 +280,9 @@ ADEV uint64_t rl64(uint64_t v, int j) {
 // instead of a lane walking its own string.  Returns false on lanes whose
 // strings differ (true on lanes without `has`).
 ADEV bool wave_verify(bool has, const uint8_t *a, const uint8_t *b, uint32_t len, uint32_t lane) {
+#ifdef MFP_PROBE_AN_NOVERIFY
+    return true;
+#endif
     bool ok = true;
     uint64_t m = __ballot(has);
     while (m) {
@@ -710,7 +713,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             const uint64_t pm = __ballot(pending);
             if (lane == 0) P.pend_bits[g] = pm;
             n_pend += (uint32_t)__builtin_popcountll(pm);
+#ifdef MFP_PROBE_AN_NOSEEN
+            uint64_t left = 0;
+#else
             uint64_t left = pm;
+#endif
             while (left) {
                 const int l0 = __builtin_ctzll(left);
                 const uint64_t h0 = rl64(fh, l0);
@@ -739,7 +746,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 }
             }
         }
+#ifdef MFP_PROBE_AN_STOP1
+        bool scored = false;
+#else
         bool scored = analyzable && entry != 0xffffffffu;
+#endif
         if (scored) {
             const mfp_entry E = D.entry[entry];
             np = E.nproc; po = E.proc_off; mdb = E.malware_db; dmz = E.generic_dmz; mbits = E.mal_bits;
@@ -804,6 +815,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             const uint32_t dport = r.dst_port;
 
             // ---- 3. the six feature lookups
+#ifdef MFP_PROBE_AN_NOFEAT
+            if (0) {
+#else
+            {
+#endif
             Hit h;
             h = probe_feature_lane(D, entry, F_ASN, asn, nullptr, 0xffffffffu);
             hoff[0] = h.off; hcnt[0] = h.cnt;
@@ -834,6 +850,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 has[1] = cand_feature_lane(D, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
                 vs[2] = sp; vl[2] = sl; vk[2] = nh;
                 has[2] = cand_feature_lane(D, entry, F_SNI, nh, sl, vh[2], voff[2]);
+            }
             }
         }
 
@@ -937,7 +954,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
 
         // ================= the rest: queued for k_analyze_wave =================
         {
+#ifdef MFP_PROBE_AN_NOLANE
+            const bool defer = false;
+#else
             const bool defer = scored && !lanep;
+#endif
             const uint64_t dm = __ballot(defer);
             if (dm) {
                 unsigned long long base = 0;

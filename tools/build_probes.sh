@@ -10,12 +10,12 @@ for spec in "$@"; do
   defs=""; for m in ${macros//,/ }; do defs="$defs -D$m"; done
   if [[ $name == an_* ]]; then   # classifier probes: recompile mfp_analysis.hip only
     ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/mfp_analysis.hip -o mercury_amd/_probe/a_$name.o &&
-      hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so $OBJ/mfp_kernels.hip.o \
-        mercury_amd/_probe/a_$name.o $OBJ/mfp_compact.hip.o $OBJ/mfp_host.cpp.o $OBJ/mfp_classifier.cpp.o $OBJ/mfp_libmerc.cpp.o $OBJ/mfp_pcap.cpp.o -lz && echo built $name ) &
+      hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so \
+        mercury_amd/_probe/a_$name.o $(ls $OBJ/*.o | grep -v mfp_analysis.hip.o) -lz && echo built $name ) &
     continue
   fi
   ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/mfp_kernels.hip -o mercury_amd/_probe/k_$name.o &&
     hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so mercury_amd/_probe/k_$name.o \
-      $OBJ/mfp_analysis.hip.o $OBJ/mfp_compact.hip.o $OBJ/mfp_host.cpp.o $OBJ/mfp_classifier.cpp.o $OBJ/mfp_libmerc.cpp.o $OBJ/mfp_pcap.cpp.o -lz && echo built $name ) &
+      $(ls $OBJ/*.o | grep -v mfp_kernels.hip.o) -lz && echo built $name ) &
 done
 wait
