@@ -110,6 +110,11 @@ enum {
     MFP_FLAG_ENCAP       = 32, /* reached through IP-in-IP encapsulation (pkt_proc.cc:959) */
     MFP_FLAG_NO_CIPHERS  = 64, /* (D)TLS ClientHello with an empty cipher-suite list: the
                                   reference writes no "tls"/"dtls" object for it (tls.h:1882-1885) */
+    MFP_FLAG_SIDECAR     = 128,/* device arena (QUIC): sni/ua spans index the sidecar that follows
+                                  the string's hash, at fp_offset + round_up(fp_len, 8) + 8:
+                                  {u16 alpn_off, u16 alpn_len} then the server name, the QUIC
+                                  user agent and the ALPN list, which exist only in the decrypted
+                                  payload.  Cleared (spans absent) when strings are packed. */
 };
 /* For MFP_MSG_TLS_SH / MFP_MSG_TLS_CERT records sni_off/sni_len hold the
  * certificate_list datum (tls.h:275-296), the bytes the JSON writer's
@@ -121,7 +126,7 @@ enum {
     MFP_MSG_NONE = 0, MFP_MSG_TLS_CH, MFP_MSG_TLS_SH, MFP_MSG_TLS_CERT,
     MFP_MSG_SSH_INIT, MFP_MSG_SSH_KEX, MFP_MSG_HTTP_REQ, MFP_MSG_HTTP_RESP,
     MFP_MSG_TCP_SYN, MFP_MSG_TCP_SYNACK, MFP_MSG_DTLS_CH, MFP_MSG_DTLS_SH,
-    MFP_MSG_DTLS_HVR,
+    MFP_MSG_DTLS_HVR, MFP_MSG_QUIC,
 };
 
 /* semantics of the reference entry point to follow */
@@ -137,8 +142,10 @@ typedef struct mfp_context_s *mfp_context;
  * "key=value;..." with select=/format=.  Supported selections: tls,
  * tls.client_hello, tls.server_hello, tls.server_certificate, ssh,
  * ssh.client, ssh.server, http, http.request, http.response, tcp,
- * tcp.syn_ack, dtls; NULL/""/"all" select all of these.  Returns NULL on
- * error (unknown protocol, no HIP device, extension not loadable). */
+ * tcp.syn_ack, dtls, quic (QUIC Initial packets: decrypted and fingerprinted
+ * on the device); "format=" takes tls/N and quic/N.  ""/"all" (the reference's
+ * ~45 protocols) are refused.  Returns NULL on error (unknown protocol, no HIP
+ * device, extension not loadable). */
 MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode);
 MFP_EXPORT void mfp_finalize(mfp_context ctx);
 
@@ -175,7 +182,8 @@ MFP_EXPORT int mfp_reserve(mfp_context ctx, size_t n);
 MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen);
 
 /* Parse a packet_filter_cfg string exactly as mfp_init does (host only, no
- * device needed): *select receives the MFP selection bits, *tls_format 0/1/2.
+ * device needed): *select receives the MFP selection bits, *tls_format the TLS
+ * format (0/1/2) in bits 0-7 and the QUIC format (0/1) in bits 8-15.
  * Returns 0, or -1 with mfp_last_error() set.  Mirrors global_config's
  * parser (global_config.h:143-153,246-275,348-368). */
 MFP_EXPORT int mfp_parse_filter(const char *packet_filter_cfg, uint32_t *select, uint32_t *tls_format);

@@ -104,6 +104,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device);
 void mfp_classifier_free(mfp_classifier *c);
 void mfp_classifier_free_device(mfp_classifier_dev &d);
 int mfp_classifier_tls_format(const mfp_classifier *c);
+int mfp_classifier_quic_format(const mfp_classifier *c);
 bool mfp_classifier_disabled(const mfp_classifier *c);
 const char *mfp_classifier_process_name(const mfp_classifier *c, uint32_t id);
 const char *mfp_classifier_attr_name(const mfp_classifier *c, uint32_t i);

@@ -641,11 +641,16 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         a.proc_slot = MFP_NO_PROCESS; a.reserved = 0;
         // messages whose do_analysis calls the classifier: TLS ClientHello
         // (tls.h:1977), HTTP request (http.cc:571), SSH client KEXINIT
-        // (ssh.h:480); their type must also be in the archive (fp_types)
-        const bool typed = live && r.fp_len != 0 && (r.fp_type == 1 || r.fp_type == 3 || r.fp_type == 5);
+        // (ssh.h:480), QUIC Initial (quic.h:1722); their type must also be in
+        // the archive (fp_types)
+        const bool typed = live && r.fp_len != 0 &&
+                           (r.fp_type == 1 || r.fp_type == 3 || r.fp_type == 5 || r.fp_type == 12);
         const bool analyzable = typed && ((D.types_mask >> r.fp_type) & 1u);
         if (typed && !analyzable) { a.status = 4; a.flags = MFP_AN_VALID; }   // fingerprint_status_unanalyzed
-        const uint64_t am = __ballot(analyzable);
+        // the classifier-agnostic attributes of TLS and QUIC ClientHellos, analysed
+        // or not (check_additional_attributes analysis.h:544-549, pkt_proc.cc:1686)
+        const bool xcheck = typed && (r.fp_type == 1 || r.fp_type == 12) && (D.doh_enabled | D.faking_enabled);
+        const uint64_t am = __ballot(analyzable || xcheck);
         if (!am) {
             if (live) P.out[i] = a;
             if (lane == 0) P.pend_bits[g] = 0;
@@ -768,8 +773,9 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         bool has[3] = {false, false, false};
         // ---- destination context (destination_context::init, result.h:346)
         // and the classifier-agnostic attributes of a ClientHello
-        const bool xcheck = analyzable && r.fp_type == 1 && (D.doh_enabled | D.faking_enabled);
         const uint8_t *pkt = P.arena + (scored || xcheck ? P.desc[i].offset : 0);
+        // server name / user agent: packet bytes, or the QUIC sidecar behind the string's hash
+        const uint8_t *sbase = (r.flags & MFP_FLAG_SIDECAR) ? fp + ((r.fp_len + 7) & ~7u) + 8 : pkt;
         Dst dd;
         dd.ipv = 0; dd.v4 = 0; dd.hi = 0; dd.lo = 0;
         if (scored || xcheck) dd = dst_of(pkt, r.net);
@@ -778,9 +784,9 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             // sn_str: the server name as a C string (strncpy MAX_SNI_LEN, result.h:348)
             const uint32_t sl0 = r.sni_len == 0xffff ? 0u : r.sni_len;
             uint64_t ch = 0;
-            const uint32_t cl = cstr_hash(pkt + r.sni_off, sl0 < 256 ? sl0 : 256u, ch);
-            if (D.doh_enabled && doh_hit(D, pkt + r.sni_off, cl, ch, dd)) xattr |= 1u << D.doh_idx;
-            if (D.faking_enabled && domain_faking(D, pkt + r.sni_off, cl, dd)) xattr |= 1u << D.domain_faking_idx;
+            const uint32_t cl = cstr_hash(sbase + r.sni_off, sl0 < 256 ? sl0 : 256u, ch);
+            if (D.doh_enabled && doh_hit(D, sbase + r.sni_off, cl, ch, dd)) xattr |= 1u << D.doh_idx;
+            if (D.faking_enabled && domain_faking(D, sbase + r.sni_off, cl, dd)) xattr |= 1u << D.domain_faking_idx;
         }
         if (pending && faketls_fp(fp, fl)) xattr |= 1u << D.faketls_idx;   // randomized ClientHellos only
         if (scored) {
@@ -802,14 +808,15 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             }
             // server name: TLS SNI / HTTP Host (strncpy 256, NUL stops)
             const uint32_t sl = r.sni_len == 0xffff ? 0u : r.sni_len;
-            const uint8_t *sp = pkt + r.sni_off;
+            const uint8_t *sp = sbase + r.sni_off;
             uint32_t tld = 0;
             uint64_t nh = 0;
             plain = plain_server_name(sp, sl, tld, nh);   // no NUL in a plain name
-            // user agent (strncpy 511, NUL stops); TLS has none
-            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH ? 0u : r.ua_len;   // (ClientHello: the ALPN slot)
+            // user agent (strncpy 511, NUL stops); TLS has none (its slot holds
+            // the ALPN list); QUIC's is transport parameter 0x3129 (tls.h:1346-1355)
+            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH ? 0u : r.ua_len;
             if (ul > 511) ul = 511;
-            const uint8_t *up = pkt + r.ua_off;
+            const uint8_t *up = sbase + r.ua_off;
             uint64_t uh = 0;
             ul = cstr_hash(up, ul, uh);
             const uint32_t dport = r.dst_port;
@@ -982,6 +989,8 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             // analyze_ip_packet: a truncated message reports "unlabeled" and
             // keeps its classification (pkt_proc.cc:1716-1719)
             if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED) && !pending) a.status = 3;
+        } else if (xcheck) {
+            a.attr = (uint16_t)xattr;   // unanalyzed type: only the classifier-agnostic attributes
         }
         if (live) P.out[i] = a;   // the status lives in the analysis record only (no 1-byte record rewrite)
     }
@@ -1022,7 +1031,8 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
             const mfp_record r = P.rec[i];
             const uint32_t sni = rfl((uint32_t)r.sni_off | ((uint32_t)r.sni_len << 16));
             const uint32_t sl = (sni >> 16) == 0xffff ? 0 : (sni >> 16);
-            const uint8_t *sp = P.arena + P.desc[i].offset + (sni & 0xffff);
+            const uint8_t *sp = ((r.flags & MFP_FLAG_SIDECAR) ? P.fp_arena + r.fp_offset + ((r.fp_len + 7) & ~7u) + 8
+                                                             : P.arena + P.desc[i].offset) + (sni & 0xffff);
             int nlen = 0;
             if (lane == 0) nlen = normalize_server_name(sp, (int)sl, nbuf);
             nlen = (int)rfl((uint32_t)nlen);

@@ -749,6 +749,11 @@ int mfp_classifier_tls_format(const mfp_classifier *c) {
     auto it = c->fp_count_and_format.find("tls");
     return it == c->fp_count_and_format.end() ? 0 : (int)it->second.second;
 }
+// classifier::get_quic_fingerprint_format (analysis.h:488)
+int mfp_classifier_quic_format(const mfp_classifier *c) {
+    auto it = c->fp_count_and_format.find("quic");
+    return it == c->fp_count_and_format.end() ? 0 : (int)it->second.second;
+}
 bool mfp_classifier_disabled(const mfp_classifier *c) { return c->disabled; }
 const char *mfp_classifier_process_name(const mfp_classifier *c, uint32_t id) {
     return id < c->proc_names.size() ? c->proc_names[id].c_str() : nullptr;

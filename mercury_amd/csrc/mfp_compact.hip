@@ -100,6 +100,11 @@ __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t 
         if (i < n && len) {
             rec[i].fp_offset = dof;
             rec[i].flags &= (uint8_t)~MFP_FLAG_HASHED;   // the hashes stay behind
+            if (rec[i].flags & MFP_FLAG_SIDECAR) {       // ... and so do QUIC sidecars (include/mfp.h)
+                rec[i].flags &= (uint8_t)~MFP_FLAG_SIDECAR;
+                rec[i].sni_off = 0; rec[i].sni_len = 0xffff;
+                rec[i].ua_off = 0; rec[i].ua_len = 0xffff;
+            }
         }
     }
 }

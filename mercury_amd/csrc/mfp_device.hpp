@@ -1292,6 +1292,7 @@ struct Out {
     uint32_t sni_off, sni_len, ua_off, ua_len;
     uint32_t src_port, dst_port;
     uint32_t net;        // innermost IP header offset | version << 16 (flow key, flow_key.h:71)
+    uint32_t pay_off, pay_len;   // QUIC: the UDP payload (k_quic takes it from here)
 };
 // the certificate_list datum in the record's server-name slot (TLS server
 // messages have no server name): the JSON writer's certs array (tls.h:2183)
@@ -1314,7 +1315,7 @@ enum : uint32_t {
 enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
     SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
-    SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9,
+    SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9, SEL_QUIC = 1u << 10,
 };
 
 // masked 8/16-byte matchers (match.h:64-103)
@@ -1349,6 +1350,7 @@ DEV void fp_type_prefix(E &b, uint32_t t) {             // fingerprint::set_type
     case 7: b.lit("tcp/"); break;
     case 10: b.lit("dtls/"); break;
     case 11: b.lit("dtls_server/"); break;
+    case 12: b.lit("quic/"); break;
     case 13: b.lit("tcp_server/"); break;
     case 17: b.lit("ssh_init/"); break;
     case 18: b.lit("ssh_server/"); break;
@@ -1585,6 +1587,16 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
 // set_udp_protocol pkt_proc.cc:677 (selection subset: DTLS, dtls.h)
 template <uint32_t FAM, class E>
 DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
+    // 8-byte matchers before 16-byte ones (get_udp_msg_type proto_identify.h:955-960):
+    // the QUIC long header (quic_initial_packet::matcher quic.h:544).  Only
+    // k_quic (mfp_quic.hip) parses QUIC; every other walker hands it over.
+    if ((cfg.select & SEL_QUIC) && clen(pkt) >= 8 && (ld(pkt.d) & 0x80) && !(ld(pkt.d + 5) & 0xe0)) {
+        o.msg = MFP_MSG_QUIC;
+        o.pay_off = (uint32_t)(pkt.d - base);
+        o.pay_len = (uint32_t)clen(pkt);
+        if (!cfg.classify) b.punt_pkt();
+        return;
+    }
     if (!(cfg.select & SEL_DTLS) || clen(pkt) < 16) return;
     uint64_t w0 = 0, w1 = 0;
     for (int i = 0; i < 8; i++) { w0 |= (uint64_t)ld(pkt.d + i) << (8 * i); w1 |= (uint64_t)ld(pkt.d + 8 + i) << (8 * i); }
@@ -1802,6 +1814,7 @@ DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t
     o.sni_off = o.ua_off = 0; o.sni_len = o.ua_len = 0xffff;
     o.src_port = o.dst_port = 0;
     o.net = 0;
+    o.pay_off = o.pay_len = 0;
     Cur p = cmk(data, data + len);
     switch (linktype) {
     case 1: {                                           // eth::eth eth.h:137
@@ -1858,5 +1871,21 @@ DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t
     if (cnull(p)) return;
     ip_path<FAM>(b, cfg, o, p, data);
 }
+
+// parameters of the fingerprint kernels (mfp_kernels.hip, mfp_quic.hip)
+struct KParams {
+    Cfg cfg;
+    const uint8_t *arena;
+    const mfp_pkt_desc *desc;
+    uint64_t n;
+    mfp_record *rec;
+    uint8_t *fp_arena;
+    uint64_t fp_cap;
+    unsigned long long *fp_used;     // [0] bytes reserved, [1] overflow flag, [2] bytes written, [3] fallback count
+    const uint32_t *idx;             // packet indices (count = *count); nullptr = all n packets
+    const unsigned long long *count;
+    uint32_t *quic_idx;              // QUIC packets found by the walkers, for k_quic (count *quic_count)
+    unsigned long long *quic_count;
+};
 
 }  // namespace mfp

@@ -39,7 +39,9 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
-                                      uint32_t bin_lds_mask, hipStream_t stream, mfp_prof *prof);
+                                      uint32_t bin_lds_mask, uint32_t quic_format, uint8_t *quic_scratch,
+                                      uint32_t quic_grid, hipStream_t stream, mfp_prof *prof);
+extern "C" size_t mfp_quic_scratch_bytes(uint32_t grid);
 
 extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
                                   unsigned long long *block_sum, hipStream_t stream, mfp_prof *prof);
@@ -63,8 +65,8 @@ extern "C" MFP_EXPORT uint32_t mfp_reference_version(void) { return (2u << 16) |
 enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
     SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
-    SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9,
-    SEL_ALL = (1u << 10) - 1,
+    SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9, SEL_QUIC = 1u << 10,
+    SEL_ALL = (1u << 11) - 1,
 };
 
 static std::string strip(const std::string &s) {
@@ -85,13 +87,13 @@ static std::string trim(const std::string &s) {
 static bool parse_select(const std::string &list, uint32_t &sel) {
     // "all" (and the empty selection, which the reference reads as "all",
     // global_config.h:248) selects ~45 protocols this path does not parse
-    // (DNS, QUIC, SMTP, ...) and the GRE/VXLAN/Geneve decapsulations: the
+    // (DNS, SMTP, ...) and the GRE/VXLAN/Geneve decapsulations: the
     // reference would write records the device cannot, so it is refused
     // rather than silently diverging
     if (strip(list).empty() || strip(list) == "all") {
         mfp_set_error("protocol selection \"%s\" includes protocols outside the device path; select from: tls, "
                       "tls.client_hello, tls.server_hello, tls.server_certificate, ssh, ssh.client, ssh.server, "
-                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, none", list.empty() ? "" : list.c_str());
+                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, quic, none", list.empty() ? "" : list.c_str());
         return false;
     }
     const std::string &s = list;
@@ -101,7 +103,7 @@ static bool parse_select(const std::string &list, uint32_t &sel) {
         {"tls.server_hello", SEL_TLS_SH}, {"tls.server_certificate", SEL_TLS_CERT},
         {"ssh", SEL_SSH_CLIENT | SEL_SSH_SERVER}, {"ssh.client", SEL_SSH_CLIENT}, {"ssh.server", SEL_SSH_SERVER},
         {"http", SEL_HTTP_REQ | SEL_HTTP_RESP}, {"http.request", SEL_HTTP_REQ}, {"http.response", SEL_HTTP_RESP},
-        {"tcp", SEL_TCP_SYN}, {"tcp.syn_ack", SEL_TCP_SYNACK}, {"dtls", SEL_DTLS},
+        {"tcp", SEL_TCP_SYN}, {"tcp.syn_ack", SEL_TCP_SYNACK}, {"dtls", SEL_DTLS}, {"quic", SEL_QUIC},
     };
     bool none = false;
     size_t pos = 0;
@@ -122,7 +124,8 @@ static bool parse_select(const std::string &list, uint32_t &sel) {
     return true;
 }
 
-// fingerprint_format::set_fingerprint_format (global_config.h:92)
+// fingerprint_format::set_fingerprint_format (global_config.h:55-121); the
+// result packs the TLS format in bits 0-7 and the QUIC format in bits 8-15
 static bool parse_format(const std::string &s, uint32_t &tls_format) {
     size_t pos = 0;
     while (pos <= s.size()) {
@@ -132,11 +135,15 @@ static bool parse_format(const std::string &s, uint32_t &tls_format) {
             size_t sl = tok.find('/');
             std::string proto = tok.substr(0, sl), ver = sl == std::string::npos ? "" : tok.substr(sl + 1);
             if (proto == "tls") {
-                if (ver == "") tls_format = 0;
-                else if (ver == "1") tls_format = 1;
-                else if (ver == "2") tls_format = 2;
+                if (ver == "") tls_format = tls_format & ~0xffu;
+                else if (ver == "1") tls_format = (tls_format & ~0xffu) | 1u;
+                else if (ver == "2") tls_format = (tls_format & ~0xffu) | 2u;
                 else { mfp_set_error("unknown fingerprint format %s", tok.c_str()); return false; }
-            } else if (proto != "quic") {
+            } else if (proto == "quic") {
+                if (ver == "") tls_format &= ~0xff00u;
+                else if (ver == "1") tls_format = (tls_format & ~0xff00u) | (1u << 8);
+                else { mfp_set_error("unknown fingerprint format %s", tok.c_str()); return false; }
+            } else {
                 mfp_set_error("unknown fingerprint format %s", tok.c_str());
                 return false;
             }
@@ -240,7 +247,8 @@ void mfp_prof_end(mfp_prof *p, hipStream_t s) {
 // mfp_process_pipelined, so two batches can be in flight on two streams.
 struct Slot {
     unsigned long long *d_used = nullptr;   // fp arena counters of host batches
-    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass (8 bins)
+    unsigned long long *d_bins = nullptr;   // per-bin packet counts of the classify pass (9 bins)
+    uint8_t *d_quic = nullptr;              // k_quic's per-lane scratch (decrypted payload, CRYPTO buffer)
     uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list / bin ids
     unsigned long long *d_an_stats = nullptr;
     uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings (bitmap)
@@ -270,14 +278,14 @@ struct Slot {
 
     bool init() {
         return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
-               hipMalloc(&d_bins, 8 * sizeof(unsigned long long)) == hipSuccess &&
+               hipMalloc(&d_bins, 16 * sizeof(unsigned long long)) == hipSuccess &&
                hipMalloc(&d_an_stats, 4 * sizeof(unsigned long long)) == hipSuccess &&
                hipMemset(d_an_stats, 0, 4 * sizeof(unsigned long long)) == hipSuccess &&
                hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
-        void *p[] = {d_used, d_bins, d_work, d_an_stats, d_pending, d_deferred, d_an, d_ap, d_arena, d_desc, d_rec, d_fp, d_fp2,
+        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_deferred, d_an, d_ap, d_arena, d_desc, d_rec, d_fp, d_fp2,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         if (h_used) (void)hipHostFree(h_used);
@@ -288,6 +296,8 @@ struct Slot {
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
+    uint32_t quic_format = 0;            // fingerprint_format::quic_fingerprint_format (global_config.h:41)
+    uint32_t quic_grid = 512;            // k_quic workgroups (x 128 lanes, each with a scratch slot)
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|lane (A/B, debugging)
     // bin b -> kernel: k_fp_lds (LDS-staged walk) if bit b of bin_lds_mask
     // (MFP_BIN_LDS_MASK), else the HBM lane walker; the bins of bin_seg_mask
@@ -327,7 +337,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     }
     if (device < 0 || device >= ndev) { mfp_set_error("bad device %d", device); return nullptr; }
     auto *c = new mfp_context_s;
-    c->device = device; c->select = sel; c->tls_format = fmt; c->mode = mode;
+    c->device = device; c->select = sel; c->tls_format = fmt & 0xff; c->quic_format = (fmt >> 8) & 0xff; c->mode = mode;
     const char *st = getenv("MFP_STRATEGY");
     if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
     const char *sm = getenv("MFP_BIN_SEG_MASK");
@@ -353,6 +363,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
             mfp_classifier_free(clf);
         } else {
             c->tls_format = (uint32_t)mfp_classifier_tls_format(clf);
+            c->quic_format = (uint32_t)mfp_classifier_quic_format(clf);
             if (mfp_classifier_upload(clf, device) != 0) {
                 mfp_classifier_free(clf);
                 mfp_finalize(c);
@@ -383,7 +394,7 @@ extern "C" MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen) {
 }
 
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode) {
-    c->select = select; c->tls_format = tls_format; c->mode = mode;
+    c->select = select; c->tls_format = tls_format & 0xff; c->quic_format = (tls_format >> 8) & 0xff; c->mode = mode;
     return 0;
 }
 
@@ -402,7 +413,7 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    if (grow(c->slot[0].d_work, c->slot[0].cap_work, 10 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(c->slot[0].d_work, c->slot[0].cap_work, 11 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     return 0;
 }
 
@@ -410,12 +421,19 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
                                  hipStream_t s) {
     HIPCHK(hipSetDevice(c->device));
-    if (grow(S.d_work, S.cap_work, 10 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if (grow(S.d_work, S.cap_work, 11 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
+    if ((c->select & SEL_QUIC) && !S.d_quic &&
+        hipMalloc(&S.d_quic, mfp_quic_scratch_bytes(c->quic_grid)) != hipSuccess) {
+        S.d_quic = nullptr;
+        mfp_set_error("device allocation failed (QUIC scratch)");
+        return -2;
+    }
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(S.d_bins, 0, 8 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(S.d_bins, 0, 16 * sizeof(unsigned long long), s));
     if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
                                fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
-                               c->bin_seg_mask, c->bin_lds_mask, s, c->prof) != 0) {
+                               c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
+                               c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

@@ -340,6 +340,9 @@ struct TsCache { uint64_t sec = ~0ull, usec = ~0ull; int len = 0; char text[40];
 bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const char *fp_arena,
                   uint64_t sec, uint64_t nsec, mfp_context ctx, const mfp_analysis *an, const double *ap) {
     if (!(r.flags & MFP_FLAG_EMIT)) return true;
+    // QUIC records carry a "quic" object with the decrypted payload
+    // (quic_init::write_json quic.h:1662-1690), which the device does not return
+    if (r.msg == MFP_MSG_QUIC) return false;
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
     // IP-in-IP: outer headers sit back to back before the inner one (IPv4
     // fixed 20 B, ip.h:124-137; IPv6 40 B when it has no extension headers)

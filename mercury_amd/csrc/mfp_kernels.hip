@@ -18,19 +18,6 @@ namespace mfp {
 
 constexpr int TILE = 256;
 
-struct KParams {
-    Cfg cfg;
-    const uint8_t *arena;
-    const mfp_pkt_desc *desc;
-    uint64_t n;
-    mfp_record *rec;
-    uint8_t *fp_arena;
-    uint64_t fp_cap;
-    unsigned long long *fp_used;     // [0] bytes reserved, [1] overflow flag, [2] bytes written, [3] fallback count
-    const uint32_t *idx;             // packet indices (count = *count); nullptr = all n packets
-    const unsigned long long *count;
-};
-
 // k_fingerprint -- lane-per-packet walker straight from HBM, grid-stride
 // over tiles of TILE packets.  The fallback lane of the other bin kernels
 // (packets larger than k_fp_lds's stage, segment lists that overflow); with
@@ -77,13 +64,24 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
             else o.fp_type = 0;       // fingerprint::final drops truncated fingerprints
         }
     }
-    if (FAM != FAM_ALL) {             // a parser this instance lacks: the fallback lane
-        const uint64_t pm = __ballot(punt);
+    {
+        // a parser this instance lacks: the fallback lane; QUIC (which only
+        // k_quic parses): the QUIC list
+        const bool to_quic = punt && o.msg == MFP_MSG_QUIC;
+        const bool to_fb = punt && !to_quic && FAM != FAM_ALL;
+        const uint64_t pm = __ballot(to_fb);
         if (pm) {
             uint32_t b = 0;
             if ((tid & 63) == 0) b = (uint32_t)atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(pm));
             b = (uint32_t)__shfl((int)b, 0, 64);
-            if (punt) fallback[b + __builtin_popcountll(pm & ((1ull << (tid & 63)) - 1))] = (uint32_t)i;
+            if (to_fb) fallback[b + __builtin_popcountll(pm & ((1ull << (tid & 63)) - 1))] = (uint32_t)i;
+        }
+        const uint64_t qm = __ballot(to_quic);
+        if (qm) {
+            uint32_t b = 0;
+            if ((tid & 63) == 0) b = (uint32_t)atomicAdd(P.quic_count, (unsigned long long)__builtin_popcountll(qm));
+            b = (uint32_t)__shfl((int)b, 0, 64);
+            if (to_quic) P.quic_idx[b + __builtin_popcountll(qm & ((1ull << (tid & 63)) - 1))] = (uint32_t)i;
         }
     }
 
@@ -507,7 +505,8 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
 // protocol bins of the classify pass: each bin is then fingerprinted by its
 // own k_fingerprint launch over a compact index list, so the lanes of a wave
 // walk the same protocol (same parser, similar loop trip counts)
-constexpr int NBINS = 8;
+constexpr int NBINS = 9;
+constexpr int QUIC_BIN = 8;   // run by k_quic after every other bin (mfp_quic.hip)
 DEV int msg_bin(uint32_t msg) {
     switch (msg) {
     case MFP_MSG_TLS_CH: return 0;
@@ -517,6 +516,7 @@ DEV int msg_bin(uint32_t msg) {
     case MFP_MSG_TLS_SH: case MFP_MSG_TLS_CERT: return 5;
     case MFP_MSG_SSH_INIT: case MFP_MSG_SSH_KEX: return 6;
     case MFP_MSG_DTLS_CH: case MFP_MSG_DTLS_SH: case MFP_MSG_DTLS_HVR: return 7;
+    case MFP_MSG_QUIC: return QUIC_BIN;
     default: return 4;   // no message of a selected protocol
     }
 }
@@ -612,6 +612,9 @@ __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, ui
 
 #include "mfp_internal.h"
 
+extern "C" int mfp_launch_quic(const void *kparams, uint8_t *scratch, uint32_t quic_format, uint32_t grid,
+                               hipStream_t stream, mfp_prof *prof);
+
 // launchers used by the host library (mfp_host.cpp)
 #ifndef MFP_LDS_STAGE
 #define MFP_LDS_STAGE (36 * 1024)   // per-wave stage of k_fp_lds: 40 KiB of LDS per wave, 4 waves per CU
@@ -623,7 +626,8 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
-                                      uint32_t bin_lds_mask, hipStream_t stream, mfp_prof *prof) {
+                                      uint32_t bin_lds_mask, uint32_t quic_format, uint8_t *quic_scratch,
+                                      uint32_t quic_grid, hipStream_t stream, mfp_prof *prof) {
 #define MFP_LAUNCH(name, ...)                                \
     do {                                                     \
         if (prof) mfp_prof_begin(prof, name, stream);        \
@@ -636,11 +640,24 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
     P.idx = nullptr; P.count = nullptr;
+    // QUIC packets (bin 8 of the classify pass, plus any a walker hands over)
+    P.quic_idx = work + (uint64_t)mfp::QUIC_BIN * n;
+    P.quic_count = bin_count + mfp::QUIC_BIN;
+    const bool quic = (select & mfp::SEL_QUIC) != 0;
+    if (quic && !quic_scratch) return -1;
+    auto launch_quic = [&]() -> int {
+        if (!quic) return 0;
+        mfp::KParams Q = P;
+        Q.idx = P.quic_idx;
+        Q.count = P.quic_count;
+        return mfp_launch_quic(&Q, quic_scratch, quic_format, quic_grid, stream, prof);
+    };
     const uint64_t tiles = (n + mfp::TILE - 1) / mfp::TILE;
     if (strategy == MFP_STRATEGY_LANE) {
         MFP_LAUNCH("k_fingerprint", mfp::k_fingerprint<mfp::FAM_ALL>, dim3((uint32_t)tiles), dim3(mfp::TILE), 0, stream,
                    P, nullptr);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
+        if (hipGetLastError() != hipSuccess) return -1;
+        return launch_quic();
     }
     // classify, then one launch per protocol bin over its index list: the
     // LDS-staged walker (bin_lds_mask), the HBM lane walker, or for the HTTP
@@ -654,17 +671,18 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     const uint64_t lblocks = ((n + 63) / 64) < 2048 ? (n + 63) / 64 : 2048;
     static const char *const lane_name[mfp::NBINS] = {"k_fingerprint/tls_ch", "k_fingerprint/http_req",
         "k_fingerprint/tcp_syn", "k_fingerprint/http_resp", "k_fingerprint/other", "k_fingerprint/tls_sh",
-        "k_fingerprint/ssh", "k_fingerprint/dtls"};
+        "k_fingerprint/ssh", "k_fingerprint/dtls", "k_quic"};
     static const char *const seg_name[mfp::NBINS] = {"k_fp_seg/tls_ch", "k_fp_seg/http_req",
         "k_fp_seg/tcp_syn", "k_fp_seg/http_resp", "k_fp_seg/other", "k_fp_seg/tls_sh",
-        "k_fp_seg/ssh", "k_fp_seg/dtls"};
+        "k_fp_seg/ssh", "k_fp_seg/dtls", "k_quic"};
     static const char *const lds_name[mfp::NBINS] = {"k_fp_lds/tls_ch", "k_fp_lds/http_req",
         "k_fp_lds/tcp_syn", "k_fp_lds/http_resp", "k_fp_lds/other", "k_fp_lds/tls_sh",
-        "k_fp_lds/ssh", "k_fp_lds/dtls"};
+        "k_fp_lds/ssh", "k_fp_lds/dtls", "k_quic"};
     // each bin's kernel carries its protocol's parser family only (bin 4,
     // "other", all of them); misbinned packets are punted to the fallback lane
     using namespace mfp;
     for (int b = 0; b < NBINS; b++) {
+        if (b == QUIC_BIN) continue;
         P.idx = work + (uint64_t)b * n;
         P.count = bin_count + b;
         const bool seg = bin_seg_mask & (1u << b);
@@ -699,6 +717,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
         MFP_LAUNCH("k_fingerprint/fallback", k_fingerprint<FAM_ALL>, dim3((uint32_t)fb), dim3(TILE), 0, stream, P,
                    nullptr);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (hipGetLastError() != hipSuccess) return -1;
+    return launch_quic();
 }
 #undef MFP_LAUNCH
