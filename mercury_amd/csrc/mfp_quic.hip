@@ -212,7 +212,7 @@ DEV int quic_decrypt(const QHdr &h, uint8_t *pt, const uint32_t *te, uint64_t *g
     if (aad_len > 1024) return -1;                              // data_buffer<1024> (quic.h:811, 982)
     // unprotected packet number bytes (big-endian in pnw's top bytes)
     const uint32_t pn_raw = ld_be32n(h.payload.d, 4);
-    const uint32_t pnw = (pn_raw ^ (mask[0] << 8)) & (0xffffffffu << (8 * (4 - pnl)));
+    const uint32_t pnw = (pn_raw ^ ((mask[0] << 8) | (mask[1] >> 24))) & (0xffffffffu << (8 * (4 - pnl)));
     // AEAD nonce: iv with the packet number XORed into its last bytes (quic.h:988-990)
     {
         const uint64_t pn = (uint64_t)(pnw >> (8 * (4 - pnl)));
