@@ -143,7 +143,8 @@ typedef struct mfp_context_s *mfp_context;
  * tls.client_hello, tls.server_hello, tls.server_certificate, ssh,
  * ssh.client, ssh.server, http, http.request, http.response, tcp,
  * tcp.syn_ack, dtls, quic (QUIC Initial packets: decrypted and fingerprinted
- * on the device); "format=" takes tls/N and quic/N.  ""/"all" (the reference's
+ * on the device), gre, vxlan, geneve (decapsulation, pkt_proc.cc:959-1049);
+ * "format=" takes tls/N and quic/N.  ""/"all" (the reference's
  * ~45 protocols) are refused.  Returns NULL on error (unknown protocol, no HIP
  * device, extension not loadable). */
 MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode);

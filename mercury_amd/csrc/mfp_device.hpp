@@ -1316,6 +1316,7 @@ enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
     SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
     SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9, SEL_QUIC = 1u << 10,
+    SEL_GRE = 1u << 11, SEL_VXLAN = 1u << 12, SEL_GENEVE = 1u << 13,   // decapsulations (proto_identify.h:812-886)
 };
 
 // masked 8/16-byte matchers (match.h:64-103)
@@ -1726,18 +1727,120 @@ DEV void tcp_syn_fp(E &b, int ipv, const uint8_t *iph, const uint8_t *tcph, Cur 
     b.putc(')');
 }
 
+DEV bool ppp_is_ip(Cur &p) {                            // ppp::is_ip ppp.h:76
+    uint32_t b = look_u8(p);
+    if (b == 0x7e) {
+        rd_u8(p);
+        b = look_u8(p);
+        if (b == 0xff) { rd_u8(p); rd_u8(p); }
+    } else if (b == 0xff) {
+        rd_u8(p); rd_u8(p);
+    }
+    uint32_t proto;
+    b = look_u8(p);
+    if (b & 1) { uint32_t x; if (!(p.d && p.e > p.d)) { cset_null(p); proto = 0; } else { x = rd_u8(p); proto = x; } }
+    else { uint32_t v = 0; for (int i = 0; i < 2; i++) { v *= 256; v += rd_u8(p); } proto = v; }
+    return proto == 0x21 || proto == 0x57;
+}
+
+// eth::get_ip (eth.h:114-133 over the eth ctor eth.h:137-187): Ethernet
+// (802.1ad, 802.1Q, MPLS, Cisco metadata) down to IP, or PPPoE -> PPP -> IP
+DEV bool eth_get_ip(Cur &p) {
+    uint64_t et;
+    cskip(p, 12);
+    if (!rd_uint(p, 2, et)) return false;
+    if (et == 0x88a8) { cskip(p, 2); if (!rd_uint(p, 2, et)) return false; }
+    while (et == 0x8100) { cskip(p, 2); if (!rd_uint(p, 2, et)) return false; }
+    if (et == 0x8847) {
+        uint64_t lbl = 0;
+        while (!(lbl & 0x100)) { if (!rd_uint(p, 4, lbl)) return false; }
+        et = 0x0800;
+    }
+    if (et == 0x8909) { cskip(p, 6); if (!rd_uint(p, 2, et)) return false; }
+    if (et == 0x0800 || et == 0x86dd) return true;
+    if (et == 0x8864) {
+        Cur t; cparse(t, p, 1); cparse(t, p, 1); cparse(t, p, 2); cparse(t, p, 2);
+        return ppp_is_ip(p);
+    }
+    return false;
+}
+
+// GRE header (gre_header gre.h): flags/version, protocol type, the checksum
+// word when C is set; an inner IP packet follows for IPv4 / IPv6
+DEV bool gre_next(Cur &p) {
+    uint64_t crv, pt;
+    rd_uint(p, 2, crv);
+    rd_uint(p, 2, pt);
+    if (crv & 0x8000) cskip(p, 4);
+    if (cnull(p)) pt = 0;
+    return pt == 0x0800 || pt == 0x86dd;
+}
+
 // IP layer: ip_write_json pkt_proc.cc:1063 / analyze_ip_packet pkt_proc.cc:1597
 template <uint32_t FAM, class E>
 DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
     const uint8_t *iph; int ipv;
     uint32_t proto = ip_parse(pkt, iph, ipv);
     uint32_t enc = 0;            // net bits 20-27: levels, v6 mask, irregular (include/mfp.h)
-    for (int n = 0; n < 4 && (proto == 4 || proto == 41); n++) {   // pkt_proc.cc:959
+    // encapsulations::process_encapsulations (pkt_proc.cc:972-1028): up to
+    // four levels of IP-in-IP, GRE (IP protocol 47 or UDP port 4754), VXLAN
+    // (UDP 4789) and Geneve (UDP 6081), each re-parsing the inner IP header.
+    // A tunnel header whose payload is not IP ends the walk with the cursor
+    // past it, as in the reference.  Only IP-in-IP levels are described in the
+    // record (the JSON writer rebuilds their "encapsulations" entries); any
+    // other tunnel marks the chain irregular.
+    for (int n = 0; n < 4; n++) {
         const uint8_t *oh = iph; const int ov = ipv;
+        bool ipip = false;
+        if (proto == 4 || proto == 41) {
+            ipip = true;
+        } else if (proto == 47) {
+            if (!(cfg.select & SEL_GRE)) break;
+            if (!gre_next(pkt)) break;
+        } else if (proto == 17 && (cfg.select & (SEL_GRE | SEL_VXLAN | SEL_GENEVE))) {
+            Cur u = pkt;
+            const uint8_t *uh = cget_ptr(u, 8);
+            const uint32_t dport = uh ? (ld(uh + 2) << 8) | ld(uh + 3) : 0u;
+            if ((cfg.select & SEL_VXLAN) && dport == 4789) {            // vxlan.hpp
+                pkt = u;
+                const uint32_t fl = rd_u8(pkt);
+                Cur t; cparse(t, pkt, 3); cparse(t, pkt, 3); cparse(t, pkt, 1);
+                if (!(fl & 0x08)) break;
+                if (!eth_get_ip(pkt)) break;
+            } else if ((cfg.select & SEL_GENEVE) && dport == 6081) {    // geneve.hpp
+                pkt = u;
+                const uint32_t fb = rd_u8(pkt);
+                rd_u8(pkt);
+                uint64_t pt;
+                rd_uint(pkt, 2, pt);
+                Cur t; cparse(t, pkt, 3);
+                rd_u8(pkt);
+                cparse(t, pkt, 4 * (long)(fb & 0x3f));
+                if (pt == 0x6558) { if (!eth_get_ip(pkt)) break; }
+                else if (pt == 0x0800 || pt == 0x86dd) { }
+                else if (pt == 0) {                                      // BSD loopback (loopback.hpp)
+                    uint64_t lt;
+                    rd_uint(pkt, 4, lt);
+                    if (cnull(pkt)) break;
+                    if (!(lt == 2 || lt == 0x02000000 || lt == 24 || lt == 0x18000000 || lt == 28 || lt == 0x1c000000 ||
+                          lt == 30 || lt == 0x1e000000))
+                        break;
+                } else {
+                    break;
+                }
+            } else if ((cfg.select & SEL_GRE) && dport == 4754) {       // GRE over UDP
+                pkt = u;
+                if (!gre_next(pkt)) break;
+            } else {
+                break;
+            }
+        } else {
+            break;
+        }
         proto = ip_parse(pkt, iph, ipv);
         o.flags |= MFP_FLAG_ENCAP;
         if (ov == 6) enc |= 8u << n;
-        if (!oh || !iph || iph - oh != (ov == 6 ? 40 : 20)) enc |= 128u;
+        if (!ipip || !oh || !iph || iph - oh != (ov == 6 ? 40 : 20)) enc |= 128u;
         enc = (enc & ~7u) | (uint32_t)(n + 1);
     }
     if (iph) o.net = (uint32_t)(iph - base) | ((uint32_t)ipv << 16) | (enc << 20);
@@ -1790,22 +1893,6 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
     }
 }
 
-DEV bool ppp_is_ip(Cur &p) {                            // ppp::is_ip ppp.h:76
-    uint32_t b = look_u8(p);
-    if (b == 0x7e) {
-        rd_u8(p);
-        b = look_u8(p);
-        if (b == 0xff) { rd_u8(p); rd_u8(p); }
-    } else if (b == 0xff) {
-        rd_u8(p); rd_u8(p);
-    }
-    uint32_t proto;
-    b = look_u8(p);
-    if (b & 1) { uint32_t x; if (!(p.d && p.e > p.d)) { cset_null(p); proto = 0; } else { x = rd_u8(p); proto = x; } }
-    else { uint32_t v = 0; for (int i = 0; i < 2; i++) { v *= 256; v += rd_u8(p); } proto = v; }
-    return proto == 0x21 || proto == 0x57;
-}
-
 // link layer: stateful_pkt_proc::write_json(..., linktype) pkt_proc.cc:1328
 // and analyze_packet pkt_proc.cc:1814
 template <uint32_t FAM = FAM_ALL, class E>
@@ -1817,26 +1904,9 @@ DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t
     o.pay_off = o.pay_len = 0;
     Cur p = cmk(data, data + len);
     switch (linktype) {
-    case 1: {                                           // eth::eth eth.h:137
-        uint64_t et;
-        cskip(p, 12);
-        if (!rd_uint(p, 2, et)) return;
-        if (et == 0x88a8) { cskip(p, 2); if (!rd_uint(p, 2, et)) return; }
-        while (et == 0x8100) { cskip(p, 2); if (!rd_uint(p, 2, et)) return; }
-        if (et == 0x8847) {
-            uint64_t lbl = 0;
-            while (!(lbl & 0x100)) { if (!rd_uint(p, 4, lbl)) return; }
-            et = 0x0800;
-        }
-        if (et == 0x8909) { cskip(p, 6); if (!rd_uint(p, 2, et)) return; }
-        if (et == 0x0800 || et == 0x86dd) break;
-        if (et == 0x8864) {
-            Cur t; cparse(t, p, 1); cparse(t, p, 1); cparse(t, p, 2); cparse(t, p, 2);
-            if (!ppp_is_ip(p)) return;
-            break;
-        }
-        return;
-    }
+    case 1:                                             // eth::get_ip eth.h:114
+        if (!eth_get_ip(p)) return;
+        break;
     case 9:
         if (!ppp_is_ip(p)) return;
         break;

@@ -66,7 +66,8 @@ enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
     SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
     SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9, SEL_QUIC = 1u << 10,
-    SEL_ALL = (1u << 11) - 1,
+    SEL_GRE = 1u << 11, SEL_VXLAN = 1u << 12, SEL_GENEVE = 1u << 13,
+    SEL_ALL = (1u << 14) - 1,
 };
 
 static std::string strip(const std::string &s) {
@@ -87,13 +88,13 @@ static std::string trim(const std::string &s) {
 static bool parse_select(const std::string &list, uint32_t &sel) {
     // "all" (and the empty selection, which the reference reads as "all",
     // global_config.h:248) selects ~45 protocols this path does not parse
-    // (DNS, SMTP, ...) and the GRE/VXLAN/Geneve decapsulations: the
-    // reference would write records the device cannot, so it is refused
-    // rather than silently diverging
+    // (DNS, SMTP, ...): the reference would write records the device
+    // cannot, so it is refused rather than silently diverging
     if (strip(list).empty() || strip(list) == "all") {
         mfp_set_error("protocol selection \"%s\" includes protocols outside the device path; select from: tls, "
                       "tls.client_hello, tls.server_hello, tls.server_certificate, ssh, ssh.client, ssh.server, "
-                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, quic, none", list.empty() ? "" : list.c_str());
+                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, quic, gre, vxlan, geneve, none",
+                      list.empty() ? "" : list.c_str());
         return false;
     }
     const std::string &s = list;
@@ -104,6 +105,7 @@ static bool parse_select(const std::string &list, uint32_t &sel) {
         {"ssh", SEL_SSH_CLIENT | SEL_SSH_SERVER}, {"ssh.client", SEL_SSH_CLIENT}, {"ssh.server", SEL_SSH_SERVER},
         {"http", SEL_HTTP_REQ | SEL_HTTP_RESP}, {"http.request", SEL_HTTP_REQ}, {"http.response", SEL_HTTP_RESP},
         {"tcp", SEL_TCP_SYN}, {"tcp.syn_ack", SEL_TCP_SYNACK}, {"dtls", SEL_DTLS}, {"quic", SEL_QUIC},
+        {"gre", SEL_GRE}, {"vxlan", SEL_VXLAN}, {"geneve", SEL_GENEVE},
     };
     bool none = false;
     size_t pos = 0;
