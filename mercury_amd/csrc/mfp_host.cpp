@@ -361,11 +361,13 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
         // classifier is disabled
         mfp_classifier *clf = mfp_classifier_load(resources.c_str());
         if (!clf) { mfp_finalize(c); return nullptr; }
+        // the formats follow the archive even when its classifier is then
+        // disabled (missing members, VERSION qualifiers): pkt_proc.h:92-104
+        c->tls_format = (uint32_t)mfp_classifier_tls_format(clf);
+        c->quic_format = (uint32_t)mfp_classifier_quic_format(clf);
         if (mfp_classifier_disabled(clf)) {
             mfp_classifier_free(clf);
         } else {
-            c->tls_format = (uint32_t)mfp_classifier_tls_format(clf);
-            c->quic_format = (uint32_t)mfp_classifier_quic_format(clf);
             if (mfp_classifier_upload(clf, device) != 0) {
                 mfp_classifier_free(clf);
                 mfp_finalize(c);

@@ -137,3 +137,62 @@ def test_quic_replicated_batch():
         sl = slice(r * n, (r + 1) * n)
         assert not compare(rec[sl], fps[sl], ref, sources), f"replica {r}"
     assert int((rec["fp_type"] == 12).sum()) == reps * MANIFEST["counts"]["q0"]["quic_fp"]
+
+
+# ---------------------------------------------------------------------------
+# --analysis on QUIC Initials (quic_init::do_analysis quic.h:1722-1752): the
+# classifier reads the server name and the QUIC user agent from the sidecar
+# k_quic writes behind the fingerprint; the archive's quic/1 entries force the
+# QUIC format (pkt_proc.h:97-99)
+# ---------------------------------------------------------------------------
+def load_attr():
+    rows = []
+    with gzip.open(os.path.join(GOLD, "quic_attr.tsv.gz"), "rt", encoding="latin-1") as f:
+        for line in f:
+            p = line.rstrip("\n").split("\t")
+            attrs = {}
+            for kv in p[3].split(";"):
+                if kv:
+                    k, v = kv.split("=")
+                    attrs[k] = v
+            rows.append((int(p[1]), int(p[2]), attrs))
+    return rows
+
+
+@pytest.mark.gpu
+def test_quic_analysis_vs_reference():
+    from tests import test_analysis
+    arena, desc, sources = load()
+    cfg = f"select=quic;resources={os.path.join(GOLD, 'quic_resources.tgz')};analysis"
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        assert ctx.analysis_enabled
+        rec, fp, an, ap = ctx.process_host_analysis(arena, desc, attr_prob=True)
+        names = [ctx.process_name(int(p)) for p in an["process"]]
+        tag_names = {b: ctx.attribute_name(b) for b in range(16)}
+    finally:
+        ctx.close()
+    ref = test_analysis.load_ref_an("quic_an.tsv.gz")
+    bad = test_analysis.compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+    assert sum(r["valid"] for r in ref) > 700 and sum(r["status"] == 1 for r in ref) > 300
+    # attributes: names and probabilities (%.17g of the same doubles)
+    bad = []
+    for i, (valid, status, want) in enumerate(load_attr()):
+        got = {}
+        for b in range(16):
+            if not (int(an["attr"][i]) >> b) & 1:
+                continue
+            name = tag_names[b]
+            if b >= mercury_amd.api.ATTR_DB_FIRST:
+                p = float(ap[i][b - mercury_amd.api.ATTR_DB_FIRST])
+            elif name == "encrypted_channel":
+                p = float(an["malware_prob"][i])
+            else:
+                p = 1.0
+            if p != 0:
+                got[name] = "%.17g" % p
+        if got != want:
+            bad.append((i, got, want))
+    assert not bad, f"{len(bad)} attribute mismatches, first {bad[:3]}"
+    assert sum("encrypted_dns" in w for _, _, w in load_attr()) > 500
