@@ -585,11 +585,19 @@ def main():
                 cpu = cpu_baseline(workload, draw_seed, 200_000, cpu_threads(), args.cpu_seconds, analysis, resources)
             except Exception as e:   # baseline is reported, never the target
                 log(f"cpu baseline failed: {e}")
-        cfg_key = f"{workload}/{n}/{'analysis' if analysis else 'fp'}"
+        cfg_key = f"{workload}/{n}/" + (f"analysis/{args.resources}" if analysis else "fp")
         tr = find_traffic(cfg_key)
         traffic = None
         if tr:
-            traffic = tr[1]["hbm_bytes_per_step"]
+            # per-launch counter bytes (dispatch order == the order the step's
+            # kernels were first profiled in), and the step total
+            traffic = {"step": tr[1]["hbm_bytes_per_step"]}
+            names = [k for k in kern_ms]
+            fams = {k.split("/")[0] for k in names}
+            pl = [x for x in tr[1].get("per_launch") or [] if x["kernel"].split("<")[0] in fams]
+            if len(pl) == len(names) and all(abs(prof[k][0] / args.steps - 1.0) < 1e-9 for k in names):
+                for k, x in zip(names, pl):
+                    traffic[k] = x["hbm_bytes"]
         n_fp = int((rec["fp_type"] > 0).sum())
         if workload == "mixed":
             wl = ("config 4: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint + --analysis classifier "
@@ -648,6 +656,7 @@ def main():
             },
             "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4),
                             "algorithmic_bytes": kbytes.get(k),
+                            "hbm_bytes": traffic.get(k) if traffic else None,
                             "achieved_gb_s": round(kbytes[k] / (v * 1e-3) / 1e9, 2) if kbytes.get(k) and v else None}
                         for k, v in kern_ms.items()},
             "cpu_baseline": cpu,

@@ -76,6 +76,7 @@ struct mfp_classifier_dev {
     mfp_update *upd = nullptr;
     char *pool = nullptr;
     mfp_asn4 *asn4 = nullptr; uint32_t n_asn4 = 0;
+    uint32_t *asn4_bucket = nullptr;   // 65537 entries: first interval with hi >= b << 16 (narrows the search)
     mfp_asn6 *asn6 = nullptr; uint32_t n_asn6 = 0;
     uint32_t types_mask = 0;           // analyzable fingerprint types (fp_types)
     uint32_t enc_channel_idx = 7, faketls_idx = 9, doh_idx = 6, domain_faking_idx = 8;

@@ -329,7 +329,11 @@ ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_
 }
 
 ADEV uint32_t asn_v4_lane(const mfp_classifier_dev &D, uint32_t addr_host) {
-    int lo = 0, hi = (int)D.n_asn4 - 1;
+    // the bucket index narrows ~17 dependent probes of the whole table to the
+    // few intervals that can hold an address of this /16
+    const uint32_t b = addr_host >> 16;
+    int lo = (int)D.asn4_bucket[b], hi = (int)D.asn4_bucket[b + 1];
+    if (hi > (int)D.n_asn4 - 1) hi = (int)D.n_asn4 - 1;
     while (lo <= hi) {
         const int mid = (lo + hi) >> 1;
         const mfp_asn4 r = D.asn4[mid];

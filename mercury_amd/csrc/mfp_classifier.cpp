@@ -1023,6 +1023,16 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     if (t.dom_info.empty()) { t.dom_info.push_back(0); t.dom_info.push_back(0); }
     if (t.dom_bytes.empty()) t.dom_bytes.push_back(0);
 
+    // ASN bucket index: bucket[b] = first interval whose end reaches b << 16;
+    // the interval holding an address of bucket b lies in [bucket[b], bucket[b + 1]]
+    std::vector<uint32_t> asn4_bucket(65537);
+    {
+        size_t i = 0;
+        for (uint64_t b = 0; b <= 65536; b++) {
+            while (i < t.asn4.size() && (uint64_t)t.asn4[i].hi < (b << 16)) i++;
+            asn4_bucket[b] = (uint32_t)i;
+        }
+    }
     mfp_classifier_dev &d = c->dev;
     mfp_classifier_free_device(d);
     if (hipSetDevice(device) != hipSuccess) return -1;
@@ -1035,7 +1045,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     bool ok = up(d.fp_slots, t.fp_slots) && up(d.prev_slots, t.prev_slots) && up(d.entry, t.entry) &&
               up(d.prior, t.prior) && up(d.proc_id, t.proc_id) && up(d.proc_mal, t.proc_mal) &&
               up(d.proc_attr, t.proc_attr) && up(d.feat_slots, t.feat_slots) && up(d.upd, t.upd) && up(d.pool, t.pool) &&
-              up(d.asn4, t.asn4) && up(d.asn6, t.asn6) && up(d.doh_names, t.doh_names) &&
+              up(d.asn4, t.asn4) && up(d.asn4_bucket, asn4_bucket) && up(d.asn6, t.asn6) && up(d.doh_names, t.doh_names) &&
               up(d.doh_v4, t.doh_v4) && up(d.doh_v6, t.doh_v6) && up(d.dom_slots, t.dom_slots) &&
               up(d.dom4, t.dom4) && up(d.dom6, t.dom6) && up(d.dom_info, t.dom_info) && up(d.dom_bytes, t.dom_bytes);
     if (!ok) { mfp_set_error("classifier device upload failed"); return -2; }
@@ -1043,6 +1053,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
         auto nb = [](const auto &v) { return (uint64_t)(v.size() * sizeof(v[0])); };
         c->device_bytes = nb(t.fp_slots) + nb(t.prev_slots) + nb(t.entry) + nb(t.prior) + nb(t.proc_id) +
                           nb(t.proc_mal) + nb(t.proc_attr) + nb(t.feat_slots) + nb(t.upd) + nb(t.pool) + nb(t.asn4) +
+                          nb(asn4_bucket) +
                           nb(t.asn6) + nb(t.doh_names) + nb(t.doh_v4) + nb(t.doh_v6) + nb(t.dom_slots) + nb(t.dom4) +
                           nb(t.dom6) + nb(t.dom_info) + nb(t.dom_bytes);
     }
@@ -1077,7 +1088,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
 
 void mfp_classifier_free_device(mfp_classifier_dev &d) {
     void *ptrs[] = {d.fp_slots, d.prev_slots, d.entry, d.prior, d.proc_id, d.proc_mal, d.proc_attr,
-                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn6, d.doh_names, d.doh_v4, d.doh_v6,
+                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn4_bucket, d.asn6, d.doh_names, d.doh_v4, d.doh_v6,
                     d.dom_slots, d.dom4, d.dom6, d.dom_info, d.dom_bytes};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = mfp_classifier_dev{};
