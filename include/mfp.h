@@ -127,6 +127,8 @@ enum {
     MFP_MSG_SSH_INIT, MFP_MSG_SSH_KEX, MFP_MSG_HTTP_REQ, MFP_MSG_HTTP_RESP,
     MFP_MSG_TCP_SYN, MFP_MSG_TCP_SYNACK, MFP_MSG_DTLS_CH, MFP_MSG_DTLS_SH,
     MFP_MSG_DTLS_HVR, MFP_MSG_QUIC,
+    MFP_MSG_STUN,     /* stun::message (stun.h:783); sni_off/sni_len: the STUN message, ua: SOFTWARE */
+    MFP_MSG_OPENVPN,  /* openvpn_tcp (openvpn.h:353); sni_off/sni_len: the TCP payload         */
 };
 
 /* semantics of the reference entry point to follow */

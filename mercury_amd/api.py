@@ -31,7 +31,7 @@ FP_TYPE_NAMES = ["unknown", "tls", "tls_server", "http", "http_server", "ssh", "
                  "ssh_init", "ssh_server", "ssh_kex_server", "ssh_init_server"]
 MSG_NAMES = ["none", "tls.client_hello", "tls.server_hello", "tls.certificate", "ssh.init", "ssh.kex",
              "http.request", "http.response", "tcp.syn", "tcp.syn_ack", "dtls.client_hello",
-             "dtls.server_hello", "dtls.hello_verify_request", "quic.initial"]
+             "dtls.server_hello", "dtls.hello_verify_request", "quic.initial", "stun", "openvpn_tcp"]
 
 MODE_WRITE_JSON = 0
 MODE_ANALYSIS = 1

@@ -645,10 +645,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         a.proc_slot = MFP_NO_PROCESS; a.reserved = 0;
         // messages whose do_analysis calls the classifier: TLS ClientHello
         // (tls.h:1977), HTTP request (http.cc:571), SSH client KEXINIT
-        // (ssh.h:480), QUIC Initial (quic.h:1722); their type must also be in
-        // the archive (fp_types)
+        // (ssh.h:480), QUIC Initial (quic.h:1722), STUN request (stun.h:1021);
+        // their type must also be in the archive (fp_types)
         const bool typed = live && r.fp_len != 0 &&
-                           (r.fp_type == 1 || r.fp_type == 3 || r.fp_type == 5 || r.fp_type == 12);
+                           (r.fp_type == 1 || r.fp_type == 3 || r.fp_type == 5 || r.fp_type == 12 || r.fp_type == 16);
         const bool analyzable = typed && ((D.types_mask >> r.fp_type) & 1u);
         if (typed && !analyzable) { a.status = 4; a.flags = MFP_AN_VALID; }   // fingerprint_status_unanalyzed
         // the classifier-agnostic attributes of TLS and QUIC ClientHellos, analysed
@@ -810,8 +810,9 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 if (!(gu || mapped)) { v6w0 = 0xfd; v6w1 = 1ull << 56; }
                 ipkey = hash_final(word_term(v6w0, 0) ^ word_term(v6w1, 1), 16);
             }
-            // server name: TLS SNI / HTTP Host (strncpy 256, NUL stops)
-            const uint32_t sl = r.sni_len == 0xffff ? 0u : r.sni_len;
+            // server name: TLS SNI / HTTP Host (strncpy 256, NUL stops); STUN has
+            // none (its span holds the message, for the JSON writer)
+            const uint32_t sl = r.sni_len == 0xffff || r.msg == MFP_MSG_STUN ? 0u : r.sni_len;
             const uint8_t *sp = sbase + r.sni_off;
             uint32_t tld = 0;
             uint64_t nh = 0;

@@ -1309,14 +1309,15 @@ struct Cfg {
 // message needs a family that is compiled out is punted (Em::punt /
 // SegEm::ovf) to the fallback lane, which carries every family
 enum : uint32_t {
-    FAM_TLS = 1, FAM_SSH = 2, FAM_HTTP = 4, FAM_TCP = 8, FAM_DTLS = 16,
-    FAM_ALL = 31,
+    FAM_TLS = 1, FAM_SSH = 2, FAM_HTTP = 4, FAM_TCP = 8, FAM_DTLS = 16, FAM_STUN = 32,
+    FAM_ALL = 63,
 };
 enum : uint32_t {
     SEL_TLS_CH = 1u << 0, SEL_TLS_SH = 1u << 1, SEL_TLS_CERT = 1u << 2, SEL_SSH_CLIENT = 1u << 3,
     SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
     SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9, SEL_QUIC = 1u << 10,
     SEL_GRE = 1u << 11, SEL_VXLAN = 1u << 12, SEL_GENEVE = 1u << 13,   // decapsulations (proto_identify.h:812-886)
+    SEL_STUN = 1u << 14, SEL_OPENVPN = 1u << 15,                       // "stun", "openvpn_tcp" (proto_identify.h:834,868)
 };
 
 // masked 8/16-byte matchers (match.h:64-103)
@@ -1353,6 +1354,8 @@ DEV void fp_type_prefix(E &b, uint32_t t) {             // fingerprint::set_type
     case 11: b.lit("dtls_server/"); break;
     case 12: b.lit("quic/"); break;
     case 13: b.lit("tcp_server/"); break;
+    case 14: b.lit("openvpn/"); break;
+    case 16: b.lit("stun/"); break;
     case 17: b.lit("ssh_init/"); break;
     case 18: b.lit("ssh_server/"); break;
     case 19: b.lit("ssh_kex_server/"); break;
@@ -1423,6 +1426,16 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         else if ((sel & (SEL_SSH_CLIENT | SEL_SSH_SERVER)) &&
                  m8(pkt, LE8(0xff, 0xff, 0xf0, 0, 0, 0xff, 0, 0), LE8(0, 0, 0, 0, 0, 0x14, 0, 0)))
             msg = MFP_MSG_SSH_KEX;
+    }
+    // tcp_msg_type_from_ports (proto_identify.h:1028-1030): OpenVPN over TCP
+    // on port 1194, before the keyword matchers.  k_quic parses it (the
+    // ClientHello may span several control records, openvpn.h:388-403).
+    if (msg == 0 && (sel & SEL_OPENVPN) && (sport == 1194 || dport == 1194)) {
+        o.msg = MFP_MSG_OPENVPN;
+        o.pay_off = (uint32_t)(pkt.d - base);
+        o.pay_len = (uint32_t)clen(pkt);
+        if (!cfg.classify) b.punt_pkt();
+        return;
     }
     if (msg == 0) {
         if (clen(pkt) < 4) return;
@@ -1585,7 +1598,93 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
     }
 }
 
-// set_udp_protocol pkt_proc.cc:677 (selection subset: DTLS, dtls.h)
+// STUN attribute (stun::attribute stun.h:323-338): type, length, value and
+// padding to a 4-byte boundary; false (cursor null) when any part is missing
+DEV bool stun_attr(Cur &d, uint32_t &type, Cur &value) {
+    uint64_t t, l;
+    rd_uint(d, 2, t);
+    rd_uint(d, 2, l);
+    cparse(value, d, cnull(d) ? 0 : (long)l);
+    const long pad = (4 - (long)(l & 3)) & 3;             // pad_len datum.h:2344
+    if (!cnull(d)) { if (clen(d) < pad) cset_null(d); else d.d += pad; }
+    type = (uint32_t)t;
+    return !cnull(d);
+}
+
+// STUN message (stun::message stun.h:783-1013), reached through udp4's
+// length matcher: the header's length field + 20 equals the UDP payload
+// length (protocol_identifier<4>, proto_identify.h:387-390).  The record
+// exists when is_not_empty() holds (stun.h:902-916); responses set the
+// fingerprint buffer's truncated bit, so they carry no fingerprint
+// (stun.h:932-941).  The record's server-name span holds the message (for the
+// JSON writer's "stun" object), its user-agent span the last SOFTWARE value
+// (do_analysis stun.h:1021-1036).
+template <uint32_t FAM, class E>
+DEV void stun_msg(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
+    o.msg = MFP_MSG_STUN;
+    if (cfg.classify) return;
+    if constexpr (E::SEG || !(FAM & FAM_STUN)) {
+        b.punt_pkt();
+        return;
+    } else {
+    const uint8_t *h = pkt.d;
+    const uint32_t mtf = (ld(h) << 8) | ld(h + 1);
+    const bool cookie = ld(h + 4) == 0x21 && ld(h + 5) == 0x12 && ld(h + 6) == 0xa4 && ld(h + 7) == 0x42;
+    Cur body = cmk(h + 20, pkt.e);
+    bool present = cookie;
+    if (!present) {
+        const bool classic = mtf == 0x0001 || mtf == 0x0101 || mtf == 0x0111 || mtf == 0x0002 || mtf == 0x0102 ||
+                             mtf == 0x0112;                          // message_type_is_valid_for_classic_stun
+        if (classic) {
+            if (clen(body) == 0) {
+                uint32_t z = 0;
+                for (int k = 4; k < 20; k++) z += ld(h + k) == 0;     // tid_zero_count
+                present = z < 2;
+            } else {
+                Cur t = body, v; uint32_t ty;
+                present = stun_attr(t, ty, v);                    // lookahead<stun::attribute>
+            }
+        }
+    }
+    if (!present) return;
+    o.flags |= MFP_FLAG_EMIT;
+    o.sni_off = (uint32_t)(h - base); o.sni_len = (uint32_t)clen(pkt);
+    // SOFTWARE (the last one) for the classifier, recorded while fingerprinting
+    Cur sw; cset_null(sw);
+    if (mtf & 0x100) {                                          // is_response(): no fingerprint
+        Cur t = body, v; uint32_t ty;
+        while (clen(t) > 0 && stun_attr(t, ty, v)) if (ty == 0x8022) sw = v;
+    } else {
+        o.fp_type = 16;
+        fp_type_prefix(b, 16);
+        b.putc('1'); b.putc('/');                               // set_type(stun, 1) fingerprint.h:48-51
+        const uint32_t cls = ((mtf & 0x100) >> 7) | ((mtf & 0x10) >> 4);
+        const uint32_t method = (mtf & 0x0f) | ((mtf & 0xe0) >> 1) | ((mtf & 0x3e00) >> 2);
+        b.putc('('); b.hex8(cls); b.putc(')');
+        b.putc('('); b.hex16(method); b.putc(')');
+        b.putc('('); b.hex8(cookie ? 1u : 0u); b.putc(')');
+        b.putc('(');
+        Cur t = body, v; uint32_t ty;
+        while (clen(t) > 0 && stun_attr(t, ty, v)) {
+            // attr_fp_type (stun.h:957-970): type only, or type + length + value
+            const bool tlv = ty == 0x8037 || ty == 0x8070;
+            const bool only = ty == 0x0006 || ty == 0x0008 || ty == 0x0020 || ty == 0x8007 || ty == 0x8008 ||
+                              ty == 0x8022 || ty == 0x8028 || ty == 0xc003 || ty == 0xc057 || ty == 0xdaba;
+            if (tlv || only) {
+                b.putc('(');
+                b.hex16(ty);
+                if (tlv) { b.hex16((uint32_t)clen(v)); b.hex(v.d, clen(v)); }
+                b.putc(')');
+            }
+            if (ty == 0x8022) sw = v;
+        }
+        b.putc(')');
+    }
+    if (!cnull(sw)) { o.ua_off = (uint32_t)(sw.d - base); o.ua_len = (uint32_t)clen(sw); }
+    }
+}
+
+// set_udp_protocol pkt_proc.cc:677 (selection subset: QUIC, DTLS, STUN)
 template <uint32_t FAM, class E>
 DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
     // 8-byte matchers before 16-byte ones (get_udp_msg_type proto_identify.h:955-960):
@@ -1598,15 +1697,23 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         if (!cfg.classify) b.punt_pkt();
         return;
     }
-    if (!(cfg.select & SEL_DTLS) || clen(pkt) < 16) return;
-    uint64_t w0 = 0, w1 = 0;
-    for (int i = 0; i < 8; i++) { w0 |= (uint64_t)ld(pkt.d + i) << (8 * i); w1 |= (uint64_t)ld(pkt.d + 8 + i) << (8 * i); }
-    const uint64_t M0 = LE8(0xff, 0xff, 0xfd, 0, 0, 0, 0, 0), V0 = LE8(0x16, 0xfe, 0xfd, 0, 0, 0, 0, 0);
-    const uint64_t M1 = LE8(0, 0, 0, 0, 0, 0xff, 0, 0);
-    if ((w0 & M0) != V0) return;
-    uint32_t hb = (uint32_t)((w1 & M1) >> 40);
-    uint32_t msg = hb == 1 ? MFP_MSG_DTLS_CH : hb == 2 ? MFP_MSG_DTLS_SH : hb == 3 ? MFP_MSG_DTLS_HVR : 0;
-    if (!msg) return;
+    if (clen(pkt) < 16) return;
+    uint32_t msg = 0;
+    if (cfg.select & SEL_DTLS) {                       // udp16 matchers
+        uint64_t w0 = 0, w1 = 0;
+        for (int i = 0; i < 8; i++) { w0 |= (uint64_t)ld(pkt.d + i) << (8 * i); w1 |= (uint64_t)ld(pkt.d + 8 + i) << (8 * i); }
+        const uint64_t M0 = LE8(0xff, 0xff, 0xfd, 0, 0, 0, 0, 0), V0 = LE8(0x16, 0xfe, 0xfd, 0, 0, 0, 0, 0);
+        const uint64_t M1 = LE8(0, 0, 0, 0, 0, 0xff, 0, 0);
+        if ((w0 & M0) == V0) {
+            uint32_t hb = (uint32_t)((w1 & M1) >> 40);
+            msg = hb == 1 ? MFP_MSG_DTLS_CH : hb == 2 ? MFP_MSG_DTLS_SH : hb == 3 ? MFP_MSG_DTLS_HVR : 0;
+        }
+    }
+    if (!msg) {                                        // udp4: STUN's length matcher
+        if ((cfg.select & SEL_STUN) && 20 + ((ld(pkt.d + 2) << 8) | ld(pkt.d + 3)) == (uint32_t)clen(pkt))
+            stun_msg<FAM>(b, cfg, o, pkt, base);
+        return;
+    }
     o.msg = msg;
     if (cfg.classify) return;
     if constexpr (E::SEG || !(FAM & FAM_DTLS)) {

@@ -67,7 +67,8 @@ enum : uint32_t {
     SEL_SSH_SERVER = 1u << 4, SEL_HTTP_REQ = 1u << 5, SEL_HTTP_RESP = 1u << 6, SEL_TCP_SYN = 1u << 7,
     SEL_TCP_SYNACK = 1u << 8, SEL_DTLS = 1u << 9, SEL_QUIC = 1u << 10,
     SEL_GRE = 1u << 11, SEL_VXLAN = 1u << 12, SEL_GENEVE = 1u << 13,
-    SEL_ALL = (1u << 14) - 1,
+    SEL_STUN = 1u << 14, SEL_OPENVPN = 1u << 15,
+    SEL_ALL = (1u << 16) - 1,
 };
 
 static std::string strip(const std::string &s) {
@@ -93,7 +94,8 @@ static bool parse_select(const std::string &list, uint32_t &sel) {
     if (strip(list).empty() || strip(list) == "all") {
         mfp_set_error("protocol selection \"%s\" includes protocols outside the device path; select from: tls, "
                       "tls.client_hello, tls.server_hello, tls.server_certificate, ssh, ssh.client, ssh.server, "
-                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, quic, gre, vxlan, geneve, none",
+                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, quic, stun, openvpn_tcp, gre, vxlan, "
+                      "geneve, none",
                       list.empty() ? "" : list.c_str());
         return false;
     }
@@ -106,6 +108,7 @@ static bool parse_select(const std::string &list, uint32_t &sel) {
         {"http", SEL_HTTP_REQ | SEL_HTTP_RESP}, {"http.request", SEL_HTTP_REQ}, {"http.response", SEL_HTTP_RESP},
         {"tcp", SEL_TCP_SYN}, {"tcp.syn_ack", SEL_TCP_SYNACK}, {"dtls", SEL_DTLS}, {"quic", SEL_QUIC},
         {"gre", SEL_GRE}, {"vxlan", SEL_VXLAN}, {"geneve", SEL_GENEVE},
+        {"stun", SEL_STUN}, {"openvpn_tcp", SEL_OPENVPN},
     };
     bool none = false;
     size_t pos = 0;
@@ -426,7 +429,7 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
                                  hipStream_t s) {
     HIPCHK(hipSetDevice(c->device));
     if (grow(S.d_work, S.cap_work, 11 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
-    if ((c->select & SEL_QUIC) && !S.d_quic &&
+    if ((c->select & (SEL_QUIC | SEL_OPENVPN)) && !S.d_quic &&
         hipMalloc(&S.d_quic, mfp_quic_scratch_bytes(c->quic_grid)) != hipSuccess) {
         S.d_quic = nullptr;
         mfp_set_error("device allocation failed (QUIC scratch)");

@@ -343,6 +343,9 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     // QUIC records carry a "quic" object with the decrypted payload
     // (quic_init::write_json quic.h:1662-1690), which the device does not return
     if (r.msg == MFP_MSG_QUIC) return false;
+    // STUN and OpenVPN records carry "stun" / "openvpn" objects (stun.h:795-826,
+    // openvpn.h:411-442) that are not rebuilt here yet
+    if (r.msg == MFP_MSG_STUN || r.msg == MFP_MSG_OPENVPN) return false;
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
     // IP-in-IP: outer headers sit back to back before the inner one (IPv4
     // fixed 20 B, ip.h:124-137; IPv6 40 B when it has no extension headers)

@@ -65,9 +65,9 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
         }
     }
     {
-        // a parser this instance lacks: the fallback lane; QUIC (which only
-        // k_quic parses): the QUIC list
-        const bool to_quic = punt && o.msg == MFP_MSG_QUIC;
+        // a parser this instance lacks: the fallback lane; QUIC and OpenVPN
+        // (which only k_quic parses): the k_quic list
+        const bool to_quic = punt && (o.msg == MFP_MSG_QUIC || o.msg == MFP_MSG_OPENVPN);
         const bool to_fb = punt && !to_quic && FAM != FAM_ALL;
         const uint64_t pm = __ballot(to_fb);
         if (pm) {
@@ -516,7 +516,7 @@ DEV int msg_bin(uint32_t msg) {
     case MFP_MSG_TLS_SH: case MFP_MSG_TLS_CERT: return 5;
     case MFP_MSG_SSH_INIT: case MFP_MSG_SSH_KEX: return 6;
     case MFP_MSG_DTLS_CH: case MFP_MSG_DTLS_SH: case MFP_MSG_DTLS_HVR: return 7;
-    case MFP_MSG_QUIC: return QUIC_BIN;
+    case MFP_MSG_QUIC: case MFP_MSG_OPENVPN: return QUIC_BIN;
     default: return 4;   // no message of a selected protocol
     }
 }
@@ -640,10 +640,10 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
     P.idx = nullptr; P.count = nullptr;
-    // QUIC packets (bin 8 of the classify pass, plus any a walker hands over)
+    // QUIC and OpenVPN packets (bin 8 of the classify pass, plus any a walker hands over)
     P.quic_idx = work + (uint64_t)mfp::QUIC_BIN * n;
     P.quic_count = bin_count + mfp::QUIC_BIN;
-    const bool quic = (select & mfp::SEL_QUIC) != 0;
+    const bool quic = (select & (mfp::SEL_QUIC | mfp::SEL_OPENVPN)) != 0;
     if (quic && !quic_scratch) return -1;
     auto launch_quic = [&]() -> int {
         if (!quic) return 0;

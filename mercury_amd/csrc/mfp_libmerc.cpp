@@ -219,7 +219,8 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
         // (QUIC, GRE/VXLAN/Geneve encapsulations, IP-in-IP with an outer IPv6
         // extension header): say so instead of returning a silent 0
         log_error("write_json: record not rebuilt by the MI355X JSON writer (%s)\n",
-                  rec.msg == MFP_MSG_QUIC ? "QUIC Initial" : "encapsulation chain");
+                  rec.msg == MFP_MSG_QUIC ? "QUIC Initial" : rec.msg == MFP_MSG_STUN ? "STUN message"
+                  : rec.msg == MFP_MSG_OPENVPN ? "OpenVPN record" : "encapsulation chain");
         return 0;
     }
     if (n <= 0 || (size_t)n >= buffer_size) return 0;    // buffer_stream keeps one byte for its NUL

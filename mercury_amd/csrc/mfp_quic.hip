@@ -449,6 +449,113 @@ DEV QMeta quic_meta(Cur exts) {
 }
 DEV uint32_t span_len(Cur c) { return cnull(c) ? 0u : (uint32_t)clen(c); }
 
+// ---- OpenVPN over TCP (openvpn_tcp openvpn.h:353-500)
+// One record (openvpn_tcp_record openvpn.h:272-290 over openvpn_payload
+// openvpn.h:116-246).  Only the fields the fingerprint needs are kept; the
+// cursor advances over exactly what the reference reads (a record that is
+// not P_CONTROL_V1 consumes its header only, not its length field's span).
+struct OvRec { uint32_t opcode, key, hmac_len; Cur data; bool ctrl, valid; };
+DEV OvRec ovpn_record(Cur &d) {
+    OvRec r; r.hmac_len = 0; r.valid = false; cset_null(r.data);
+    uint64_t len, code, t;
+    rd_uint(d, 2, len);
+    rd_uint(d, 1, code);
+    r.opcode = (uint32_t)code >> 3;                      // code.slice<0,5>
+    r.key = (uint32_t)code & 7;                          // code.slice<5,8>
+    const uint32_t op = r.opcode;
+    const int type = (op >= 1 && op <= 4) || op == 7 || op == 8 || op == 10 || op == 11 ? 1   // ctrl
+                   : op == 5 ? 0 : (op == 6 || op == 9) ? 2 : 3;                            // ack, data, unknown
+    r.ctrl = type == 1;
+    const bool have_data = op == 4;
+    // openvpn_payload::parse
+    rd_uint(d, 8, t);                                    // session_id
+    uint64_t hm = 0;
+    { Cur la = d; rd_uint(la, 4, hm); }                  // lookahead: 0 when short
+    uint32_t zeros = 0;
+    for (int k = 0; k < 4; k++) zeros += ((hm >> (8 * k)) & 0xff) == 0;
+    bool tls_auth = false;
+    if (zeros <= 1) {                                    // valid_HMAC: entropy check
+        if (clen(d) < 16) return r;
+        // datum::find_delim(0x00 0x00) (datum.h:546-567): index just past the
+        // first two zero bytes, or minus the bytes scanned; then - 2 as uint8_t
+        long at = 0, m = 0;
+        const long dl = clen(d);
+        while (m < 2 && at < dl) { m = ld(d.d + at) == 0 ? m + 1 : 0; at++; }
+        const long fd = m == 2 ? at : -at;
+        const uint32_t hl = (uint32_t)(uint8_t)(fd - 2);
+        if (hl < 16 || (long)hl >= clen(d)) return r;
+        r.hmac_len = hl;
+        cskip(d, (long)hl);
+        tls_auth = true;
+    }
+    (void)tls_auth;
+    rd_uint(d, 4, t);                                    // replay_pkt_id
+    bool net_time = false;
+    {
+        Cur dc = d;
+        const uint32_t b1 = rd_u8(dc), b2 = rd_u8(dc);
+        if ((long)b1 * 4 > clen(dc) || b2) net_time = true;
+    }
+    if (net_time) rd_uint(d, 4, t);
+    const uint32_t nid = rd_u8(d);                       // pkt_id_array_len
+    if (clen(d) < 4 * (long)nid) return r;
+    if (nid) { cskip(d, 4 * (long)nid); rd_uint(d, 8, t); }   // the array, remote_session_id
+    if (r.ctrl) rd_uint(d, 4, t);                        // msg_pkt_id
+    const uint32_t hdr = 1 + 8 + r.hmac_len + 4 + (net_time ? 4 : 0) + 1 + 4 * nid + (nid ? 8 : 0) + (r.ctrl ? 4 : 0);
+    if (have_data) {
+        if (hdr >= (uint32_t)len) return r;
+        const long dl = (long)((uint32_t)len - hdr) & 0xffff;   // data_len is a uint16_t
+        if (clen(d) < dl) return r;
+        r.data = cmk(d.d, d.d + dl);
+        cskip(d, dl);
+    }
+    r.valid = type != 3;
+    return r;
+}
+
+struct OvRes { bool present, hello; uint32_t nctrl, opcode, key, hmac_len; Ch ch; };
+// openvpn_tcp::openvpn_tcp: the records, then the control records' data
+// gathered into an 800-byte buffer (data_buffer<800>, a copy that does not
+// fit nulls it) and parsed as a TLS record + handshake + ClientHello
+DEV OvRes ovpn_process(Cur d, uint8_t *buf) {
+    OvRes v; v.present = false; v.hello = false; v.nctrl = 0; v.opcode = 0; v.key = 0; v.hmac_len = 0;
+    uint32_t nrec = 0, used = 0;
+    bool buf_null = false;
+    while (clen(d) > 0) {
+        const OvRec r = ovpn_record(d);
+        if (cnull(d) || !r.valid) return v;
+        if (r.ctrl) {
+            if (v.nctrl == 0) { v.opcode = r.opcode; v.key = r.key; v.hmac_len = r.hmac_len; }
+            v.nctrl++;
+            if (!cnull(r.data) && !buf_null) {
+                const long dl = clen(r.data);
+                if (used + (uint32_t)dl > 800) buf_null = true;
+                else { for (long j = 0; j < dl; j++) buf[used + j] = (uint8_t)ld(r.data.d + j); used += (uint32_t)dl; }
+            }
+        }
+        nrec++;
+    }
+    v.present = (uint8_t)nrec != 0;                      // is_not_empty: valid && num_records (uint8_t)
+    if (!v.present || v.nctrl == 0 || buf_null || used == 0) return v;
+    Cur p = cmk(buf, buf + used);
+    Cur frag = tls_record_fragment(p);
+    Hs hs = tls_hs_parse(frag);
+    v.ch = tls_ch_parse(hs.body);
+    v.hello = cnotempty(v.ch.compression);
+    return v;
+}
+
+// openvpn_tcp::fingerprint + tls_client_hello::fingerprint (format 0)
+template <class E>
+DEV void ovpn_fp(E &b, const OvRes &v) {
+    fp_type_prefix(b, 14);
+    b.lit("(06)");
+    b.putc('('); b.hex8(v.nctrl & 0xff); b.putc(')');
+    b.putc('('); b.hex8(v.opcode); b.hex8(v.key ? 1u : 0u); b.putc(')');
+    b.putc('('); b.hex8(v.hmac_len); b.putc(')');
+    tls_ch_fp(b, v.ch, 0);
+}
+
 __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32_t quic_format) {
     __shared__ uint32_t s_te[256];
     __shared__ uint64_t s_gh[32 * QT];
@@ -482,8 +589,14 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         }
         QRes q;
         q.flags = 0; q.hello = false; q.pre = false; q.ver = nullptr;
+        const bool ovpn = live && o.msg == MFP_MSG_OPENVPN;
+        OvRes v; v.present = false; v.hello = false;
         if (live && o.msg == MFP_MSG_QUIC)
             q = quic_process(cmk(data + o.pay_off, data + o.pay_off + o.pay_len), pt, cb, s_te, s_gh, (uint32_t)tid);
+        if (ovpn) {
+            v = ovpn_process(cmk(data + o.pay_off, data + o.pay_off + o.pay_len), pt);
+            q.flags = v.present ? MFP_FLAG_EMIT : 0;
+        }
         const uint32_t fmt = q.pre ? 0u : quic_format;
         uint32_t len = 0, fp_type = 0;
         QMeta m; cset_null(m.sni); cset_null(m.ua); cset_null(m.alpn);
@@ -492,8 +605,14 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             quic_fp(e, q, fmt);
             if (e.valid()) { len = e.n; fp_type = 12; }       // fingerprint::final drops truncated strings
             m = quic_meta(q.ch.extensions);
+        } else if (v.hello) {
+            Em<false> e;
+            TlsPlan plan;
+            e.plan = &plan;
+            ovpn_fp(e, v);
+            if (e.valid()) { len = e.n; fp_type = 14; }
         }
-        const uint32_t side = len ? 4 + span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
+        const uint32_t side = len && !ovpn ? 4 + span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
 
         // tile reservation of 64-byte slots: string, hash, sidecar
         const int lane = tid & 63, wid = tid >> 6;
@@ -537,11 +656,12 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             uint8_t *out = P.fp_arena + base + excl;
             Em<true> e;
             e.begin(out, out_line[tid]);
-            quic_fp(e, q, fmt);
+            if (ovpn) ovpn_fp(e, v); else quic_fp(e, q, fmt);
             e.finish();
             uint8_t *sc = out + ((len + 7) & ~7u);
             *(uint64_t *)sc = e.hash();
             sc += 8;
+            if (!ovpn) {
             // sidecar: {u16 alpn_off, u16 alpn_len}, server name, user agent, ALPN
             uint32_t at = 4;
             const Cur parts[3] = {m.sni, m.ua, m.alpn};
@@ -555,7 +675,10 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             sc[0] = (uint8_t)offs[2]; sc[1] = (uint8_t)(offs[2] >> 8);
             sc[2] = (uint8_t)lens[2]; sc[3] = (uint8_t)(lens[2] >> 8);
             sni_off = offs[0]; sni_len = lens[0]; ua_off = offs[1]; ua_len = lens[1];
+            }
         }
+        // OpenVPN: the TCP payload, which the JSON writer re-reads for the "openvpn" object
+        if (ovpn) { sni_off = o.pay_off; sni_len = o.pay_len; }
         if (live) {
             mfp_record r;
             r.fp_offset = fits ? base + excl : 0;
@@ -563,7 +686,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             r.fp_type = (uint8_t)(fits ? fp_type : 0);
             r.msg = (uint8_t)o.msg;
             r.flags = (uint8_t)(q.flags | (o.flags & MFP_FLAG_ENCAP) |
-                                (fits && len ? (MFP_FLAG_HASHED | MFP_FLAG_SIDECAR) : 0));
+                                (fits && len ? (ovpn ? MFP_FLAG_HASHED : (MFP_FLAG_HASHED | MFP_FLAG_SIDECAR)) : 0));
             r.status = 0;
             r.sni_off = (uint16_t)(sni_len == 0xffff ? 0 : sni_off);
             r.sni_len = (uint16_t)sni_len;

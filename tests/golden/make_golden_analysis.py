@@ -83,7 +83,7 @@ def main():
         "ref": {"packets": "ref_packets.npz", "resources": "resources-test.tgz (test/data of the reference)"},
         "survey": {"archive": "tests/golden/_gen/survey_resources.tgz (tests/synth_db.py build_survey)",
                    "params": {k: v for k, v in synth_db.SURVEY.items()},
-                   "sha256": hashlib.sha256(open(survey, "rb").read()).hexdigest()},
+                   "tar_sha256": hashlib.sha256(gzip.decompress(open(survey, "rb").read())).hexdigest()},
         "columns": ["idx", "valid", "fp_type", "status", "process", "score", "malware", "p_malware"],
     }
     with open(os.path.join(HERE, "an_manifest.json"), "w") as f:

@@ -249,6 +249,9 @@ def build_survey(path=None):
     path = path or survey_path()
     if not os.path.exists(path):
         data, _ = build(**SURVEY)
+        # gzip header without a timestamp: the same bytes wherever it is built
+        import gzip
+        data = gzip.compress(gzip.decompress(data), compresslevel=9, mtime=0)
         os.makedirs(os.path.dirname(path), exist_ok=True)
         with open(path + ".tmp", "wb") as f:
             f.write(data)

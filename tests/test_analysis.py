@@ -176,8 +176,9 @@ def survey_archive():
     when absent and checked against the golden's sha256."""
     from tests import synth_db
     path = synth_db.build_survey()
-    want = json.load(open(os.path.join(GOLD, "an_manifest.json")))["survey"]["sha256"]
-    assert hashlib.sha256(open(path, "rb").read()).hexdigest() == want, "survey archive differs from the golden's"
+    want = json.load(open(os.path.join(GOLD, "an_manifest.json")))["survey"]["tar_sha256"]
+    got = hashlib.sha256(gzip.decompress(open(path, "rb").read())).hexdigest()
+    assert got == want, "survey archive differs from the golden's"
     return path
 
 

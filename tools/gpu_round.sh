@@ -1,13 +1,12 @@
 #!/bin/bash
-# GPU box: full -m gpu suite, then smoke(); results under gpurun_out/$TAG
-set -o pipefail
-cd /tmp && export TMPDIR=/tmp
-cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/${TAG:-round}
-mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
-grep -E "FAIL|ERROR|passed|failed" $O/pytest.log | tail -30
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u __graft_entry__.py smoke > $O/smoke.log 2>&1; rc=$?
-tail -3 $O/smoke.log
+# GPU check: new-feature tests first (their failures do not stop the run),
+# then the whole -m gpu suite; stops on a fault, abort or timeout.
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest ${FIRST:-tests/test_stun_ovpn.py} -v --timeout 200 --timeout-method thread > gpurun_out/first.log 2>&1
+rc=$?
+echo "first exit $rc" >> gpurun_out/first.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/gpu.log 2>&1
+rc=$?
+echo "gpu exit $rc" >> gpurun_out/gpu.log
 exit $rc
