@@ -131,6 +131,22 @@ enum {
     MFP_MSG_OPENVPN,  /* openvpn_tcp (openvpn.h:353); sni_off/sni_len: the TCP payload         */
 };
 
+/* TCP reassembly inputs, one per packet (the device walk's view of
+ * tcp_packet, tcpip.h:137-173, after set_tcp_protocol pkt_proc.cc:488-572) */
+typedef struct {
+    uint32_t seq;        /* TCP sequence number (host order)                          */
+    uint32_t more;       /* additional_bytes_needed of the message parsed here        */
+    uint32_t pay_off;    /* TCP data: offset in the packet                            */
+    uint16_t pay_len;    /* TCP data length (tcp_packet::data_length)                 */
+    uint8_t  kind;       /* MFP_SEG_* bits; 0 = not a data segment                    */
+    uint8_t  reserved;
+} mfp_tcp_seg;
+enum {
+    MFP_SEG_DATA = 1,           /* a TCP data segment process_tcp_data sees (pkt_proc.cc:773) */
+    MFP_SEG_SUPPLEMENTARY = 2,  /* tcp_packet::supplementary_reassembly (SSH KEXINIT)          */
+    MFP_SEG_SSH = 4,            /* reassembly_type::ssh (indefinite, pkt_proc.cc:552)          */
+};
+
 /* semantics of the reference entry point to follow */
 enum {
     MFP_MODE_WRITE_JSON = 0,  /* stateful_pkt_proc::write_json (pkt_proc.cc:1063)      */
@@ -240,6 +256,40 @@ MFP_EXPORT long long mfp_process_pipelined(mfp_context ctx, const uint8_t *arena
  * every analysis call decides its own batch (the call waits for its kernels);
  * shards of one stream (several contexts) defer the decision and resolve their
  * batches in shard order against one shared object. */
+/* ---- TCP reassembly ("reassembly" in the config) ----
+ * The reference's write_json path with reassembly (process_tcp_data
+ * pkt_proc.cc:773-893, tcp_reassembler reassembly.hpp:140-900): a message
+ * whose first segment needs more bytes is buffered per flow; the flow's later
+ * segments are added by sequence number; the completing (or truncating)
+ * segment's record carries the fingerprint of the reassembled message, and
+ * the segments before it write no record. */
+typedef struct mfp_reassembler_s *mfp_reassembler;   /* the processor's tcp_reassembler */
+MFP_EXPORT mfp_reassembler mfp_reassembler_create(void);
+MFP_EXPORT void mfp_reassembler_destroy(mfp_reassembler r);
+MFP_EXPORT uint64_t mfp_reassembler_flows(mfp_reassembler r);   /* flows in reassembly */
+MFP_EXPORT int mfp_reassembly_enabled(mfp_context ctx);
+/* The device walk plus, per packet, the reassembly inputs (mfp_tcp_seg). */
+MFP_EXPORT long long mfp_process_batch_host_seg(mfp_context ctx, const uint8_t *arena, size_t arena_len,
+                                                const mfp_pkt_desc *desc, size_t n, mfp_record *rec, char *fp_arena,
+                                                size_t fp_cap, mfp_tcp_seg *seg);
+/* One host batch in stream order through the reassembler (state persists in
+ * r across calls).  ts_ns: per-packet capture times (the 15 s flow timeout;
+ * NULL = all 0).  props[i]: bit 0 = the record is a reassembled message
+ * ("reassembled":true), bits 1-7 = reassembly_flag_val (missing_segment,
+ * timeout, out_of_order, out_of_buffer, max_segments_exceed,
+ * segment_overlaps, truncated), bits 8-11 = reassembly_overlap_flags.
+ * Reassembled messages are rebuilt as frames (IP + TCP headers of the
+ * completing packet, then the buffer; LINKTYPE_RAW), kept in r until its
+ * next call (mfp_reassembler_frames); out_desc (optional) = desc with those
+ * packets' entries pointing at their frames at offset arena_len + offset, so
+ * arena ++ frames with out_desc is the input the records index (the JSON
+ * writer's input).  Returns the fingerprint bytes used, or < 0. */
+MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mfp_reassembler r, const uint8_t *arena,
+                                                  size_t arena_len, const mfp_pkt_desc *desc, size_t n,
+                                                  const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
+                                                  size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc);
+MFP_EXPORT const uint8_t *mfp_reassembler_frames(mfp_reassembler r, size_t *len);
+
 typedef struct mfp_prevalence_s *mfp_prevalence;
 
 /* one distinct fingerprint of a batch's sightings */

@@ -33,6 +33,16 @@ MSG_NAMES = ["none", "tls.client_hello", "tls.server_hello", "tls.certificate", 
              "http.request", "http.response", "tcp.syn", "tcp.syn_ack", "dtls.client_hello",
              "dtls.server_hello", "dtls.hello_verify_request", "quic.initial", "stun", "openvpn_tcp"]
 
+# mfp_tcp_seg (include/mfp.h): reassembly inputs per packet
+SEG_DTYPE = np.dtype([("seq", "<u4"), ("more", "<u4"), ("pay_off", "<u4"), ("pay_len", "<u2"), ("kind", "u1"),
+                      ("reserved", "u1")])
+SEG_DATA, SEG_SUPPLEMENTARY, SEG_SSH = 1, 2, 4
+# mfp_process_batch_reassembly props bits: reassembled, then reassembly_flag_val
+# (reassembly.hpp:73-91) and reassembly_overlap_flags (reassembly.hpp:93-105)
+REASM_FLAGS = ["missing_segment", "timeout", "out_of_order", "out_of_buffer", "max_segments_exceed",
+               "segment_overlaps", "truncated"]
+REASM_OVERLAPS = ["back_partial_overlap", "back_subset_overlap", "front_partial_overlap", "front_superset_overlap"]
+
 MODE_WRITE_JSON = 0
 MODE_ANALYSIS = 1
 
@@ -74,6 +84,18 @@ def load_library():
     lib.mfp_analysis_enabled.argtypes = [vp]
     lib.mfp_analyze_batch_device.restype = ctypes.c_int
     lib.mfp_analyze_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.mfp_process_batch_host_seg.restype = ctypes.c_longlong
+    lib.mfp_process_batch_host_seg.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp]
+    lib.mfp_reassembler_create.restype = vp
+    lib.mfp_reassembler_destroy.argtypes = [vp]
+    lib.mfp_reassembler_flows.restype = ctypes.c_uint64
+    lib.mfp_reassembler_flows.argtypes = [vp]
+    lib.mfp_reassembler_frames.restype = vp
+    lib.mfp_reassembler_frames.argtypes = [vp, ctypes.POINTER(sz)]
+    lib.mfp_reassembly_enabled.restype = ctypes.c_int
+    lib.mfp_reassembly_enabled.argtypes = [vp]
+    lib.mfp_process_batch_reassembly.restype = ctypes.c_longlong
+    lib.mfp_process_batch_reassembly.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp, sz, vp, vp]
     lib.mfp_process_batch_host_ex.restype = ctypes.c_longlong
     lib.mfp_process_batch_host_ex.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, vp]
     lib.mfp_analysis_device_bytes.restype = ctypes.c_uint64
@@ -172,6 +194,9 @@ class Context:
             raise MercuryAmdError("mfp_init failed: " + _err(self.lib))
 
     def close(self):
+        if getattr(self, "reasm", None):
+            self.lib.mfp_reassembler_destroy(self.reasm)
+            self.reasm = None
         if self.h:
             self.lib.mfp_finalize(self.h)
             self.h = None
@@ -198,6 +223,52 @@ class Context:
         if used < 0:
             raise MercuryAmdError("mfp_process_batch_host failed: " + _err(self.lib))
         return rec, fp[:used].tobytes()
+
+    def process_host_segments(self, arena, desc):
+        """The device walk with the per-packet reassembly inputs -> (records,
+        fp arena bytes, SEG_DTYPE array)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        n = len(desc)
+        rec = np.zeros(n, dtype=RECORD_DTYPE)
+        seg = np.zeros(max(n, 1), dtype=SEG_DTYPE)
+        cap = self.fp_arena_bound(desc)
+        fp = np.zeros(cap, dtype=np.uint8)
+        used = self.lib.mfp_process_batch_host_seg(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
+                                                   rec.ctypes.data, fp.ctypes.data, cap, seg.ctypes.data)
+        if used < 0:
+            raise MercuryAmdError("mfp_process_batch_host_seg failed: " + _err(self.lib))
+        return rec, fp[:used].tobytes(), seg[:n]
+
+    def process_host_reassembly(self, arena, desc, ts_ns=None):
+        """A host batch in stream order through the context's TCP reassembler
+        (config with "reassembly"; state persists across calls) -> (records,
+        fp arena bytes, props (uint16, REASM_* bits), arena ++ rebuilt frames,
+        desc indexing it)."""
+        if not self.lib.mfp_reassembly_enabled(self.h):
+            raise MercuryAmdError("the configuration has no \"reassembly\"")
+        if not getattr(self, "reasm", None):
+            self.reasm = self.lib.mfp_reassembler_create()
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        n = len(desc)
+        rec = np.zeros(n, dtype=RECORD_DTYPE)
+        props = np.zeros(max(n, 1), dtype=np.uint16)
+        out_desc = np.zeros(max(n, 1), dtype=DESC_DTYPE)
+        ts = None if ts_ns is None else np.ascontiguousarray(ts_ns, dtype=np.uint64)
+        cap = self.fp_arena_bound(desc) + int(self.lib.mfp_fp_arena_bound(n, n * 8400))
+        fp = np.zeros(cap, dtype=np.uint8)
+        used = self.lib.mfp_process_batch_reassembly(self.h, self.reasm, arena.ctypes.data, arena.nbytes,
+                                                     desc.ctypes.data, n, None if ts is None else ts.ctypes.data,
+                                                     rec.ctypes.data, fp.ctypes.data, cap, props.ctypes.data,
+                                                     out_desc.ctypes.data)
+        if used < 0:
+            raise MercuryAmdError("mfp_process_batch_reassembly failed: " + _err(self.lib))
+        flen = ctypes.c_size_t(0)
+        ptr = self.lib.mfp_reassembler_frames(self.reasm, ctypes.byref(flen))
+        frames = np.ctypeslib.as_array((ctypes.c_uint8 * flen.value).from_address(ptr)).copy() if flen.value else \
+            np.zeros(0, np.uint8)
+        return rec, fp[:used].tobytes(), props[:n], np.concatenate([arena, frames]), out_desc[:n]
 
     @property
     def analysis_enabled(self):

@@ -620,7 +620,7 @@ constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.
 #define MFP_AN_PL 16
 #endif
 #ifndef MFP_AN_MINW
-#define MFP_AN_MINW 4
+#define MFP_AN_MINW 3
 #endif
 constexpr uint32_t PL = MFP_AN_PL;   // phase L: fingerprints with at most PL processes, scored lane per packet
 constexpr int AW = 2;                // waves per k_analyze block (LDS: PL * 512 bytes of score rows per wave)

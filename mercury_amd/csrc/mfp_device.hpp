@@ -1292,7 +1292,11 @@ struct Out {
     uint32_t sni_off, sni_len, ua_off, ua_len;
     uint32_t src_port, dst_port;
     uint32_t net;        // innermost IP header offset | version << 16 (flow key, flow_key.h:71)
-    uint32_t pay_off, pay_len;   // QUIC: the UDP payload (k_quic takes it from here)
+    uint32_t pay_off, pay_len;   // QUIC: the UDP payload (k_quic takes it from here); TCP: the data
+    // TCP reassembly inputs (tcp_packet tcpip.h:137-173): sequence number,
+    // additional_bytes_needed of the message parsed from this segment, and
+    // MFP_SEG_* kind bits (a data segment, supplementary, SSH-type reassembly)
+    uint32_t seq, more, seg_kind;
 };
 // the certificate_list datum in the record's server-name slot (TLS server
 // messages have no server name): the JSON writer's certs array (tls.h:2183)
@@ -1480,6 +1484,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         Cur frag = tls_record_fragment(p);
         Hs hs = tls_hs_parse(frag);
         if (hs.more) o.flags |= MFP_FLAG_TRUNCATED;
+        o.more = (uint32_t)hs.more;                    // pkt_proc.cc:527-531
         Ch ch = tls_ch_parse(hs.body);
         if (!cnotempty(ch.compression)) return;
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 1;
@@ -1512,6 +1517,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         if (hs2.msg_type == 11) tls_cert_parse(cert, hs2.body);
         cert_record(o, cert.list, base);            // tls.h:605-627 (the JSON writer's certs)
         if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
+        o.more = (uint32_t)cert.more;                  // tls.h:596-598
         bool hello = tls_sh_not_empty(sh);
         if (hello || cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
         if (hello) { o.fp_type = 2; fp_type_prefix(b, 2); tls_sh_fp(b, sh); }
@@ -1533,6 +1539,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         }
         cert_record(o, cert.list, base);
         if (cert.more) o.flags |= MFP_FLAG_TRUNCATED;
+        o.more = (uint32_t)cert.more;                  // tls.h:735-737
         if (cnotempty(cert.list)) o.flags |= MFP_FLAG_EMIT;
         return;
         }
@@ -1553,6 +1560,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         }
         uint64_t more = kex ? bin.more : 8192;
         if (more) o.flags |= MFP_FLAG_TRUNCATED;
+        if (more) { o.more = (uint32_t)more; o.seg_kind |= MFP_SEG_SSH; }   // pkt_proc.cc:550-553
         if (!cnotempty(proto)) return;
         o.flags |= MFP_FLAG_EMIT;
         if (kex) {
@@ -1586,6 +1594,8 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         Cur p = pkt;
         SshBin bin = ssh_bin_parse(p);
         if (bin.more) o.flags |= MFP_FLAG_TRUNCATED;
+        if (bin.more) o.more = (uint32_t)bin.more;     // pkt_proc.cc:563-569
+        else o.seg_kind |= MFP_SEG_SUPPLEMENTARY;
         if (!ssh_kex_fp<E>(nullptr, bin.payload)) return;
         o.flags |= MFP_FLAG_EMIT;
         o.fp_type = server ? 19 : 6;
@@ -1960,6 +1970,12 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         o.dst_port = (ld(tcph + 2) << 8) | ld(tcph + 3);
         uint32_t fl = ld(tcph + 13);
         bool syn = fl & 0x02, ack = fl & 0x10;
+        o.seq = (ld(tcph + 4) << 24) | (ld(tcph + 5) << 16) | (ld(tcph + 6) << 8) | ld(tcph + 7);
+        if (!(syn && cfg.mode == MFP_MODE_WRITE_JSON) && clen(pkt) > 0) {   // process_tcp_data's data segments
+            o.seg_kind = MFP_SEG_DATA;
+            o.pay_off = (uint32_t)(pkt.d - base);
+            o.pay_len = (uint32_t)clen(pkt);
+        }
         if (cfg.mode == MFP_MODE_WRITE_JSON) {
             if (syn && !ack) {
                 if (cfg.select & SEL_TCP_SYN) {
@@ -2009,6 +2025,7 @@ DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t
     o.src_port = o.dst_port = 0;
     o.net = 0;
     o.pay_off = o.pay_len = 0;
+    o.seq = o.more = o.seg_kind = 0;
     Cur p = cmk(data, data + len);
     switch (linktype) {
     case 1:                                             // eth::get_ip eth.h:114
@@ -2059,10 +2076,21 @@ struct KParams {
     uint8_t *fp_arena;
     uint64_t fp_cap;
     unsigned long long *fp_used;     // [0] bytes reserved, [1] overflow flag, [2] bytes written, [3] fallback count
+    mfp_tcp_seg *seg;                // reassembly inputs per packet (nullptr: not requested)
     const uint32_t *idx;             // packet indices (count = *count); nullptr = all n packets
     const unsigned long long *count;
     uint32_t *quic_idx;              // QUIC packets found by the walkers, for k_quic (count *quic_count)
     unsigned long long *quic_count;
 };
+// the reassembly inputs of packet i (when the caller asked for them)
+DEV void write_seg(const KParams &P, uint64_t i, const Out &o) {
+    if (!P.seg) return;
+    mfp_tcp_seg t;
+    t.seq = o.seq; t.more = o.more; t.pay_off = o.pay_off;
+    t.pay_len = (uint16_t)(o.pay_len > 0xffff ? 0xffff : o.pay_len);
+    t.kind = (uint8_t)o.seg_kind; t.reserved = 0;
+    P.seg[i] = t;
+}
+
 
 }  // namespace mfp

@@ -36,7 +36,8 @@ extern "C" int mfp_launch_analysis_resolve(const mfp_classifier_dev *D, const mf
                                            mfp_prof *prof);
 
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
-                                      const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
+                                      const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, mfp_tcp_seg *seg,
+                                      uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
                                       uint32_t bin_lds_mask, uint32_t quic_format, uint8_t *quic_scratch,
@@ -159,7 +160,8 @@ static bool parse_format(const std::string &s, uint32_t &tls_format) {
     return true;
 }
 
-bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis) {
+bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
+                      bool *reassembly) {
     sel = 0; tls_format = 0;
     std::string s = cfg ? cfg : "";
     if (s.find(';') == std::string::npos) return parse_select(s, sel);   // global_config.h:148-152
@@ -176,9 +178,8 @@ bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std:
             else if (key == "format") { if (!parse_format(val, tls_format)) return false; }
             else if (key == "resources") { if (resources) *resources = val; }
             else if (key == "analysis") { if (analysis) *analysis = val.empty() || val == "1"; }
-            else if (key == "reassembly" || key == "tcp-reassembly") {
-                mfp_set_error("reassembly is not part of the device path");
-                return false;
+            else if (key == "reassembly" || key == "tcp-reassembly") {   // global_config.h:354-355
+                if (reassembly) *reassembly = true;
             }
             // other keys (metadata, stats, ...) do not affect fingerprints
         }
@@ -190,7 +191,7 @@ bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std:
 
 extern "C" MFP_EXPORT int mfp_parse_filter(const char *cfg, uint32_t *select, uint32_t *tls_format) {
     uint32_t sel = 0, fmt = 0;
-    if (!mfp_parse_config(cfg, sel, fmt, nullptr, nullptr)) return -1;
+    if (!mfp_parse_config(cfg, sel, fmt, nullptr, nullptr, nullptr)) return -1;
     if (select) *select = sel;
     if (tls_format) *tls_format = fmt;
     return 0;
@@ -276,6 +277,8 @@ struct Slot {
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
     mfp_record *d_rec = nullptr; size_t cap_rec = 0;
+    mfp_tcp_seg *d_seg = nullptr; size_t cap_seg = 0;   // reassembly inputs (when seg_on)
+    bool seg_on = false;
     char *d_fp = nullptr; size_t cap_fp = 0;
     char *d_fp2 = nullptr; size_t cap_fp2 = 0;   // dense (compacted) fingerprints of a host batch
     unsigned long long *h_used = nullptr;   // pinned copy of d_used
@@ -290,7 +293,7 @@ struct Slot {
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
-        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_deferred, d_an, d_ap, d_arena, d_desc, d_rec, d_fp, d_fp2,
+        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_deferred, d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         if (h_used) (void)hipHostFree(h_used);
@@ -315,6 +318,7 @@ struct mfp_context_s {
     mfp_prevalence prev = nullptr;       // the one its sightings are decided against (own or shared)
     bool defer = false;                  // mfp_analysis_defer
     bool report_os = false;              // libmerc_config.report_os (mfp_analysis_report_os)
+    bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
     Slot slot[3];
     int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
@@ -333,8 +337,18 @@ struct mfp_context_s {
 extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode) {
     uint32_t sel, fmt;
     std::string resources;
-    bool analysis = false;
-    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis)) return nullptr;
+    bool analysis = false, reassembly = false;
+    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly)) return nullptr;
+    if (reassembly && mode != MFP_MODE_WRITE_JSON) {
+        mfp_set_error("reassembly is supported on the write_json path (MFP_MODE_WRITE_JSON) only");
+        return nullptr;
+    }
+    if (reassembly && (sel & (SEL_QUIC | SEL_DTLS))) {
+        // process_udp_data's reassembly (QUIC CRYPTO frames, DTLS fragments,
+        // pkt_proc.cc:926-944) is not on the device path: refuse, do not diverge
+        mfp_set_error("reassembly covers TCP only here; remove quic and dtls from the selection");
+        return nullptr;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         mfp_set_error("no HIP device available: the mercury_amd fingerprint path runs only on the GPU");
@@ -343,6 +357,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
     if (device < 0 || device >= ndev) { mfp_set_error("bad device %d", device); return nullptr; }
     auto *c = new mfp_context_s;
     c->device = device; c->select = sel; c->tls_format = fmt & 0xff; c->quic_format = (fmt >> 8) & 0xff; c->mode = mode;
+    c->reassembly = reassembly;
     const char *st = getenv("MFP_STRATEGY");
     if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
     const char *sm = getenv("MFP_BIN_SEG_MASK");
@@ -437,7 +452,12 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
     }
     HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(S.d_bins, 0, 16 * sizeof(unsigned long long), s));
-    if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, (uint8_t *)d_fp_arena,
+    mfp_tcp_seg *d_seg = nullptr;
+    if (S.seg_on) {
+        if (grow(S.d_seg, S.cap_seg, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
+        d_seg = S.d_seg;
+    }
+    if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, d_seg, (uint8_t *)d_fp_arena,
                                fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
                                c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
                                c->prof) != 0) {
@@ -705,6 +725,31 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     if (used) HIPCHK(hipMemcpy(fp_arena, S.d_fp2, used, hipMemcpyDeviceToHost));
     return (long long)used;
 }
+
+extern "C" MFP_EXPORT long long mfp_process_batch_host_seg(mfp_context c, const uint8_t *arena, size_t arena_len,
+                                                           const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
+                                                           char *fp_arena, size_t fp_cap, mfp_tcp_seg *seg) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    if (!seg && n) { mfp_set_error("null segment array"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
+    Slot &S = c->slot[0];
+    S.seg_on = true;
+    int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, false, false);
+    S.seg_on = false;
+    if (r) return r;
+    if (n) HIPCHK(hipMemcpyAsync(rec, S.d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, S.stream));
+    if (n) HIPCHK(hipMemcpyAsync(seg, S.d_seg, n * sizeof(mfp_tcp_seg), hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    const unsigned long long used = S.h_used[2];
+    if (S.h_used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    if (used) HIPCHK(hipMemcpy(fp_arena, S.d_fp2, used, hipMemcpyDeviceToHost));
+    return (long long)used;
+}
+
+extern "C" MFP_EXPORT int mfp_reassembly_enabled(mfp_context c) { return c && c->reassembly ? 1 : 0; }
 
 extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                        const mfp_pkt_desc *desc, size_t n, mfp_record *rec,

@@ -10,7 +10,8 @@
 #include "../../include/mfp.h"
 
 void mfp_set_error(const char *fmt, ...);
-bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis);
+bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
+                      bool *reassembly);
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode);
 
 // kernel strategies of the fingerprint pass (mfp_kernels.hip)

@@ -155,6 +155,7 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
         r.dst_port = (uint16_t)o.dst_port;
         r.net = o.net;
         P.rec[i] = r;
+            write_seg(P, i, o);
     }
     __syncthreads();   // tile_base / wave_tot reuse
     }
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             r.dst_port = (uint16_t)o.dst_port;
             r.net = o.net;
             P.rec[i] = r;
+            write_seg(P, i, o);
         }
         __syncthreads();   // tile_base / wave_tot / segs reuse
     }
@@ -495,6 +497,7 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
                 r.dst_port = (uint16_t)o.dst_port;
                 r.net = o.net;
                 P.rec[i] = r;
+            write_seg(P, i, o);
             }
             todo = todo && !in;
             __builtin_amdgcn_wave_barrier();   // the stage is rewritten by the next sub-round
@@ -623,7 +626,8 @@ extern "C" int mfp_launch_quic(const void *kparams, uint8_t *scratch, uint32_t q
 #define MFP_LDS_STAGE_SEG (32 * 1024)
 #endif
 extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
-                                      const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, uint8_t *fp_arena,
+                                      const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, mfp_tcp_seg *seg,
+                                      uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
                                       uint32_t bin_lds_mask, uint32_t quic_format, uint8_t *quic_scratch,
@@ -639,6 +643,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
+    P.seg = seg;
     P.idx = nullptr; P.count = nullptr;
     // QUIC and OpenVPN packets (bin 8 of the classify pass, plus any a walker hands over)
     P.quic_idx = work + (uint64_t)mfp::QUIC_BIN * n;

@@ -696,6 +696,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             r.dst_port = (uint16_t)o.dst_port;
             r.net = o.net;
             P.rec[i] = r;
+            write_seg(P, i, o);
         }
         __syncthreads();   // tile_base / wave_tot reuse
     }

@@ -1,0 +1,188 @@
+"""Synthetic TCP streams for the reassembly fixtures
+(tests/golden/make_golden_reasm.py; test infrastructure, the expected values
+come from the reference libmerc with "reassembly" configured).
+
+Scenarios (process_tcp_data pkt_proc.cc:773-893, reassembly.hpp:140-520):
+ClientHellos split into 2..6 segments in order, reordered, duplicated,
+with partial / subset / superset overlaps, a missing middle segment, more than
+20 segments, sequence numbers wrapping 2^32, continuing segments with
+sequence number 0, several flows interleaved, IPv6 flows, a ClientHello
+longer than the 8192-byte buffer, an oversized segment, a complete message in
+the middle of a flow in reassembly; SSH banners followed by their KEXINIT in
+later segments (indefinite SSH reassembly), split standalone KEXINITs;
+TLS ServerHello + Certificate split; HTTP requests split (no reassembly).
+"""
+import struct
+
+import numpy as np
+
+from tests import synth
+
+
+class Flow:
+    def __init__(self, sport, dport=443, v6=False, seq=1000, src=0x0a000001, dst=0x0d59b21b):
+        self.sport, self.dport, self.v6, self.seq0, self.src, self.dst = sport, dport, v6, seq, src, dst
+
+    def pkt(self, data, off, seq=None, flags=0x18):
+        s = (self.seq0 + off) & 0xffffffff if seq is None else seq
+        l4 = synth.tcp(data, sport=self.sport, dport=self.dport, seq=s, flags=flags)
+        if self.v6:
+            return synth.eth(synth.ipv6(l4, 6), 0x86dd)
+        return synth.eth(synth.ipv4(l4, 6, src=self.src, dst=self.dst))
+
+
+def cuts(n, k, rng):
+    c = sorted(set(int(x) for x in rng.integers(1, n, k - 1)))
+    return [0] + c + [n]
+
+
+def ssh_banner(comment=True):
+    return b"SSH-2.0-OpenSSH_9.6" + (b" Ubuntu-3ubuntu13\r\n" if comment else b"\r\n")
+
+
+def scenarios(seed=0x5EED000F):
+    rng = np.random.default_rng(seed)
+    out = []   # (label, frame)
+    port = [40000]
+
+    def flow(**kw):
+        port[0] += 1
+        return Flow(port[0], **kw)
+
+    def ch(name="reasm.example.com", big=False):
+        prof = ["chrome", "firefox", "safari", "openssl"][int(rng.integers(4))]
+        return synth.client_hello(rng, prof, ("x" * 300 + ".") * 20 + "example.com" if big else name)
+
+    def emit(label, f, parts, order=None, seqs=None):
+        order = range(len(parts)) if order is None else order
+        for j in order:
+            data, off = parts[j]
+            out.append((f"{label}.{j}", f.pkt(data, off, None if seqs is None else seqs[j])))
+
+    def split(data, c):
+        return [(data[c[k]:c[k + 1]], c[k]) for k in range(len(c) - 1)]
+
+    # in order, 2..6 segments
+    for k in range(2, 7):
+        d = ch(big=False)
+        emit(f"inorder{k}", flow(), split(d, cuts(len(d), k, rng)))
+    # post-quantum sized hello (about 1.8 kB) over 2 MTU-sized segments
+    d = synth.client_hello(rng, "chrome", "pq.example.com") + b""
+    emit("pq", flow(), split(d, [0, min(1400, len(d) - 1), len(d)]))
+    # reordered: later segments before the second
+    d = ch(); c = cuts(len(d), 4, rng)
+    emit("reorder", flow(), split(d, c), order=[0, 2, 1, 3])
+    d = ch(); c = cuts(len(d), 3, rng)
+    emit("first_late", flow(), split(d, c), order=[1, 0, 2])
+    # duplicates and overlaps
+    d = ch(); c = cuts(len(d), 3, rng); p = split(d, c)
+    emit("dup", flow(), [p[0], p[1], p[1], p[2]])
+    d = ch(); n = len(d)
+    f = flow()
+    emit("back_partial", f, [(d[:n // 2], 0), (d[n // 3:], n // 3)])
+    d = ch(); n = len(d); f = flow()
+    emit("back_subset", f, [(d[:n // 2], 0), (d[n // 4:n // 3], n // 4), (d[n // 2:], n // 2)])
+    d = ch(); n = len(d); f = flow()
+    emit("front_superset", f, [(d[:n // 4], 0), (d[n // 2:3 * n // 4], n // 2), (d[3 * n // 4:], 3 * n // 4),
+                               (d[n // 4:n], n // 4)])
+    d = ch(); n = len(d); f = flow()
+    emit("front_partial", f, [(d[:n // 4], 0), (d[n // 2:], n // 2), (d[n // 4:n // 2 + 10], n // 4)])
+    # a missing middle segment: never completes
+    d = ch(); c = cuts(len(d), 4, rng); p = split(d, c)
+    emit("missing", flow(), [p[0], p[2], p[3]])
+    # more than 20 segments
+    d = ch(); c = list(range(0, len(d), max(1, len(d) // 25))) + [len(d)]
+    emit("maxseg", flow(), split(d, sorted(set(c))))
+    # sequence numbers wrapping 2^32
+    d = ch(); c = cuts(len(d), 3, rng)
+    emit("wrap", flow(seq=0xffffff00), split(d, c))
+    # continuing segments with sequence number 0 (in-order placement)
+    d = ch(); c = cuts(len(d), 3, rng); p = split(d, c)
+    f = flow()
+    emit("seq0", f, p, seqs=[None, 0, 0])
+    # interleaved flows
+    fs = [flow() for _ in range(4)]
+    ps = []
+    for f in fs:
+        d = ch(); ps.append(split(d, cuts(len(d), int(rng.integers(2, 5)), rng)))
+    idx = [0] * 4
+    while any(idx[k] < len(ps[k]) for k in range(4)):
+        k = int(rng.integers(4))
+        if idx[k] < len(ps[k]):
+            data, off = ps[k][idx[k]]
+            out.append((f"interleave{k}.{idx[k]}", fs[k].pkt(data, off)))
+            idx[k] += 1
+    # IPv6
+    d = ch(); emit("v6", flow(v6=True), split(d, cuts(len(d), 3, rng)))
+    # longer than the buffer: more > 8192 -> a truncated record, no reassembly
+    d = ch(big=True); emit("big", flow(), split(d, [0, 1200, len(d)]))
+    # a hello of about 7 kB (a padding extension), over five segments
+    d = synth.client_hello(rng, "chrome", "y" * 200 + ".example.com")
+    hs = bytearray(d[9:])                          # ClientHello body (after record + handshake headers)
+    p = 2 + 32
+    p += 1 + hs[p]                                 # session id
+    p += 2 + struct.unpack(">H", hs[p:p + 2])[0]   # cipher suites
+    p += 1 + hs[p]                                 # compression methods
+    ext = struct.pack(">HH", 0x0015, 6000) + bytes(6000)
+    el = struct.unpack(">H", hs[p:p + 2])[0]
+    hs[p:p + 2] = struct.pack(">H", el + len(ext))
+    hs += ext
+    rec = b"\x16\x03\x01" + struct.pack(">H", len(hs) + 4) + b"\x01" + len(hs).to_bytes(3, "big") + bytes(hs)
+    emit("padded6k", flow(), split(rec, [0, 1400, 2800, 4200, 5600, len(rec)]))
+    # a complete hello in the middle of a flow in reassembly (on the same flow)
+    d = ch(); c = cuts(len(d), 3, rng); p = split(d, c)
+    f = flow()
+    whole = ch("whole.example.com")
+    out.append(("midwhole.0", f.pkt(p[0][0], 0)))
+    out.append(("midwhole.x", f.pkt(whole, 5000)))
+    out.append(("midwhole.1", f.pkt(p[1][0], p[1][1])))
+    out.append(("midwhole.2", f.pkt(p[2][0], p[2][1])))
+    # non-matching data on a flow not in reassembly, and ACKs with no data
+    f = flow(); out.append(("junk", f.pkt(b"hello world, not a protocol", 0)))
+    out.append(("ack", f.pkt(b"", 0, flags=0x10)))
+    # SSH: banner, then KEXINIT in the next segment(s) (indefinite reassembly)
+    for k, comment in enumerate((True, False)):
+        f = flow(dport=22)
+        kex = synth.ssh_kexinit(rng)
+        out.append((f"ssh{k}.banner", f.pkt(ssh_banner(comment), 0)))
+        bl = len(ssh_banner(comment))
+        c = [0, len(kex) // 3, len(kex)]
+        out.append((f"ssh{k}.kex0", f.pkt(kex[c[0]:c[1]], bl)))
+        out.append((f"ssh{k}.kex1", f.pkt(kex[c[1]:], bl + c[1])))
+    f = flow(dport=22)
+    kex = synth.ssh_kexinit(rng)
+    out.append(("sshkex.0", f.pkt(kex[:40], 0)))
+    out.append(("sshkex.1", f.pkt(kex[40:], 40)))
+    f = flow(dport=22)                                              # banner + partial KEXINIT together
+    kex = synth.ssh_kexinit(rng)
+    b = ssh_banner()
+    out.append(("sshpart.0", f.pkt(b + kex[:50], 0)))
+    out.append(("sshpart.1", f.pkt(kex[50:], len(b) + 50)))
+    # TLS ServerHello + Certificate split over segments
+    f = Flow(443, dport=port[0] + 1)
+    port[0] += 1
+    sh = synth.server_hello(rng, cert_bytes=3000)
+    out.append(("sh.0", f.pkt(sh[:1000], 0)))
+    out.append(("sh.1", f.pkt(sh[1000:2200], 1000)))
+    out.append(("sh.2", f.pkt(sh[2200:], 2200)))
+    # HTTP request split: the reference does not reassemble HTTP
+    f = flow(dport=80)
+    req = synth.http_request(rng, "split.example.org")
+    out.append(("http.0", f.pkt(req[:40], 0)))
+    out.append(("http.1", f.pkt(req[40:], 40)))
+    # random streams: splits, drops, duplicates and reorderings
+    for r in range(120):
+        f = flow(seq=int(rng.integers(0, 1 << 32)), v6=bool(rng.random() < 0.2))
+        d = ch()
+        p = split(d, cuts(len(d), int(rng.integers(2, 6)), rng))
+        order = list(range(len(p)))
+        if rng.random() < 0.3:
+            j = int(rng.integers(0, len(p) - 1)); order[j], order[j + 1] = order[j + 1], order[j]
+        if rng.random() < 0.15:
+            order.insert(int(rng.integers(0, len(order) + 1)), int(rng.integers(0, len(p))))
+        if rng.random() < 0.1 and len(order) > 2:
+            del order[int(rng.integers(1, len(order)))]
+        for j in order:
+            data, off = p[j]
+            out.append((f"rand{r}.{j}", f.pkt(data, off)))
+    return out
