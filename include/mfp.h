@@ -289,6 +289,13 @@ MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mfp_reassembl
                                                   const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
                                                   size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc);
 MFP_EXPORT const uint8_t *mfp_reassembler_frames(mfp_reassembler r, size_t *len);
+/* mfp_write_json_batch for the output of mfp_process_batch_reassembly (arena ++
+ * frames, out_desc, records, props): completing records carry the
+ * reassembler's "reassembly_properties" (reassembly.hpp:860-880,1231-1247). */
+MFP_EXPORT long long mfp_write_json_batch_reassembly(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+                                                     const mfp_record *rec, const char *fp_arena, const uint16_t *props,
+                                                     const uint64_t *ts_ns, char *out, size_t out_cap,
+                                                     uint64_t *line_end, uint64_t *skipped, int threads);
 
 typedef struct mfp_prevalence_s *mfp_prevalence;
 

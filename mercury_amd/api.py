@@ -94,6 +94,8 @@ def load_library():
     lib.mfp_reassembler_frames.argtypes = [vp, ctypes.POINTER(sz)]
     lib.mfp_reassembly_enabled.restype = ctypes.c_int
     lib.mfp_reassembly_enabled.argtypes = [vp]
+    lib.mfp_write_json_batch_reassembly.restype = ctypes.c_longlong
+    lib.mfp_write_json_batch_reassembly.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, sz, vp, vp, ctypes.c_int]
     lib.mfp_process_batch_reassembly.restype = ctypes.c_longlong
     lib.mfp_process_batch_reassembly.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp, sz, vp, vp]
     lib.mfp_process_batch_host_ex.restype = ctypes.c_longlong
@@ -618,11 +620,14 @@ def tpacket3_block(block, max_pkts=4096):
     return desc[:n], ts[:n]
 
 
-def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1, ctx=None, analysis=None, attr_prob=None):
+def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1, ctx=None, analysis=None, attr_prob=None,
+               props=None):
     """JSON record lines for a fingerprinted batch (mfp_write_json_batch: the
     text of stateful_pkt_proc::write_json, src/libmerc/pkt_proc.cc:1157-1253);
     with ctx + analysis (+ attr_prob), the --analysis "analysis" objects
-    (mfp_write_json_batch_analysis).  Returns (list of per-packet lines as
+    (mfp_write_json_batch_analysis); with props (process_host_reassembly's
+    output, whose arena/desc go with it) the reassembler's properties
+    (mfp_write_json_batch_reassembly).  Returns (list of per-packet lines as
     bytes, b"" when the reference writes nothing; count of records that could
     not be rebuilt). Host only."""
     lib = load_library()
@@ -639,7 +644,13 @@ def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1, ctx=None, anal
     cap = 1 << 16
     while True:
         out = np.empty(cap, np.uint8)
-        if an is not None:
+        if props is not None:
+            pr = np.ascontiguousarray(props, dtype=np.uint16)
+            got = lib.mfp_write_json_batch_reassembly(arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data,
+                                                      fp.ctypes.data, pr.ctypes.data,
+                                                      None if ts is None else ts.ctypes.data, out.ctypes.data, cap,
+                                                      ends.ctypes.data, ctypes.byref(skipped), int(threads))
+        elif an is not None:
             got = lib.mfp_write_json_batch_analysis(ctx.h, arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data,
                                                     fp.ctypes.data, an.ctypes.data,
                                                     None if ap is None else ap.ctypes.data,

@@ -583,7 +583,7 @@ ADEV float expf_ref(float x) {
 
 // a packet k_analyze hands to k_analyze_wave, with its feature lookups done
 struct Deferred {
-    uint32_t i, entry, slow_sni, pad;   // slow_sni: domain / SNI lookups still to do
+    uint32_t i, entry, slow_sni, slow_ua;   // slow_sni: domain / SNI lookups still to do; slow_ua: the SSH user agent
     uint32_t off[6], cnt[6];
 };
 
@@ -620,8 +620,8 @@ constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.
 #define MFP_AN_PL 16
 #endif
 #ifndef MFP_AN_MINW
-#define MFP_AN_MINW 3
-#endif
+#define MFP_AN_MINW 3      // waves/SIMD: 4 spills 168 B/lane to scratch, 2 leaves latency exposed;
+#endif                     // 3 measured best on the SURVEY archive (profiles/r02u_ab_analyze_*)
 constexpr uint32_t PL = MFP_AN_PL;   // phase L: fingerprints with at most PL processes, scored lane per packet
 constexpr int AW = 2;                // waves per k_analyze block (LDS: PL * 512 bytes of score rows per wave)
 
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 scored = false;
             }
         }
-        bool plain = false;
+        bool plain = false, ssh_ua = false;
         // string features UA, domain, SNI (hoff/hcnt slots 3..5)
         const uint8_t *vs[3] = {nullptr, nullptr, nullptr};
         uint32_t vl[3] = {0, 0, 0}, voff[3] = {0, 0, 0};
@@ -819,7 +819,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             plain = plain_server_name(sp, sl, tld, nh);   // no NUL in a plain name
             // user agent (strncpy 511, NUL stops); TLS has none (its slot holds
             // the ALPN list); QUIC's is transport parameter 0x3129 (tls.h:1346-1355)
-            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH ? 0u : r.ua_len;
+            // SSH (protocol + comment, the delimiting space dropped) is built and
+            // probed by k_analyze_wave
+            ssh_ua = r.msg == MFP_MSG_SSH_INIT && r.ua_len != 0xffff;
+            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH || ssh_ua ? 0u : r.ua_len;
             if (ul > 511) ul = 511;
             const uint8_t *up = sbase + r.ua_off;
             uint64_t uh = 0;
@@ -856,7 +859,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             }
             // string features: candidate slots here, byte-exact check by the wave below
             vs[0] = up; vl[0] = ul; vk[0] = uh;
-            has[0] = cand_feature_lane(D, entry, F_UA, uh, ul, vh[0], voff[0]);
+            has[0] = !ssh_ua && cand_feature_lane(D, entry, F_UA, uh, ul, vh[0], voff[0]);
             if (plain) {   // else k_analyze_wave normalises the name (wave, LDS)
                 vs[1] = sp + tld; vl[1] = sl - tld; vk[1] = lane_hash(sp + tld, sl - tld);
                 has[1] = cand_feature_lane(D, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
@@ -884,7 +887,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
 #ifdef MFP_PROBE_AN_NOSCORE
         const bool lanep = false;
 #else
-        const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain;
+        const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain && !ssh_ua;
 #endif
         if (lanep) {
             double *S = scl + lane;                    // S[p * 64]
@@ -978,7 +981,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 base = rfl64(base);
                 if (defer) {
                     Deferred &d = P.deferred[base + __builtin_popcountll(dm & ((1ull << lane) - 1))];
-                    d.i = (uint32_t)i; d.entry = entry; d.slow_sni = plain ? 0u : 1u; d.pad = 0;
+                    d.i = (uint32_t)i; d.entry = entry; d.slow_sni = plain ? 0u : 1u; d.slow_ua = ssh_ua ? 1u : 0u;
 #pragma unroll
                     for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
                 }
@@ -1012,6 +1015,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
 // reference's addition order; lists flagged MFP_UPD_SERIAL go one by one).
 __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
     __shared__ char sni_buf[4][336];
+    __shared__ char ua_buf[4][520];
     __shared__ double sc_lds[4][64 * MAXP_CHUNKS];
     __shared__ uint8_t fl_lds[4][64 * MAXP_CHUNKS];   // per process: malware (bit 0), archive tags (1-6), swapped out (7)
     const uint32_t lane = lane_id();
@@ -1050,6 +1054,37 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
             h = probe_feature(D, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
                               (const uint8_t *)nbuf, (uint32_t)nlen, true, lane);
             off[5] = h.off; cnt[5] = h.cnt;
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (rfl(dq.slow_ua)) {
+            // the SSH user agent (ssh_init_packet::do_analysis ssh.h:480-487):
+            // protocol then comment into a data_buffer<512> (nulled -- empty --
+            // when they do not fit), strncpy 511, NUL stops.  The record's span
+            // is "protocol SP comment"; its first space is the delimiter.
+            const mfp_record r = P.rec[i];
+            const uint8_t *sp = P.arena + P.desc[i].offset + r.ua_off;
+            const uint32_t L = r.ua_len;
+            char *ub = ua_buf[wid];
+            int ulen = 0;
+            if (lane == 0) {
+                uint32_t pl = 0;
+                while (pl < L && sp[pl] != ' ') pl++;
+                const uint32_t total = pl < L ? L - 1 : L;
+                uint32_t n = total > 512 ? 0u : (total > 511 ? 511u : total);
+                uint32_t k = 0;
+                for (uint32_t j = 0; k < n && j < L; j++) {
+                    if (j == pl) continue;
+                    const char c = (char)sp[j];
+                    if (c == 0) break;
+                    ub[k++] = c;
+                }
+                ulen = (int)k;
+            }
+            ulen = (int)rfl((uint32_t)ulen);
+            __builtin_amdgcn_wave_barrier();
+            const Hit h = probe_feature(D, entry, F_UA, wave_hash((const uint8_t *)ub, (uint32_t)ulen, lane),
+                                        (const uint8_t *)ub, (uint32_t)ulen, true, lane);
+            off[3] = h.off; cnt[3] = h.cnt;
             __builtin_amdgcn_wave_barrier();
         }
         // ---- scores: prior, then the six features in the reference's order

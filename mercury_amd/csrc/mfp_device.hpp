@@ -1582,8 +1582,11 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
             }
             b.putc(')');
         }
-        // analysis: user agent = protocol + comment strings (ssh.h:480)
-        o.ua_off = (uint32_t)(proto.d - base); o.ua_len = (uint32_t)clen(proto);
+        // analysis: user agent = protocol + comment strings (do_analysis
+        // ssh.h:480-487: a data_buffer<512> that a null comment nulls).  The
+        // span runs from the protocol string to the comment's end; its first
+        // space is the delimiter, which the classifier drops (k_analyze_wave).
+        if (!cnull(comment)) { o.ua_off = (uint32_t)(proto.d - base); o.ua_len = (uint32_t)(comment.e - proto.d); }
         return;
         }
     }

@@ -337,8 +337,22 @@ void write_analysis(W &w, mfp_context ctx, const mfp_analysis &a, const double *
 // one record; returns false when the record cannot be written exactly here
 struct TsCache { uint64_t sec = ~0ull, usec = ~0ull; int len = 0; char text[40]; };
 
+// tcp_reassembler::write_json (reassembly.hpp:860-880) from the props bits of
+// mfp_process_batch_reassembly
+void write_reassembled(W &w, uint16_t props) {
+    static const char *flag[7] = {"missing_segment", "timeout", "out_of_order", "out_of_buffer", "max_segments_exceed",
+                                  "segment_overlaps", "truncated"};
+    static const char *ovl[4] = {"back_partial_overlap", "back_subset_overlap", "front_partial_overlap",
+                                 "front_superset_overlap"};
+    w.puts("{\"reassembled\":true");
+    for (int k = 0; k < 7; k++) if (props >> (1 + k) & 1) { w.puts(",\""); w.putz(flag[k]); w.puts("\":true"); }
+    for (int k = 0; k < 4; k++) if (props >> (8 + k) & 1) { w.puts(",\""); w.putz(ovl[k]); w.puts("\":true"); }
+    w.put('}');
+}
+
 bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const char *fp_arena,
-                  uint64_t sec, uint64_t nsec, mfp_context ctx, const mfp_analysis *an, const double *ap) {
+                  uint64_t sec, uint64_t nsec, mfp_context ctx, const mfp_analysis *an, const double *ap,
+                  uint16_t props) {
     if (!(r.flags & MFP_FLAG_EMIT)) return true;
     // QUIC records carry a "quic" object with the decrypted payload
     // (quic_init::write_json quic.h:1662-1690), which the device does not return
@@ -427,7 +441,8 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
         break;
     }
     if (with_an) { rec.key("analysis"); write_analysis(w, ctx, *an, ap); }   // pkt_proc.cc:1211-1213
-    if (r.flags & MFP_FLAG_TRUNCATED) { rec.key("reassembly_properties"); w.puts("{\"truncated\":true}"); }
+    if (props & 1) { rec.key("reassembly_properties"); write_reassembled(w, props); }   // reassembly.hpp:1238-1241
+    else if (r.flags & MFP_FLAG_TRUNCATED) { rec.key("reassembly_properties"); w.puts("{\"truncated\":true}"); }
     if (r.flags & MFP_FLAG_ENCAP) {                      // encapsulations::write_json pkt_proc.cc:1021-1031
         rec.key("encapsulations");
         w.put('[');
@@ -466,7 +481,8 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
 
 }  // namespace
 
-static long long write_json_batch(mfp_context ctx, const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+static long long write_json_batch(mfp_context ctx, const uint16_t *props, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                   size_t n,
                                    const mfp_record *rec, const char *fp_arena, const mfp_analysis *an, const double *ap,
                                    const uint64_t *ts_ns, char *out, size_t out_cap, uint64_t *line_end,
                                    uint64_t *skipped, int threads) {
@@ -508,7 +524,7 @@ static long long write_json_batch(mfp_context ctx, const uint8_t *arena, const m
             if (sec == 0) { sec = (uint64_t)now.tv_sec; nsec = (uint64_t)now.tv_nsec; }
             size_t mark = o.len;
             if (!write_record(o, tc, arena + desc[i].offset, desc[i].caplen, rec[i], fp_arena, sec, nsec, ctx,
-                              an ? an + i : nullptr, ap ? ap + i * MFP_ATTR_DB_TAGS : nullptr)) {
+                              an ? an + i : nullptr, ap ? ap + i * MFP_ATTR_DB_TAGS : nullptr, props ? props[i] : (uint16_t)0)) {
                 o.len = mark;
                 bad[(size_t)t]++;
             }
@@ -547,7 +563,7 @@ MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_de
                                           const mfp_record *rec, const char *fp_arena, const uint64_t *ts_ns,
                                           char *out, size_t out_cap, uint64_t *line_end, uint64_t *skipped,
                                           int threads) {
-    return write_json_batch(nullptr, arena, desc, n, rec, fp_arena, nullptr, nullptr, ts_ns, out, out_cap, line_end,
+    return write_json_batch(nullptr, nullptr, arena, desc, n, rec, fp_arena, nullptr, nullptr, ts_ns, out, out_cap, line_end,
                             skipped, threads);
 }
 
@@ -567,6 +583,17 @@ MFP_EXPORT long long mfp_write_json_batch_analysis(mfp_context ctx, const uint8_
                 mfp_set_error("mfp_write_json_batch_analysis: record %zu carries archive tags but attr_prob is NULL", i);
                 return -1;
             }
-    return write_json_batch(ctx, arena, desc, n, rec, fp_arena, analysis, attr_prob, ts_ns, out, out_cap, line_end,
-                            skipped, threads);
+    return write_json_batch(ctx, nullptr, arena, desc, n, rec, fp_arena, analysis, attr_prob, ts_ns, out, out_cap,
+                            line_end, skipped, threads);
+}
+
+// the records of mfp_process_batch_reassembly: arena ++ its frames with its
+// out_desc, and its props (the reassembler's "reassembly_properties")
+MFP_EXPORT long long mfp_write_json_batch_reassembly(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+                                                     const mfp_record *rec, const char *fp_arena, const uint16_t *props,
+                                                     const uint64_t *ts_ns, char *out, size_t out_cap,
+                                                     uint64_t *line_end, uint64_t *skipped, int threads) {
+    if (n && !props) { mfp_set_error("mfp_write_json_batch_reassembly: null props"); return -1; }
+    return write_json_batch(nullptr, props, arena, desc, n, rec, fp_arena, nullptr, nullptr, ts_ns, out, out_cap,
+                            line_end, skipped, threads);
 }

@@ -51,6 +51,8 @@ struct mercury_packet_processor_s {
     analysis_context ac;
     std::vector<uint8_t> arena;
     std::vector<char> fp;
+    mfp_reassembler reasm = nullptr;   // the processor's tcp_reassembler ("reassembly" configured)
+    ~mercury_packet_processor_s() { if (reasm) mfp_reassembler_destroy(reasm); }
 };
 
 static printf_err_ptr g_printf_err = nullptr;
@@ -141,10 +143,29 @@ static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *p
                          const char *fp, const mfp_analysis *an, const double *ap) {
     ac.fp_type = rec.fp_type;
     copy_cstr(ac.fp, sizeof ac.fp, (const uint8_t *)fp + rec.fp_offset, rec.fp_type ? rec.fp_len : 0);
-    const bool cert_slot = rec.msg == MFP_MSG_TLS_SH || rec.msg == MFP_MSG_TLS_CERT;   // sni slot = certificate_list
-    const bool hello = rec.msg == MFP_MSG_TLS_CH || rec.msg == MFP_MSG_DTLS_CH;        // ua slot = ALPN list
-    copy_cstr(ac.sn, sizeof ac.sn, pkt + rec.sni_off, rec.sni_len == 0xffff || cert_slot ? 0 : rec.sni_len);
-    copy_cstr(ac.ua, sizeof ac.ua, pkt + rec.ua_off, rec.ua_len == 0xffff || hello ? 0 : rec.ua_len);
+    // the sni slot holds the certificate_list (TLS server), the STUN message or
+    // the OpenVPN payload for those messages; the ua slot holds the ALPN list
+    // of (D)TLS ClientHellos; QUIC spans index the sidecar behind the string
+    const bool no_sn = rec.msg == MFP_MSG_TLS_SH || rec.msg == MFP_MSG_TLS_CERT || rec.msg == MFP_MSG_STUN ||
+                       rec.msg == MFP_MSG_OPENVPN;
+    const bool hello = rec.msg == MFP_MSG_TLS_CH || rec.msg == MFP_MSG_DTLS_CH;
+    const uint8_t *sb = (rec.flags & MFP_FLAG_SIDECAR)
+                            ? (const uint8_t *)fp + rec.fp_offset + ((rec.fp_len + 7) & ~7u) + 8 : pkt;
+    copy_cstr(ac.sn, sizeof ac.sn, sb + rec.sni_off, rec.sni_len == 0xffff || no_sn ? 0 : rec.sni_len);
+    if (rec.msg == MFP_MSG_SSH_INIT && rec.ua_len != 0xffff) {
+        // protocol + comment (ssh.h:480-487): the span's first space is the
+        // delimiter; a data_buffer<512> that does not hold both is null
+        std::string u;
+        bool skipped = false;
+        for (uint32_t j = 0; j < rec.ua_len; j++) {
+            if (!skipped && pkt[rec.ua_off + j] == ' ') { skipped = true; continue; }
+            u.push_back((char)pkt[rec.ua_off + j]);
+        }
+        if (u.size() > 512) u.clear();
+        copy_cstr(ac.ua, sizeof ac.ua, (const uint8_t *)u.data(), u.size());
+    } else {
+        copy_cstr(ac.ua, sizeof ac.ua, sb + rec.ua_off, rec.ua_len == 0xffff || hello ? 0 : rec.ua_len);
+    }
     ac.alpn_len = 0;
     ac.alpn[0] = 0;
     if (hello && rec.ua_len != 0xffff) {   // alpn.write_to_buffer(alpn_array, 128) (result.h:352-353)
@@ -205,15 +226,35 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
     size_t cap = mfp_fp_arena_bound(1, len);
     p->fp.resize(cap);
     const bool want_an = mfp_analysis_enabled(ctx);
-    long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap,
-                                               want_an ? &an : nullptr, want_an ? ap : nullptr);
-    if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
-    fill_context(ctx, p->ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
     uint64_t t = (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec, end = 0, skipped = 0;
-    long long n = want_an ? mfp_write_json_batch_analysis(ctx, p->arena.data(), &d, 1, &rec, p->fp.data(), &an, ap, &t,
-                                                          (char *)buffer, buffer_size, &end, &skipped, 1)
-                          : mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
-                                                 buffer_size, &end, &skipped, 1);
+    long long n;
+    if (mfp_reassembly_enabled(ctx)) {
+        // process_tcp_data with the processor's reassembler (pkt_proc.cc:773-893)
+        if (!p->reasm) p->reasm = mfp_reassembler_create();
+        cap += mfp_fp_arena_bound(1, 8192 + 256);
+        p->fp.resize(cap);
+        uint16_t props = 0;
+        mfp_pkt_desc d2 = d;
+        long long used = mfp_process_batch_reassembly(ctx, p->reasm, p->arena.data(), p->arena.size(), &d, 1, &t, &rec,
+                                                      p->fp.data(), cap, &props, &d2);
+        if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
+        // the record indexes arena ++ the reassembler's frames
+        size_t flen = 0;
+        const uint8_t *fr = mfp_reassembler_frames(p->reasm, &flen);
+        if (d2.offset >= len + 16 && fr) p->arena.insert(p->arena.end(), fr, fr + flen);
+        fill_context(ctx, p->ac, p->arena.data() + d2.offset, rec, p->fp.data(), nullptr, ap);
+        n = mfp_write_json_batch_reassembly(p->arena.data(), &d2, 1, &rec, p->fp.data(), &props, &t, (char *)buffer,
+                                            buffer_size, &end, &skipped, 1);
+    } else {
+        long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(),
+                                                   cap, want_an ? &an : nullptr, want_an ? ap : nullptr);
+        if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
+        fill_context(ctx, p->ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+        n = want_an ? mfp_write_json_batch_analysis(ctx, p->arena.data(), &d, 1, &rec, p->fp.data(), &an, ap, &t,
+                                                    (char *)buffer, buffer_size, &end, &skipped, 1)
+                    : mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
+                                           buffer_size, &end, &skipped, 1);
+    }
     if (skipped) {
         // the reference writes a record here; the writer cannot rebuild it
         // (QUIC, GRE/VXLAN/Geneve encapsulations, IP-in-IP with an outer IPv6

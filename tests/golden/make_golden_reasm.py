@@ -16,6 +16,7 @@ Outputs (committed):
                            truncated, fingerprint
   reasm_props_<cfg>.txt.gz the record's "reassembly_properties" object text
                            per packet ("" when none)
+  reasm_json_<cfg>.txt.gz  the record's whole JSON line per packet
   reasm_manifest.json      configurations, counts
 """
 import gzip
@@ -69,6 +70,8 @@ def main():
             props.append(m.group(1) if m else "")
         with gzip.open(os.path.join(HERE, f"reasm_props_{key}.txt.gz"), "wt", encoding="latin-1") as f:
             f.write("\n".join(props) + "\n")
+        with gzip.open(os.path.join(HERE, f"reasm_json_{key}.txt.gz"), "wt", encoding="latin-1") as f:
+            f.write("\n".join(lines) + "\n")
         rows = [l.split(b"\t") for l in out.splitlines()]
         counts[key] = {"emit": sum(int(r[1]) for r in rows), "fp": sum(r[2] != b"0" for r in rows),
                        "reassembled": sum('"reassembled":true' in p for p in props),

@@ -63,7 +63,7 @@ def test_parse_filter(cfg, sel, fmt):
     assert mercury_amd.parse_filter(cfg) == (sel, fmt)
 
 
-@pytest.mark.parametrize("cfg", ["select=tls", "quic,dns", "tls,dns", "select=tls;format=tls/9", "select=tls;reassembly",
+@pytest.mark.parametrize("cfg", ["select=tls", "quic,dns", "tls,dns", "select=tls;format=tls/9",
                                  None, "", "all", " all ", "select=all;format=tls/1", "tls,all"])
 def test_parse_filter_rejects(cfg):
     with pytest.raises(mercury_amd.MercuryAmdError):

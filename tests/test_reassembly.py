@@ -131,3 +131,66 @@ def test_reassembly_refusals():
         mercury_amd.Context("select=tls,quic;reassembly", device=0)
     with pytest.raises(mercury_amd.MercuryAmdError):
         mercury_amd.Context("select=tls;reassembly", device=0, mode=api.MODE_ANALYSIS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["r0", "r1"])
+def test_reassembly_json_vs_reference(key):
+    """The whole JSON line of every packet (mfp_write_json_batch_reassembly over
+    the reassembled frames: server names, flow keys, the reassembler's
+    properties) equals the reference's write_json text."""
+    from tests import test_json
+    arena, desc = load_stream()
+    ctx = mercury_amd.Context(MANIFEST["configs"][key], device=0)
+    try:
+        rec, fp, props, arena2, desc2 = ctx.process_host_reassembly(arena, desc,
+                                                                    ts_ns=np.full(len(desc), TS, np.uint64))
+    finally:
+        ctx.close()
+    lines, skipped = mercury_amd.write_json(arena2, desc2, rec, fp, ts_ns=np.full(len(desc), TS, np.uint64),
+                                            threads=4, props=props)
+    test_json._check(lines, test_json._golden_lines(f"reasm_json_{key}.txt.gz"), skipped, allow_skip=True)
+
+
+@pytest.mark.gpu
+def test_libmerc_write_json_with_reassembly():
+    """mercury_packet_processor_write_json_linktype with "reassembly" in the
+    configuration: the processor's own reassembler, packet by packet, gives
+    the reference's text for the synthetic streams."""
+    from tests import test_json
+    lib = mercury_amd.load_library()
+    vp = ctypes.c_void_p
+
+    class Timespec(ctypes.Structure):
+        _fields_ = [("tv_sec", ctypes.c_long), ("tv_nsec", ctypes.c_long)]
+
+    lib.mercury_init.restype = vp
+    lib.mercury_init.argtypes = [ctypes.POINTER(test_json._LibmercConfig), ctypes.c_int]
+    lib.mercury_packet_processor_construct.restype = vp
+    lib.mercury_packet_processor_construct.argtypes = [vp]
+    lib.mercury_packet_processor_destruct.argtypes = [vp]
+    lib.mercury_finalize.argtypes = [vp]
+    f = lib.mercury_packet_processor_write_json_linktype
+    f.restype = ctypes.c_size_t
+    f.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(Timespec), ctypes.c_uint16]
+    cfg = test_json._LibmercConfig()
+    cfg.packet_filter_cfg = MANIFEST["configs"]["r0"].encode()
+    mc = lib.mercury_init(ctypes.byref(cfg), 0)
+    assert mc
+    p = lib.mercury_packet_processor_construct(mc)
+    arena, desc = load_stream()
+    gold = test_json._golden_lines("reasm_json_r0.txt.gz")
+    buf = ctypes.create_string_buffer(1 << 16)
+    first = MANIFEST["pcap_packets"]           # the synthetic streams follow the pcap packets
+    bad = []
+    for i in range(len(desc)):
+        off, ln, lt = int(desc[i]["offset"]), int(desc[i]["caplen"]), int(desc[i]["linktype"])
+        pkt = ctypes.create_string_buffer(arena[off:off + ln].tobytes() + bytes(16))
+        ts = Timespec(1700000000, 0)
+        n = f(p, buf, len(buf), pkt, ln, ctypes.byref(ts), lt)
+        want = gold[i] + b"\n" if gold[i] else b""
+        if i >= first and buf.raw[:n] != want:
+            bad.append((i, buf.raw[:n][:200], want[:200]))
+    lib.mercury_packet_processor_destruct(p)
+    lib.mercury_finalize(mc)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:2]}"
