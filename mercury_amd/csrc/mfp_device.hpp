@@ -1306,6 +1306,7 @@ DEV void cert_record(Out &o, Cur l, const uint8_t *base) {
 struct Cfg {
     uint32_t select, tls_format, mode;
     uint32_t classify;   // stop after protocol identification (o.msg), emit nothing
+    uint32_t seg;        // the caller wants the reassembly inputs (KParams::seg)
 };
 // parser families compiled into a walker instance (template argument FAM):
 // a bin kernel carries only its protocol's parser, so its code and register
@@ -1973,8 +1974,8 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         o.dst_port = (ld(tcph + 2) << 8) | ld(tcph + 3);
         uint32_t fl = ld(tcph + 13);
         bool syn = fl & 0x02, ack = fl & 0x10;
-        o.seq = (ld(tcph + 4) << 24) | (ld(tcph + 5) << 16) | (ld(tcph + 6) << 8) | ld(tcph + 7);
-        if (!(syn && cfg.mode == MFP_MODE_WRITE_JSON) && clen(pkt) > 0) {   // process_tcp_data's data segments
+        if (cfg.seg && !(syn && cfg.mode == MFP_MODE_WRITE_JSON) && clen(pkt) > 0) {   // process_tcp_data's data segments
+            o.seq = (ld(tcph + 4) << 24) | (ld(tcph + 5) << 16) | (ld(tcph + 6) << 8) | ld(tcph + 7);
             o.seg_kind = MFP_SEG_DATA;
             o.pay_off = (uint32_t)(pkt.d - base);
             o.pay_len = (uint32_t)clen(pkt);

@@ -82,6 +82,12 @@ struct W {
         memcpy(p, tab.s[v & 255], 4);              // over-copy by design; need() reserved room
         p += tab.n[v & 255];
     }
+    void hexb(const uint8_t *x, size_t n) {         // raw_as_hex
+        for (size_t k = 0; k < n; k++) { put(HEX[x[k] >> 4]); put(HEX[x[k] & 15]); }
+    }
+    void hexu(uint64_t v, int digits) {             // append_uint{8,16,32,64}_hex: fixed width
+        for (int k = digits - 1; k >= 0; k--) put(HEX[(v >> (4 * k)) & 15]);
+    }
     void udec(uint64_t v) {
         char t[24]; int n = 0;
         do { t[n++] = '0' + v % 10; v /= 10; } while (v);
@@ -337,6 +343,348 @@ void write_analysis(W &w, mfp_context ctx, const mfp_analysis &a, const double *
 // one record; returns false when the record cannot be written exactly here
 struct TsCache { uint64_t sec = ~0ull, usec = ~0ull; int len = 0; char text[40]; };
 
+// ---- STUN and OpenVPN objects, rebuilt from the message bytes the record's
+// server-name span holds (host cursor over struct datum semantics)
+struct HC { const uint8_t *d, *e; };
+inline long hlen(HC c) { return c.d ? (long)(c.e - c.d) : 0; }
+inline void hnull(HC &c) { c.d = c.e = nullptr; }
+inline uint64_t hrd(HC &c, int n) {                 // encoded<T>: 0 and null when short
+    if (c.d && c.d + n <= c.e) { uint64_t v = 0; for (int i = 0; i < n; i++) v = v << 8 | c.d[i]; c.d += n; return v; }
+    hnull(c); return 0;
+}
+inline HC hparse(HC &r, long n) {                   // datum(datum &, n)
+    HC o;
+    if (hlen(r) < n || n < 0) { hnull(r); hnull(o); return o; }
+    o.d = r.d; o.e = r.d ? r.d + n : nullptr; if (r.d) r.d += n;
+    return o;
+}
+
+// stun_params.h: method and attribute names (IANA registry names)
+const char *stun_method_name(unsigned m) {
+    switch (m) {
+    case 0x001: return "Binding"; case 0x002: return "SharedSecret"; case 0x003: return "Allocate";
+    case 0x004: return "Refresh"; case 0x006: return "Send"; case 0x007: return "Data";
+    case 0x008: return "CreatePermission"; case 0x009: return "ChannelBind"; case 0x00A: return "Connect";
+    case 0x00B: return "ConnectionBind"; case 0x00C: return "ConnectionAttempt"; case 0x080: return "GOOG_PING";
+    }
+    return nullptr;
+}
+const char *stun_attr_name(unsigned t) {
+    static const struct { uint16_t t; const char *n; } tab[] = {
+        {0x0001, "MAPPED_ADDRESS"}, {0x0002, "RESPONSE_ADDRESS"}, {0x0004, "SOURCE_ADDRESS"},
+        {0x0005, "CHANGED_ADDRESS"}, {0x0006, "USERNAME"}, {0x0008, "MESSAGE_INTEGRITY"}, {0x0009, "ERROR_CODE"},
+        {0x000A, "UNKNOWN_ATTRIBUTES"}, {0x000B, "REFLECTED_FROM"}, {0x000C, "CHANNEL_NUMBER"}, {0x000D, "LIFETIME"},
+        {0x0010, "BANDWIDTH"}, {0x0012, "XOR_PEER_ADDRESS"}, {0x0013, "DATA"}, {0x0014, "REALM"}, {0x0015, "NONCE"},
+        {0x0016, "XOR_RELAYED_ADDRESS"}, {0x0017, "REQUESTED_ADDRESS_FAMILY"}, {0x0018, "EVEN_PORT"},
+        {0x0019, "REQUESTED_TRANSPORT"}, {0x001A, "DONT_FRAGMENT"}, {0x001B, "ACCESS_TOKEN"},
+        {0x001C, "MESSAGE_INTEGRITY_SHA256"}, {0x001D, "PASSWORD_ALGORITHM"}, {0x001E, "USERHASH"},
+        {0x0020, "XOR_MAPPED_ADDRESS"}, {0x0022, "RESERVATION_TOKEN"}, {0x0024, "PRIORITY"}, {0x0025, "USE_CANDIDATE"},
+        {0x0026, "PADDING"}, {0x0027, "RESPONSE_PORT"}, {0x002A, "CONNECTION_ID"}, {0x8000, "ADDITIONAL_ADDRESS_FAMILY"},
+        {0x8001, "ADDRESS_ERROR_CODE"}, {0x8002, "PASSWORD_ALGORITHMS"}, {0x8003, "ALTERNATE_DOMAIN"}, {0x8004, "ICMP"},
+        {0x8008, "MS_VERSION"}, {0x8020, "MS_XOR_MAPPED_ADDRESS"}, {0x8022, "SOFTWARE"}, {0x8023, "ALTERNATE_SERVER"},
+        {0x8025, "TRANSACTION_TRANSMIT_COUNTER"}, {0x8027, "CACHE_TIMEOUT"}, {0x8028, "FINGERPRINT"},
+        {0x8029, "ICE_CONTROLLED"}, {0x802A, "ICE_CONTROLLING"}, {0x802B, "RESPONSE_ORIGIN"}, {0x802C, "OTHER_ADDRESS"},
+        {0x802D, "ECN_CHECK_STUN"}, {0x802E, "THIRD_PARTY_AUTHORIZATION"}, {0x8030, "MOBILITY_TICKET"},
+        {0x8032, "MS_ALTERNATE_HOST_NAME"}, {0x8037, "MS_APP_ID"}, {0x8039, "MS_SECURE_TAG"},
+        {0x8050, "MS_SEQUENCE_NUMBER"}, {0x8055, "MS_SERVICE_QUALITY"}, {0x8056, "MS_BANDWIDTH_ADMISSION_CONTROL_MESSAGE"},
+        {0x8070, "MS_IMPLEMENTATION_VERSION"}, {0x8090, "MS_ALTERNATE_MAPPED_ADDRESS"},
+        {0x8095, "MS_MULTIPLEXED_TURN_SESSION_ID"}, {0xC000, "CISCO_STUN_FLOWDATA"}, {0xC001, "ENF_FLOW_DESCRIPTION"},
+        {0xC002, "ENF_NETWORK_STATUS"}, {0xC057, "GOOG_NETWORK_INFO"}, {0xC058, "GOOG_LAST_ICE_CHECK_RECEIVED"},
+        {0xC059, "GOOG_MISC_INFO"}, {0xC05A, "GOOG_OBSOLETE_1"}, {0xC05B, "GOOG_CONNECTION_ID"}, {0xC05C, "GOOG_DELTA"},
+        {0xC05D, "GOOG_DELTA_ACK"}, {0xC060, "GOOG_MESSAGE_INTEGRITY_32"},
+    };
+    for (const auto &x : tab) if (x.t == t) return x.n;
+    return nullptr;
+}
+// stun::method_usage / attribute_type_usage (stun.h:513-584): 1 stun, 2 turn, 4 ice
+unsigned stun_method_usage(unsigned m) { return m == 1 || m == 2 ? 1u : (m >= 3 && m <= 9 && m != 5) ? 2u : 0u; }
+unsigned stun_attr_usage(unsigned t) {
+    switch (t) {
+    case 0x0001: case 0x0002: case 0x0003: case 0x0004: case 0x0005: case 0x0006: case 0x0007: case 0x0008:
+    case 0x0009: case 0x000A: case 0x000B: case 0x0010: case 0x0014: case 0x0015: case 0x001C: case 0x001D:
+    case 0x001E: case 0x0020: case 0x8002: case 0x8003: case 0x8022: case 0x8023: case 0x8028: return 1;
+    case 0x000C: case 0x000D: case 0x0012: case 0x0013: case 0x0016: case 0x0017: case 0x0018: case 0x0019:
+    case 0x001A: case 0x0021: case 0x0022: case 0x8000: case 0x8001: case 0x8004: return 2;
+    case 0x0024: case 0x0025: case 0x8029: case 0x802A: return 4;
+    }
+    return 0;
+}
+// stun::attribute (stun.h:323-338): false (cursor null) when incomplete
+bool stun_attr(HC &d, unsigned &t, HC &v) {
+    t = (unsigned)hrd(d, 2);
+    const long l = (long)hrd(d, 2);
+    v = hparse(d, d.d ? l : 0);
+    const long pad = (4 - (l & 3)) & 3;
+    if (d.d) { if (hlen(d) < pad) hnull(d); else d.d += pad; }
+    return d.d != nullptr;
+}
+void unknown_code(W &w, uint64_t v, int digits) { w.puts("\"UNKNOWN ("); w.hexu(v, digits); w.puts(")\""); }
+
+// stun::message::write_json (stun.h:795-826) with attribute::write_json (stun.h:340-439)
+void write_stun(W &w, const uint8_t *m, size_t len) {
+    const unsigned mtf = (unsigned)m[0] << 8 | m[1], ml = (unsigned)m[2] << 8 | m[3];
+    const bool cookie = m[4] == 0x21 && m[5] == 0x12 && m[6] == 0xa4 && m[7] == 0x42;
+    w.puts("{");
+    Obj o{w};
+    if (ml % 4) { o.key("malformed"); w.puts("true"); }
+    const unsigned method = (mtf & 0x0f) | ((mtf & 0xe0) >> 1) | ((mtf & 0x3e00) >> 2);
+    o.key("method");
+    if (const char *n = stun_method_name(method)) { w.put('"'); w.putz(n); w.put('"'); } else unknown_code(w, method, 4);
+    o.key("class");
+    switch (mtf & 0x0110) {
+    case 0x0000: w.puts("\"request\""); break;
+    case 0x0010: w.puts("\"indication\""); break;
+    case 0x0100: w.puts("\"success_resp\""); break;
+    default: w.puts("\"err_resp\""); break;
+    }
+    o.key("message_length"); w.udec(ml);
+    o.key("transaction_id"); w.put('"'); w.hexb(m + (cookie ? 8 : 4), cookie ? 12 : 16); w.put('"');
+    o.key("magic_cookie"); if (cookie) w.puts("true"); else w.puts("false");
+    o.key("attributes"); w.put('[');
+    unsigned usage = stun_method_usage(method);
+    HC tmp{m + 20, m + len};
+    bool first = true;
+    while (hlen(tmp) > 0) {
+        HC la = tmp, v; unsigned t;
+        if (!first) w.put(',');
+        first = false;
+        if (!stun_attr(la, t, v)) {
+            w.puts("{\"unparseable\":\""); w.hexb(tmp.d, (size_t)hlen(tmp)); w.puts("\"}");
+            break;
+        }
+        w.put('{');
+        Obj a{w};
+        a.key("type");
+        if (const char *n = stun_attr_name(t)) { w.put('"'); w.putz(n); w.put('"'); } else unknown_code(w, t, 4);
+        a.key("length"); w.udec((uint64_t)hlen(v));
+        auto addr = [&](bool x) {                    // mapped_address / xor_mapped_address (stun.h:61-166)
+            HC d = v;
+            hrd(d, 1);
+            const unsigned fam = (unsigned)hrd(d, 1), port = (unsigned)hrd(d, 2);
+            HC ad = hparse(d, fam == 2 ? 16 : 4);
+            if (!d.d || !(ad.d && ad.d < ad.e)) return;       // lookahead failed / !valid()
+            a.key("family"); w.put('"'); w.putz(fam == 1 ? "ipv4" : fam == 2 ? "ipv6" : "UNKNOWN"); w.put('"');
+            if (!x) {
+                a.key("port"); w.udec(port);
+                if (fam == 1) { if (hlen(ad) == 4) { a.key("address"); w.put('"'); w.ipv4(ad.d); w.put('"'); } }
+                else if (fam == 2) { if (hlen(ad) == 16) { a.key("address"); w.put('"'); w.ipv6(ad.d); w.put('"'); } }
+                else { a.key("address"); w.puts("\"malformed\""); }
+            } else {
+                a.key("x_port"); w.udec((port ^ 0x2112u) & 0xffff);
+                if (fam == 1) {
+                    const uint32_t xa = ((uint32_t)ad.d[0] << 24 | (uint32_t)ad.d[1] << 16 | (uint32_t)ad.d[2] << 8 | ad.d[3]) ^
+                                        0x2112a442u;
+                    const uint8_t b[4] = {(uint8_t)(xa >> 24), (uint8_t)(xa >> 16), (uint8_t)(xa >> 8), (uint8_t)xa};
+                    a.key("x_address"); w.put('"'); w.ipv4(b); w.put('"');
+                } else {
+                    a.key("x_address"); w.put('"'); w.hexb(ad.d, (size_t)hlen(ad)); w.put('"');
+                }
+            }
+        };
+        auto u32 = [&](const char *k) {
+            HC d = v; const uint64_t x = hrd(d, 4);
+            if (d.d) { w.put(','); w.put('"'); w.putz(k); w.puts("\":"); w.udec(x); }
+        };
+        switch (t) {
+        case 0x0025: break;                                            // USE_CANDIDATE
+        case 0x0001: case 0x0002: case 0x0004: case 0x0005: case 0x000B: case 0x8023: case 0x802B: case 0x802C:
+            addr(false); break;
+        case 0x0020: case 0x0012: case 0x0016: addr(true); break;
+        case 0x8022: case 0x0006: case 0x0015:                         // utf8_string
+            if (v.d) { a.key("value"); w.put('"'); w.utf8(v.d, (size_t)hlen(v)); w.put('"'); }
+            break;
+        case 0x0009: {                                                 // error_code
+            HC d = v; const uint64_t rc = hrd(d, 4);
+            if (d.d) {
+                a.key("class"); w.udec((rc >> 8) & 7);
+                a.key("number"); w.udec(rc & 0xff);
+                if (hlen(d) > 0) { a.key("reason_phrase"); w.put('"'); w.utf8(d.d, (size_t)hlen(d)); w.put('"'); }
+            }
+            break;
+        }
+        case 0x0024: u32("priority"); break;
+        case 0x8029: case 0x802A: {
+            HC d = v; const uint64_t x = hrd(d, 8);
+            if (d.d) { a.key("tiebreaker"); w.put('"'); w.hexu(x, 16); w.put('"'); }
+            break;
+        }
+        case 0x000C: {
+            HC d = v; const uint64_t x = hrd(d, 2); hrd(d, 2);
+            if (d.d) { a.key("channel_number"); w.udec(x); }
+            break;
+        }
+        case 0x000D: u32("seconds"); break;
+        case 0x0010: u32("kbps"); break;
+        case 0x0019: {
+            HC d = v; const uint64_t x = hrd(d, 1); hparse(d, 3);
+            if (d.d) { a.key("protocol"); w.udec(x); }
+            break;
+        }
+        case 0x8056: {
+            HC d = v; hparse(d, 2); const unsigned x = (unsigned)hrd(d, 2);
+            if (d.d) {
+                a.key("message_type");
+                if (x <= 2) { w.put('"'); w.putz(x == 0 ? "reservation_check" : x == 1 ? "reservation_commit" : "reservation_update"); w.put('"'); }
+                else unknown_code(w, x, 4);
+            }
+            break;
+        }
+        case 0x8070: u32("number"); break;
+        default:
+            a.key("hex_value"); w.put('"'); if (v.d && v.e > v.d) w.hexb(v.d, (size_t)hlen(v)); w.put('"');
+        }
+        w.put('}');
+        usage |= stun_attr_usage(t);
+        tmp = la;
+    }
+    w.put(']');
+    o.key("usage");
+    w.put('"'); w.putz(usage == 1 ? "stun" : (usage == 2 || usage == 3) ? "turn" : (usage == 4 || usage == 5) ? "ice" : "unknown");
+    w.put('"');
+    w.put('}');
+}
+
+// openvpn_tcp::write_json (openvpn.h:411-442) + tls_client_hello::write_json
+// (tls.h:1882-1917, metadata off); false when the hello carries QUIC
+// transport parameters (printed by the reference, not rebuilt here)
+bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
+    struct R { unsigned op, replay, nid, msg; bool ctrl; };
+    std::vector<R> ctrl, ack;
+    uint8_t buf[800];
+    size_t used = 0;
+    bool buf_null = false;
+    uint64_t total = 0;
+    unsigned nrec = 0;
+    HC d{m, m + len};
+    while (hlen(d) > 0) {                                   // openvpn_tcp_record / openvpn_payload
+        const unsigned plen = (unsigned)hrd(d, 2), code = (unsigned)hrd(d, 1);
+        const unsigned op = code >> 3;
+        const int type = (op >= 1 && op <= 4) || op == 7 || op == 8 || op == 10 || op == 11 ? 1 : op == 5 ? 0
+                         : (op == 6 || op == 9) ? 2 : 3;
+        R r{op, 0, 0, 0, type == 1};
+        hrd(d, 8);
+        uint64_t hm = 0;
+        { HC la = d; hm = hrd(la, 4); }
+        unsigned zeros = 0;
+        for (int k = 0; k < 4; k++) zeros += ((hm >> (8 * k)) & 0xff) == 0;
+        unsigned hmac_len = 0;
+        if (zeros <= 1) {
+            if (hlen(d) < 16) return true;                  // invalid record: no object (valid stays false)
+            long at = 0, z = 0;
+            const long dl = hlen(d);
+            while (z < 2 && at < dl) { z = d.d[at] == 0 ? z + 1 : 0; at++; }
+            const unsigned hl = (unsigned)(uint8_t)((z == 2 ? at : -at) - 2);
+            if (hl < 16 || (long)hl >= hlen(d)) return true;
+            hmac_len = hl;
+            d.d += hl;
+        }
+        r.replay = (unsigned)hrd(d, 4);
+        bool net_time = false;
+        { HC dc = d; const unsigned b1 = (unsigned)hrd(dc, 1), b2 = (unsigned)hrd(dc, 1); if ((long)b1 * 4 > hlen(dc) || b2) net_time = true; }
+        if (net_time) hrd(d, 4);
+        r.nid = (unsigned)hrd(d, 1);
+        if (hlen(d) < 4 * (long)r.nid) return true;
+        if (r.nid) { hparse(d, 4 * (long)r.nid); hrd(d, 8); }
+        if (r.ctrl) r.msg = (unsigned)hrd(d, 4);
+        const unsigned hdr = 1 + 8 + hmac_len + 4 + (net_time ? 4 : 0) + 1 + 4 * r.nid + (r.nid ? 8 : 0) + (r.ctrl ? 4 : 0);
+        if (op == 4) {
+            if (hdr >= plen) return true;
+            const long dl = (long)((plen - hdr) & 0xffff);
+            if (hlen(d) < dl) return true;
+            if (!buf_null) {
+                if (used + (size_t)dl > sizeof buf) buf_null = true;
+                else { memcpy(buf + used, d.d, (size_t)dl); used += (size_t)dl; }
+            }
+            total += (uint64_t)dl;
+            d.d += dl;
+        }
+        if (!d.d || type == 3) return true;                 // the packet has no record
+        if (type == 0) ack.push_back(r); else if (type == 1) ctrl.push_back(r);
+        nrec++;
+    }
+    if ((uint8_t)nrec == 0) return true;
+    // the ClientHello: tls_record -> tls_handshake -> tls_client_hello
+    HC ext{nullptr, nullptr};
+    bool hello = false, ciphers = false;
+    if (!ctrl.empty() && !buf_null && used) {
+        // tls_record::parse tls.h:153 / tls_handshake::parse tls.h:244 (outer-bounded),
+        // tls_client_hello::parse tls.h:1811
+        auto outer = [](HC &r, uint64_t n) {
+            HC o{nullptr, nullptr};
+            if (!(r.d && r.d < r.e)) return o;
+            o.d = r.d; o.e = n > (uint64_t)(r.e - r.d) ? r.e : r.d + n; r.d = o.e;
+            return o;
+        };
+        HC p{buf, buf + used}, frag{nullptr, nullptr}, body{nullptr, nullptr};
+        if (hlen(p) >= 5) { hrd(p, 1); hrd(p, 2); frag = outer(p, hrd(p, 2)); }
+        if (hlen(frag) >= 4) { hrd(frag, 1); const uint64_t hl = hrd(frag, 3); if (hl <= 32768) body = outer(frag, hl); }
+        HC b = body;
+        HC ver = hparse(b, 2);
+        if (ver.d && ver.e > ver.d) {
+            const bool dtls = ver.d[0] == 0xfe;
+            hparse(b, 32);
+            bool ok = true;
+            if (!b.d || hlen(b) < 1) ok = false;
+            if (ok) { const long sl = (long)hrd(b, 1); hparse(b, sl); }
+            if (ok && dtls) {
+                if (hlen(b) < 1) ok = false;
+                else { const long cl0 = b.d[0]; if (cl0 + 1 > hlen(b)) { b.d = b.e; ok = false; } else b.d += cl0 + 1; }
+            }
+            if (ok && hlen(b) < 2) ok = false;
+            long cl = 0;
+            if (ok) { cl = (long)hrd(b, 2); if (cl & 1) ok = false; }
+            HC cs{nullptr, nullptr}, cm{nullptr, nullptr};
+            if (ok) { cs = hparse(b, cl); if (hlen(b) < 1) ok = false; }
+            if (ok) { const long ml = (long)hrd(b, 1); cm = hparse(b, ml); }
+            ciphers = cs.d && cs.e > cs.d;
+            hello = cm.d && cm.e > cm.d;
+            if (ok && hlen(b) >= 2) { const long el = (long)hrd(b, 2); ext.d = b.d; ext.e = b.d + std::min(el, hlen(b)); }
+        }
+    }
+    rec.key("openvpn");
+    w.put('{');
+    Obj o{w};
+    o.key("num_records"); w.udec((uint8_t)nrec);
+    o.key("records"); w.put('[');
+    bool first = true;
+    static const char *names[12] = {nullptr, "P_CONTROL_HARD_RESET_CLIENT_V1", "P_CONTROL_HARD_RESET_SERVER_V1",
+                                    "P_CONTROL_SOFT_RESET_V1", "P_CONTROL_V1", "P_ACK_V1", "P_DATA_V1",
+                                    "P_CONTROL_HARD_RESET_CLIENT_V2", "P_CONTROL_HARD_RESET_SERVER_V2", "P_DATA_V2",
+                                    "P_CONTROL_HARD_RESET_CLIENT_V3", "P_CONTROL_WKC_V1"};
+    for (int pass = 0; pass < 2; pass++)
+        for (const R &r : pass ? ack : ctrl) {
+            if (!first) w.put(',');
+            first = false;
+            w.puts("{\"opcode\":\""); w.putz(names[r.op]); w.puts("\",\"replay_pkt_id\":"); w.udec(r.replay);
+            w.puts(",\"id_array_len\":"); w.udec(r.nid);
+            if (r.ctrl) { w.puts(",\"msg_pkt_id\":"); w.udec(r.msg); }
+            w.put('}');
+        }
+    w.put(']');
+    if (total) { o.key("data_len"); w.udec(total); }
+    if (hello) { o.key("has_tls"); w.puts("true"); }
+    w.put('}');
+    if (hello && ciphers) {
+        // extensions: the first server_name, and no QUIC transport parameters
+        HC sn{nullptr, nullptr};
+        HC e = ext;
+        while (hlen(e) > 0) {
+            const uint8_t *st = e.d;
+            const unsigned t = (unsigned)hrd(e, 2);
+            const long l = (long)hrd(e, 2);
+            if (!e.d || l > hlen(e)) break;
+            e.d += l;
+            if (t == 0 && !sn.d) { sn.d = st + 9 < e.d ? st + 9 : e.d; sn.e = e.d; }
+            if (t == 0x39 || t == 0xffa5) return false;
+        }
+        rec.key("tls");
+        w.puts("{\"client\":{");
+        if (sn.d && sn.e > sn.d) { w.puts("\"server_name\":\""); w.utf8(sn.d, (size_t)(sn.e - sn.d)); w.put('"'); }
+        w.puts("}}");
+    }
+    return true;
+}
+
 // tcp_reassembler::write_json (reassembly.hpp:860-880) from the props bits of
 // mfp_process_batch_reassembly
 void write_reassembled(W &w, uint16_t props) {
@@ -357,9 +705,7 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     // QUIC records carry a "quic" object with the decrypted payload
     // (quic_init::write_json quic.h:1662-1690), which the device does not return
     if (r.msg == MFP_MSG_QUIC) return false;
-    // STUN and OpenVPN records carry "stun" / "openvpn" objects (stun.h:795-826,
-    // openvpn.h:411-442) that are not rebuilt here yet
-    if (r.msg == MFP_MSG_STUN || r.msg == MFP_MSG_OPENVPN) return false;
+
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
     // IP-in-IP: outer headers sit back to back before the inner one (IPv4
     // fixed 20 B, ip.h:124-137; IPv6 40 B when it has no extension headers)
@@ -380,7 +726,9 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     // worst case: fixed keys/addresses/numbers and 4 encapsulations < 1000 B, the fp string, and at most
     // 6 output bytes per input byte of a JSON string ("\\ufffd") or a base64 cert list
     const bool with_an = ctx && an && (an->flags & MFP_AN_VALID);
-    o.need(1000 + (size_t)r.fp_len + 6 * ((r.sni_len == 0xffff ? 0 : r.sni_len) + (r.ua_len == 0xffff ? 0 : r.ua_len)) +
+    const size_t sni_x = r.msg == MFP_MSG_STUN ? 32 : r.msg == MFP_MSG_OPENVPN ? 16 : 6;   // object text per input byte
+    o.need(1000 + (size_t)r.fp_len + sni_x * (r.sni_len == 0xffff ? 0 : r.sni_len) +
+           6 * (r.ua_len == 0xffff ? 0 : r.ua_len) +
            (with_an ? analysis_bound(ctx, *an) : 0));
     W w{o.buf.get() + o.len};
     // a readable, non-empty datum (print_key_json_string skips empty ones, json_object.h:104-108)
@@ -430,6 +778,12 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     case MFP_MSG_DTLS_SH:                                // write_metadata pkt_proc_util.h:315-321
         rec.key("dtls");
         w.puts("{\"server\":{}}");
+        break;
+    case MFP_MSG_STUN:                                   // stun::message::write_json (stun.h:795)
+        if (span_ok(r.sni_off, r.sni_len) && r.sni_len >= 20) { rec.key("stun"); write_stun(w, pkt + r.sni_off, r.sni_len); }
+        break;
+    case MFP_MSG_OPENVPN:                                // openvpn_tcp::write_json (openvpn.h:411)
+        if (span_ok(r.sni_off, r.sni_len) && !write_openvpn(w, rec, pkt + r.sni_off, r.sni_len)) return false;
         break;
     case MFP_MSG_HTTP_REQ:
         rec.key("http");

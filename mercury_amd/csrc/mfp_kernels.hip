@@ -571,6 +571,7 @@ __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, ui
             e.plan = &plan;
             Cfg c = P.cfg;
             c.classify = 1;
+            c.seg = 0;
             packet_walk(e, c, o, (const uint8_t *)&win[tid][0] + sh, take, dsc.linktype);
             bin = msg_bin(o.msg);
             cls[i] = (uint8_t)bin;
@@ -641,6 +642,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     if (n == 0) return 0;
     mfp::KParams P;
     P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0;
+    P.cfg.seg = seg ? 1u : 0u;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
     P.seg = seg;

@@ -13,6 +13,7 @@ Outputs (committed):
                            tests/stun_ovpn_synth.py and 3000 mutations of them
   stun_ovpn_fp_<cfg>.tsv.gz reference output per packet (write_json path):
                            idx, emit, fp_type, truncated, fingerprint
+  stun_ovpn_json_<cfg>.txt.gz the write_json text per packet (so, mix)
   stun_ovpn_an.tsv.gz      reference analysis_context path with
                            stun_resources.tgz (a synthetic archive in the
                            reference format with stun/1 entries)
@@ -116,6 +117,10 @@ def main():
         out = ref("fp", tmp, cfg)
         with gzip.open(os.path.join(HERE, f"stun_ovpn_fp_{key}.tsv.gz"), "wb") as f:
             f.write(out)
+        if key in ("so", "mix"):                      # the write_json text
+            js = ref("json", tmp, cfg).decode("latin-1").split("\n")[:len(desc)]
+            with gzip.open(os.path.join(HERE, f"stun_ovpn_json_{key}.txt.gz"), "wt", encoding="latin-1") as f:
+                f.write("\n".join(js) + "\n")
         rows = [l.split(b"\t") for l in out.splitlines()]
         counts[key] = {"emit": sum(int(r[1]) for r in rows), "stun_fp": sum(r[2] == b"16" for r in rows),
                        "openvpn_fp": sum(r[2] == b"14" for r in rows), "truncated": sum(int(r[3]) for r in rows)}

@@ -123,3 +123,22 @@ def test_stun_analysis_vs_reference():
     bad = test_analysis.compare(ref, rec, an, names)
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
     assert sum(r["status"] == 1 for r in ref) == MANIFEST["counts"]["an"]["labeled"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["so", "mix"])
+def test_stun_ovpn_json_vs_reference(key):
+    """The "stun" objects (attributes, addresses, usage) and "openvpn" objects
+    (records, data length, the ClientHello's "tls" object) rebuilt by the host
+    JSON writer from the records equal the reference's write_json text."""
+    from tests import test_json
+    arena, desc, sources = load()
+    ctx = mercury_amd.Context(MANIFEST["configs"][key], device=0)
+    try:
+        rec, fp = ctx.process_host(arena, desc)
+    finally:
+        ctx.close()
+    lines, skipped = mercury_amd.write_json(arena, desc, rec, fp, ts_ns=np.full(len(desc), test_json.TS, np.uint64),
+                                            threads=4)
+    gold = test_json._golden_lines(f"stun_ovpn_json_{key}.txt.gz")
+    test_json._check(lines, gold, skipped, allow_skip=True)
