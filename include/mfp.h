@@ -161,11 +161,16 @@ typedef struct mfp_context_s *mfp_context;
  * tls.client_hello, tls.server_hello, tls.server_certificate, ssh,
  * ssh.client, ssh.server, http, http.request, http.response, tcp,
  * tcp.syn_ack, dtls, quic (QUIC Initial packets: decrypted and fingerprinted
- * on the device), gre, vxlan, geneve (decapsulation, pkt_proc.cc:959-1049);
- * "format=" takes tls/N and quic/N.  ""/"all" (the reference's
- * ~45 protocols) are refused.  Returns NULL on error (unknown protocol, no HIP
+ * on the device), stun, openvpn_tcp, gre, vxlan, geneve (decapsulation,
+ * pkt_proc.cc:959-1049); "format=" takes tls/N and quic/N; "reassembly"
+ * enables mfp_process_batch_reassembly.  ""/"all" (the reference's ~45
+ * protocols) are refused.  Returns NULL on error (unknown protocol, no HIP
  * device, extension not loadable). */
 MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode);
+/* mfp_init with the resource archive's decryption key (libmerc_config.enc_key,
+ * libmerc.h:124-125): 16 bytes, AES-128-CBC with the IV as the file's first
+ * block (encrypted_file enc_file_reader.h:86-231); NULL or all zero = plain. */
+MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int device, int mode, const uint8_t *enc_key);
 MFP_EXPORT void mfp_finalize(mfp_context ctx);
 
 /* Device-resident batch: all pointers are device (HBM) pointers.  The fp
@@ -380,6 +385,7 @@ MFP_EXPORT uint64_t mfp_analysis_device_bytes(mfp_context ctx);
  * processes, feature updates, known-prevalence, asn prefixes, disabled,
  * distinct process names} */
 MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]);
+MFP_EXPORT int mfp_resource_stats_ex(const char *path, const uint8_t *enc_key, uint64_t out[8]);   /* keyed archive */
 
 /* host only (tests): server_identifier::get_normalized_domain_name (the
  * normalisation the device applies to server names); returns the length */

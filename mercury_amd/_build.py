@@ -40,7 +40,7 @@ def build(verbose=False):
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)
     if _newer(LIB, objs):
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lz"]
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lcrypto"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -71,6 +71,10 @@ def load_library():
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     lib.mfp_init.restype = vp
     lib.mfp_init.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    lib.mfp_init_ex.restype = vp
+    lib.mfp_init_ex.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+    lib.mfp_resource_stats_ex.restype = ctypes.c_int
+    lib.mfp_resource_stats_ex.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
     lib.mfp_finalize.argtypes = [vp]
     lib.mfp_process_batch_device.restype = ctypes.c_int
     lib.mfp_process_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, sz, vp, vp]
@@ -189,9 +193,11 @@ class Context:
     """One device context (the analogue of libmerc's mercury_context plus a
     processor).  `config` uses the reference's packet_filter_cfg syntax."""
 
-    def __init__(self, config="tls,dtls,ssh,http,tcp,tcp.syn_ack", device=0, mode=MODE_WRITE_JSON):
+    def __init__(self, config="tls,dtls,ssh,http,tcp,tcp.syn_ack", device=0, mode=MODE_WRITE_JSON, enc_key=None):
+        """enc_key: the 16-byte key of an encrypted resource archive (libmerc_config.enc_key)."""
         self.lib = load_library()
-        self.h = self.lib.mfp_init(config.encode() if config is not None else None, device, mode)
+        key = None if enc_key is None else ctypes.create_string_buffer(bytes(enc_key), 16)
+        self.h = self.lib.mfp_init_ex(config.encode() if config is not None else None, device, mode, key)
         if not self.h:
             raise MercuryAmdError("mfp_init failed: " + _err(self.lib))
 
@@ -510,11 +516,13 @@ class Prevalence:
         return True
 
 
-def resource_stats(path):
-    """Host-only load of a resource archive: {fingerprints, entries, processes, updates, ...}."""
+def resource_stats(path, enc_key=None):
+    """Host-only load of a resource archive (enc_key: 16-byte key of an
+    encrypted one): {fingerprints, entries, processes, updates, ...}."""
     lib = load_library()
     out = (ctypes.c_uint64 * 8)()
-    if lib.mfp_resource_stats(path.encode(), out) != 0:
+    key = None if enc_key is None else ctypes.create_string_buffer(bytes(enc_key), 16)
+    if lib.mfp_resource_stats_ex(path.encode(), key, out) != 0:
         raise MercuryAmdError(_err(lib))
     keys = ["fingerprints", "entries", "processes", "updates", "known_prevalence", "asn_prefixes", "disabled",
             "process_names"]

@@ -100,7 +100,7 @@ struct mfp_classifier_dev {
 
 typedef struct mfp_classifier_s mfp_classifier;
 
-mfp_classifier *mfp_classifier_load(const char *path);
+mfp_classifier *mfp_classifier_load(const char *path, const uint8_t *enc_key = nullptr);
 int mfp_classifier_upload(mfp_classifier *c, int device);
 void mfp_classifier_free(mfp_classifier *c);
 void mfp_classifier_free_device(mfp_classifier_dev &d);

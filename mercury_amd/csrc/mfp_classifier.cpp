@@ -18,6 +18,7 @@
 // The loader runs once per context; the per-packet work is on the device.
 #include <hip/hip_runtime.h>
 #include <zlib.h>
+#include <openssl/evp.h>
 
 #include <algorithm>
 #include <cmath>
@@ -158,16 +159,68 @@ bool parse_json(const std::string &line, JV &out) {
 // ---------------------------------------------------------------------------
 // .tgz reader (gzip via zlib, ustar headers): calls f(name, contents)
 // ---------------------------------------------------------------------------
-template <class F>
-bool read_tgz(const char *path, F f) {
-    gzFile gz = gzopen(path, "rb");
-    if (!gz) return false;
-    std::string all;
+// encrypted_file (enc_file_reader.h:86-231): AES-128-CBC under the 16-byte
+// key with a zero IV; the file's first block is the real IV, so the first
+// plaintext block is discarded; PKCS#7 padding checked by the final block
+bool decrypt_archive(const char *path, const uint8_t *key, std::string &out) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return false;
+    std::string ct;
+    char buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof buf, fp)) > 0) ct.append(buf, r);
+    fclose(fp);
+    EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
+    if (!ctx) return false;
+    const uint8_t iv[16] = {0};
+    out.resize(ct.size() + 32);
+    int n1 = 0, n2 = 0;
+    bool ok = EVP_DecryptInit_ex(ctx, EVP_aes_128_cbc(), nullptr, key, iv) == 1 &&
+              EVP_DecryptUpdate(ctx, (unsigned char *)&out[0], &n1, (const unsigned char *)ct.data(), (int)ct.size()) == 1 &&
+              EVP_DecryptFinal_ex(ctx, (unsigned char *)&out[0] + n1, &n2) == 1;
+    EVP_CIPHER_CTX_free(ctx);
+    if (!ok || n1 + n2 < 16) return false;
+    out.resize((size_t)(n1 + n2));
+    out.erase(0, 16);
+    return true;
+}
+
+// gzip stream in memory -> bytes
+bool gunzip(const std::string &in, std::string &out) {
+    z_stream z{};
+    if (inflateInit2(&z, 16 + MAX_WBITS) != Z_OK) return false;
+    z.next_in = (Bytef *)in.data();
+    z.avail_in = (uInt)in.size();
     char buf[1 << 16];
     int r;
-    while ((r = gzread(gz, buf, sizeof buf)) > 0) all.append(buf, r);
-    gzclose(gz);
-    if (r < 0) return false;
+    do {
+        z.next_out = (Bytef *)buf;
+        z.avail_out = sizeof buf;
+        r = inflate(&z, Z_NO_FLUSH);
+        if (r != Z_OK && r != Z_STREAM_END) { inflateEnd(&z); return false; }
+        out.append(buf, sizeof buf - z.avail_out);
+    } while (r != Z_STREAM_END && (z.avail_in > 0 || z.avail_out == 0));
+    inflateEnd(&z);
+    return r == Z_STREAM_END;
+}
+
+template <class F>
+bool read_tgz(const char *path, F f, const uint8_t *key = nullptr) {
+    std::string all;
+    bool keyed = false;
+    if (key) for (int k = 0; k < 16; k++) keyed |= key[k] != 0;   // cryptovar::is_null: plain file
+    if (keyed) {
+        std::string gz;
+        if (!decrypt_archive(path, key, gz) || !gunzip(gz, all)) return false;
+    } else {
+        gzFile gz = gzopen(path, "rb");
+        if (!gz) return false;
+        char buf[1 << 16];
+        int r;
+        while ((r = gzread(gz, buf, sizeof buf)) > 0) all.append(buf, r);
+        gzclose(gz);
+        if (r < 0) return false;
+    }
     size_t off = 0;
     std::string longname;
     while (off + 512 <= all.size()) {
@@ -663,7 +716,7 @@ void build_domain_prefixes(mfp_classifier_s &c) {
 // ---------------------------------------------------------------------------
 // C++ API used by mfp_host.cpp
 // ---------------------------------------------------------------------------
-mfp_classifier *mfp_classifier_load(const char *path) {
+mfp_classifier *mfp_classifier_load(const char *path, const uint8_t *enc_key) {
     auto c = std::make_unique<mfp_classifier_s>();
     for (const char *a : kReservedAttrs) attr_index(*c, a);
     bool got_db = false, got_prev = false, got_ver = false, got_asn = false;
@@ -694,7 +747,7 @@ mfp_classifier *mfp_classifier_load(const char *path) {
                 for_lines(data, [&](const std::string &l) { process_domain_line(*c, l); });
                 c->faking_enabled = true;
             }
-        });
+        }, enc_key);
         if (!ok) { mfp_set_error("cannot read resource archive %s", path); return nullptr; }
         c->fp_types.push_back(1);   // tls is always expected (analysis.h:833)
         bool dual = c->version.find("dual") != std::string::npos, lite = c->version.find("lite") != std::string::npos,

@@ -335,6 +335,11 @@ struct mfp_context_s {
     } while (0)
 
 extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode) {
+    return mfp_init_ex(packet_filter_cfg, device, mode, nullptr);
+}
+
+extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int device, int mode,
+                                               const uint8_t *enc_key) {
     uint32_t sel, fmt;
     std::string resources;
     bool analysis = false, reassembly = false;
@@ -381,7 +386,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
         // mercury ctor (pkt_proc.h:76-110): load the archive, force the TLS
         // fingerprint format to the database's, keep parsing if the
         // classifier is disabled
-        mfp_classifier *clf = mfp_classifier_load(resources.c_str());
+        mfp_classifier *clf = mfp_classifier_load(resources.c_str(), enc_key);
         if (!clf) { mfp_finalize(c); return nullptr; }
         // the formats follow the archive even when its classifier is then
         // disabled (missing members, VERSION qualifiers): pkt_proc.h:92-104
@@ -987,7 +992,11 @@ extern "C" MFP_EXPORT uint64_t mfp_analysis_device_bytes(mfp_context c) {
 
 // host-only: load a resource archive and report its size (no device needed)
 extern "C" MFP_EXPORT int mfp_resource_stats(const char *path, uint64_t out[8]) {
-    mfp_classifier *clf = mfp_classifier_load(path);
+    return mfp_resource_stats_ex(path, nullptr, out);
+}
+
+extern "C" MFP_EXPORT int mfp_resource_stats_ex(const char *path, const uint8_t *enc_key, uint64_t out[8]) {
+    mfp_classifier *clf = mfp_classifier_load(path, enc_key);
     if (!clf) return -1;
     mfp_classifier_stats(clf, out);
     mfp_classifier_free(clf);

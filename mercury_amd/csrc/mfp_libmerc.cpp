@@ -25,6 +25,8 @@ struct mercury {
     // one fingerprint_prevalence for the mercury context (the reference's
     // classifier owns one, shared by every processor and entry point)
     mfp_prevalence prev = nullptr;
+    uint8_t enc_key[16] = {0};    // libmerc_config.enc_key (encrypted resource archive)
+    bool keyed = false;
 };
 
 struct analysis_context {       // the fields libmerc's accessors read (result.h:174-420)
@@ -72,11 +74,10 @@ MFP_EXPORT void register_printf_err_callback(printf_err_ptr callback) { g_printf
 MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int verbosity) {
     (void)verbosity;
     if (!vars) return nullptr;
-    if (vars->enc_key || vars->key_type != enc_key_type_none) {
-        log_error("encrypted resource archives are not supported by the MI355X path\n");
-        return nullptr;
-    }
     auto *m = new mercury;
+    // the archive key: 16 bytes whatever key_type says (analysis.h:1211,
+    // "TODO: key type"; cryptovar<16>)
+    if (vars->enc_key) { memcpy(m->enc_key, vars->enc_key, 16); m->keyed = true; }
     std::string filt = vars->packet_filter_cfg ? vars->packet_filter_cfg : "";
     // global_config.h:148-152: "key=value;..." only when the string holds ';'
     // a bare list stays bare (mfp_init parses it the same way); key=value options are added in the ';' form
@@ -109,7 +110,7 @@ MFP_EXPORT int mercury_finalize(mercury_context mc) {
 static mfp_context get_ctx(mercury *m, int mode) {
     std::lock_guard<std::mutex> lk(m->mu);
     if (!m->ctx[mode]) {
-        mfp_context c = mfp_init(m->cfg.c_str(), 0, mode);
+        mfp_context c = mfp_init_ex(m->cfg.c_str(), 0, mode, m->keyed ? m->enc_key : nullptr);
         if (!c) { log_error("%s\n", mfp_last_error()); return nullptr; }
         if (mfp_analysis_enabled(c)) {
             if (!m->prev) m->prev = mfp_prevalence_create(100000);   // analysis.h:433

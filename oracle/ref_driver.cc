@@ -19,7 +19,8 @@
 // (prob %.17Lg, set tags only), os_info: name=prevalence;... from
 // analysis_context_get_os_info, alpn: hex of analysis_context_get_alpns
 // (first min(len, 128) bytes) and ":len".
-// Environment: MERC_REPORT_OS=1 sets libmerc_config.report_os.
+// Environment: MERC_REPORT_OS=1 sets libmerc_config.report_os; MERC_ENC_KEY=<32
+// hex digits> sets libmerc_config.enc_key (an encrypted resource archive).
 // Mode "time": run write_json (or, with a trailing "an", the analysis_context
 // entry) with T threads (one processor per thread over contiguous shards),
 // print packets/s.
@@ -120,6 +121,13 @@ int main(int argc, char **argv) {
         res = argv[4];
         cfg.resources = (char *)res.c_str();
         cfg.do_analysis = true;
+    }
+    static uint8_t key[16];
+    const char *ek = getenv("MERC_ENC_KEY");
+    if (ek && strlen(ek) == 32) {
+        for (int k = 0; k < 16; k++) { unsigned v = 0; sscanf(ek + 2 * k, "%2x", &v); key[k] = (uint8_t)v; }
+        cfg.enc_key = key;
+        cfg.key_type = enc_key_type_aes_128;
     }
     const char *ros = getenv("MERC_REPORT_OS");
     cfg.report_os = ros && ros[0] == '1';

@@ -104,9 +104,9 @@ def test_server_name_normalisation_reference_golden():
 # ---------------------------------------------------------------------------
 # GPU: per-packet parity with the reference's classifier
 # ---------------------------------------------------------------------------
-def run_analysis(arena, desc, resources):
+def run_analysis(arena, desc, resources, enc_key=None):
     cfg = f"select={SELECT};resources={os.path.join(GOLD, resources)};analysis"
-    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS, enc_key=enc_key)
     try:
         assert ctx.analysis_enabled
         rec, fp, an = ctx.process_host_analysis(arena, desc)
@@ -265,3 +265,30 @@ def test_pipelined_host_path_vs_reference(chunk):
         ctx3.close()
     assert mercury_amd.fingerprints(rec3, fp) == mercury_amd.fingerprints(rec1, fp1)
     assert (rec3["fp_type"] == rec1["fp_type"]).all() and (rec3["flags"] == rec1["flags"]).all()
+
+
+# ---------------------------------------------------------------------------
+# encrypted resource archives (encrypted_file enc_file_reader.h:86-231):
+# tests/golden/resources-test.tgz.enc is resources-test.tgz under AES-128-CBC
+# with key ENC_KEY, its first block the IV; the reference itself
+# (oracle/_ref/merc_ref_drv with MERC_ENC_KEY) gives identical results for it
+# and the plain archive on the reference packets
+# ---------------------------------------------------------------------------
+ENC_KEY = bytes.fromhex("00112233445566778899aabbccddeeff")
+
+
+def test_encrypted_archive_loads_like_plain():
+    plain = mercury_amd.resource_stats(os.path.join(GOLD, "resources-test.tgz"))
+    enc = mercury_amd.resource_stats(os.path.join(GOLD, "resources-test.tgz.enc"), enc_key=ENC_KEY)
+    assert enc == plain and enc["fingerprints"] > 0
+    with pytest.raises(mercury_amd.MercuryAmdError):            # wrong key: bad padding / not gzip
+        mercury_amd.resource_stats(os.path.join(GOLD, "resources-test.tgz.enc"), enc_key=bytes(range(1, 17)))
+
+
+@pytest.mark.gpu
+def test_analysis_encrypted_archive():
+    z = np.load(os.path.join(GOLD, "ref_packets.npz"))
+    ref = load_ref_an("an_ref.tsv.gz")
+    rec, fp, an, names, _ = run_analysis(z["arena"], z["desc"], "resources-test.tgz.enc", enc_key=ENC_KEY)
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
