@@ -253,7 +253,9 @@ struct Obj {
     }
 };
 
-bool is_tcp_msg(unsigned m) { return m != MFP_MSG_DTLS_CH && m != MFP_MSG_DTLS_SH && m != MFP_MSG_DTLS_HVR; }
+bool is_tcp_msg(unsigned m) {
+    return m != MFP_MSG_DTLS_CH && m != MFP_MSG_DTLS_SH && m != MFP_MSG_DTLS_HVR && m != MFP_MSG_QUIC && m != MFP_MSG_STUN;
+}
 
 // "%f" (json_object::print_key_float json_object.h:174-177)
 void put_float(W &w, double d) {
