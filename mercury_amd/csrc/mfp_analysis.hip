@@ -620,8 +620,8 @@ constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.
 #define MFP_AN_PL 16
 #endif
 #ifndef MFP_AN_MINW
-#define MFP_AN_MINW 3      // waves/SIMD: 4 spills 168 B/lane to scratch, 2 leaves latency exposed;
-#endif                     // 3 measured best on the SURVEY archive (profiles/r02u_ab_analyze_*)
+#define MFP_AN_MINW 4      // waves/SIMD: 4 spills 168 B/lane to scratch but hides more latency;
+#endif                     // at 50 M: 37.2 ms vs 39.4 (3), 2 is slower still (profiles/r02u_ab_*)
 constexpr uint32_t PL = MFP_AN_PL;   // phase L: fingerprints with at most PL processes, scored lane per packet
 constexpr int AW = 2;                // waves per k_analyze block (LDS: PL * 512 bytes of score rows per wave)
 

@@ -517,13 +517,13 @@ void write_stun(W &w, const uint8_t *m, size_t len) {
         }
         case 0x000D: u32("seconds"); break;
         case 0x0010: u32("kbps"); break;
-        case 0x0019: {
-            HC d = v; const uint64_t x = hrd(d, 1); hparse(d, 3);
+        case 0x0019: {                                                 // skip_bytes<3>: datum::skip clamps
+            HC d = v; const uint64_t x = hrd(d, 1); if (d.d) d.d = hlen(d) < 3 ? d.e : d.d + 3;
             if (d.d) { a.key("protocol"); w.udec(x); }
             break;
         }
         case 0x8056: {
-            HC d = v; hparse(d, 2); const unsigned x = (unsigned)hrd(d, 2);
+            HC d = v; if (d.d) d.d = hlen(d) < 2 ? d.e : d.d + 2; const unsigned x = (unsigned)hrd(d, 2);
             if (d.d) {
                 a.key("message_type");
                 if (x <= 2) { w.put('"'); w.putz(x == 0 ? "reservation_check" : x == 1 ? "reservation_commit" : "reservation_update"); w.put('"'); }
@@ -593,11 +593,14 @@ bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
             if (hdr >= plen) return true;
             const long dl = (long)((plen - hdr) & 0xffff);
             if (hlen(d) < dl) return true;
+            // data_buffer<800>::parse consumes the record's data datum when it
+            // fits, so total_data (openvpn.h:388-395) counts only the data
+            // from the first record that did not fit onward
             if (!buf_null) {
                 if (used + (size_t)dl > sizeof buf) buf_null = true;
                 else { memcpy(buf + used, d.d, (size_t)dl); used += (size_t)dl; }
             }
-            total += (uint64_t)dl;
+            if (buf_null) total += (uint64_t)dl;
             d.d += dl;
         }
         if (!d.d || type == 3) return true;                 // the packet has no record

@@ -11,6 +11,6 @@ while [ $# -ge 2 ]; do
   src=${SRC:-mfp_kernels.hip}
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $flags -c mercury_amd/csrc/$src -o /tmp/var_$name.o
   objs=$(ls mercury_amd/_obj/*.o | grep -v "/$src.o")
-  hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_variants/libmercury_amd_$name.so /tmp/var_$name.o $objs -lz
+  hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_variants/libmercury_amd_$name.so /tmp/var_$name.o $objs -lz -lcrypto
   echo "built mercury_amd/_variants/libmercury_amd_$name.so ($flags)"
 done
