@@ -79,6 +79,7 @@ struct mfp_classifier_dev {
     uint32_t *asn4_bucket = nullptr;   // 65537 entries: first interval with hi >= b << 16 (narrows the search)
     mfp_asn6 *asn6 = nullptr; uint32_t n_asn6 = 0;
     uint32_t types_mask = 0;           // analyzable fingerprint types (fp_types)
+    uint32_t max_nproc = 0;            // the largest process count of an entry (k_analyze_big when > 512)
     uint32_t enc_channel_idx = 7, faketls_idx = 9, doh_idx = 6, domain_faking_idx = 8;
     uint32_t randomized_entry[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};   // "tls/", "tls/1/", "tls/2/" + "randomized"
     uint32_t db_tags = 0;              // bits of the archive's own attribute tags (>= MFP_ATTR_DB_FIRST)

@@ -37,7 +37,8 @@ namespace mfpa {
 #define ADEV __device__ __forceinline__
 using namespace mfpc;
 
-constexpr int MAXP_CHUNKS = 8;     // up to 512 processes per fingerprint
+constexpr int MAXP_CHUNKS = 8;     // up to 512 processes per fingerprint in k_analyze_wave
+constexpr int MAXP_CHUNKS_BIG = 64; // up to 4096 in k_analyze_big
 
 ADEV uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 ADEV uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -763,7 +764,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         if (scored) {
             const mfp_entry E = D.entry[entry];
             np = E.nproc; po = E.proc_off; mdb = E.malware_db; dmz = E.generic_dmz; mbits = E.mal_bits;
-            if (np > 64 * MAXP_CHUNKS) {
+            if (np > 64 * MAXP_CHUNKS_BIG) {   // beyond the big scorer: counted, left unscored
                 atomicAdd(&P.stats[2], 1ull);
                 scored = false;
             }
@@ -1013,19 +1014,19 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
 // round trip, then the lists are applied feature by feature as lane-parallel
 // scatters (a list names each process at most once, so every process sees the
 // reference's addition order; lists flagged MFP_UPD_SERIAL go one by one).
-__global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
-    __shared__ char sni_buf[4][336];
-    __shared__ char ua_buf[4][520];
-    __shared__ double sc_lds[4][64 * MAXP_CHUNKS];
-    __shared__ uint8_t fl_lds[4][64 * MAXP_CHUNKS];   // per process: malware (bit 0), archive tags (1-6), swapped out (7)
+// the scorer, one wave per deferred packet; CH chunks of 64 processes live
+// in registers (sc) and in the wave's LDS rows (scl, fl); WPB waves per block
+template <int CH, int WPB>
+__device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[336], char (*ua_buf)[520],
+                                            double (*sc_lds)[64 * CH], uint8_t (*fl_lds)[64 * CH]) {
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
     char *nbuf = sni_buf[wid];
     double *scl = sc_lds[wid];
     const mfp_classifier_dev &D = P.D;
     const uint64_t total = P.stats[3];
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t q = (uint64_t)blockIdx.x * 4 + wid; q < total; q += nw) {
+    const uint64_t nw = (uint64_t)gridDim.x * WPB;
+    for (uint64_t q = (uint64_t)blockIdx.x * WPB + wid; q < total; q += nw) {
         const Deferred &dq = P.deferred[q];
         const uint32_t i = rfl(dq.i), entry = rfl(dq.entry), slow = rfl(dq.slow_sni);
         uint32_t off[NFEAT], cnt[NFEAT];
@@ -1033,6 +1034,9 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
         for (uint32_t f = 0; f < NFEAT; f++) { off[f] = rfl(dq.off[f]); cnt[f] = rfl(dq.cnt[f]); }
         const mfp_entry E = D.entry[entry];
         const uint32_t np = rfl(E.nproc), po = rfl(E.proc_off), mdb = rfl(E.malware_db), dmz = rfl(E.generic_dmz);
+        // each instance takes its own size class: up to 64 * CH
+        // processes here, the rest (up to 64 * MAXP_CHUNKS_BIG) in k_analyze_big
+        if ((CH == MAXP_CHUNKS) != (np <= 64u * MAXP_CHUNKS)) continue;
         const uint32_t ft = rfl((uint32_t)P.rec[i].fp_type);
         if (slow) {
             // server name: full normalisation on lane 0 into LDS, hashed and
@@ -1097,13 +1101,13 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
             u[f].idx = 0; u[f].value = 0.0;
             if (lane < (cnt[f] & ~MFP_UPD_SERIAL)) u[f] = D.upd[off[f] + lane];
         }
-        uint32_t malbits = 0;
+        uint64_t malbits = 0;   // one bit per chunk (CH <= 64)
 #pragma unroll
-        for (int c = 0; c < MAXP_CHUNKS; c++) {
+        for (int c = 0; c < CH; c++) {
             const uint32_t pi = (uint32_t)c * 64 + lane;
             if ((uint32_t)c * 64 < np) {
                 scl[pi] = pi < np ? D.prior[po + pi] : 0.0;
-                if (pi < np && D.proc_mal[po + pi]) malbits |= 1u << c;
+                if (pi < np && D.proc_mal[po + pi]) malbits |= 1ull << c;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1131,16 +1135,16 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
-        double sc[MAXP_CHUNKS];
+        double sc[CH];
 #pragma unroll
-        for (int c = 0; c < MAXP_CHUNKS; c++) sc[c] = (uint32_t)c * 64 < np ? scl[c * 64 + lane] : 0.0;
+        for (int c = 0; c < CH; c++) sc[c] = (uint32_t)c * 64 < np ? scl[c * 64 + lane] : 0.0;
         __builtin_amdgcn_wave_barrier();
 
         // ---- max / second max (sequential first-index rule)
         double mx = -1.7976931348623157e308;
         uint32_t imx = 0xffffffffu;
 #pragma unroll
-        for (int c = 0; c < MAXP_CHUNKS; c++) {
+        for (int c = 0; c < CH; c++) {
             const uint32_t pi = (uint32_t)c * 64 + lane;
             if (pi < np && (imx == 0xffffffffu || sc[c] > mx)) { mx = sc[c]; imx = pi; }
         }
@@ -1155,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
         double sx = -1.7976931348623157e308;
         uint32_t isx = 0xffffffffu;
 #pragma unroll
-        for (int c = 0; c < MAXP_CHUNKS; c++) {
+        for (int c = 0; c < CH; c++) {
             const uint32_t pi = (uint32_t)c * 64 + lane;
             if (pi < np && pi != imx && (isx == 0xffffffffu || sc[c] > sx)) { sx = sc[c]; isx = pi; }
         }
@@ -1178,11 +1182,11 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
         // score_sum_without_max, 2 malware_prob, 3.. the archive tags
         uint8_t *fl = fl_lds[wid];
 #pragma unroll
-        for (int c = 0; c < MAXP_CHUNKS; c++) {
+        for (int c = 0; c < CH; c++) {
             const uint32_t pi = (uint32_t)c * 64 + lane;
             if (pi < np) {
                 scl[pi] = (double)expf_ref((float)(sc[c] - mx));
-                uint32_t f = (malbits >> c) & 1u;
+                uint32_t f = (uint32_t)((malbits >> c) & 1u);
                 if (tags) f |= ((D.proc_attr[po + pi] & tags) >> MFP_ATTR_DB_FIRST) << 1;
                 if (swap && pi == imx) f |= 0x80u;   // process_score[index_max] = 0 (analysis.h:264)
                 fl[pi] = (uint8_t)f;
@@ -1246,6 +1250,25 @@ __global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
         }
         __builtin_amdgcn_wave_barrier();
     }
+}
+
+
+__global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
+    __shared__ char sni_buf[4][336];
+    __shared__ char ua_buf[4][520];
+    __shared__ double sc_lds[4][64 * MAXP_CHUNKS];
+    __shared__ uint8_t fl_lds[4][64 * MAXP_CHUNKS];   // per process: malware (bit 0), archive tags (1-6), swapped out (7)
+    wave_scorer<MAXP_CHUNKS, 4>(P, sni_buf, ua_buf, sc_lds, fl_lds);
+}
+
+// fingerprints with more than 64 * MAXP_CHUNKS processes (production
+// archives have a few): one wave per block, the wider rows in LDS
+__global__ __launch_bounds__(64) void k_analyze_big(AParams P) {
+    __shared__ char sni_buf[1][336];
+    __shared__ char ua_buf[1][520];
+    __shared__ double sc_lds[1][64 * MAXP_CHUNKS_BIG];
+    __shared__ uint8_t fl_lds[1][64 * MAXP_CHUNKS_BIG];
+    wave_scorer<MAXP_CHUNKS_BIG, 1>(P, sni_buf, ua_buf, sc_lds, fl_lds);
 }
 
 // k_seen_export: the batch's distinct unknown-TLS fingerprints, in the order
@@ -1351,6 +1374,8 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
     if (hipGetLastError() != hipSuccess) return -1;
     if (prof) mfp_prof_begin(prof, "k_analyze_wave", stream);
     hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(1024), dim3(256), 0, stream, P);
+    if (D->max_nproc > 64u * mfpa::MAXP_CHUNKS)
+        hipLaunchKernelGGL(mfpa::k_analyze_big, dim3(256), dim3(64), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1122,6 +1122,8 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     }
     d.types_mask = 0;
     for (uint32_t ty : c->fp_types) d.types_mask |= 1u << ty;
+    d.max_nproc = 0;
+    for (const auto &me : t.entry) d.max_nproc = std::max(d.max_nproc, me.nproc);
     d.enc_channel_idx = 7;
     d.faketls_idx = 9;
     d.doh_idx = 6;

@@ -142,3 +142,24 @@ def test_stun_ovpn_json_vs_reference(key):
                                             threads=4)
     gold = test_json._golden_lines(f"stun_ovpn_json_{key}.txt.gz")
     test_json._check(lines, gold, skipped, allow_skip=True)
+
+
+@pytest.mark.gpu
+def test_classifier_more_than_512_processes():
+    """Fingerprints with 513..4096 processes (k_analyze_big: one wave per
+    packet, 64 process chunks in LDS) equal the reference
+    (tests/golden/make_golden_bigp.py)."""
+    m = json.load(open(os.path.join(GOLD, "bigp_manifest.json")))
+    arena, desc, sources = load()
+    cfg = f"select=stun;resources={os.path.join(GOLD, 'bigp_resources.tgz')};analysis"
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        rec, fp, an = ctx.process_host_analysis(arena, desc)
+        names = [ctx.process_name(int(p)) for p in an["process"]]
+        stats = ctx.analysis_stats()
+    finally:
+        ctx.close()
+    ref = test_analysis.load_ref_an("bigp_an.tsv.gz")
+    bad = test_analysis.compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+    assert m["valid_big_p"] > 50
