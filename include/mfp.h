@@ -294,6 +294,15 @@ MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mfp_reassembl
                                                   const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
                                                   size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc);
 MFP_EXPORT const uint8_t *mfp_reassembler_frames(mfp_reassembler r, size_t *len);
+/* With --analysis (a context with resources=...;analysis;reassembly): the same,
+ * then the records the reference writes -- packets with a record, the
+ * reassembled messages -- fingerprinted and classified once more in stream
+ * order; analysis/attr_prob as in mfp_process_batch_host_ex; out_desc required. */
+MFP_EXPORT long long mfp_process_batch_reassembly_analysis(mfp_context ctx, mfp_reassembler r, const uint8_t *arena,
+                                                           size_t arena_len, const mfp_pkt_desc *desc, size_t n,
+                                                           const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
+                                                           size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc,
+                                                           mfp_analysis *analysis, double *attr_prob);
 /* mfp_write_json_batch for the output of mfp_process_batch_reassembly (arena ++
  * frames, out_desc, records, props): completing records carry the
  * reassembler's "reassembly_properties" (reassembly.hpp:860-880,1231-1247). */
@@ -301,6 +310,12 @@ MFP_EXPORT long long mfp_write_json_batch_reassembly(const uint8_t *arena, const
                                                      const mfp_record *rec, const char *fp_arena, const uint16_t *props,
                                                      const uint64_t *ts_ns, char *out, size_t out_cap,
                                                      uint64_t *line_end, uint64_t *skipped, int threads);
+MFP_EXPORT long long mfp_write_json_batch_reassembly_analysis(mfp_context ctx, const uint8_t *arena,
+                                                              const mfp_pkt_desc *desc, size_t n, const mfp_record *rec,
+                                                              const char *fp_arena, const uint16_t *props,
+                                                              const mfp_analysis *analysis, const double *attr_prob,
+                                                              const uint64_t *ts_ns, char *out, size_t out_cap,
+                                                              uint64_t *line_end, uint64_t *skipped, int threads);
 
 typedef struct mfp_prevalence_s *mfp_prevalence;
 

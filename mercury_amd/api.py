@@ -98,6 +98,11 @@ def load_library():
     lib.mfp_reassembler_frames.argtypes = [vp, ctypes.POINTER(sz)]
     lib.mfp_reassembly_enabled.restype = ctypes.c_int
     lib.mfp_reassembly_enabled.argtypes = [vp]
+    lib.mfp_process_batch_reassembly_analysis.restype = ctypes.c_longlong
+    lib.mfp_process_batch_reassembly_analysis.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp, sz, vp, vp, vp, vp]
+    lib.mfp_write_json_batch_reassembly_analysis.restype = ctypes.c_longlong
+    lib.mfp_write_json_batch_reassembly_analysis.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, vp, sz, vp, vp,
+                                                             ctypes.c_int]
     lib.mfp_write_json_batch_reassembly.restype = ctypes.c_longlong
     lib.mfp_write_json_batch_reassembly.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, sz, vp, vp, ctypes.c_int]
     lib.mfp_process_batch_reassembly.restype = ctypes.c_longlong
@@ -248,7 +253,7 @@ class Context:
             raise MercuryAmdError("mfp_process_batch_host_seg failed: " + _err(self.lib))
         return rec, fp[:used].tobytes(), seg[:n]
 
-    def process_host_reassembly(self, arena, desc, ts_ns=None):
+    def process_host_reassembly(self, arena, desc, ts_ns=None, analysis=False):
         """A host batch in stream order through the context's TCP reassembler
         (config with "reassembly"; state persists across calls) -> (records,
         fp arena bytes, props (uint16, REASM_* bits), arena ++ rebuilt frames,
@@ -266,17 +271,27 @@ class Context:
         ts = None if ts_ns is None else np.ascontiguousarray(ts_ns, dtype=np.uint64)
         cap = self.fp_arena_bound(desc) + int(self.lib.mfp_fp_arena_bound(n, n * 8400))
         fp = np.zeros(cap, dtype=np.uint8)
-        used = self.lib.mfp_process_batch_reassembly(self.h, self.reasm, arena.ctypes.data, arena.nbytes,
-                                                     desc.ctypes.data, n, None if ts is None else ts.ctypes.data,
-                                                     rec.ctypes.data, fp.ctypes.data, cap, props.ctypes.data,
-                                                     out_desc.ctypes.data)
+        an = ap = None
+        if analysis:
+            an = np.zeros(max(n, 1), dtype=ANALYSIS_DTYPE)
+            ap = np.zeros((max(n, 1), ATTR_DB_TAGS), np.float64)
+            used = self.lib.mfp_process_batch_reassembly_analysis(
+                self.h, self.reasm, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
+                None if ts is None else ts.ctypes.data, rec.ctypes.data, fp.ctypes.data, cap, props.ctypes.data,
+                out_desc.ctypes.data, an.ctypes.data, ap.ctypes.data)
+        else:
+            used = self.lib.mfp_process_batch_reassembly(self.h, self.reasm, arena.ctypes.data, arena.nbytes,
+                                                         desc.ctypes.data, n, None if ts is None else ts.ctypes.data,
+                                                         rec.ctypes.data, fp.ctypes.data, cap, props.ctypes.data,
+                                                         out_desc.ctypes.data)
         if used < 0:
             raise MercuryAmdError("mfp_process_batch_reassembly failed: " + _err(self.lib))
         flen = ctypes.c_size_t(0)
         ptr = self.lib.mfp_reassembler_frames(self.reasm, ctypes.byref(flen))
         frames = np.ctypeslib.as_array((ctypes.c_uint8 * flen.value).from_address(ptr)).copy() if flen.value else \
             np.zeros(0, np.uint8)
-        return rec, fp[:used].tobytes(), props[:n], np.concatenate([arena, frames]), out_desc[:n]
+        out = (rec, fp[:used].tobytes(), props[:n], np.concatenate([arena, frames]), out_desc[:n])
+        return out + (an[:n], ap[:n]) if analysis else out
 
     @property
     def analysis_enabled(self):
@@ -652,7 +667,13 @@ def write_json(arena, desc, rec, fp_arena, ts_ns=None, threads=1, ctx=None, anal
     cap = 1 << 16
     while True:
         out = np.empty(cap, np.uint8)
-        if props is not None:
+        if props is not None and an is not None:
+            pr = np.ascontiguousarray(props, dtype=np.uint16)
+            got = lib.mfp_write_json_batch_reassembly_analysis(
+                ctx.h, arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data, fp.ctypes.data, pr.ctypes.data,
+                an.ctypes.data, None if ap is None else ap.ctypes.data, None if ts is None else ts.ctypes.data,
+                out.ctypes.data, cap, ends.ctypes.data, ctypes.byref(skipped), int(threads))
+        elif props is not None:
             pr = np.ascontiguousarray(props, dtype=np.uint16)
             got = lib.mfp_write_json_batch_reassembly(arena.ctypes.data, desc.ctypes.data, n, rec.ctypes.data,
                                                       fp.ctypes.data, pr.ctypes.data,

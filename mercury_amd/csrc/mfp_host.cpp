@@ -348,10 +348,6 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
         mfp_set_error("reassembly is supported on the write_json path (MFP_MODE_WRITE_JSON) only");
         return nullptr;
     }
-    if (reassembly && analysis) {
-        mfp_set_error("reassembly together with --analysis is not on the device path yet");
-        return nullptr;
-    }
     if (reassembly && (sel & (SEL_QUIC | SEL_DTLS))) {
         // process_udp_data's reassembly (QUIC CRYPTO frames, DTLS fragments,
         // pkt_proc.cc:926-944) is not on the device path: refuse, do not diverge

@@ -956,3 +956,16 @@ MFP_EXPORT long long mfp_write_json_batch_reassembly(const uint8_t *arena, const
     return write_json_batch(nullptr, props, arena, desc, n, rec, fp_arena, nullptr, nullptr, ts_ns, out, out_cap,
                             line_end, skipped, threads);
 }
+
+// ... and with the --analysis objects (mfp_process_batch_reassembly_analysis)
+MFP_EXPORT long long mfp_write_json_batch_reassembly_analysis(mfp_context ctx, const uint8_t *arena,
+                                                              const mfp_pkt_desc *desc, size_t n, const mfp_record *rec,
+                                                              const char *fp_arena, const uint16_t *props,
+                                                              const mfp_analysis *analysis, const double *attr_prob,
+                                                              const uint64_t *ts_ns, char *out, size_t out_cap,
+                                                              uint64_t *line_end, uint64_t *skipped, int threads) {
+    if (!ctx || !mfp_analysis_enabled(ctx)) { mfp_set_error("the context has no classifier"); return -1; }
+    if (n && (!props || !analysis)) { mfp_set_error("mfp_write_json_batch_reassembly_analysis: null argument"); return -1; }
+    return write_json_batch(ctx, props, arena, desc, n, rec, fp_arena, analysis, attr_prob, ts_ns, out, out_cap,
+                            line_end, skipped, threads);
+}

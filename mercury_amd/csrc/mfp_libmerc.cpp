@@ -236,16 +236,21 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
         p->fp.resize(cap);
         uint16_t props = 0;
         mfp_pkt_desc d2 = d;
-        long long used = mfp_process_batch_reassembly(ctx, p->reasm, p->arena.data(), p->arena.size(), &d, 1, &t, &rec,
-                                                      p->fp.data(), cap, &props, &d2);
+        long long used = want_an ? mfp_process_batch_reassembly_analysis(ctx, p->reasm, p->arena.data(), p->arena.size(),
+                                                                         &d, 1, &t, &rec, p->fp.data(), cap, &props, &d2,
+                                                                         &an, ap)
+                                 : mfp_process_batch_reassembly(ctx, p->reasm, p->arena.data(), p->arena.size(), &d, 1,
+                                                                &t, &rec, p->fp.data(), cap, &props, &d2);
         if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
         // the record indexes arena ++ the reassembler's frames
         size_t flen = 0;
         const uint8_t *fr = mfp_reassembler_frames(p->reasm, &flen);
         if (d2.offset >= len + 16 && fr) p->arena.insert(p->arena.end(), fr, fr + flen);
-        fill_context(ctx, p->ac, p->arena.data() + d2.offset, rec, p->fp.data(), nullptr, ap);
-        n = mfp_write_json_batch_reassembly(p->arena.data(), &d2, 1, &rec, p->fp.data(), &props, &t, (char *)buffer,
-                                            buffer_size, &end, &skipped, 1);
+        fill_context(ctx, p->ac, p->arena.data() + d2.offset, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+        n = want_an ? mfp_write_json_batch_reassembly_analysis(ctx, p->arena.data(), &d2, 1, &rec, p->fp.data(), &props,
+                                                               &an, ap, &t, (char *)buffer, buffer_size, &end, &skipped, 1)
+                    : mfp_write_json_batch_reassembly(p->arena.data(), &d2, 1, &rec, p->fp.data(), &props, &t,
+                                                      (char *)buffer, buffer_size, &end, &skipped, 1);
     } else {
         long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(),
                                                    cap, want_an ? &an : nullptr, want_an ? ap : nullptr);

@@ -238,6 +238,9 @@ struct mfp_reassembler_s {
     std::vector<uint8_t> frames;
     std::vector<size_t> who;                        // packet index of each rebuilt frame
     std::vector<uint16_t> who_props;
+    std::vector<uint8_t> quiet;                     // 1: a segment that writes no record (return false)
+    std::vector<uint8_t> merged;                    // arena ++ frames (the classifier pass)
+    std::vector<mfp_pkt_desc> desc3;
 };
 
 extern "C" MFP_EXPORT mfp_reassembler mfp_reassembler_create(void) { return new mfp_reassembler_s; }
@@ -292,6 +295,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
     if (used < 0) return used;
     // 2. the flow table in stream order (process_tcp_data pkt_proc.cc:773-893)
     R->frames.clear(); R->desc2.clear(); R->who.clear(); R->who_props.clear();
+    R->quiet.assign(n, 0);
     for (size_t i = 0; i < n; i++) {
         props[i] = 0;
         const mfp_tcp_seg &s = R->seg[i];
@@ -312,7 +316,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
         const uint32_t avail = s.pay_off + (uint64_t)data_len <= desc[i].caplen ? data_len : 0;
         if (it == R->table.end()) {
             if (supp) continue;                             // not in reassembly: taken as complete
-            if (!more) { r.flags &= (uint8_t)~MFP_FLAG_EMIT; r.fp_type = 0; r.fp_len = 0; continue; }
+            if (!more) { r.flags &= (uint8_t)~MFP_FLAG_EMIT; r.fp_type = 0; r.fp_len = 0; R->quiet[i] = 1; continue; }
             if (R->table.size() >= kMaxFlows) {             // active_reap (two entries)
                 for (int d = 0; d < 2 && !R->age.empty(); d++) {
                     auto old = R->table.find(R->age.front().first);
@@ -349,6 +353,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
             R->table.erase(it);                             // consumed, then clean_curr_flow
         } else {
             r.flags &= (uint8_t)~MFP_FLAG_EMIT; r.fp_type = 0; r.fp_len = 0;   // no record for this segment
+            R->quiet[i] = 1;
         }
     }
     // 3. the reassembled messages through the device; their records replace
@@ -378,5 +383,32 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
         }
         used += used2;
     }
+    return used;
+}
+
+// --analysis with reassembly (write_json with a classifier, pkt_proc.cc:1195-1238):
+// the batch through the reassembler, then fingerprint + classify once more in
+// stream order over what the reference analyses -- the packets that write a
+// record, the reassembled messages in their completing packets' places, and
+// nothing for the segments that only fed a buffer (zero-length descriptors),
+// so the classifier's unknown-TLS sightings follow the reference's order.
+extern "C" MFP_EXPORT long long mfp_process_batch_reassembly_analysis(
+    mfp_context ctx, mfp_reassembler R, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc, size_t n,
+    const uint64_t *ts_ns, mfp_record *rec, char *fp_arena, size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc,
+    mfp_analysis *analysis, double *attr_prob) {
+    if (!mfp_analysis_enabled(ctx)) { mfp_set_error("the context has no classifier"); return -1; }
+    if (n && (!analysis || !out_desc)) { mfp_set_error("null argument"); return -1; }
+    long long used = mfp_process_batch_reassembly(ctx, R, arena, arena_len, desc, n, ts_ns, rec, fp_arena, fp_cap, props,
+                                                  out_desc);
+    if (used < 0) return used;
+    R->merged.assign(arena, arena + arena_len);
+    R->merged.insert(R->merged.end(), R->frames.begin(), R->frames.end());
+    R->merged.resize(R->merged.size() + 16, 0);
+    R->desc3.assign(out_desc, out_desc + n);
+    for (size_t i = 0; i < n; i++) if (R->quiet[i]) R->desc3[i].caplen = 0;
+    used = mfp_process_batch_host_ex(ctx, R->merged.data(), R->merged.size(), R->desc3.data(), n, rec, fp_arena, fp_cap,
+                                     analysis, attr_prob);
+    if (used < 0) return used;
+    for (size_t i = 0; i < n; i++) if (props[i] & 1) rec[i].flags &= (uint8_t)~MFP_FLAG_TRUNCATED;
     return used;
 }

@@ -77,6 +77,12 @@ def main():
                        "reassembled": sum('"reassembled":true' in p for p in props),
                        "truncated": sum(int(r[3]) for r in rows),
                        "overlaps": sum("overlap" in p for p in props)}
+    # with --analysis (the reference's test archive): the whole JSON text
+    res = os.path.join(HERE, "resources-test.tgz")
+    js = subprocess.run([REF, "json", tmp, CONFIGS["r0"], res], capture_output=True, check=True).stdout.decode("latin-1")
+    with gzip.open(os.path.join(HERE, "reasm_json_an.txt.gz"), "wt", encoding="latin-1") as f:
+        f.write("\n".join(js.split("\n")[:len(desc)]) + "\n")
+    counts["an"] = {"analysis_objects": js.count('"analysis":')}
     os.unlink(tmp)
     manifest = {"reference": "cisco/mercury 2.18.0 (/root/reference), libmerc built by oracle/Makefile.ref",
                 "driver": "oracle/_ref/merc_ref_drv fp|json <stream> <config> - (fixed ts 1700000000)",

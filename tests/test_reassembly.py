@@ -194,3 +194,23 @@ def test_libmerc_write_json_with_reassembly():
     lib.mercury_packet_processor_destruct(p)
     lib.mercury_finalize(mc)
     assert not bad, f"{len(bad)} mismatches, first {bad[:2]}"
+
+
+@pytest.mark.gpu
+def test_reassembly_with_analysis_json_vs_reference():
+    """--analysis with reassembly: the reassembled ClientHellos classified in
+    their completing packets' places (resources-test.tgz), the whole JSON text
+    equal to the reference's."""
+    from tests import test_json
+    arena, desc = load_stream()
+    cfg = MANIFEST["configs"]["r0"] + f";resources={os.path.join(GOLD, 'resources-test.tgz')};analysis"
+    ctx = mercury_amd.Context(cfg, device=0)
+    try:
+        rec, fp, props, arena2, desc2, an, ap = ctx.process_host_reassembly(
+            arena, desc, ts_ns=np.full(len(desc), TS, np.uint64), analysis=True)
+        lines, skipped = mercury_amd.write_json(arena2, desc2, rec, fp, ts_ns=np.full(len(desc), TS, np.uint64),
+                                                threads=4, ctx=ctx, analysis=an, attr_prob=ap, props=props)
+    finally:
+        ctx.close()
+    test_json._check(lines, test_json._golden_lines("reasm_json_an.txt.gz"), skipped, allow_skip=True)
+    assert MANIFEST["counts"]["an"]["analysis_objects"] > 50
