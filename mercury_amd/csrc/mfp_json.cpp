@@ -876,7 +876,7 @@ static long long write_json_batch(mfp_context ctx, const uint16_t *props, const 
         size_t lo = (size_t)t * per, hi = lo + per < n ? lo + per : n;
         Out o = std::move(part[(size_t)t]);   // thread-local copy: no shared lines while formatting
         TsCache tc;
-        o.need((hi > lo ? hi - lo : 0) * 320 + 65536);   // grows (x2) if the records are longer
+        o.need((hi > lo ? hi - lo : 0) * 320 + 65536);   // exact; grows x1.5 if the records are longer
         for (size_t i = lo; i < hi; i++) {
             uint64_t sec = 0, nsec = 0;
             if (ts_ns) { sec = ts_ns[i] / 1000000000ull; nsec = ts_ns[i] % 1000000000ull; }
