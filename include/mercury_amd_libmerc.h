@@ -11,7 +11,9 @@
  *   - the returned analysis_context points into the processor and is
  *     overwritten by the next call on it (libmerc.cc:173-175);
  *   - errors return 0 / NULL, never abort (libmerc.cc:138-240).
- * Not provided on this path: stats, FDC/CBOR, encrypted resource archives.
+ * Not provided on this path (the entry points exist, so the reference's own
+ * binaries link, and refuse): stats (do_stats is refused at mercury_init;
+ * mercury_write_stats_data returns false) and FDC/CBOR output.
  */
 #ifndef MERCURY_AMD_LIBMERC_H
 #define MERCURY_AMD_LIBMERC_H
@@ -20,6 +22,7 @@
 #include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <time.h>
 
 #include "mfp.h"
@@ -148,13 +151,46 @@ MFP_EXPORT bool analysis_context_get_alpns(const struct analysis_context *ac, co
 MFP_EXPORT const struct attribute_context *mercury_packet_processor_get_attributes(mercury_packet_processor processor);
 /* libmerc.h:647 -- opaque classifier handle (the analysis context), NULL without one */
 MFP_EXPORT void *mercury_get_classifier(mercury_context mc);
-/* libmerc.h:754 -- reassembly is off on this path */
+/* libmerc.h:754 -- flow_state_pkts_needed of the last get_analysis_context call
+ * ("reassembly" configured: a flow waits for more segments) */
 MFP_EXPORT bool mercury_packet_processor_more_pkts_needed(mercury_packet_processor processor);
 /* libmerc.h:603, :617, :556, :638 */
 MFP_EXPORT uint32_t mercury_get_version_number(void);
 MFP_EXPORT void mercury_get_version_string(char *buf, size_t size);
 MFP_EXPORT const char *mercury_get_license_string(void);
 MFP_EXPORT const char *mercury_get_resource_version(mercury_context mc);
+/* libmerc.h:570 -- "2.18.0\n" */
+MFP_EXPORT void mercury_print_version_string(FILE *f);
+/* libmerc.h:584 -- the commit this library was built from */
+MFP_EXPORT void mercury_print_git_commit(FILE *f);
+/* libmerc.h:536 -- no stats aggregator on this path: false */
+MFP_EXPORT bool mercury_write_stats_data(mercury_context mc, const char *stats_data_file_path);
+/* libmerc.h:771 -- 0 */
+MFP_EXPORT size_t get_stats_aggregator_num_entries(mercury_context mc);
+
+/* libmerc.h:799-829 */
+struct ipv6_addr_ext { uint32_t a, b, c, d; };
+struct flow_key_ext {
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint8_t protocol;
+    uint8_t ip_vers;
+    union {
+        struct { uint32_t src; uint32_t dst; } ipv4;
+        struct { struct ipv6_addr_ext src; struct ipv6_addr_ext dst; } ipv6;
+    } addr;
+};
+/* libmerc.h:833-840 */
+enum fdc_return {
+    FDC_NO_DATA = 0, FDC_WRITE_INSUFFICIENT_SPACE = -1, FDC_WRITE_FAILURE = -2, MORE_PACKETS_NEEDED = -3,
+    UNKNOWN_ERROR = -4, INVALID_INPUT = -5,
+};
+/* libmerc.h:877 -- FDC/CBOR output is not provided: UNKNOWN_ERROR (INVALID_INPUT
+ * for a NULL processor), *ac = NULL, and a log line */
+MFP_EXPORT int mercury_packet_processor_get_analysis_context_fdc(mercury_packet_processor processor,
+                                                                 const struct flow_key_ext *key, const uint8_t *data,
+                                                                 size_t len, uint8_t *buffer, size_t *buffer_size,
+                                                                 const struct analysis_context **ac);
 
 #ifdef __cplusplus
 }

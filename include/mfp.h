@@ -145,6 +145,9 @@ enum {
     MFP_SEG_DATA = 1,           /* a TCP data segment process_tcp_data sees (pkt_proc.cc:773) */
     MFP_SEG_SUPPLEMENTARY = 2,  /* tcp_packet::supplementary_reassembly (SSH KEXINIT)          */
     MFP_SEG_SSH = 4,            /* reassembly_type::ssh (indefinite, pkt_proc.cc:552)          */
+    MFP_SEG_TCP = 8,            /* a TCP packet with a whole header (tcp_packet::is_valid)     */
+    MFP_SEG_SYN_RST = 16,       /* SYN, SYN/ACK or RST: analyze_ip_packet skips it in reassembly
+                                   mode (pkt_proc.cc:1632-1634)                                */
 };
 
 /* semantics of the reference entry point to follow */
@@ -303,6 +306,22 @@ MFP_EXPORT long long mfp_process_batch_reassembly_analysis(mfp_context ctx, mfp_
                                                            const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
                                                            size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc,
                                                            mfp_analysis *analysis, double *attr_prob);
+/* The analysis_context path with reassembly (analyze_ip_packet
+ * pkt_proc.cc:1597-1662, a context created with MFP_MODE_ANALYSIS and
+ * "reassembly"): TCP SYN, SYN/ACK and RST packets are skipped; every other TCP
+ * data segment goes through the flow table as in mfp_process_batch_reassembly;
+ * the packets with a result and the reassembled messages are then fingerprinted
+ * and (analysis != NULL) classified in stream order; a reassembled message
+ * whose flow was truncated (timeout, max segments, ...) is "unlabeled"
+ * (pkt_proc.cc:1716-1719).  more_pkts[i] (optional) =
+ * analysis_context::flow_state_pkts_needed after packet i: cleared by every
+ * TCP packet, set while its flow is in reassembly, kept by other packets
+ * (the state carries across calls in r). */
+MFP_EXPORT long long mfp_process_batch_reassembly_context(mfp_context ctx, mfp_reassembler r, const uint8_t *arena,
+                                                          size_t arena_len, const mfp_pkt_desc *desc, size_t n,
+                                                          const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
+                                                          size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc,
+                                                          mfp_analysis *analysis, double *attr_prob, uint8_t *more_pkts);
 /* mfp_write_json_batch for the output of mfp_process_batch_reassembly (arena ++
  * frames, out_desc, records, props): completing records carry the
  * reassembler's "reassembly_properties" (reassembly.hpp:860-880,1231-1247). */

@@ -10,7 +10,8 @@ OBJ = os.path.join(HERE, "_obj")
 
 SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_compact.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp",
            "mfp_pcap.cpp", "mfp_json.cpp", "mfp_prevalence.cpp", "mfp_quic.hip", "mfp_reassembly.cpp"]
-HEADERS = ["mfp_device.hpp", "mfp_internal.h", "mfp_analysis.h", "mfp_common.hpp", "mfp_cipher_ranges.inc", "mfp_quic_crypto.hpp"]
+HEADERS = ["mfp_device.hpp", "mfp_internal.h", "mfp_analysis.h", "mfp_common.hpp", "mfp_cipher_ranges.inc", "mfp_quic_crypto.hpp",
+           "mfp_encap.hpp"]
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 
 

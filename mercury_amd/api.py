@@ -105,6 +105,8 @@ def load_library():
                                                              ctypes.c_int]
     lib.mfp_write_json_batch_reassembly.restype = ctypes.c_longlong
     lib.mfp_write_json_batch_reassembly.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, sz, vp, vp, ctypes.c_int]
+    lib.mfp_process_batch_reassembly_context.restype = ctypes.c_longlong
+    lib.mfp_process_batch_reassembly_context.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     lib.mfp_process_batch_reassembly.restype = ctypes.c_longlong
     lib.mfp_process_batch_reassembly.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp, sz, vp, vp]
     lib.mfp_process_batch_host_ex.restype = ctypes.c_longlong
@@ -292,6 +294,43 @@ class Context:
             np.zeros(0, np.uint8)
         out = (rec, fp[:used].tobytes(), props[:n], np.concatenate([arena, frames]), out_desc[:n])
         return out + (an[:n], ap[:n]) if analysis else out
+
+    def analyze_host_reassembly(self, arena, desc, ts_ns=None, analysis=True):
+        """The analysis_context path with reassembly (a MODE_ANALYSIS context
+        with "reassembly"; mfp_process_batch_reassembly_context) -> (records, fp
+        arena bytes, props, arena ++ frames, desc indexing it, analysis records
+        or None, attribute probabilities or None, more_pkts_needed (uint8))."""
+        if not self.lib.mfp_reassembly_enabled(self.h):
+            raise MercuryAmdError("the configuration has no \"reassembly\"")
+        if not getattr(self, "reasm", None):
+            self.reasm = self.lib.mfp_reassembler_create()
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        n = len(desc)
+        rec = np.zeros(n, dtype=RECORD_DTYPE)
+        props = np.zeros(max(n, 1), dtype=np.uint16)
+        out_desc = np.zeros(max(n, 1), dtype=DESC_DTYPE)
+        more = np.zeros(max(n, 1), dtype=np.uint8)
+        ts = None if ts_ns is None else np.ascontiguousarray(ts_ns, dtype=np.uint64)
+        cap = self.fp_arena_bound(desc) + int(self.lib.mfp_fp_arena_bound(n, n * 8400))
+        fp = np.zeros(cap, dtype=np.uint8)
+        an = ap = None
+        if analysis:
+            an = np.zeros(max(n, 1), dtype=ANALYSIS_DTYPE)
+            ap = np.zeros((max(n, 1), ATTR_DB_TAGS), np.float64)
+        used = self.lib.mfp_process_batch_reassembly_context(
+            self.h, self.reasm, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n,
+            None if ts is None else ts.ctypes.data, rec.ctypes.data, fp.ctypes.data, cap, props.ctypes.data,
+            out_desc.ctypes.data, None if an is None else an.ctypes.data, None if ap is None else ap.ctypes.data,
+            more.ctypes.data)
+        if used < 0:
+            raise MercuryAmdError("mfp_process_batch_reassembly_context failed: " + _err(self.lib))
+        flen = ctypes.c_size_t(0)
+        ptr = self.lib.mfp_reassembler_frames(self.reasm, ctypes.byref(flen))
+        frames = np.ctypeslib.as_array((ctypes.c_uint8 * flen.value).from_address(ptr)).copy() if flen.value else \
+            np.zeros(0, np.uint8)
+        return (rec, fp[:used].tobytes(), props[:n], np.concatenate([arena, frames]), out_desc[:n],
+                None if an is None else an[:n], None if ap is None else ap[:n], more[:n])
 
     @property
     def analysis_enabled(self):

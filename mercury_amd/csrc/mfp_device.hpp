@@ -1974,11 +1974,16 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         o.dst_port = (ld(tcph + 2) << 8) | ld(tcph + 3);
         uint32_t fl = ld(tcph + 13);
         bool syn = fl & 0x02, ack = fl & 0x10;
-        if (cfg.seg && !(syn && cfg.mode == MFP_MODE_WRITE_JSON) && clen(pkt) > 0) {   // process_tcp_data's data segments
-            o.seq = (ld(tcph + 4) << 24) | (ld(tcph + 5) << 16) | (ld(tcph + 6) << 8) | ld(tcph + 7);
-            o.seg_kind = MFP_SEG_DATA;
-            o.pay_off = (uint32_t)(pkt.d - base);
-            o.pay_len = (uint32_t)clen(pkt);
+        if (cfg.seg) {
+            // every whole TCP header resets flow_state_pkts_needed on the analysis
+            // path, which skips SYN, SYN/ACK and RST (pkt_proc.cc:1629-1634)
+            o.seg_kind = MFP_SEG_TCP | ((fl & 0x06) ? MFP_SEG_SYN_RST : 0u);
+            if (!(syn && cfg.mode == MFP_MODE_WRITE_JSON) && clen(pkt) > 0) {   // process_tcp_data's data segments
+                o.seq = (ld(tcph + 4) << 24) | (ld(tcph + 5) << 16) | (ld(tcph + 6) << 8) | ld(tcph + 7);
+                o.seg_kind |= MFP_SEG_DATA;
+                o.pay_off = (uint32_t)(pkt.d - base);
+                o.pay_len = (uint32_t)clen(pkt);
+            }
         }
         if (cfg.mode == MFP_MODE_WRITE_JSON) {
             if (syn && !ack) {

@@ -344,10 +344,6 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     std::string resources;
     bool analysis = false, reassembly = false;
     if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly)) return nullptr;
-    if (reassembly && mode != MFP_MODE_WRITE_JSON) {
-        mfp_set_error("reassembly is supported on the write_json path (MFP_MODE_WRITE_JSON) only");
-        return nullptr;
-    }
     if (reassembly && (sel & (SEL_QUIC | SEL_DTLS))) {
         // process_udp_data's reassembly (QUIC CRYPTO frames, DTLS fragments,
         // pkt_proc.cc:926-944) is not on the device path: refuse, do not diverge
@@ -755,6 +751,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_seg(mfp_context c, const 
 }
 
 extern "C" MFP_EXPORT int mfp_reassembly_enabled(mfp_context c) { return c && c->reassembly ? 1 : 0; }
+uint32_t mfp_context_mode(mfp_context c) { return c ? c->mode : 0; }
 
 extern "C" MFP_EXPORT long long mfp_process_batch_host(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                        const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
@@ -909,6 +906,16 @@ extern "C" MFP_EXPORT int mfp_analysis_resolve(mfp_context c, const mfp_sighting
     Slot *S = deferred_slot(c);
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
+    if (u && !d) { mfp_set_error("mfp_analysis_resolve: null decisions"); return -1; }
+    {   // one decision per distinct entry of the pending batch (the resolve kernel indexes them by position)
+        std::vector<mfp_sighting> have;
+        const long long cnt = slot_distinct(c, *S, have);
+        if (cnt < 0) return (int)cnt;
+        if ((size_t)cnt != u) {
+            mfp_set_error("mfp_analysis_resolve: %zu decisions, the batch has %lld distinct fingerprints", u, cnt);
+            return -1;
+        }
+    }
     std::vector<uint8_t> bits(u);
     for (size_t i = 0; i < u; i++) bits[i] = (uint8_t)d[i].first_seen;
     const int r = slot_apply(c, *S, bits.data(), u, false);

@@ -13,6 +13,7 @@ void mfp_set_error(const char *fmt, ...);
 bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
                       bool *reassembly);
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode);
+uint32_t mfp_context_mode(mfp_context c);   // MFP_MODE_*
 
 // kernel strategies of the fingerprint pass (mfp_kernels.hip)
 enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_LANE = 2 };

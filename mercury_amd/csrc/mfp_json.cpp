@@ -32,6 +32,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include "mfp_encap.hpp"
 #include "mfp_internal.h"
 
 namespace {
@@ -703,7 +705,8 @@ void write_reassembled(W &w, uint16_t props) {
     w.put('}');
 }
 
-bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const char *fp_arena,
+bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint32_t linktype, const mfp_record &r,
+                  const char *fp_arena,
                   uint64_t sec, uint64_t nsec, mfp_context ctx, const mfp_analysis *an, const double *ap,
                   uint16_t props) {
     if (!(r.flags & MFP_FLAG_EMIT)) return true;
@@ -712,21 +715,10 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     if (r.msg == MFP_MSG_QUIC) return false;
 
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
-    // IP-in-IP: outer headers sit back to back before the inner one (IPv4
-    // fixed 20 B, ip.h:124-137; IPv6 40 B when it has no extension headers)
-    const uint32_t levels = (r.net >> 20) & 7;
-    uint32_t outer[4], outer_v[4];
-    if (r.flags & MFP_FLAG_ENCAP) {
-        if (levels == 0 || levels > 4 || (r.net >> 27) & 1) return false;   // irregular: not rebuilt
-        uint32_t at = ip;
-        for (int k = (int)levels - 1; k >= 0; k--) {
-            outer_v[k] = (r.net >> (23 + k)) & 1 ? 6 : 4;
-            const uint32_t sz = outer_v[k] == 6 ? 40 : 20;
-            if (at < sz) return false;
-            at -= sz;
-            outer[k] = at;
-        }
-    }
+    // the encapsulation levels above the innermost IP header (IP-in-IP, GRE,
+    // VXLAN, Geneve), found again from the link layer (mfp_encap.hpp)
+    mfpe::Chain chain;
+    if ((r.flags & MFP_FLAG_ENCAP) && (!mfpe::walk(pkt, caplen, linktype, ip, chain) || chain.n == 0)) return false;
     if ((ipv != 4 && ipv != 6) || ip + (ipv == 4 ? 20u : 40u) > caplen) return false;
     // worst case: fixed keys/addresses/numbers and 4 encapsulations < 1000 B, the fp string, and at most
     // 6 output bytes per input byte of a JSON string ("\\ufffd") or a base64 cert list
@@ -802,17 +794,21 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, cons
     if (with_an) { rec.key("analysis"); write_analysis(w, ctx, *an, ap); }   // pkt_proc.cc:1211-1213
     if (props & 1) { rec.key("reassembly_properties"); write_reassembled(w, props); }   // reassembly.hpp:1238-1241
     else if (r.flags & MFP_FLAG_TRUNCATED) { rec.key("reassembly_properties"); w.puts("{\"truncated\":true}"); }
-    if (r.flags & MFP_FLAG_ENCAP) {                      // encapsulations::write_json pkt_proc.cc:1021-1031
+    if (r.flags & MFP_FLAG_ENCAP) {                      // encapsulations::write_json pkt_proc.cc:1033-1043
+        static const char *type[4] = {"ip encapsulation", "gre", "vxlan", "geneve"};
         rec.key("encapsulations");
         w.put('[');
-        for (uint32_t k = 0; k < levels; k++) {           // ip_encapsulation::write_json ip.h:788-793
-            const uint8_t *oh = pkt + outer[k];
+        for (int k = 0; k < chain.n; k++) {               // ip.h:788-793, gre.h:69-75, vxlan.hpp:60-68, geneve.hpp:85-91
+            const mfpe::Level &L = chain.lv[k];
+            const uint8_t *oh = pkt + L.ip_off;
             if (k) w.put(',');
-            w.puts("{\"type\":\"ip encapsulation\",\"src_ip\":\"");
-            if (outer_v[k] == 4) w.ipv4(oh + 12); else w.ipv6(oh + 8);
+            w.puts("{\"type\":\""); w.putz(type[L.kind]); w.puts("\",\"src_ip\":\"");   // key::write_ip_address
+            if (L.ipv == 4) w.ipv4(oh + 12); else w.ipv6(oh + 8);
             w.puts("\",\"dst_ip\":\"");
-            if (outer_v[k] == 4) w.ipv4(oh + 16); else w.ipv6(oh + 24);
-            w.puts("\"}");
+            if (L.ipv == 4) w.ipv4(oh + 16); else w.ipv6(oh + 24);
+            w.put('"');
+            if (L.kind == mfpe::GRE || L.kind == mfpe::GENEVE) { w.puts(",\"protocol_type\":"); w.udec(L.proto_type); }
+            w.put('}');
         }
         w.put(']');
     }
@@ -882,7 +878,8 @@ static long long write_json_batch(mfp_context ctx, const uint16_t *props, const 
             if (ts_ns) { sec = ts_ns[i] / 1000000000ull; nsec = ts_ns[i] % 1000000000ull; }
             if (sec == 0) { sec = (uint64_t)now.tv_sec; nsec = (uint64_t)now.tv_nsec; }
             size_t mark = o.len;
-            if (!write_record(o, tc, arena + desc[i].offset, desc[i].caplen, rec[i], fp_arena, sec, nsec, ctx,
+            if (!write_record(o, tc, arena + desc[i].offset, desc[i].caplen, desc[i].linktype, rec[i], fp_arena, sec, nsec,
+                              ctx,
                               an ? an + i : nullptr, ap ? ap + i * MFP_ATTR_DB_TAGS : nullptr, props ? props[i] : (uint16_t)0)) {
                 o.len = mark;
                 bad[(size_t)t]++;

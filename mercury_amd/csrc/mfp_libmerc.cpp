@@ -54,26 +54,52 @@ struct mercury_packet_processor_s {
     std::vector<uint8_t> arena;
     std::vector<char> fp;
     mfp_reassembler reasm = nullptr;   // the processor's tcp_reassembler ("reassembly" configured)
+    bool more_pkts = false;            // analysis_context::flow_state_pkts_needed (result.h:386)
     ~mercury_packet_processor_s() { if (reasm) mfp_reassembler_destroy(reasm); }
 };
 
-static printf_err_ptr g_printf_err = nullptr;
+// printf_err_func (printf_err.hpp:22-45): the default emitter, a level prefix
+// and the message on stderr
+static int stderr_err(enum log_level level, const char *format, va_list args) {
+    static const char *pfx[] = {"emergency: ", "alert: ", "critical: ", "error: ", "warning: ",
+                                "notice: ", "informational: ", "debug: ", ""};
+    const int r = std::fprintf(stderr, "%s", pfx[(unsigned)level <= log_none ? (unsigned)level : (unsigned)log_none]);
+    if (r < 0) return r;
+    const int s = std::vfprintf(stderr, format, args);
+    return s < 0 ? s : r + s;
+}
+static int silent_err(enum log_level, const char *, va_list) { return 0; }   // silent_err_func printf_err.hpp:47
+
+static printf_err_ptr g_printf_err = stderr_err;
 
 static void log_error(const char *fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
-    if (g_printf_err) g_printf_err(log_err, fmt, ap);
+    g_printf_err(log_err, fmt, ap);
     va_end(ap);
 }
 
+#ifndef MFP_GIT_COMMIT
+#define MFP_GIT_COMMIT "commit unknown"   // libmerc.cc:29-36
+#endif
+
 extern "C" {
 
-MFP_EXPORT void register_printf_err_callback(printf_err_ptr callback) { g_printf_err = callback; }
+// register_printf_err_callback libmerc.cc:473-475: NULL silences the library
+MFP_EXPORT void register_printf_err_callback(printf_err_ptr callback) {
+    g_printf_err = callback ? callback : silent_err;
+}
 
 // mercury_init libmerc.cc:92-128 / struct mercury pkt_proc.h:56-114
 MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int verbosity) {
     (void)verbosity;
     if (!vars) return nullptr;
+    if (vars->do_stats) {
+        // the stats aggregator (stats.h, --stats) is outside this path: refuse at
+        // init, as the reference refuses a configuration it cannot honour
+        log_error("do_stats: fingerprint/destination statistics are not provided by libmercury_amd\n");
+        return nullptr;
+    }
     auto *m = new mercury;
     // the archive key: 16 bytes whatever key_type says (analysis.h:1211,
     // "TODO: key type"; cryptovar<16>)
@@ -278,7 +304,8 @@ MFP_EXPORT size_t mercury_packet_processor_write_json(mercury_packet_processor p
     return mercury_packet_processor_write_json_linktype(p, buffer, buffer_size, pkt, len, ts, 1);   // LINKTYPE_ETHERNET
 }
 
-static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt, size_t len, uint16_t linktype) {
+static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt, size_t len, struct timespec *ts,
+                                      uint16_t linktype) {
     if (!p || !pkt) return nullptr;
     mfp_context ctx = get_ctx(p->mc, MFP_MODE_ANALYSIS);
     if (!ctx) return nullptr;
@@ -291,26 +318,50 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
     size_t cap = mfp_fp_arena_bound(1, len);
     p->fp.resize(cap);
     bool want_an = mfp_analysis_enabled(ctx);
-    long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(), cap,
-                                               want_an ? &an : nullptr, want_an ? ap : nullptr);
-    if (used < 0) { log_error("%s\n", mfp_last_error()); return nullptr; }
+    const uint8_t *base = pkt;
+    if (mfp_reassembly_enabled(ctx)) {
+        // analyze_ip_packet with the processor's reassembler (pkt_proc.cc:1597-1662):
+        // the flow table in stream order, flow_state_pkts_needed per packet
+        if (!p->reasm) p->reasm = mfp_reassembler_create();
+        if (ts && ts->tv_sec == 0) clock_gettime(CLOCK_REALTIME, ts);   // pkt_proc.cc:1619-1622
+        const uint64_t t = ts ? (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec : 0;
+        cap += mfp_fp_arena_bound(1, 8192 + 256);
+        p->fp.resize(cap);
+        uint16_t props = 0;
+        uint8_t more = 0;
+        mfp_pkt_desc d2 = d;
+        const long long used = mfp_process_batch_reassembly_context(
+            ctx, p->reasm, p->arena.data(), p->arena.size(), &d, 1, &t, &rec, p->fp.data(), cap, &props, &d2,
+            want_an ? &an : nullptr, want_an ? ap : nullptr, &more);
+        if (used < 0) { log_error("%s\n", mfp_last_error()); return nullptr; }
+        p->more_pkts = more != 0;
+        size_t flen = 0;
+        const uint8_t *fr = mfp_reassembler_frames(p->reasm, &flen);
+        if (d2.offset >= len + 16 && fr) p->arena.insert(p->arena.end(), fr, fr + flen);
+        base = p->arena.data() + d2.offset;
+    } else {
+        const long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec,
+                                                         p->fp.data(), cap, want_an ? &an : nullptr,
+                                                         want_an ? ap : nullptr);
+        if (used < 0) { log_error("%s\n", mfp_last_error()); return nullptr; }
+    }
     analysis_context &ac = p->ac;
-    fill_context(ctx, ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+    fill_context(ctx, ac, base, rec, p->fp.data(), want_an ? &an : nullptr, ap);
     if (!want_an) return nullptr;   // no classifier: analysis result never valid
     return (an.flags & MFP_AN_VALID) ? &ac : nullptr;
 }
 
 MFP_EXPORT const struct analysis_context *mercury_packet_processor_ip_get_analysis_context(
-    mercury_packet_processor processor, uint8_t *packet, size_t length, struct timespec *) {
-    return analyze(processor, packet, length, 101);
+    mercury_packet_processor processor, uint8_t *packet, size_t length, struct timespec *ts) {
+    return analyze(processor, packet, length, ts, 101);
 }
 MFP_EXPORT const struct analysis_context *mercury_packet_processor_get_analysis_context(
-    mercury_packet_processor processor, uint8_t *packet, size_t length, struct timespec *) {
-    return analyze(processor, packet, length, 1);
+    mercury_packet_processor processor, uint8_t *packet, size_t length, struct timespec *ts) {
+    return analyze(processor, packet, length, ts, 1);
 }
 MFP_EXPORT const struct analysis_context *mercury_packet_processor_get_analysis_context_linktype(
-    mercury_packet_processor processor, uint8_t *packet, size_t length, struct timespec *, uint16_t linktype) {
-    return analyze(processor, packet, length, linktype);
+    mercury_packet_processor processor, uint8_t *packet, size_t length, struct timespec *ts, uint16_t linktype) {
+    return analyze(processor, packet, length, ts, linktype);
 }
 
 MFP_EXPORT enum fingerprint_status analysis_context_get_fingerprint_status(const struct analysis_context *ac) {
@@ -380,12 +431,46 @@ MFP_EXPORT void *mercury_get_classifier(mercury_context mc) {
     return c && mfp_analysis_enabled(c) ? (void *)c : nullptr;
 }
 
-MFP_EXPORT bool mercury_packet_processor_more_pkts_needed(mercury_packet_processor) { return false; }
+// libmerc.cc:242-253: analysis_context::flow_state_pkts_needed of the
+// processor's last get_analysis_context call (reassembly configured)
+MFP_EXPORT bool mercury_packet_processor_more_pkts_needed(mercury_packet_processor p) {
+    return p ? p->more_pkts : false;
+}
 
 MFP_EXPORT uint32_t mercury_get_version_number(void) { return mfp_reference_version(); }
+// semantic_version::print_version_string version.h:34-36 (size - 1, as the reference)
 MFP_EXPORT void mercury_get_version_string(char *buf, size_t size) {
-    if (buf && size) snprintf(buf, size, "%u.%u.%u", mfp_reference_version() >> 16, (mfp_reference_version() >> 8) & 0xff,
-                              mfp_reference_version() & 0xff);
+    if (buf && size) snprintf(buf, size - 1, "%u.%u.%u", mfp_reference_version() >> 16,
+                              (mfp_reference_version() >> 8) & 0xff, mfp_reference_version() & 0xff);
+}
+// mercury_print_version_string libmerc.cc:59-62 (semantic_version::print version.h:30-32)
+MFP_EXPORT void mercury_print_version_string(FILE *f) {
+    if (f) fprintf(f, "%u.%u.%u\n", mfp_reference_version() >> 16, (mfp_reference_version() >> 8) & 0xff,
+                   mfp_reference_version() & 0xff);
+}
+// mercury_print_git_commit libmerc.cc:64-66: the commit this library was built from
+MFP_EXPORT void mercury_print_git_commit(FILE *f) {
+    if (f) fprintf(f, "%s\n", MFP_GIT_COMMIT);
+}
+// mercury_write_stats_data libmerc.cc:377-396: false without a stats
+// aggregator (do_stats is refused at init, so there never is one)
+MFP_EXPORT bool mercury_write_stats_data(mercury_context mc, const char *stats_data_file_path) {
+    if (mc && stats_data_file_path) log_error("mercury_write_stats_data: stats are not provided by libmercury_amd\n");
+    return false;
+}
+// get_stats_aggregator_num_entries libmerc.cc:477-484
+MFP_EXPORT size_t get_stats_aggregator_num_entries(mercury_context) { return 0; }
+// mercury_packet_processor_get_analysis_context_fdc libmerc.cc:199-216: the
+// FDC/CBOR encoding is outside this path; the call fails as the reference's
+// does on an internal error (fdc_return::UNKNOWN_ERROR), with a log line
+MFP_EXPORT int mercury_packet_processor_get_analysis_context_fdc(mercury_packet_processor processor,
+                                                                 const struct flow_key_ext *, const uint8_t *, size_t,
+                                                                 uint8_t *, size_t *,
+                                                                 const struct analysis_context **context) {
+    if (!processor) return -5;   // fdc_return::INVALID_INPUT
+    if (context) *context = nullptr;
+    log_error("mercury_packet_processor_get_analysis_context_fdc: FDC output is not provided by libmercury_amd\n");
+    return -4;                   // fdc_return::UNKNOWN_ERROR
 }
 MFP_EXPORT const char *mercury_get_license_string(void) {
     return "libmercury_amd: MI355X fingerprint/classify path for the libmerc API";

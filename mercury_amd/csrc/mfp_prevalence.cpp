@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <unordered_set>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../../include/mfp.h"
@@ -122,10 +123,21 @@ struct Lru {
 
 }  // namespace
 
+// One object may be shared by several contexts used from several threads (the
+// libmerc shim's write_json and analysis contexts; shards): every entry point
+// holds its lock, as the reference guards its LRU (analysis.h:372,390)
 struct mfp_prevalence_s {
     Lru lru;
+    std::mutex mu;
     explicit mfp_prevalence_s(uint32_t c) : lru(c) {}
 };
+
+static bool exact_locked(mfp_prevalence p, const mfp_sighting *d, size_t u) {
+    std::unordered_set<uint64_t> fresh;
+    for (size_t i = 0; i < u; i++)
+        if (!p->lru.contains(d[i].hash)) fresh.insert(d[i].hash);
+    return (uint64_t)p->lru.size + fresh.size() <= p->lru.cap;
+}
 
 extern "C" {
 
@@ -136,14 +148,21 @@ MFP_EXPORT mfp_prevalence mfp_prevalence_create(uint32_t capacity) {
 
 MFP_EXPORT void mfp_prevalence_destroy(mfp_prevalence p) { delete p; }
 
-MFP_EXPORT uint64_t mfp_prevalence_size(mfp_prevalence p) { return p ? p->lru.size : 0; }
+MFP_EXPORT uint64_t mfp_prevalence_size(mfp_prevalence p) {
+    if (!p) return 0;
+    std::lock_guard<std::mutex> lk(p->mu);
+    return p->lru.size;
+}
 
 MFP_EXPORT int mfp_prevalence_contains(mfp_prevalence p, uint64_t hash) {
-    return p && p->lru.contains(hash) ? 1 : 0;
+    if (!p) return 0;
+    std::lock_guard<std::mutex> lk(p->mu);
+    return p->lru.contains(hash) ? 1 : 0;
 }
 
 MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t cap) {
     if (!p) return -1;
+    std::lock_guard<std::mutex> lk(p->mu);
     std::vector<uint64_t> k;
     p->lru.export_keys(k);
     const size_t m = k.size() < cap ? k.size() : cap;
@@ -153,6 +172,7 @@ MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t
 
 MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen) {
     if (!p || (m && (!hash || !seen))) { mfp_set_error("mfp_prevalence_resolve_sequence: bad arguments"); return -1; }
+    std::lock_guard<std::mutex> lk(p->mu);
     for (size_t j = 0; j < m; j++) seen[j] = p->lru.access(hash[j]) ? 1 : 0;
     return 0;
 }
@@ -162,10 +182,8 @@ MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t 
 // Entries may repeat a hash (the same fingerprint in several shards).
 MFP_EXPORT int mfp_prevalence_distinct_exact(mfp_prevalence p, const mfp_sighting *d, size_t u) {
     if (!p || (u && !d)) return -1;
-    std::unordered_set<uint64_t> fresh;
-    for (size_t i = 0; i < u; i++)
-        if (!p->lru.contains(d[i].hash)) fresh.insert(d[i].hash);
-    return (uint64_t)p->lru.size + fresh.size() <= p->lru.cap ? 1 : 0;
+    std::lock_guard<std::mutex> lk(p->mu);
+    return exact_locked(p, d, u) ? 1 : 0;
 }
 
 // Decide the first sighting of every entry and apply the entries to the set.
@@ -176,7 +194,8 @@ MFP_EXPORT int mfp_prevalence_distinct_exact(mfp_prevalence p, const mfp_sightin
 // the batch could evict: resolve the sighting sequence then.
 MFP_EXPORT int mfp_prevalence_resolve_distinct(mfp_prevalence p, mfp_sighting *d, size_t u) {
     if (!p || (u && !d)) { mfp_set_error("mfp_prevalence_resolve_distinct: bad arguments"); return -1; }
-    if (mfp_prevalence_distinct_exact(p, d, u) != 1) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!exact_locked(p, d, u)) {
         mfp_set_error("mfp_prevalence_resolve_distinct: the batch can evict (set %u + new fingerprints > capacity %u); "
                       "resolve the sighting sequence instead", p->lru.size, p->lru.cap);
         return -2;

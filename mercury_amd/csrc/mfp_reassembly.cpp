@@ -31,13 +31,14 @@
 
 #include <cstdint>
 #include <cstring>
-#include <deque>
+#include <list>
 #include <string>
 #include <unordered_map>
 #include <utility>
 #include <vector>
 
 #include "../../include/mfp.h"
+#include "mfp_encap.hpp"
 #include "mfp_internal.h"
 
 namespace {
@@ -128,7 +129,7 @@ struct FlowKeyHash {
 struct Flow {
     uint8_t flags = 0, ovl = 0;      // reassembly_flag_val, reassembly_overlap_flags
     int state = S_PROGRESS;
-    uint64_t init_time = 0, order = 0;
+    uint64_t init_time = 0;
     uint32_t init_seq = 0, init_seg_len = 0, total_needed = 0;
     bool ssh_type = false;           // reassembly_type::ssh (indefinite)
     size_t contiguous = 0;
@@ -229,9 +230,12 @@ struct Flow {
 }  // namespace
 
 struct mfp_reassembler_s {
-    std::unordered_map<FlowKey, Flow, FlowKeyHash> table;
-    std::deque<std::pair<FlowKey, uint64_t>> age;   // insertion order (for the 10000-flow bound)
-    uint64_t order = 0;
+    // flows in reassembly, and their keys in insertion order (the reaping order
+    // here; each flow holds its position, so a consumed flow leaves the list)
+    struct Entry { Flow f; std::list<FlowKey>::iterator age; };
+    std::unordered_map<FlowKey, Entry, FlowKeyHash> table;
+    std::list<FlowKey> age;
+    bool more_state = false;                        // analysis_context::flow_state_pkts_needed (sticky)
     std::vector<mfp_tcp_seg> seg;
     std::vector<mfp_record> rec2;
     std::vector<mfp_pkt_desc> desc2;
@@ -260,32 +264,62 @@ static bool flow_key(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, F
     return false;
 }
 
-// the reassembled message as a frame: the packet's IP header and TCP header
-// (bytes [ip, data)), the IP length fields set for the new data, the buffer
-static void rebuild(std::vector<uint8_t> &out, const uint8_t *pkt, const mfp_record &r, const mfp_tcp_seg &s,
-                    const uint8_t *data, size_t len) {
-    const uint32_t ip = r.net & 0xffff, v = (r.net >> 16) & 15;
-    const size_t hdr = s.pay_off - ip;
+// the reassembled message as a frame: the packet's headers up to its TCP data
+// (link layer, any encapsulation levels, IP, TCP), then the buffer; every IP
+// length field on the way is set to reach the end of the new data, so the
+// device's re-walk finds the same levels (the JSON record's
+// "encapsulations" come from the current packet, pkt_proc.cc:1231-1233) and
+// the message.  Returns the frame's length (its link type is the packet's).
+static uint32_t rebuild(std::vector<uint8_t> &out, const uint8_t *pkt, uint32_t caplen, uint32_t linktype,
+                        const mfp_record &r, const mfp_tcp_seg &s, const uint8_t *data, size_t len) {
+    const uint32_t ip = r.net & 0xffff;
+    uint32_t start = 0;
+    mfpe::Chain chain;
+    const bool levels = (r.flags & MFP_FLAG_ENCAP) && mfpe::walk(pkt, caplen, linktype, ip, chain);
+    if (!levels) start = ip;                                // the inner IP header on its own (LINKTYPE_RAW)
     const size_t at = out.size();
-    out.insert(out.end(), pkt + ip, pkt + s.pay_off);
+    out.insert(out.end(), pkt + start, pkt + s.pay_off);
     out.insert(out.end(), data, data + len);
-    uint8_t *h = out.data() + at;
-    if (v == 4) {
-        const size_t tl = hdr + len;                        // ipv4_packet::parse trims to tot_len - 20 (ip.h:124-137)
-        h[2] = (uint8_t)(tl >> 8); h[3] = (uint8_t)tl;
-    } else {
-        const size_t pl = hdr - 40 + len;                   // ipv6 payload_len (ip.h:448-474)
-        h[4] = (uint8_t)(pl >> 8); h[5] = (uint8_t)pl;
-    }
+    const uint32_t flen = (uint32_t)(out.size() - at);
+    auto patch = [&](uint32_t off, uint32_t v) {            // ipv4 tot_len (ip.h:124-137) / ipv6 payload_len (:448-474)
+        uint8_t *h = out.data() + at + (off - start);
+        const uint32_t rest = flen - (off - start);
+        if (v == 4) { h[2] = (uint8_t)(rest >> 8); h[3] = (uint8_t)rest; }
+        else { h[4] = (uint8_t)((rest - 40) >> 8); h[5] = (uint8_t)(rest - 40); }
+    };
+    if (levels) for (int k = 0; k < chain.n; k++) patch(chain.lv[k].ip_off, chain.lv[k].ipv);
+    patch(ip, (r.net >> 16) & 15);
     while (out.size() % 8) out.push_back(0);                // keep frames 8-byte aligned
     out.resize(out.size() + 16, 0);                         // the readable tail block (include/mfp.h)
+    return flen | (levels ? 0x80000000u : 0u);
 }
 
-extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mfp_reassembler R, const uint8_t *arena,
-                                                             size_t arena_len, const mfp_pkt_desc *desc, size_t n,
-                                                             const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
-                                                             size_t fp_cap, uint16_t *props,
-                                                             mfp_pkt_desc *out_desc) {
+// check_flow's housekeeping (reassembly.hpp:645-655): at max_entries flows two
+// are dropped (active_reap), otherwise up to two expired ones (passive_reap).
+// The reference walks its unordered_map from a persistent iterator; here the
+// two oldest flows are the candidates.
+static void housekeeping(mfp_reassembler R, uint64_t sec) {
+    const bool active = R->table.size() >= kMaxFlows;
+    for (int d = 0; d < 2 && !R->age.empty(); d++) {
+        auto it = R->table.find(R->age.front());
+        if (!active && sec - it->second.f.init_time < kTimeout) break;   // reassembly_flow_context::is_expired
+        R->age.pop_front();
+        R->table.erase(it);
+    }
+}
+
+static void drop(mfp_reassembler R, decltype(R->table)::iterator it) {
+    R->age.erase(it->second.age);
+    R->table.erase(it);
+}
+
+// the flow table over one batch, in stream order (process_tcp_data
+// pkt_proc.cc:773-893).  an_path: the analysis_context path
+// (analyze_ip_packet pkt_proc.cc:1624-1646): SYN, SYN/ACK and RST are skipped
+// and every TCP packet resets flow_state_pkts_needed (more[i], sticky).
+static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *arena, size_t arena_len,
+                            const mfp_pkt_desc *desc, size_t n, const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
+                            size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc, bool an_path, uint8_t *more) {
     if (!ctx || !R) { mfp_set_error("null context or reassembler"); return -1; }
     if (!mfp_reassembly_enabled(ctx)) { mfp_set_error("the context's configuration has no \"reassembly\""); return -1; }
     if (n && (!arena || !desc || !rec || !fp_arena || !props)) { mfp_set_error("null argument"); return -1; }
@@ -296,41 +330,50 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
     // 2. the flow table in stream order (process_tcp_data pkt_proc.cc:773-893)
     R->frames.clear(); R->desc2.clear(); R->who.clear(); R->who_props.clear();
     R->quiet.assign(n, 0);
+    auto no_record = [&](size_t i) {                        // process_tcp_data returned false
+        rec[i].flags &= (uint8_t)~MFP_FLAG_EMIT; rec[i].fp_type = 0; rec[i].fp_len = 0; R->quiet[i] = 1;
+    };
     for (size_t i = 0; i < n; i++) {
         props[i] = 0;
         const mfp_tcp_seg &s = R->seg[i];
-        if (!(s.kind & MFP_SEG_DATA)) continue;
+        if (an_path && (s.kind & MFP_SEG_TCP)) {
+            R->more_state = false;                          // pkt_proc.cc:1630
+            if (s.kind & MFP_SEG_SYN_RST) {                 // handshake control packets (pkt_proc.cc:1631-1633)
+                no_record(i);
+                if (more) more[i] = 0;
+                continue;
+            }
+        }
+        if (more) more[i] = R->more_state;
+        if (!(s.kind & MFP_SEG_DATA)) {
+            if (an_path && (s.kind & MFP_SEG_TCP)) no_record(i);   // empty data: process_tcp_data returns false
+            continue;
+        }
         mfp_record &r = rec[i];
         const uint8_t *pkt = arena + desc[i].offset;
         const uint32_t data_len = s.pay_len;
-        const uint32_t more = s.more;
+        const uint32_t more_bytes = s.more;
         const bool supp = s.kind & MFP_SEG_SUPPLEMENTARY;
         const bool mono = r.msg == 0;                       // std::monostate: no message parsed
-        if (!more && !mono && !supp) continue;              // a complete message
-        if (more > kMaxData || data_len > kMaxData) continue;   // cannot be reassembled
+        if (!more_bytes && !mono && !supp) continue;        // a complete message
+        if (more_bytes > kMaxData || data_len > kMaxData) continue;   // cannot be reassembled
         FlowKey k;
         if (!flow_key(pkt, desc[i].caplen, r, k)) continue;
         const uint64_t sec = ts_ns ? ts_ns[i] / 1000000000ull : 0;
+        housekeeping(R, sec);
         auto it = R->table.find(k);
         const uint8_t *data = pkt + s.pay_off;
         const uint32_t avail = s.pay_off + (uint64_t)data_len <= desc[i].caplen ? data_len : 0;
         if (it == R->table.end()) {
             if (supp) continue;                             // not in reassembly: taken as complete
-            if (!more) { r.flags &= (uint8_t)~MFP_FLAG_EMIT; r.fp_type = 0; r.fp_len = 0; R->quiet[i] = 1; continue; }
-            if (R->table.size() >= kMaxFlows) {             // active_reap (two entries)
-                for (int d = 0; d < 2 && !R->age.empty(); d++) {
-                    auto old = R->table.find(R->age.front().first);
-                    if (old != R->table.end() && old->second.order == R->age.front().second) R->table.erase(old);
-                    R->age.pop_front();
-                }
-            }
-            Flow &f = R->table[k];
-            f.order = ++R->order;
-            R->age.emplace_back(k, f.order);
-            f.init(data_len, s.seq, more, (s.kind & MFP_SEG_SSH) != 0, sec, data, avail);
+            if (!more_bytes) { no_record(i); continue; }
+            R->age.push_back(k);
+            auto &e = R->table[k];
+            e.age = std::prev(R->age.end());
+            e.f.init(data_len, s.seq, more_bytes, (s.kind & MFP_SEG_SSH) != 0, sec, data, avail);
             it = R->table.find(k);
         } else {
-            Flow &f = it->second;
+            Flow &f = it->second.f;
             if (sec - f.init_time >= kTimeout) {            // continue_reassembly: set_expired
                 f.state = S_TRUNCATED;
                 f.flags |= 1u << F_TIMEOUT;
@@ -339,22 +382,24 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
                 f.add(data_len, seq, data, avail);
             }
         }
-        Flow &f = it->second;
+        Flow &f = it->second.f;
         if (f.state == S_SUCCESS || f.state == S_TRUNCATED) {   // is_ready: fingerprint the buffer
             R->who.push_back(i);
             R->who_props.push_back((uint16_t)(1u | (uint32_t)f.flags << 1 | (uint32_t)f.ovl << 8));
             mfp_pkt_desc d2;
             d2.offset = R->frames.size();
-            rebuild(R->frames, pkt, r, s, f.buf, f.contiguous);
-            d2.caplen = (uint32_t)(s.pay_off - (r.net & 0xffff) + f.contiguous);
-            d2.linktype = 101;                              // LINKTYPE_RAW
+            const uint32_t fl = rebuild(R->frames, pkt, desc[i].caplen, desc[i].linktype, r, s, f.buf, f.contiguous);
+            d2.caplen = fl & 0x7fffffffu;
+            d2.linktype = (fl >> 31) ? desc[i].linktype : (uint16_t)101;   // the packet's, or LINKTYPE_RAW
             d2.flags = 0;
             R->desc2.push_back(d2);
-            R->table.erase(it);                             // consumed, then clean_curr_flow
+            drop(R, it);                                    // consumed, then clean_curr_flow
+            if (an_path) R->more_state = false;             // finalize_reassembly_flow (reassembly.hpp:1218-1228)
         } else {
-            r.flags &= (uint8_t)~MFP_FLAG_EMIT; r.fp_type = 0; r.fp_len = 0;   // no record for this segment
-            R->quiet[i] = 1;
+            no_record(i);                                   // no record for this segment
+            if (an_path) R->more_state = true;              // in_progress (pkt_proc.cc:1636-1638)
         }
+        if (more) more[i] = R->more_state;
     }
     // 3. the reassembled messages through the device; their records replace
     // the completing packets' (their strings follow the batch's)
@@ -373,7 +418,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
             if (r2.fp_type) r2.fp_offset += (uint64_t)used;
             // the reassembler's own "reassembly_properties" replace {"truncated":true}
             // (write_reassembly_properties reassembly.hpp:1231-1247)
-            r2.flags &= (uint8_t)~MFP_FLAG_TRUNCATED;
+            if (!an_path) r2.flags &= (uint8_t)~MFP_FLAG_TRUNCATED;
             rec[i] = r2;
             props[i] = R->who_props[j];
             if (out_desc) {
@@ -386,29 +431,69 @@ extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mf
     return used;
 }
 
-// --analysis with reassembly (write_json with a classifier, pkt_proc.cc:1195-1238):
-// the batch through the reassembler, then fingerprint + classify once more in
-// stream order over what the reference analyses -- the packets that write a
-// record, the reassembled messages in their completing packets' places, and
-// nothing for the segments that only fed a buffer (zero-length descriptors),
-// so the classifier's unknown-TLS sightings follow the reference's order.
+extern "C" MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mfp_reassembler R, const uint8_t *arena,
+                                                             size_t arena_len, const mfp_pkt_desc *desc, size_t n,
+                                                             const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
+                                                             size_t fp_cap, uint16_t *props,
+                                                             mfp_pkt_desc *out_desc) {
+    return reassemble(ctx, R, arena, arena_len, desc, n, ts_ns, rec, fp_arena, fp_cap, props, out_desc, false, nullptr);
+}
+
+// the packets the reference analyses -- those with a record, the reassembled
+// messages in their completing packets' places, nothing for the segments that
+// only fed a buffer (zero-length descriptors) -- fingerprinted and classified
+// once more in stream order, so the unknown-TLS sightings keep the
+// reference's order
+static long long classify_pass(mfp_context ctx, mfp_reassembler R, const uint8_t *arena, size_t arena_len, size_t n,
+                               mfp_record *rec, char *fp_arena, size_t fp_cap, const mfp_pkt_desc *out_desc,
+                               mfp_analysis *analysis, double *attr_prob) {
+    R->merged.assign(arena, arena + arena_len);
+    R->merged.insert(R->merged.end(), R->frames.begin(), R->frames.end());
+    R->merged.resize(R->merged.size() + 16, 0);
+    R->desc3.assign(out_desc, out_desc + n);
+    for (size_t i = 0; i < n; i++) if (R->quiet[i]) R->desc3[i].caplen = 0;
+    return mfp_process_batch_host_ex(ctx, R->merged.data(), R->merged.size(), R->desc3.data(), n, rec, fp_arena, fp_cap,
+                                     analysis, attr_prob);
+}
+
+// --analysis with reassembly (write_json with a classifier, pkt_proc.cc:1195-1238)
 extern "C" MFP_EXPORT long long mfp_process_batch_reassembly_analysis(
     mfp_context ctx, mfp_reassembler R, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc, size_t n,
     const uint64_t *ts_ns, mfp_record *rec, char *fp_arena, size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc,
     mfp_analysis *analysis, double *attr_prob) {
     if (!mfp_analysis_enabled(ctx)) { mfp_set_error("the context has no classifier"); return -1; }
     if (n && (!analysis || !out_desc)) { mfp_set_error("null argument"); return -1; }
-    long long used = mfp_process_batch_reassembly(ctx, R, arena, arena_len, desc, n, ts_ns, rec, fp_arena, fp_cap, props,
-                                                  out_desc);
+    long long used = reassemble(ctx, R, arena, arena_len, desc, n, ts_ns, rec, fp_arena, fp_cap, props, out_desc, false,
+                                nullptr);
     if (used < 0) return used;
-    R->merged.assign(arena, arena + arena_len);
-    R->merged.insert(R->merged.end(), R->frames.begin(), R->frames.end());
-    R->merged.resize(R->merged.size() + 16, 0);
-    R->desc3.assign(out_desc, out_desc + n);
-    for (size_t i = 0; i < n; i++) if (R->quiet[i]) R->desc3[i].caplen = 0;
-    used = mfp_process_batch_host_ex(ctx, R->merged.data(), R->merged.size(), R->desc3.data(), n, rec, fp_arena, fp_cap,
-                                     analysis, attr_prob);
+    used = classify_pass(ctx, R, arena, arena_len, n, rec, fp_arena, fp_cap, out_desc, analysis, attr_prob);
     if (used < 0) return used;
     for (size_t i = 0; i < n; i++) if (props[i] & 1) rec[i].flags &= (uint8_t)~MFP_FLAG_TRUNCATED;
+    return used;
+}
+
+// the analysis_context path with reassembly (analyze_ip_packet pkt_proc.cc:1597-1662)
+extern "C" MFP_EXPORT long long mfp_process_batch_reassembly_context(
+    mfp_context ctx, mfp_reassembler R, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc, size_t n,
+    const uint64_t *ts_ns, mfp_record *rec, char *fp_arena, size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc,
+    mfp_analysis *analysis, double *attr_prob, uint8_t *more_pkts) {
+    if (!ctx || !R) { mfp_set_error("null context or reassembler"); return -1; }
+    if (mfp_context_mode(ctx) != MFP_MODE_ANALYSIS) {
+        mfp_set_error("mfp_process_batch_reassembly_context needs a context created with MFP_MODE_ANALYSIS");
+        return -1;
+    }
+    if (analysis && !mfp_analysis_enabled(ctx)) { mfp_set_error("the context has no classifier"); return -1; }
+    if (n && !out_desc) { mfp_set_error("null argument"); return -1; }
+    long long used = reassemble(ctx, R, arena, arena_len, desc, n, ts_ns, rec, fp_arena, fp_cap, props, out_desc, true,
+                                more_pkts);
+    if (used < 0 || !analysis) return used;
+    used = classify_pass(ctx, R, arena, arena_len, n, rec, fp_arena, fp_cap, out_desc, analysis, attr_prob);
+    if (used < 0) return used;
+    // detect_truncation (reassembly.hpp:1183-1196): a reassembled message whose
+    // flow was truncated is a truncated fingerprint -> unlabeled (pkt_proc.cc:1716-1719)
+    const uint16_t trunc_bits = (uint16_t)(((1u << F_TRUNCATED) | (1u << F_TIMEOUT) | (1u << F_OUT_OF_BUFFER) |
+                                            (1u << F_MAX_SEG) | (1u << F_MISSING)) << 1);
+    for (size_t i = 0; i < n; i++)
+        if ((props[i] & 1) && (props[i] & trunc_bits) && (analysis[i].flags & MFP_AN_VALID)) analysis[i].status = 3;
     return used;
 }

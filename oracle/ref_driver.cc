@@ -10,6 +10,9 @@
 //   idx  emit  fp_type  truncated  fp_string
 // Output (mode "an"): analysis_context path, one TSV line per packet:
 //   idx  valid  fp_type  status  process  score  malware  p_malware  fp_string
+// Mode "anr": as "an", with mercury_packet_processor_more_pkts_needed after each
+// packet in a column before the fingerprint:
+//   idx  valid  fp_type  status  process  score  malware  p_malware  more  fp_string
 // Mode "json": the write_json record text, one line per packet (empty line
 // when the reference writes nothing).
 // Mode "attr": analysis_context path, the accessors the embedders read, one
@@ -19,7 +22,8 @@
 // (prob %.17Lg, set tags only), os_info: name=prevalence;... from
 // analysis_context_get_os_info, alpn: hex of analysis_context_get_alpns
 // (first min(len, 128) bytes) and ":len".
-// Environment: MERC_REPORT_OS=1 sets libmerc_config.report_os; MERC_ENC_KEY=<32
+// Environment: MERC_TS_FILE=<file of n little-endian u64 seconds> gives each
+// packet its own timestamp (default 1700000000 for all); MERC_REPORT_OS=1 sets libmerc_config.report_os; MERC_ENC_KEY=<32
 // hex digits> sets libmerc_config.enc_key (an encrypted resource archive).
 // Mode "time": run write_json (or, with a trailing "an", the analysis_context
 // entry) with T threads (one processor per thread over contiguous shards),
@@ -142,11 +146,16 @@ int main(int argc, char **argv) {
     if (devnull >= 0) close(devnull);
     if (!mc) { fprintf(stderr, "mercury_init failed\n"); return 1; }
 
+    std::vector<uint64_t> tsv(pkts.size(), 1700000000ull);
+    if (const char *tf = getenv("MERC_TS_FILE")) {
+        auto tb = slurp(tf);
+        for (size_t i = 0; i < pkts.size() && 8 * i + 8 <= tb.size(); i++) memcpy(&tsv[i], tb.data() + 8 * i, 8);
+    }
     std::vector<char> out(1 << 16);
     if (mode == "fp") {
         mercury_packet_processor p = mercury_packet_processor_construct(mc);
         for (size_t i = 0; i < pkts.size(); i++) {
-            struct timespec ts{1700000000, 0};
+            struct timespec ts{(time_t)tsv[i], 0};
             size_t n = mercury_packet_processor_write_json_linktype(p, out.data(), out.size(),
                                                                    (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
             std::string json(out.data(), n);
@@ -161,38 +170,40 @@ int main(int argc, char **argv) {
         // the reference's JSON record text, one line per packet ("" when none)
         mercury_packet_processor p = mercury_packet_processor_construct(mc);
         for (size_t i = 0; i < pkts.size(); i++) {
-            struct timespec ts{1700000000, 0};
+            struct timespec ts{(time_t)tsv[i], 0};
             size_t n = mercury_packet_processor_write_json_linktype(p, out.data(), out.size(),
                                                                    (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
             fwrite(out.data(), 1, n, stdout);
             if (n == 0 || out[n - 1] != '\n') fputc('\n', stdout);
         }
         mercury_packet_processor_destruct(p);
-    } else if (mode == "an") {
+    } else if (mode == "an" || mode == "anr") {
+        const bool more = mode == "anr";
         mercury_packet_processor p = mercury_packet_processor_construct(mc);
         for (size_t i = 0; i < pkts.size(); i++) {
-            struct timespec ts{1700000000, 0};
+            struct timespec ts{(time_t)tsv[i], 0};
             const analysis_context *ac = mercury_packet_processor_get_analysis_context_linktype(
                 p, (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
+            const char *mp = more ? (mercury_packet_processor_more_pkts_needed(p) ? "1\t" : "0\t") : "";
             if (!ac) {
                 int t = p->analysis.fp.get_type();
-                printf("%zu\t0\t%d\t0\t\t0\t0\t0\t%s\n", i, t, t ? p->analysis.fp.string() : "");
+                printf("%zu\t0\t%d\t0\t\t0\t0\t0\t%s%s\n", i, t, mp, t ? p->analysis.fp.string() : "");
                 continue;
             }
             const char *proc = ""; double score = 0; bool mal = false; double pm = 0;
             analysis_context_get_process_info(ac, &proc, &score);
             analysis_context_get_malware_info(ac, &mal, &pm);
-            printf("%zu\t1\t%d\t%d\t%s\t%.17g\t%d\t%.17g\t%s\n", i,
+            printf("%zu\t1\t%d\t%d\t%s\t%.17g\t%d\t%.17g\t%s%s\n", i,
                    (int)analysis_context_get_fingerprint_type(ac),
                    (int)analysis_context_get_fingerprint_status(ac),
-                   proc ? proc : "", score, (int)mal, pm,
+                   proc ? proc : "", score, (int)mal, pm, mp,
                    analysis_context_get_fingerprint_string(ac));
         }
         mercury_packet_processor_destruct(p);
     } else if (mode == "attr") {
         mercury_packet_processor p = mercury_packet_processor_construct(mc);
         for (size_t i = 0; i < pkts.size(); i++) {
-            struct timespec ts{1700000000, 0};
+            struct timespec ts{(time_t)tsv[i], 0};
             const analysis_context *ac = mercury_packet_processor_get_analysis_context_linktype(
                 p, (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
             std::string attrs, os, alpn;
@@ -240,7 +251,7 @@ int main(int argc, char **argv) {
                 auto start = std::chrono::steady_clock::now();
                 do {
                     for (size_t i = lo; i < hi; i++) {
-                        struct timespec ts{1700000000, 0};
+                        struct timespec ts{(time_t)tsv[i], 0};
                         if (an_entry)
                             mercury_packet_processor_get_analysis_context_linktype(p, (uint8_t *)pkts[i].data,
                                                                                    pkts[i].len, &ts, pkts[i].linktype);

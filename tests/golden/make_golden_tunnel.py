@@ -10,6 +10,7 @@ Outputs (committed):
                             and the scenarios of tests/tunnel_synth.py
   tunnel_fp_<cfg>.tsv.gz    reference output per packet (write_json path):
                             idx, emit, fp_type, truncated, fingerprint
+  tunnel_json_<cfg>.txt.gz  the write_json record text per packet (t0, vx, none)
   tunnel_manifest.json      configurations, sources, counts
 """
 import gzip
@@ -34,6 +35,9 @@ CONFIGS = {
     "vx": f"{BASE},vxlan",                                   # one tunnel type only
     "none": BASE,                                           # IP-in-IP only (always walked)
 }
+
+
+JSON_KEYS = ["t0", "vx", "none"]
 
 
 def ref_fp(path, cfg):
@@ -62,6 +66,15 @@ def main():
         rows = [l.split(b"\t") for l in out.splitlines()]
         counts[key] = {"emit": sum(int(r[1]) for r in rows), "fingerprints": sum(r[2] != b"0" for r in rows),
                        "truncated": sum(int(r[3]) for r in rows)}
+    # the whole write_json record text (encapsulations arrays, QUIC objects)
+    for key in JSON_KEYS:
+        js = subprocess.run([REF, "json", tmp, CONFIGS[key], "-"], capture_output=True,
+                            check=True).stdout.decode("latin-1")
+        lines = js.split("\n")[:len(desc)]
+        with gzip.open(os.path.join(HERE, f"tunnel_json_{key}.txt.gz"), "wt", encoding="latin-1") as f:
+            f.write("\n".join(lines) + "\n")
+        counts[key]["json_lines"] = sum(1 for l in lines if l)
+        counts[key]["encapsulations"] = sum('"encapsulations"' in l for l in lines)
     os.unlink(tmp)
     manifest = {"reference": "cisco/mercury 2.18.0 (/root/reference), libmerc built by oracle/Makefile.ref",
                 "driver": "oracle/_ref/merc_ref_drv fp <batch> <config> -", "configs": CONFIGS,

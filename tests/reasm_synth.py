@@ -186,3 +186,128 @@ def scenarios(seed=0x5EED000F):
             data, off = p[j]
             out.append((f"rand{r}.{j}", f.pkt(data, off)))
     return out
+
+
+def timed_scenarios(seed=0x5EED0010, t0=1700000000):
+    """A second stream with per-packet capture times (seconds), run by its own
+    processor: flows that stall past the 15 s reassembly timeout
+    (reassembly_flow_context::is_expired reassembly.hpp:307) and are reaped or
+    continued, a time going backwards (the unsigned difference wraps), SYN /
+    RST / FIN segments carrying data in the middle of a flow (skipped by the
+    analysis_context path, pkt_proc.cc:1631-1633, fed to the flow by
+    write_json), and non-TCP packets between segments
+    (flow_state_pkts_needed keeps its value).  At most three flows are in
+    reassembly at a time.  Returns [(label, frame, seconds)]."""
+    rng = np.random.default_rng(seed)
+    out = []
+    port = [41000]
+    t = [t0]
+
+    def flow(**kw):
+        port[0] += 1
+        return Flow(port[0], **kw)
+
+    def ch(name="timed.example.com"):
+        prof = ["chrome", "firefox", "safari", "openssl"][int(rng.integers(4))]
+        return synth.client_hello(rng, prof, name)
+
+    def add(label, frame, dt=1):
+        t[0] += dt
+        out.append((label, frame, t[0]))
+
+    def split(d, k):
+        c = cuts(len(d), k, rng)
+        return [(d[c[j]:c[j + 1]], c[j]) for j in range(len(c) - 1)]
+
+    udp_pkt = synth.eth(synth.ipv4(synth.udp(b"\x12\x34" + bytes(30), 5353, 5353), 17))
+    arp = bytes(12) + b"\x08\x06" + bytes(28)
+    for r in range(6):
+        # in time
+        f = flow(); p = split(ch(), 3)
+        for j, (d, o) in enumerate(p):
+            add(f"ok{r}.{j}", f.pkt(d, o), dt=int(rng.integers(0, 7)))
+        # a stall past the timeout before the last segment
+        f = flow(); p = split(ch(), 3)
+        add(f"stall{r}.0", f.pkt(*p[0]))
+        add(f"stall{r}.1", f.pkt(*p[1]), dt=3)
+        add(f"stall{r}.2", f.pkt(*p[2]), dt=15 + int(rng.integers(0, 5)))
+        # exactly at / just under the timeout
+        f = flow(); p = split(ch(), 2)
+        add(f"edge{r}.0", f.pkt(*p[0]))
+        add(f"edge{r}.1", f.pkt(*p[1]), dt=14 + (r & 1))
+        # other traffic between segments (the analysis path's flag is sticky)
+        f = flow(); p = split(ch(), 3)
+        add(f"mix{r}.0", f.pkt(*p[0]))
+        add(f"mix{r}.udp", udp_pkt)
+        add(f"mix{r}.arp", arp)
+        add(f"mix{r}.1", f.pkt(*p[1]))
+        add(f"mix{r}.ack", f.pkt(b"", 0, flags=0x10))
+        add(f"mix{r}.2", f.pkt(*p[2]))
+        # control flags on data segments
+        f = flow(); p = split(ch(), 4)
+        add(f"ctl{r}.0", f.pkt(*p[0]))
+        add(f"ctl{r}.rst", f.pkt(*p[1], flags=0x14 if r & 1 else 0x04))
+        add(f"ctl{r}.2", f.pkt(*p[2]))
+        add(f"ctl{r}.fin", f.pkt(*p[3], flags=0x19))
+        f = flow(); p = split(ch(), 2)
+        add(f"syn{r}.0", f.pkt(*p[0], flags=0x02 if r & 1 else 0x12))
+        add(f"syn{r}.1", f.pkt(*p[1]))
+        # an abandoned flow, then a new one on another port much later
+        f = flow(); p = split(ch(), 3)
+        add(f"abandon{r}.0", f.pkt(*p[0]))
+        g = flow(); q = split(ch(), 2)
+        add(f"later{r}.0", g.pkt(*q[0]), dt=30)
+        add(f"later{r}.1", g.pkt(*q[1]))
+        # the time going backwards inside a flow
+        f = flow(); p = split(ch(), 2)
+        add(f"back{r}.0", f.pkt(*p[0]))
+        add(f"back{r}.1", f.pkt(*p[1]), dt=-5)
+        t[0] += 10
+    return out
+
+
+def tunnel_scenarios(seed=0x5EED0011):
+    """ClientHellos split over two or three TCP segments inside tunnels (IP-in-IP
+    over IPv4 / IPv6, GRE, GRE over UDP, VXLAN, Geneve, two levels): the
+    reassembled record keeps the completing packet's "encapsulations"
+    (pkt_proc.cc:1231-1233).  Returns [(label, frame)]."""
+    from tests import tunnel_synth as T
+    rng = np.random.default_rng(seed)
+    out = []
+
+    def wrap(kind, inner_ip, v6_inner):
+        eth_in = T.eth_inner(inner_ip, v6=v6_inner)
+        if kind == "ipip4":
+            return synth.eth(T.ip4(inner_ip, 41 if v6_inner else 4))
+        if kind == "ipip6":
+            return synth.eth(T.ip6(inner_ip, 41 if v6_inner else 4), 0x86dd)
+        if kind == "gre":
+            return synth.eth(T.ip4(T.gre(inner_ip, 0x86dd if v6_inner else 0x0800), 47))
+        if kind == "gre_csum":
+            return synth.eth(T.ip4(T.gre(inner_ip, 0x86dd if v6_inner else 0x0800, csum=True), 47))
+        if kind == "gre_udp":
+            return synth.eth(T.ip4(synth.udp(T.gre(inner_ip, 0x86dd if v6_inner else 0x0800), 50000, 4754), 17))
+        if kind == "vxlan":
+            return synth.eth(T.ip4(synth.udp(T.vxlan(eth_in), 50001, 4789), 17))
+        if kind == "geneve":
+            return synth.eth(T.ip4(synth.udp(T.geneve(eth_in), 50002, 6081), 17))
+        if kind == "vxlan6":
+            return synth.eth(T.ip6(synth.udp(T.vxlan(eth_in), 50001, 4789), 17), 0x86dd)
+        if kind == "gre_in_ipip":
+            return synth.eth(T.ip4(T.ip4(T.gre(inner_ip, 0x86dd if v6_inner else 0x0800), 47), 4))
+        raise ValueError(kind)
+
+    kinds = ["ipip4", "ipip6", "gre", "gre_csum", "gre_udp", "vxlan", "geneve", "vxlan6", "gre_in_ipip"]
+    sport = 42000
+    for r in range(2):
+        for kind in kinds:
+            sport += 1
+            v6_inner = bool(r & 1)
+            prof = ["chrome", "firefox", "safari", "openssl"][int(rng.integers(4))]
+            d = synth.client_hello(rng, prof, f"{kind}.tunnel.example.com")
+            c = cuts(len(d), 2 + (sport & 1), rng)
+            for j in range(len(c) - 1):
+                l4 = synth.tcp(d[c[j]:c[j + 1]], sport=sport, dport=443, seq=5000 + c[j])
+                inner_ip = T.ip6(l4, 6) if v6_inner else T.ip4(l4, 6, src=0x0a000105, dst=0x5db8d822)
+                out.append((f"tun_{kind}{r}.{j}", wrap(kind, inner_ip, v6_inner)))
+    return out

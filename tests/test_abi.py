@@ -83,3 +83,42 @@ def test_record_layout_matches_header():
     assert "uint64_t offset;" in hdr and mercury_amd.DESC_DTYPE.itemsize == 16
     assert mercury_amd.RECORD_DTYPE.itemsize == 32
     assert ctypes.sizeof(ctypes.c_void_p) == 8
+
+
+def libmerc_h_symbols():
+    """Every function /root/reference/src/libmerc/libmerc.h declares
+    (tests/golden/libmerc_h_symbols.txt, made by make_libmerc_symbols.py)."""
+    with open(os.path.join(ROOT, "tests", "golden", "libmerc_h_symbols.txt")) as f:
+        return [s.strip() for s in f if s.strip()]
+
+
+def test_every_libmerc_h_function_is_exported():
+    names = libmerc_h_symbols()
+    assert len(names) == 31 and "mercury_print_git_commit" in names and "get_stats_aggregator_num_entries" in names
+    missing = set(names) - exported_symbols()
+    assert not missing, missing
+    # and each is declared in the drop-in header
+    assert not set(names) - declared_symbols()
+
+
+def test_libmerc_link_program(tmp_path):
+    """A C program calling every libmerc.h function compiles against
+    include/mercury_amd_libmerc.h and links against libmercury_amd.so alone;
+    on the CPU the packet calls fail softly (0 / NULL, logged) and the rest
+    answer as the reference's do (libmerc.cc:59-90, 242-253, 377-396, 477-484)."""
+    exe = str(tmp_path / "libmerc_link")
+    lib_dir = os.path.dirname(mercury_amd.library_path())
+    subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "libmerc_link.c"), "-L" + lib_dir, "-l:libmercury_amd.so",
+                    "-Wl,-rpath," + lib_dir, "-o", exe], check=True)
+    src = open(os.path.join(ROOT, "tests", "c", "libmerc_link.c")).read()
+    called = {n for n in libmerc_h_symbols() if re.search(r"\b" + n + r"\s*\(", src)}
+    assert called == set(libmerc_h_symbols())
+    out = subprocess.run([exe], capture_output=True, text=True, check=True, timeout=120).stdout
+    kv = dict(line.split(" ", 1) for line in out.strip().splitlines())
+    assert kv["version_string"] == "2.18.0" and kv["print_version"] == "2.18.0"
+    assert kv["version_number"] == str((2 << 16) | (18 << 8))
+    assert kv["init_with_stats"] == "0" and kv["init"] == "1"          # do_stats refused at init
+    assert kv["write_stats"] == "0" and kv["stats_entries"] == "0"
+    assert kv["fdc"] == "-4" and kv["finalize"] == "0" and kv["logged"] == "1"
+    assert kv["accessors"] == "0 0 0 0 0 0 0 0 0"

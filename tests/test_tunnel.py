@@ -70,3 +70,24 @@ def test_tunnels_vs_reference(key):
     # IP-in-IP chains are regular (the JSON writer rebuilds their entries)
     enc = (rec["flags"] & 32) != 0
     assert enc.sum() >= (50 if key in ("t0", "t1") else 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["t0", "vx", "none"])
+def test_tunnel_json_vs_reference(key):
+    """The whole write_json text of every packet of the tunnel stream:
+    "encapsulations" arrays of GRE (over IP and UDP 4754), VXLAN, Geneve and
+    IP-in-IP levels (outer IPv6 extension headers included), rebuilt by the
+    host walk of mfp_encap.hpp, byte-identical to the reference; nothing is
+    skipped."""
+    from tests import test_json
+    arena, desc, sources = load()
+    ctx = mercury_amd.Context(MANIFEST["configs"][key], device=0)
+    try:
+        rec, fp = ctx.process_host(arena, desc)
+    finally:
+        ctx.close()
+    lines, skipped = mercury_amd.write_json(arena, desc, rec, fp, ts_ns=np.full(len(desc), test_json.TS, np.uint64),
+                                            threads=2)
+    test_json._check(lines, test_json._golden_lines(f"tunnel_json_{key}.txt.gz"), skipped)
+    assert skipped == 0
