@@ -110,11 +110,15 @@ enum {
     MFP_FLAG_ENCAP       = 32, /* reached through IP-in-IP encapsulation (pkt_proc.cc:959) */
     MFP_FLAG_NO_CIPHERS  = 64, /* (D)TLS ClientHello with an empty cipher-suite list: the
                                   reference writes no "tls"/"dtls" object for it (tls.h:1882-1885) */
-    MFP_FLAG_SIDECAR     = 128,/* device arena (QUIC): sni/ua spans index the sidecar that follows
-                                  the string's hash, at fp_offset + round_up(fp_len, 8) + 8:
-                                  {u16 alpn_off, u16 alpn_len} then the server name, the QUIC
-                                  user agent and the ALPN list, which exist only in the decrypted
-                                  payload.  Cleared (spans absent) when strings are packed. */
+    MFP_FLAG_SIDECAR     = 128,/* QUIC: a sidecar follows the string's hash, at fp_offset +
+                                  round_up(fp_len, 8) + 8 (also when fp_len is 0): a header
+                                  {u16 alpn_off, u16 alpn_len, u16 side_len (bytes of the
+                                  sidecar), u16 json_off (0: none)}, then the server name, the
+                                  QUIC user agent and the ALPN list, which exist only in the
+                                  decrypted payload (sni/ua spans index the sidecar); contexts in
+                                  MFP_MODE_WRITE_JSON add at json_off what the JSON writer prints
+                                  (the plaintext, the handshake bytes, the cc frame's place, the
+                                  salt).  Packed host arenas keep it. */
 };
 /* For MFP_MSG_TLS_SH / MFP_MSG_TLS_CERT records sni_off/sni_len hold the
  * certificate_list datum (tls.h:275-296), the bytes the JSON writer's
@@ -148,6 +152,7 @@ enum {
     MFP_SEG_TCP = 8,            /* a TCP packet with a whole header (tcp_packet::is_valid)     */
     MFP_SEG_SYN_RST = 16,       /* SYN, SYN/ACK or RST: analyze_ip_packet skips it in reassembly
                                    mode (pkt_proc.cc:1632-1634)                                */
+    MFP_SEG_IP = 32,            /* the link layer led to an IP packet: analyze_ip_packet ran    */
 };
 
 /* semantics of the reference entry point to follow */
@@ -194,9 +199,9 @@ MFP_EXPORT int mfp_process_batch_device(mfp_context ctx, const uint8_t *d_arena,
                                         uint64_t *d_fp_used, void *stream);
 
 /* Host batch: copies arena/descriptors to the device, runs, copies back.
- * The strings come back packed in packet order (fp_arena holds exactly the
- * sum of fp_len).  Synchronous.  Returns bytes of fp arena used, or a
- * negative error. */
+ * The strings come back packed in packet order (fp_arena holds the strings
+ * back to back, each QUIC record's sidecar right behind its string).
+ * Synchronous.  Returns bytes of fp arena used, or a negative error. */
 MFP_EXPORT long long mfp_process_batch_host(mfp_context ctx, const uint8_t *arena, size_t arena_len,
                                             const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                             char *fp_arena, size_t fp_cap);
@@ -315,7 +320,8 @@ MFP_EXPORT long long mfp_process_batch_reassembly_analysis(mfp_context ctx, mfp_
  * whose flow was truncated (timeout, max segments, ...) is "unlabeled"
  * (pkt_proc.cc:1716-1719).  more_pkts[i] (optional) =
  * analysis_context::flow_state_pkts_needed after packet i: cleared by every
- * TCP packet, set while its flow is in reassembly, kept by other packets
+ * packet that reaches the IP layer (analysis_context::reinit result.h:434-440),
+ * set while its TCP flow is in reassembly, kept by packets that are not IP
  * (the state carries across calls in r). */
 MFP_EXPORT long long mfp_process_batch_reassembly_context(mfp_context ctx, mfp_reassembler r, const uint8_t *arena,
                                                           size_t arena_len, const mfp_pkt_desc *desc, size_t n,
@@ -472,15 +478,16 @@ MFP_EXPORT long long mfp_tpacket3_block(const uint8_t *arena_base, const uint8_t
 /* ---- JSON records (host only, no device needed) ----
  * Replaces the record text of stateful_pkt_proc::write_json
  * (pkt_proc.cc:1157-1253, metadata_output off, no --analysis object;
- * IP-in-IP "encapsulations" arrays included): one
+ * "encapsulations" arrays, QUIC "tls"/"quic" objects included): one
  * line per record with MFP_FLAG_EMIT, byte-identical to the reference, built
  * from records + packet arena + fp arena as mfp_process_batch_host /
  * mfp_process_pipelined return them.  ts_ns (optional): per-packet time; 0 or
  * NULL = now (pkt_proc.cc:1086-1089).  line_end[i] = end offset of packet
  * i's line in out (its line is [line_end[i-1], line_end[i]), empty when the
  * reference writes nothing).  *skipped (optional) = emitted records this
- * writer cannot rebuild exactly (IP-in-IP with an outer IPv6 header that
- * has extension headers: its "encapsulations" entry); they get an empty line.  `threads` host threads.
+ * writer cannot rebuild (a QUIC record without its sidecar, i.e. fingerprinted
+ * in MFP_MODE_ANALYSIS, or an encapsulation chain the host walk cannot
+ * follow); they get an empty line.  `threads` host threads.
  * Returns the bytes written, -1 on bad arguments, -2 when out_cap is too
  * small (nothing written; mfp_last_error() names the size needed). */
 MFP_EXPORT long long mfp_write_json_batch(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,

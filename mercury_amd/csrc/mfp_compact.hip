@@ -9,6 +9,9 @@
 // rewritten to point there.  Three launches: per-block scan of fp_len,
 // single-block scan of the block totals, then one wave per 64 records copies
 // the strings with coalesced byte moves (lane l moves bytes l, l+64, ...).
+// A record with a sidecar (MFP_FLAG_SIDECAR, QUIC) keeps it: its packed span
+// is string, padding to 8, hash, sidecar (side_len from the sidecar header),
+// so the record's spans stay valid; the packed total replaces used[2].
 #include <hip/hip_runtime.h>
 
 #include "../../include/mfp.h"
@@ -18,12 +21,22 @@ namespace mfpk {
 
 constexpr int B = 256;   // records per scan block
 
-__global__ __launch_bounds__(B) void k_len_scan(const mfp_record *rec, uint64_t n, uint32_t *local,
+// bytes a record takes in the packed arena
+__device__ __forceinline__ uint32_t packed_len(const mfp_record &r, const uint8_t *src) {
+    if (r.flags & MFP_FLAG_SIDECAR) {
+        const uint8_t *sc = src + r.fp_offset + ((r.fp_len + 7) & ~7u) + 8;
+        return ((r.fp_len + 7) & ~7u) + 8 + ((uint32_t)sc[4] | (uint32_t)sc[5] << 8);
+    }
+    return r.fp_type ? r.fp_len : 0u;
+}
+
+__global__ __launch_bounds__(B) void k_len_scan(const mfp_record *rec, uint64_t n, const uint8_t *src, uint32_t *local,
                                                 unsigned long long *block_sum) {
     __shared__ uint32_t wsum[B / 64];
     const uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t len = i < n && rec[i].fp_type ? rec[i].fp_len : 0u;
+    uint32_t len = 0;
+    if (i < n) { const mfp_record r = rec[i]; len = packed_len(r, src); }
     uint32_t incl = len;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -43,7 +56,8 @@ __global__ __launch_bounds__(B) void k_len_scan(const mfp_record *rec, uint64_t 
 }
 
 // exclusive scan of the block totals in place (one block; any count)
-__global__ __launch_bounds__(1024) void k_block_scan(unsigned long long *block_sum, uint64_t nb) {
+__global__ __launch_bounds__(1024) void k_block_scan(unsigned long long *block_sum, uint64_t nb,
+                                                    unsigned long long *total) {
     __shared__ unsigned long long carry;
     __shared__ unsigned long long wsum[16];
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -70,6 +84,7 @@ __global__ __launch_bounds__(1024) void k_block_scan(unsigned long long *block_s
         if (threadIdx.x == 0) carry += tot;
         __syncthreads();
     }
+    if (threadIdx.x == 0 && total) *total = carry;
 }
 
 __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t n, const uint32_t *local,
@@ -84,7 +99,7 @@ __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t 
         uint32_t len = 0;
         if (i < n) {
             const mfp_record r = rec[i];
-            len = r.fp_type ? r.fp_len : 0u;
+            len = packed_len(r, src);
             so = r.fp_offset;
             dof = block_sum[i / B] + local[i];
         }
@@ -99,26 +114,23 @@ __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t 
         }
         if (i < n && len) {
             rec[i].fp_offset = dof;
-            rec[i].flags &= (uint8_t)~MFP_FLAG_HASHED;   // the hashes stay behind
-            if (rec[i].flags & MFP_FLAG_SIDECAR) {       // ... and so do QUIC sidecars (include/mfp.h)
-                rec[i].flags &= (uint8_t)~MFP_FLAG_SIDECAR;
-                rec[i].sni_off = 0; rec[i].sni_len = 0xffff;
-                rec[i].ua_off = 0; rec[i].ua_len = 0xffff;
-            }
+            rec[i].flags &= (uint8_t)~MFP_FLAG_HASHED;   // (a sidecar keeps the hash's 8 bytes as padding)
         }
     }
 }
 
 }  // namespace mfpk
 
-// scratch: local = u32[n], block_sum = u64[(n + 255) / 256]
+// scratch: local = u32[n], block_sum = u64[(n + 255) / 256]; *total (device) =
+// the packed bytes
 extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
-                                  unsigned long long *block_sum, hipStream_t stream, mfp_prof *prof) {
+                                  unsigned long long *block_sum, unsigned long long *total, hipStream_t stream,
+                                  mfp_prof *prof) {
     if (n == 0) return 0;
     const uint64_t nb = (n + mfpk::B - 1) / mfpk::B;
     if (prof) mfp_prof_begin(prof, "k_compact", stream);
-    hipLaunchKernelGGL(mfpk::k_len_scan, dim3((uint32_t)nb), dim3(mfpk::B), 0, stream, rec, n, local, block_sum);
-    hipLaunchKernelGGL(mfpk::k_block_scan, dim3(1), dim3(1024), 0, stream, block_sum, nb);
+    hipLaunchKernelGGL(mfpk::k_len_scan, dim3((uint32_t)nb), dim3(mfpk::B), 0, stream, rec, n, src, local, block_sum);
+    hipLaunchKernelGGL(mfpk::k_block_scan, dim3(1), dim3(1024), 0, stream, block_sum, nb, total);
     uint64_t cb = (n + 255) / 256;
     if (cb > 2048) cb = 2048;
     hipLaunchKernelGGL(mfpk::k_compact_copy, dim3((uint32_t)cb), dim3(256), 0, stream, rec, n, local, block_sum, src, dst);

@@ -1900,6 +1900,7 @@ DEV bool gre_next(Cur &p) {
 // IP layer: ip_write_json pkt_proc.cc:1063 / analyze_ip_packet pkt_proc.cc:1597
 template <uint32_t FAM, class E>
 DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
+    if (cfg.seg) o.seg_kind = MFP_SEG_IP;   // analyze_ip_packet runs: analysis.reinit() (pkt_proc.cc:1609)
     const uint8_t *iph; int ipv;
     uint32_t proto = ip_parse(pkt, iph, ipv);
     uint32_t enc = 0;            // net bits 20-27: levels, v6 mask, irregular (include/mfp.h)
@@ -1977,7 +1978,7 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         if (cfg.seg) {
             // every whole TCP header resets flow_state_pkts_needed on the analysis
             // path, which skips SYN, SYN/ACK and RST (pkt_proc.cc:1629-1634)
-            o.seg_kind = MFP_SEG_TCP | ((fl & 0x06) ? MFP_SEG_SYN_RST : 0u);
+            o.seg_kind |= MFP_SEG_TCP | ((fl & 0x06) ? MFP_SEG_SYN_RST : 0u);
             if (!(syn && cfg.mode == MFP_MODE_WRITE_JSON) && clen(pkt) > 0) {   // process_tcp_data's data segments
                 o.seq = (ld(tcph + 4) << 24) | (ld(tcph + 5) << 16) | (ld(tcph + 6) << 8) | ld(tcph + 7);
                 o.seg_kind |= MFP_SEG_DATA;

@@ -45,7 +45,8 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
 extern "C" size_t mfp_quic_scratch_bytes(uint32_t grid);
 
 extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
-                                  unsigned long long *block_sum, hipStream_t stream, mfp_prof *prof);
+                                  unsigned long long *block_sum, unsigned long long *total, hipStream_t stream,
+                                  mfp_prof *prof);
 
 
 static thread_local std::string g_err;
@@ -694,8 +695,10 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     }
     // strings to a dense arena in packet order (d_fp2, d_used[2] bytes), records re-pointed;
     // the bin lists in d_work are dead by now and hold the scan scratch
-    if (mfp_launch_compact(S.d_rec, n, (const uint8_t *)S.d_fp, (uint8_t *)S.d_fp2, S.d_work,
-                           (unsigned long long *)(S.d_work + ((n + 3) & ~(size_t)1)), S.stream, c->prof) != 0) {
+    // (the packed total, strings and QUIC sidecars, replaces d_used[2])
+    if (n && mfp_launch_compact(S.d_rec, n, (const uint8_t *)S.d_fp, (uint8_t *)S.d_fp2, S.d_work,
+                                (unsigned long long *)(S.d_work + ((n + 3) & ~(size_t)1)), S.d_used + 2, S.stream,
+                                c->prof) != 0) {
         mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

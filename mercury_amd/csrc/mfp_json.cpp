@@ -705,14 +705,189 @@ void write_reassembled(W &w, uint16_t props) {
     w.put('}');
 }
 
+// ---- QUIC Initial records (quic_init::write_json quic.h:1662-1690, the
+// pre-decrypted quic_init_decry::write_json quic.h:1438-1452): the long header
+// fields come from the packet, the plaintext, the handshake bytes, the cc
+// frame's place and the decryption salt from k_quic's sidecar (include/mfp.h)
+struct QuicJson {
+    const uint8_t *pay = nullptr, *pt = nullptr, *hs = nullptr;
+    uint32_t pay_len = 0, pt_len = 0, hs_len = 0, cc_off = 0xffff, salt = 0xff;
+    bool pre = false, hello = false;
+};
+
+uint32_t rd16le(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
+
+bool quic_block(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const char *fp_arena, QuicJson &q) {
+    if (!(r.flags & MFP_FLAG_SIDECAR)) return false;
+    const uint8_t *sc = (const uint8_t *)fp_arena + r.fp_offset + ((r.fp_len + 7) & ~7u) + 8;
+    const uint32_t jo = rd16le(sc + 6);
+    if (!jo) return false;
+    const uint8_t *j = sc + jo;
+    const uint32_t po = rd16le(j);
+    q.pay_len = rd16le(j + 2); q.pt_len = rd16le(j + 4); q.hs_len = rd16le(j + 6); q.cc_off = rd16le(j + 8);
+    q.pre = j[10] & 1; q.hello = (j[10] >> 1) & 1; q.salt = j[11];
+    if ((uint64_t)po + q.pay_len > caplen) return false;
+    q.pay = pkt + po;
+    q.pt = j + 16;
+    q.hs = q.pt + q.pt_len;
+    return true;
+}
+
+// datum::parse: too short nulls both (datum.h:294-304)
+mfpe::Cur take(mfpe::Cur &d, long n) {
+    mfpe::Cur r{nullptr, nullptr};
+    if (d.null() || n < 0 || d.len() < n) { d.nullify(); return r; }
+    r.d = d.d; r.e = d.d + n; d.d += n;
+    return r;
+}
+// variable_length_integer (quic_vli.hpp): a short read nulls the datum
+uint64_t vli(mfpe::Cur &d) {
+    uint64_t b = 0;
+    if (!d.rd(1, b)) return 0;
+    const int len = (b & 0xc0) == 0xc0 ? 8 : (b & 0xc0) == 0x80 ? 4 : (b & 0xc0) == 0x40 ? 2 : 1;
+    uint64_t v = b & 0x3f, x = 0;
+    for (int k = 1; k < len; k++) { if (!d.rd(1, x)) return 0; v = v * 256 + x; }
+    return v;
+}
+
+void quic_cc(W &w, Obj &qo, const uint8_t *f, const uint8_t *end) {   // quic_frame::write_json (quic.h:1184-1200)
+    mfpe::Cur d{f + 1, end};
+    const uint8_t t = f[0];
+    if (t == 0x1c) {                                       // connection_close quic.h:354-372
+        const uint64_t ec = vli(d), ft = vli(d), rl = vli(d);
+        const mfpe::Cur rp = take(d, (long)rl);
+        if (rp.null() || rp.len() <= 0) return;
+        qo.key("connection_close");
+        w.puts("{\"error_code\":"); w.udec(ec);
+        w.puts(",\"frame_type\":"); w.udec(ft);
+        w.puts(",\"reason_phrase\":\""); w.utf8(rp.d, (size_t)rp.len()); w.puts("\"}");
+        return;
+    }
+    // ack (quic.h:123-150) / ack_ecn (quic.h:160-178)
+    const uint64_t la = vli(d), dl = vli(d), rc = vli(d), fr = vli(d);
+    bool ok = true;
+    if (rc > 1000) ok = false;
+    else for (uint64_t k = 0; k < rc && d.len() > 0; k++) { vli(d); vli(d); }
+    if (d.null()) ok = false;
+    auto ack = [&]() {
+        w.puts("{\"largest_acked\":"); w.udec(la); w.puts(",\"ack_delay\":"); w.udec(dl);
+        w.puts(",\"ack_range_count\":"); w.udec(rc); w.puts(",\"first_ack_range\":"); w.udec(fr); w.put('}');
+    };
+    if (t == 0x02) {
+        if (ok) { qo.key("ack"); ack(); }
+        return;
+    }
+    if (!ok) return;                                       // ack_ecn keeps reading from a null datum: invalid
+    const uint64_t e0 = vli(d), e1 = vli(d), ce = vli(d);
+    if (d.null()) return;
+    qo.key("ack_ecn");
+    w.puts("{\"ect0\":"); w.udec(e0); w.puts(",\"ect1\":"); w.udec(e1); w.puts(",\"ecn_ce\":"); w.udec(ce);
+    w.puts(",\"ack\":"); ack(); w.put('}');
+}
+
+// the "tls" object of a QUIC hello (tls_client_hello::write_json tls.h:1882-1917,
+// metadata off): the first server_name, every quic_transport_parameters
+// extension with the user agents inside it (tls.h:1264-1311)
+void quic_tls(W &w, Obj &rec, const uint8_t *hs, uint32_t hs_len) {
+    mfpe::Cur d{hs, hs + hs_len};
+    if (d.len() < 4) return;                               // tls_handshake::parse tls.h:244-262
+    uint64_t mt, hl;
+    d.rd(1, mt); d.rd(3, hl);
+    if (hl > 32768) return;
+    mfpe::Cur p{d.d, hl < (uint64_t)d.len() ? d.d + hl : d.e};
+    // tls_client_hello::parse tls.h:1811-1869 (QUIC: no DTLS cookie)
+    const mfpe::Cur ver = take(p, 2);
+    if (ver.null() || ver.len() <= 0) return;
+    take(p, 32);
+    uint64_t l = 0;
+    if (!p.rd(1, l)) return;
+    take(p, (long)l);
+    if (!p.rd(2, l) || (l & 1)) return;
+    const mfpe::Cur ciphers = take(p, (long)l);
+    if (!p.rd(1, l)) return;
+    const mfpe::Cur comp = take(p, (long)l);
+    if (comp.null() || comp.len() <= 0) return;            // hello.is_not_empty()
+    if (ciphers.null() || ciphers.len() == 0) return;     // ciphersuite_vector.is_not_readable()
+    mfpe::Cur ext{nullptr, nullptr};
+    if (p.rd(2, l)) { ext.d = p.d; ext.e = p.d + ((long)l < p.len() ? (long)l : p.len()); }   // parse_soft_fail
+    rec.key("tls");
+    w.puts("{\"client\":{");
+    Obj cl{w};
+    // get_server_name (tls.h:1052-1080): the first SNI extension, past its 5-byte header
+    for (mfpe::Cur e = ext; e.len() > 0;) {
+        const uint8_t *st = e.d;
+        uint64_t t, el;
+        if (!e.rd(2, t) || !e.rd(2, el) || !e.skip((long)el)) break;
+        if (t == 0) {
+            mfpe::Cur sn{st, e.d};
+            sn.skip(9);
+            if (!sn.null() && sn.len() > 0) { cl.key("server_name"); w.put('"'); w.utf8(sn.d, (size_t)sn.len()); w.put('"'); }
+            break;
+        }
+    }
+    for (mfpe::Cur e = ext; e.len() > 0;) {
+        const uint8_t *st = e.d;
+        uint64_t t, el;
+        if (!e.rd(2, t) || !e.rd(2, el) || !e.skip((long)el)) break;
+        if (t != 0x0039 && t != 0xffa5) continue;
+        if (t == 0x0039) cl.key("quic_transport_parameters"); else cl.key("quic_transport_parameters_draft");
+        w.put('"'); w.hexb(st, (size_t)(e.d - st)); w.put('"');
+        mfpe::Cur q{st + 4, e.d};
+        while (q.len() > 0) {                              // quic_transport_parameter tls.h:1237-1262
+            const uint64_t id = vli(q);
+            const uint64_t vl = vli(q);
+            const mfpe::Cur v = take(q, (long)vl);
+            if (id == 0x3129 && !v.null() && v.len() > 0) {
+                cl.key("google_user_agent"); w.put('"'); w.utf8(v.d, (size_t)v.len()); w.put('"');
+            }
+        }
+    }
+    w.puts("}}");
+}
+
+bool write_quic(W &w, Obj &rec, const QuicJson &q) {
+    static const char *salts[6] = {"d22", "d23_d28", "d29_d32", "d33_v1", "d1_d7_v2", "v2"};
+    if (q.hello && q.hs_len) quic_tls(w, rec, q.hs, q.hs_len);
+    // quic_initial_packet::write_json quic.h:531-540, fields re-read from the long header
+    mfpe::Cur d{q.pay, q.pay + q.pay_len};
+    uint64_t ci = 0, n = 0;
+    d.rd(1, ci);
+    const mfpe::Cur ver = take(d, 4);
+    d.rd(1, n);
+    const mfpe::Cur dcid = take(d, (long)n);
+    d.rd(1, n);
+    const mfpe::Cur scid = take(d, (long)n);
+    const uint64_t tl = vli(d);
+    const mfpe::Cur token = take(d, (long)tl);
+    auto hex = [&](const mfpe::Cur &c) { w.put('"'); if (!c.null() && c.len() > 0) w.hexb(c.d, (size_t)c.len()); w.put('"'); };
+    rec.key("quic");
+    w.put('{');
+    Obj qo{w};
+    qo.key("connection_info");
+    w.put('"'); for (int b = 7; b >= 0; b--) w.put((ci >> b) & 1 ? '1' : '0'); w.put('"');
+    qo.key("version"); hex(ver);
+    qo.key("dcid"); hex(dcid);
+    qo.key("scid"); hex(scid);
+    qo.key("token"); hex(token);
+    if (q.cc_off != 0xffff && q.cc_off < q.pt_len) quic_cc(w, qo, q.pt + q.cc_off, q.pt + q.pt_len);
+    if (q.pt_len) {
+        if (!q.pre && q.salt < 6) { qo.key("salt_string"); w.put('"'); w.putz(salts[q.salt]); w.put('"'); }   // quic.h:905-907
+        qo.key("plaintext"); w.put('"'); w.hexb(q.pt, q.pt_len); w.put('"');
+    } else {
+        qo.key("raw_packet_data"); w.put('"'); w.hexb(q.pay, q.pay_len); w.put('"');
+    }
+    w.put('}');
+    return true;
+}
+
 bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint32_t linktype, const mfp_record &r,
                   const char *fp_arena,
                   uint64_t sec, uint64_t nsec, mfp_context ctx, const mfp_analysis *an, const double *ap,
                   uint16_t props) {
     if (!(r.flags & MFP_FLAG_EMIT)) return true;
-    // QUIC records carry a "quic" object with the decrypted payload
-    // (quic_init::write_json quic.h:1662-1690), which the device does not return
-    if (r.msg == MFP_MSG_QUIC) return false;
+    // QUIC records: the "tls" and "quic" objects from k_quic's sidecar
+    QuicJson qj;
+    if (r.msg == MFP_MSG_QUIC && !quic_block(pkt, caplen, r, fp_arena, qj)) return false;
 
     const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
     // the encapsulation levels above the innermost IP header (IP-in-IP, GRE,
@@ -726,6 +901,7 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint
     const size_t sni_x = r.msg == MFP_MSG_STUN ? 32 : r.msg == MFP_MSG_OPENVPN ? 16 : 6;   // object text per input byte
     o.need(1000 + (size_t)r.fp_len + sni_x * (r.sni_len == 0xffff ? 0 : r.sni_len) +
            6 * (r.ua_len == 0xffff ? 0 : r.ua_len) +
+           (r.msg == MFP_MSG_QUIC ? 2 * (size_t)(qj.pay_len + qj.pt_len) + 6 * (size_t)qj.hs_len + 600 : 0) +
            (with_an ? analysis_bound(ctx, *an) : 0));
     W w{o.buf.get() + o.len};
     // a readable, non-empty datum (print_key_json_string skips empty ones, json_object.h:104-108)
@@ -771,6 +947,9 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint
             }
             w.puts("]}}");
         }
+        break;
+    case MFP_MSG_QUIC:
+        write_quic(w, rec, qj);
         break;
     case MFP_MSG_DTLS_SH:                                // write_metadata pkt_proc_util.h:315-321
         rec.key("dtls");

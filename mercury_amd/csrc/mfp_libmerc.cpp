@@ -288,9 +288,9 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
                                            buffer_size, &end, &skipped, 1);
     }
     if (skipped) {
-        // the reference writes a record here; the writer cannot rebuild it
-        // (QUIC, GRE/VXLAN/Geneve encapsulations, IP-in-IP with an outer IPv6
-        // extension header): say so instead of returning a silent 0
+        // the reference writes a record here; the writer could not rebuild it
+        // (an encapsulation chain the host walk cannot follow): say so instead
+        // of returning a silent 0
         log_error("write_json: record not rebuilt by the MI355X JSON writer (%s)\n",
                   rec.msg == MFP_MSG_QUIC ? "QUIC Initial" : rec.msg == MFP_MSG_STUN ? "STUN message"
                   : rec.msg == MFP_MSG_OPENVPN ? "OpenVPN record" : "encapsulation chain");

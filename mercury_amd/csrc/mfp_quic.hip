@@ -297,10 +297,11 @@ struct CState {
     uint32_t total, count;
     bool first_ok;        // has_first_frame()
     Cur first;            // crypto_frames[first_frame_index].data()
+    const uint8_t *cc;    // the last connection_close / ack (/ ack_ecn) frame's type byte (quic_init::cc)
 };
 DEV void cs_reset(CState &s) {
     s.buf_len = 0; s.min_off = ~0ull; s.min_len = ~0ull; s.max_off = 0; s.max_len = 0;
-    s.total = 0; s.count = 0; s.first_ok = false; cset_null(s.first);
+    s.total = 0; s.count = 0; s.first_ok = false; cset_null(s.first); s.cc = nullptr;
 }
 // extend() + update_crypto_frames(); cb[0, hw) holds this packet's bytes
 // (written or zero: the reference's buffer starts zeroed for every packet)
@@ -321,6 +322,7 @@ DEV void cb_extend(CState &s, uint64_t off, uint64_t len, Cur data, uint8_t *cb,
 // (quic.h:1532-1552: stop at the first invalid frame).  Returns strict validity.
 DEV bool quic_frames(Cur p, bool strict, CState &s, uint8_t *cb, uint32_t &hw) {
     while (cnotempty(p)) {
+        const uint8_t *at = p.d;
         const uint32_t t = rd_u8(p);            // quic_frame ctor quic.h:1131-1152
         bool crypto = false;
         uint64_t off = 0, len = 0;
@@ -345,6 +347,9 @@ DEV bool quic_frames(Cur p, bool strict, CState &s, uint8_t *cb, uint32_t &hw) {
         }
         if (strict && cnull(p)) return false;
         if (crypto && cnotempty(data)) cb_extend(s, off, len, data, cb, hw);
+        // cc = frame: connection_close or ack, and ack_ecn outside the
+        // pre-decrypted parse (quic.h:1389-1391, 1550-1552)
+        if (t == 0x1c || t == 0x02 || (t == 0x03 && !strict)) s.cc = at;
     }
     return true;
 }
@@ -355,6 +360,11 @@ struct QRes {
     bool pre;               // pre_decrypted: fingerprinted with format 0 (quic.h:1455-1463)
     const uint8_t *ver;
     Ch ch;
+    // what quic_init::write_json prints (quic.h:1662-1690, 1438-1452)
+    Cur plain;              // the plaintext (decrypted payload, or the pre-decrypted frames)
+    Cur hs;                 // the bytes the handshake was parsed from
+    const uint8_t *cc;      // the cc frame's type byte in `plain`, or null
+    uint32_t salt;          // salt of the decryption (0..5), 0xff none
 };
 
 // quic_init ctor (quic.h:1513-1591)
@@ -362,6 +372,7 @@ DEV QRes quic_process(Cur pay, uint8_t *pt, uint8_t *cb, const uint32_t *te, uin
     QRes r;
     r.flags = 0; r.hello = false; r.pre = false; r.ver = nullptr;
     cset_null(r.ch.version); cset_null(r.ch.ciphers); cset_null(r.ch.compression); cset_null(r.ch.extensions);
+    cset_null(r.plain); cset_null(r.hs); r.cc = nullptr; r.salt = 0xff;
     const QHdr h = quic_hdr(pay);
     if (!h.valid) return r;
     r.ver = h.ver;
@@ -371,15 +382,22 @@ DEV QRes quic_process(Cur pay, uint8_t *pt, uint8_t *cb, const uint32_t *te, uin
     bool use = false;
     if ((h.ci & 0x0c) == 0) {                   // already-decrypted Initial? (quic.h:1517-1523)
         const uint32_t pnl0 = (h.ci & 3) + 1;
-        if (quic_frames(cmk(h.payload.d + pnl0, h.payload.e), true, s, cb, hw)) { r.pre = true; use = true; }
+        const Cur pl = cmk(h.payload.d + pnl0, h.payload.e);
+        if (quic_frames(pl, true, s, cb, hw)) { r.pre = true; use = true; r.plain = pl; }
     }
     if (!use) {
         cs_reset(s);                            // crypto_buffer.reset(): the bytes stay
         uint32_t pt_len = 0;
         const int dr = quic_decrypt(h, pt, te, gh, lane, pt_len);
         if (dr == -2) return r;                 // not an Initial of its version: no record
-        if (dr == 0 && pt_len) quic_frames(cmk(pt, pt + pt_len), false, s, cb, hw);
+        if (dr == 0 && pt_len) {
+            r.plain = cmk(pt, pt + pt_len);
+            bool v2 = false;
+            quic_version(ld_be32n(h.ver, 4), r.salt, v2);   // quic_crypto_engine::salt_str (quic.h:821-842)
+            quic_frames(r.plain, false, s, cb, hw);
+        }
     }
+    r.cc = s.cc;
     r.flags = MFP_FLAG_EMIT;                    // is_not_empty(): the header parsed (quic.h:1623)
     if (s.buf_len == 0) return r;               // crypto_buffer.is_valid()
     Cur d;
@@ -395,6 +413,7 @@ DEV QRes quic_process(Cur pay, uint8_t *pt, uint8_t *cb, const uint32_t *te, uin
             d = s.first;
         }
     }
+    r.hs = d;
     const Hs hs = tls_hs_parse(d);
     if ((uint32_t)hs.more) r.flags |= MFP_FLAG_TRUNCATED;   // more_bytes_needed (uint32_t)
     r.ch = tls_ch_parse(hs.body);
@@ -612,11 +631,19 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             ovpn_fp(e, v);
             if (e.valid()) { len = e.n; fp_type = 14; }
         }
-        const uint32_t side = len && !ovpn ? 4 + span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
+        // the sidecar (include/mfp.h MFP_FLAG_SIDECAR): an 8-byte header, the
+        // classifier inputs, and on the write_json path the bytes the JSON
+        // writer needs for the record's "tls" and "quic" objects (quic.h:1662-1690),
+        // present also when there is no fingerprint
+        const bool json = live && o.msg == MFP_MSG_QUIC && (q.flags & MFP_FLAG_EMIT) && P.cfg.mode == MFP_MODE_WRITE_JSON;
+        const uint32_t pt_n = json ? span_len(q.plain) : 0u, hs_n = json && q.hello ? span_len(q.hs) : 0u;
+        const uint32_t meta = len && !ovpn ? span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
+        const uint32_t jlen = json ? 16 + pt_n + hs_n : 0u;
+        const uint32_t side = (len && !ovpn) || json ? 8 + meta + jlen : 0u;
 
         // tile reservation of 64-byte slots: string, hash, sidecar
         const int lane = tid & 63, wid = tid >> 6;
-        const uint32_t slot = len ? (((len + 7) & ~7u) + 8 + side + 63) & ~63u : 0u;
+        const uint32_t slot = len || side ? (((len + 7) & ~7u) + 8 + side + 63) & ~63u : 0u;
         uint32_t incl = slot;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -652,41 +679,62 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         const bool fits = base != ~0ull;
 
         uint32_t sni_off = 0, sni_len = 0xffff, ua_off = 0, ua_len = 0xffff;
+        uint8_t *out = P.fp_arena + (fits ? base + excl : 0);
+        uint8_t *sc = out + ((len + 7) & ~7u) + 8;
         if (len && fits) {
-            uint8_t *out = P.fp_arena + base + excl;
             Em<true> e;
             e.begin(out, out_line[tid]);
             if (ovpn) ovpn_fp(e, v); else quic_fp(e, q, fmt);
             e.finish();
-            uint8_t *sc = out + ((len + 7) & ~7u);
-            *(uint64_t *)sc = e.hash();
-            sc += 8;
-            if (!ovpn) {
-            // sidecar: {u16 alpn_off, u16 alpn_len}, server name, user agent, ALPN
-            uint32_t at = 4;
+            *(uint64_t *)(sc - 8) = e.hash();
+        }
+        if (side && fits) {
+            // header: {u16 alpn_off, u16 alpn_len, u16 side_len, u16 json_off}, then
+            // the server name, user agent and ALPN list (classifier inputs)
+            uint32_t at = 8;
             const Cur parts[3] = {m.sni, m.ua, m.alpn};
             uint32_t offs[3], lens[3];
             for (int k = 0; k < 3; k++) {
                 offs[k] = at;
-                lens[k] = cnull(parts[k]) ? 0xffffu : (uint32_t)clen(parts[k]);
-                for (uint32_t j = 0; j < span_len(parts[k]); j++) sc[at + j] = (uint8_t)ld(parts[k].d + j);
-                at += span_len(parts[k]);
+                lens[k] = len && !cnull(parts[k]) ? (uint32_t)clen(parts[k]) : 0xffffu;
+                const uint32_t sl = len ? span_len(parts[k]) : 0u;
+                for (uint32_t j = 0; j < sl; j++) sc[at + j] = (uint8_t)ld(parts[k].d + j);
+                at += sl;
             }
-            sc[0] = (uint8_t)offs[2]; sc[1] = (uint8_t)(offs[2] >> 8);
-            sc[2] = (uint8_t)lens[2]; sc[3] = (uint8_t)(lens[2] >> 8);
-            sni_off = offs[0]; sni_len = lens[0]; ua_off = offs[1]; ua_len = lens[1];
+            if (len) { sni_off = offs[0]; sni_len = lens[0]; ua_off = offs[1]; ua_len = lens[1]; }
+            const uint32_t json_off = json ? at : 0u;
+            if (json) {
+                // the JSON block: {u16 payload offset, u16 payload length, u16 plaintext
+                // length, u16 handshake length, u16 cc frame offset in the plaintext (0xffff
+                // none), u8 bit 0 pre-decrypted / bit 1 hello, u8 salt (0xff none), u32 0},
+                // the plaintext, the handshake bytes
+                uint8_t hdr[16];
+                const uint32_t cco = q.cc && cnotempty(q.plain) ? (uint32_t)(q.cc - q.plain.d) : 0xffffu;
+                const uint32_t hv[5] = {o.pay_off, o.pay_len, pt_n, hs_n, cco};
+                for (int k = 0; k < 5; k++) { hdr[2 * k] = (uint8_t)hv[k]; hdr[2 * k + 1] = (uint8_t)(hv[k] >> 8); }
+                hdr[10] = (uint8_t)((q.pre ? 1u : 0u) | (q.hello ? 2u : 0u));
+                hdr[11] = (uint8_t)q.salt;
+                hdr[12] = hdr[13] = hdr[14] = hdr[15] = 0;
+                for (int k = 0; k < 16; k++) sc[at + k] = hdr[k];
+                at += 16;
+                for (uint32_t j = 0; j < pt_n; j++) sc[at + j] = (uint8_t)ld(q.plain.d + j);
+                at += pt_n;
+                for (uint32_t j = 0; j < hs_n; j++) sc[at + j] = (uint8_t)ld(q.hs.d + j);
+                at += hs_n;
             }
+            const uint32_t hv2[4] = {offs[2], lens[2], side, json_off};
+            for (int k = 0; k < 4; k++) { sc[2 * k] = (uint8_t)hv2[k]; sc[2 * k + 1] = (uint8_t)(hv2[k] >> 8); }
         }
         // OpenVPN: the TCP payload, which the JSON writer re-reads for the "openvpn" object
         if (ovpn) { sni_off = o.pay_off; sni_len = o.pay_len; }
         if (live) {
             mfp_record r;
-            r.fp_offset = fits ? base + excl : 0;
+            r.fp_offset = fits && slot ? base + excl : 0;
             r.fp_len = fits ? len : 0;
             r.fp_type = (uint8_t)(fits ? fp_type : 0);
             r.msg = (uint8_t)o.msg;
-            r.flags = (uint8_t)(q.flags | (o.flags & MFP_FLAG_ENCAP) |
-                                (fits && len ? (ovpn ? MFP_FLAG_HASHED : (MFP_FLAG_HASHED | MFP_FLAG_SIDECAR)) : 0));
+            r.flags = (uint8_t)(q.flags | (o.flags & MFP_FLAG_ENCAP) | (fits && len ? MFP_FLAG_HASHED : 0) |
+                                (fits && side ? MFP_FLAG_SIDECAR : 0));
             r.status = 0;
             r.sni_off = (uint16_t)(sni_len == 0xffff ? 0 : sni_off);
             r.sni_len = (uint16_t)sni_len;

@@ -316,7 +316,7 @@ static void drop(mfp_reassembler R, decltype(R->table)::iterator it) {
 // the flow table over one batch, in stream order (process_tcp_data
 // pkt_proc.cc:773-893).  an_path: the analysis_context path
 // (analyze_ip_packet pkt_proc.cc:1624-1646): SYN, SYN/ACK and RST are skipped
-// and every TCP packet resets flow_state_pkts_needed (more[i], sticky).
+// and every IP packet resets flow_state_pkts_needed (more[i]; non-IP packets keep it).
 static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *arena, size_t arena_len,
                             const mfp_pkt_desc *desc, size_t n, const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
                             size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc, bool an_path, uint8_t *more) {
@@ -336,8 +336,8 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
     for (size_t i = 0; i < n; i++) {
         props[i] = 0;
         const mfp_tcp_seg &s = R->seg[i];
+        if (an_path && (s.kind & MFP_SEG_IP)) R->more_state = false;   // analysis.reinit() (pkt_proc.cc:1609)
         if (an_path && (s.kind & MFP_SEG_TCP)) {
-            R->more_state = false;                          // pkt_proc.cc:1630
             if (s.kind & MFP_SEG_SYN_RST) {                 // handshake control packets (pkt_proc.cc:1631-1633)
                 no_record(i);
                 if (more) more[i] = 0;

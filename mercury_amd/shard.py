@@ -13,7 +13,7 @@ LRU (fingerprint_prevalence, analysis.h:362-421): a sighting's status depends
 on every earlier sighting of the stream.  ordered_prevalence_merge is the
 host-side ordered merge of SURVEY 8(e): every rank analyses its shard with the
 decision deferred, the ranks exchange their batch's distinct unknown-TLS
-fingerprints (a few hundred entries, gloo all_gather), and every rank applies
+fingerprints (a few hundred entries, fixed-size gloo all_gathers), and every rank applies
 the same decisions, in shard order, to an identical copy of the LRU -- so the
 sharded output equals one context over the concatenated stream.
 """
@@ -83,37 +83,56 @@ def max_over_ranks(value, device=None, group=None):
     return float(t.item())
 
 
+def _all_gather_rows(arr, group=None):
+    """all_gather of one 1-D numpy array of fixed-size records per rank (any
+    length), as fixed-size int64 tensors: the lengths first, then the rows
+    padded to the longest.  Returns the ranks' arrays in rank order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    raw = np.ascontiguousarray(arr).view(np.uint8)
+    words = (raw.nbytes + 7) // 8
+    n = torch.tensor([words], dtype=torch.int64)
+    ns = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    cap = max(1, max(int(x.item()) for x in ns))
+    buf = np.zeros(cap * 8, np.uint8)
+    buf[:raw.nbytes] = raw
+    t = torch.from_numpy(buf.view(np.int64))
+    outs = [torch.zeros(cap, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    return [o.numpy().view(np.uint8)[:int(k.item()) * 8].view(arr.dtype) for o, k in zip(outs, ns)]
+
+
 def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
     """Decide the unknown-TLS sightings of this rank's last analysed batch
     (ctx deferred, see Context.defer) in stream order across the ranks of
     `group`: rank order is stream order, `shard_base` is the stream position of
     this rank's first packet.  `prev` is this rank's copy of the LRU (every
-    rank applies the same decisions to its own copy).  Returns the number of
+    rank applies the same decisions to its own copy).  The exchange is two or
+    three fixed-size int64 all_gathers (no pickling).  Returns the number of
     distinct fingerprints exchanged (or sightings, on the sequence path)."""
+    import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dl = ctx.analysis_distinct()
-    mine = (None if dl is None else dl.tobytes(), int(shard_base))
-    allp = [None] * world
-    dist.all_gather_object(allp, mine, group=group)
-    if all(p[0] is not None for p in allp):
-        lists = []
-        for b, base in allp:
-            x = np.frombuffer(b, SIGHTING_DTYPE).copy()
-            x["first"] += np.uint64(base)
-            x["last"] += np.uint64(base)
-            lists.append(x)
+    # [distinct count or -1 (table overflow), this shard's stream base]
+    hdr = torch.tensor([-1 if dl is None else len(dl), int(shard_base)], dtype=torch.int64)
+    hdrs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(hdrs, hdr, group=group)
+    if all(int(h[0]) >= 0 for h in hdrs):
+        lists = _all_gather_rows(dl if dl is not None else np.zeros(0, SIGHTING_DTYPE), group)
+        for x, h in zip(lists, hdrs):
+            x["first"] += np.uint64(int(h[1]))
+            x["last"] += np.uint64(int(h[1]))
         allv = np.concatenate(lists) if lists else np.zeros(0, SIGHTING_DTYPE)
         if prev.resolve_distinct(allv):
             k = sum(len(x) for x in lists[:rank])
             ctx.analysis_resolve(allv[k:k + len(lists[rank])])
             return len(allv)
     # the sequence form: every rank's sightings in shard order
-    seq = ctx.analysis_sequence()
-    alls = [None] * world
-    dist.all_gather_object(alls, seq.tobytes(), group=group)
-    seqs = [np.frombuffer(b, np.uint64) for b in alls]
+    seqs = _all_gather_rows(np.ascontiguousarray(ctx.analysis_sequence(), np.uint64), group)
     seen = prev.resolve_sequence(np.concatenate(seqs) if seqs else np.zeros(0, np.uint64))
     k = sum(len(x) for x in seqs[:rank])
     ctx.analysis_resolve_sequence(seen[k:k + len(seqs[rank])])

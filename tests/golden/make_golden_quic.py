@@ -70,6 +70,15 @@ def main():
         rows = [l.split(b"\t") for l in out.splitlines()]
         counts[key] = {"emit": sum(int(r[1]) for r in rows), "quic_fp": sum(r[2] == b"12" for r in rows),
                        "truncated": sum(int(r[3]) for r in rows)}
+    # the whole write_json record text ("tls" and "quic" objects)
+    for key in ("q0", "mix"):
+        js = subprocess.run([REF, "json", tmp, CONFIGS[key], "-"], capture_output=True,
+                            check=True).stdout.decode("latin-1")
+        lines = js.split("\n")[:len(desc)]
+        with gzip.open(os.path.join(HERE, f"quic_json_{key}.txt.gz"), "wt", encoding="latin-1") as f:
+            f.write("\n".join(lines) + "\n")
+        counts[key]["json_lines"] = sum(1 for l in lines if l)
+        counts[key]["quic_objects"] = sum('"quic":{' in l for l in lines)
     os.unlink(tmp)
     manifest = {"reference": "cisco/mercury 2.18.0 (/root/reference), libmerc built by oracle/Makefile.ref",
                 "driver": "oracle/_ref/merc_ref_drv fp <batch> <config> -", "configs": CONFIGS,

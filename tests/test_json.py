@@ -8,9 +8,8 @@ src/libmerc/pkt_proc.cc:1157-1253), committed by tests/golden/make_golden_json.p
 * GPU: records from the HIP walk -> writer, byte-identical to the reference
   on the crafted packets, the packets of the reference's own test pcaps and
   a synthetic mixed batch.  Bar: every emitted line byte-identical,
-  IP-in-IP "encapsulations" arrays included; the only lines the writer may
-  leave empty (counted) are encapsulated records whose outer IPv6 header has
-  extension headers.
+  "encapsulations" arrays included (IP-in-IP, GRE, VXLAN, Geneve; outer IPv6
+  extension headers); nothing is skipped.
 """
 import gzip
 import json
@@ -43,19 +42,13 @@ def _golden_lines(name):
         return f.read().split(b"\n")[:-1]
 
 
-def _check(lines, gold, skipped, allow_skip=False):
-    """Every line byte-identical; an encapsulated record the writer cannot
-    rebuild (an outer IPv6 header with extension headers) is left empty and
-    counted, and only when allow_skip."""
+def _check(lines, gold, skipped):
+    """Every line byte-identical; nothing skipped."""
     assert len(lines) == len(gold)
-    n_skip = 0
     for i, (got, want) in enumerate(zip(lines, gold)):
         exp = want + b"\n" if want else b""
-        if got == b"" and exp and b'"encapsulations":' in want and allow_skip:
-            n_skip += 1
-            continue
         assert got == exp, (i, got[:300], exp[:300])
-    assert skipped == n_skip
+    assert skipped == 0
 
 
 def test_writer_crafted_records():
@@ -126,7 +119,7 @@ def test_json_reference_pcaps_device():
     rec, fp = ctx.process_host(arena, desc)
     lines, skipped = mercury_amd.write_json(arena, desc, rec, fp, ts_ns=np.full(len(desc), TS, np.uint64),
                                             threads=4)
-    _check(lines, gold, skipped, allow_skip=True)
+    _check(lines, gold, skipped)
     ctx.close()
 
 

@@ -196,3 +196,25 @@ def test_quic_analysis_vs_reference():
             bad.append((i, got, want))
     assert not bad, f"{len(bad)} attribute mismatches, first {bad[:3]}"
     assert sum("encrypted_dns" in w for _, _, w in load_attr()) > 500
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["q0", "mix"])
+def test_quic_json_vs_reference(key):
+    """The write_json text of every packet: the "tls" object of the decrypted
+    ClientHello (first server_name, quic_transport_parameters, google user
+    agents) and the "quic" object (connection_info, version, dcid, scid,
+    token, the last ack / ack_ecn / connection_close frame, salt_string,
+    plaintext or raw_packet_data) rebuilt from k_quic's sidecar,
+    byte-identical to the reference (quic.h:531-540, 1438-1452, 1662-1690)."""
+    from tests import test_json
+    arena, desc, sources = load()
+    ctx = mercury_amd.Context(MANIFEST["configs"][key], device=0)
+    try:
+        rec, fp = ctx.process_host(arena, desc)
+    finally:
+        ctx.close()
+    lines, skipped = mercury_amd.write_json(arena, desc, rec, fp, ts_ns=np.full(len(desc), test_json.TS, np.uint64),
+                                            threads=2)
+    test_json._check(lines, test_json._golden_lines(f"quic_json_{key}.txt.gz"), skipped)
+    assert MANIFEST["counts"][key]["quic_objects"] == 833

@@ -149,7 +149,7 @@ def test_reassembly_json_vs_reference(key):
         ctx.close()
     lines, skipped = mercury_amd.write_json(arena2, desc2, rec, fp, ts_ns=np.full(len(desc), TS, np.uint64),
                                             threads=4, props=props)
-    test_json._check(lines, test_json._golden_lines(f"reasm_json_{key}.txt.gz"), skipped, allow_skip=True)
+    test_json._check(lines, test_json._golden_lines(f"reasm_json_{key}.txt.gz"), skipped)
 
 
 @pytest.mark.gpu
@@ -212,7 +212,7 @@ def test_reassembly_with_analysis_json_vs_reference():
                                                 threads=4, ctx=ctx, analysis=an, attr_prob=ap, props=props)
     finally:
         ctx.close()
-    test_json._check(lines, test_json._golden_lines("reasm_json_an.txt.gz"), skipped, allow_skip=True)
+    test_json._check(lines, test_json._golden_lines("reasm_json_an.txt.gz"), skipped)
     assert MANIFEST["counts"]["an"]["analysis_objects"] > 50
 
 

@@ -171,3 +171,61 @@ def test_ordered_prevalence_merge_world2(cap, span):
         got += res[0][0][step] + res[1][0][step]
     assert np.array_equal(np.array(got, np.uint8), want)
     assert res[0][1] == res[1][1] == key_hash(order).tolist()
+
+
+def _gpu_merge_worker(rank, world, port, q):
+    """One rank of bench.py's multi-GPU step, on cuda:0 (the one-GPU box): a
+    deferred --analysis context over its shard of the LRU stream, then
+    shard.ordered_prevalence_merge -- the function bench.py calls."""
+    import torch.distributed as dist
+    import mercury_amd
+    from tests.test_prevalence import REF_ARCHIVE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, d = synth.lru_batch(synth.lru_keys())
+        ctx = mercury_amd.Context(f"select=tls;resources={REF_ARCHIVE};analysis", device=0)
+        prev = mercury_amd.Prevalence(100000)
+        ctx.set_prevalence(prev)
+        ctx.defer(True)
+        step = 17000                      # 170 000 packets: 5 rounds of 2 shards
+        got, exchanged = [], 0
+        for lo in range(0, len(d), world * step):
+            s_lo = lo + rank * step
+            ctx.process_host_analysis(a, d[s_lo:s_lo + step])
+            exchanged += shard.ordered_prevalence_merge(ctx, prev, s_lo)
+            got.append(ctx.last_analysis()["status"].astype(np.uint8))
+        q.put((rank, np.concatenate(got).tobytes(), prev.keys().tobytes(), exchanged))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ordered_prevalence_merge_world2_hip():
+    """bench.py's multi-rank step on the HIP path: two gloo ranks, each a
+    process with its own deferred context on cuda:0, analyse alternate 17 000-
+    packet shards of the 170 000-sighting LRU stream and decide them with
+    shard.ordered_prevalence_merge; the statuses, in stream order, equal the
+    reference's (tests/golden/lru_status.bin.gz), and both ranks end with the
+    same LRU."""
+    import multiprocessing as mp
+    from tests.test_prevalence import golden_status
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ps = [ctxm.Process(target=_gpu_merge_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (np.frombuffer(s, np.uint8), k, e) for r, s, k, e in [q.get(timeout=600) for _ in ps]}
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    step = 17000
+    got = np.concatenate([res[r][0][k * step:(k + 1) * step] for k in range(5) for r in range(2)])
+    want = golden_status()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} statuses differ, first at {bad[:5]}"
+    assert res[0][1] == res[1][1] and res[0][2] > 0

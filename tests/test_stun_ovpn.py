@@ -141,7 +141,7 @@ def test_stun_ovpn_json_vs_reference(key):
     lines, skipped = mercury_amd.write_json(arena, desc, rec, fp, ts_ns=np.full(len(desc), test_json.TS, np.uint64),
                                             threads=4)
     gold = test_json._golden_lines(f"stun_ovpn_json_{key}.txt.gz")
-    test_json._check(lines, gold, skipped, allow_skip=True)
+    test_json._check(lines, gold, skipped)
 
 
 @pytest.mark.gpu

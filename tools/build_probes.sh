@@ -11,11 +11,11 @@ for spec in "$@"; do
   if [[ $name == an_* ]]; then   # classifier probes: recompile mfp_analysis.hip only
     ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/mfp_analysis.hip -o mercury_amd/_probe/a_$name.o &&
       hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so \
-        mercury_amd/_probe/a_$name.o $(ls $OBJ/*.o | grep -v mfp_analysis.hip.o) -lz && echo built $name ) &
+        mercury_amd/_probe/a_$name.o $(ls $OBJ/*.o | grep -v mfp_analysis.hip.o) -lz -lcrypto && echo built $name ) &
     continue
   fi
   ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/mfp_kernels.hip -o mercury_amd/_probe/k_$name.o &&
     hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so mercury_amd/_probe/k_$name.o \
-      $(ls $OBJ/*.o | grep -v mfp_kernels.hip.o) -lz && echo built $name ) &
+      $(ls $OBJ/*.o | grep -v mfp_kernels.hip.o) -lz -lcrypto && echo built $name ) &
 done
 wait
