@@ -64,12 +64,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_device_batch(torch, n, workload, draw_seed, unique):
+def build_device_batch(torch, n, workload, draw_seed, unique, diverse_tls=0.0):
     """`unique` distinct packets generated on the host, replicated on the device."""
     from tests import synth
     u = min(unique, n)
     ua, ud = synth.batch(u, seed=TEMPLATE_SEED[workload], workload=workload, n_templates=N_TEMPLATES,
-                         draw_seed=draw_seed)
+                         draw_seed=draw_seed, diverse_tls=diverse_tls)
     span = int(ud["offset"][-1] + ud["caplen"][-1])
     stride = (span + 64 + 255) // 256 * 256
     reps = (n + u - 1) // u
@@ -323,7 +323,7 @@ BIN_NAMES = ["tls_ch", "http_req", "tcp_syn", "http_resp", "other", "tls_sh", "s
 MSG_BIN = np.array([4, 0, 5, 5, 6, 6, 1, 3, 2, 2, 7, 7, 7] + [4] * 243, np.int64)
 
 
-def kernel_bytes(rec, desc, an):
+def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
     """Algorithmic HBM bytes per step of each kernel:
     what the kernel must read and write at least, from the packets' own
     sizes.  k_classify: descriptor + the packet's first 128 bytes + the bin id
@@ -339,13 +339,31 @@ def kernel_bytes(rec, desc, an):
     out = {"k_classify": int((16 + np.minimum(cap, 128) + 5).sum())}
     sums = np.bincount(b, weights=per_pkt, minlength=8)
     for k, nm in enumerate(BIN_NAMES):
-        for kern in ("k_fingerprint/", "k_fp_seg/", "k_wave_fp/"):
+        for kern in ("k_fingerprint/", "k_fp_seg/", "k_wave_fp/", "k_fp_lds/"):
             out[kern + nm] = int(sums[k])
+    # the fallback lane re-walks the packets the bin kernels hand back (count
+    # only: their mean per-packet bytes stand in for theirs)
+    out["k_fingerprint/fallback"] = int(n_fallback * per_pkt.mean()) if len(per_pkt) else 0
     if an is not None:
         valid = (an["flags"] & 1) != 0
         sn = np.where(rec["sni_len"] == 0xffff, 0, rec["sni_len"]).astype(np.int64)
         ua = np.where(rec["ua_len"] == 0xffff, 0, rec["ua_len"]).astype(np.int64)
-        out["k_analyze"] = int(len(rec) * (32 + an.dtype.itemsize) + (valid * (8 + 16 + 32 + sn + ua)).sum())
+        # k_analyze: record in, analysis record out; per classified packet the
+        # string hash, descriptor, address bytes, server name / user agent, the
+        # fingerprint (verified) and SURVEY 8(d)'s table reads: the pool copy of
+        # the string, 8 B per prior and 12 B per update entry of the lane-scored
+        # packets (device counters, mfp_analysis_stats)
+        st = an_stats or {}
+        out["k_analyze"] = int(len(rec) * (32 + an.dtype.itemsize) +
+                               (valid * (8 + 16 + 32 + sn + ua + 2 * fl)).sum() +
+                               8 * st.get("lane_priors", 0) + 12 * st.get("lane_updates", 0))
+        # k_analyze_wave: the 64-byte deferred entry, record, priors, update
+        # entries and the analysis record of each wave-scored packet
+        out["k_analyze_wave"] = int(st.get("deferred", 0) * (64 + 32 + 32) + 8 * st.get("wave_priors", 0) +
+                                    12 * st.get("wave_updates", 0))
+        # k_analyze_resolve: one 8-byte sighting bitmap word per 64 packets, and per
+        # pending sighting its record, its sighting-table slot (24 B) and its result
+        out["k_analyze_resolve"] = int(8 * ((len(rec) + 63) // 64) + st.get("pending", 0) * (32 + 24 + 32))
     return out
 
 

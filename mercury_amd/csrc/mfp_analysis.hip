@@ -689,6 +689,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             if (cid != 0xffffffffu && !ok) cid = probe_string_lane(D.fp_slots, D.fp_mask, D.pool, fp, fl, fh);
         }
         entry = cid;
+#ifdef MFP_PROBE_AN_STOP0
+        if (live) P.out[i] = a;
+        continue;
+#endif
         const bool tls_unknown = analyzable && entry == 0xffffffffu && fl >= 4 && (uint32_t)w0 == 0x2f736c74u;  // "tls/"
         uint32_t pid = 0xffffffffu, poff = 0;
         if (tls_unknown) pid = cand_string_lane(D.prev_slots, D.prev_mask, fh, fl, poff);
@@ -696,6 +700,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             const bool ok = wave_verify(pid != 0xffffffffu, fp, (const uint8_t *)D.pool + poff, fl, lane);
             if (pid != 0xffffffffu && !ok) pid = probe_string_lane(D.prev_slots, D.prev_mask, D.pool, fp, fl, fh);
         }
+#ifdef MFP_PROBE_AN_STOPA
+        if (live) P.out[i] = a;
+        continue;
+#endif
         if (analyzable) {
             if (entry != 0xffffffffu) {
                 status = 1;                                                   // labeled
@@ -756,6 +764,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 }
             }
         }
+#ifdef MFP_PROBE_AN_STOPB
+        if (live) P.out[i] = a;
+        continue;
+#endif
 #ifdef MFP_PROBE_AN_STOP1
         bool scored = false;
 #else
@@ -784,8 +796,16 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         Dst dd;
         dd.ipv = 0; dd.v4 = 0; dd.hi = 0; dd.lo = 0;
         if (scored || xcheck) dd = dst_of(pkt, r.net);
+#ifdef MFP_PROBE_AN_STOPC
+        if (live) P.out[i] = a;
+        continue;
+#endif
         uint32_t xattr = 0;   // encrypted_dns, domain_faking, faketls
+#ifdef MFP_PROBE_AN_NOXCHECK
+        if (0) {
+#else
         if (xcheck) {
+#endif
             // sn_str: the server name as a C string (strncpy MAX_SNI_LEN, result.h:348)
             const uint32_t sl0 = r.sni_len == 0xffff ? 0u : r.sni_len;
             uint64_t ch = 0;
@@ -793,7 +813,9 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             if (D.doh_enabled && doh_hit(D, sbase + r.sni_off, cl, ch, dd)) xattr |= 1u << D.doh_idx;
             if (D.faking_enabled && domain_faking(D, sbase + r.sni_off, cl, dd)) xattr |= 1u << D.domain_faking_idx;
         }
+#ifndef MFP_PROBE_AN_NOFAKETLS
         if (pending && faketls_fp(fp, fl)) xattr |= 1u << D.faketls_idx;   // randomized ClientHellos only
+#endif
         if (scored) {
             const uint32_t ipv = dd.ipv;
             uint32_t asn = 0;

@@ -357,10 +357,14 @@ def templates(seed, n_templates, workload="mixed"):
     return [make_template(rng, c) for c in classes], classes
 
 
-def batch(n, seed=0x5EED0003, workload="mixed", n_templates=4096, randomize=True, align=1, draw_seed=None):
+def batch(n, seed=0x5EED0003, workload="mixed", n_templates=4096, randomize=True, align=1, draw_seed=None,
+          diverse_tls=0.0):
     """n packets drawn from a seeded template pool; returns (arena, desc).
     `draw_seed` (default seed + 1) drives which templates are drawn and the
-    per-packet randomisation, so shards can share one template pool."""
+    per-packet randomisation, so shards can share one template pool.
+    `diverse_tls`: the fraction of TLS ClientHellos whose first two cipher
+    suites are re-drawn per packet (a fingerprint of its own: unknown to the
+    archive, a new sighting for the prevalence LRU)."""
     tpl, _ = templates(seed, n_templates, workload)
     rng = np.random.default_rng(seed + 1 if draw_seed is None else draw_seed)
     tid = rng.integers(0, len(tpl), n)
@@ -383,6 +387,8 @@ def batch(n, seed=0x5EED0003, workload="mixed", n_templates=4096, randomize=True
         arena[idx] = tb
         if randomize:
             _randomize(arena, offs[sel], tpl[t], rng)
+        if diverse_tls > 0:
+            _diversify(arena, offs[sel], tpl[t], rng, diverse_tls)
     desc = np.zeros(n, dtype=DESC_DTYPE)
     desc["offset"] = offs
     desc["caplen"] = plen
@@ -429,6 +435,32 @@ def _randomize(arena, offs, tb, rng):
             # client random (32 bytes after version)
             for k in range(32):
                 arena[offs + pl + 11 + k] = rng.integers(0, 256, m, dtype=np.uint8)
+
+
+def _diversify(arena, offs, tb, rng, frac):
+    """Re-draw the first two cipher suites of a TLS ClientHello template's
+    copies (a fraction `frac` of them) with random non-GREASE values."""
+    et = (tb[12] << 8) | tb[13]
+    ip = 14
+    if et == 0x0800 and tb[ip + 9] == 6:
+        l4 = ip + 20
+    elif et == 0x86dd and tb[ip + 6] == 6:
+        l4 = ip + 40
+    else:
+        return
+    pl = l4 + (tb[l4 + 12] >> 4) * 4
+    if len(tb) < pl + 48 or tb[pl] != 0x16 or tb[pl + 5] != 0x01:
+        return
+    c = pl + 9 + 2 + 32
+    c += 1 + tb[c]                                   # session id
+    if len(tb) < c + 6 or ((tb[c] << 8) | tb[c + 1]) < 4:
+        return
+    sel = offs[rng.random(len(offs)) < frac]
+    for k in range(4):                               # bytes of the first two suites
+        v = rng.integers(0, 256, len(sel), dtype=np.uint8)
+        if k in (1, 3):
+            v = np.where((v & 0x0f) == 0x0a, v ^ 0x01, v).astype(np.uint8)   # never a GREASE value
+        arena[sel + c + 2 + k] = v
 
 
 # ---------------------------------------------------------------------------
