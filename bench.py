@@ -435,6 +435,9 @@ def main():
                     help="packets in each rank's page-locked source buffer (looped up to its share)")
     ap.add_argument("--e2e-chunk", type=int, default=2_000_000)
     ap.add_argument("--no-json-leg", action="store_true")
+    ap.add_argument("--diverse-leg", type=float, default=1.0,
+                    help="fraction of TLS ClientHellos with per-packet cipher suites in the realistic-diversity "
+                         "leg (reported beside value; 0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check without a GPU: ranks start, join the gloo group, report, exit")
     args = ap.parse_args()
@@ -581,10 +584,48 @@ def main():
     step_kern_ms = sum(kern_ms.values())
     dominant = max(kern_ms, key=kern_ms.get)
     achieved = alg_bytes / (step_kern_ms * 1e-3) / 1e9
-    kbytes = kernel_bytes(rec, desc, an if analysis else None)
 
     total_pkts = n * world
     value = total_pkts * args.steps / elapsed / 1e6
+    an_counters = ctx.analysis_counters() if analysis else None
+    kbytes = kernel_bytes(rec, desc, an if analysis else None, n_fallback, an_counters)
+    diverse = None
+    if analysis and args.diverse_leg > 0 and world == 1:
+        # realistic diversity: the same step over a batch whose TLS ClientHellos
+        # carry per-packet cipher suites -- hundreds of thousands of distinct
+        # fingerprints per step, unknown to the archive, cycling the 100 000-entry LRU
+        del d_arena, d_desc
+        torch.cuda.empty_cache()
+        ua2, ud2, d_arena, desc2, d_desc = build_device_batch(torch, n, workload, draw_seed, args.unique,
+                                                              diverse_tls=args.diverse_leg)
+        rec2u, fp2u = ctx.process_host(ua2, ud2)
+        distinct2 = len(set(mercury_amd.fingerprints(rec2u, fp2u)) - {""})
+        step()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        steps2 = max(1, min(args.steps, 5))
+        t2 = time.perf_counter()
+        for _ in range(steps2):
+            step()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t2
+        prof2 = ctx.profile_read()
+        ctx.profile(False)
+        an2 = d_an.cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)
+        v2 = (an2["flags"] & 1) != 0
+        st2 = np.bincount(an2["status"][v2], minlength=5)
+        diverse = {"value": round(n * steps2 / el2 / 1e6, 3), "unit": "Mpkt/s", "steps": steps2,
+                   "ms_per_step": round(el2 / steps2 * 1e3, 4),
+                   "diverse_tls_fraction": args.diverse_leg,
+                   "distinct_fingerprints_per_step": distinct2,
+                   "k_analyze_ms": round(prof2["k_analyze"][1] / steps2, 4) if "k_analyze" in prof2 else None,
+                   "k_analyze_wave_ms": round(prof2["k_analyze_wave"][1] / steps2, 4) if "k_analyze_wave" in prof2 else None,
+                   "k_analyze_resolve_ms": round(prof2["k_analyze_resolve"][1] / steps2, 4)
+                   if "k_analyze_resolve" in prof2 else None,
+                   "status": {mercury_amd.api.STATUS_NAMES[i]: int(st2[i]) for i in range(5)},
+                   "lru_entries": int(ctx.analysis_stats()[3]),
+                   "what": "same step, same archive; the unique packets' TLS ClientHellos get random first two "
+                           "cipher suites (tests/synth.py diverse_tls), replicated like the main leg"}
     e2e = None
     if args.e2e_total:
         del d_arena, d_desc, d_fp          # room for the pipeline's staging buffers
@@ -678,6 +719,8 @@ def main():
                             "achieved_gb_s": round(kbytes[k] / (v * 1e-3) / 1e9, 2) if kbytes.get(k) and v else None}
                         for k, v in kern_ms.items()},
             "cpu_baseline": cpu,
+            "diversity": diverse,
+            "analysis_counters": an_counters,
             "end_to_end": e2e,
         }
         print(json.dumps(out), flush=True)

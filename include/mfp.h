@@ -418,6 +418,13 @@ MFP_EXPORT int mfp_process_os_info(mfp_context ctx, uint32_t proc_slot, uint32_t
  * [3] fingerprints in the context's prevalence LRU */
 MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
 
+/* the last analysis batch's counters, up to n of: [0] packets classified,
+ * [1] unknown-TLS sightings, [2] fingerprints with too many processes,
+ * [3] packets scored wave-per-packet (k_analyze_wave), [4] / [5] prior and
+ * update-list entries read by the lane-per-packet scorer, [6] / [7] the same
+ * for the wave scorer (SURVEY 8(d)'s 8*P + 12*U table bytes) */
+MFP_EXPORT int mfp_analysis_counters(mfp_context ctx, uint64_t *out, size_t n);
+
 /* bytes of the classifier's device tables in HBM */
 MFP_EXPORT uint64_t mfp_analysis_device_bytes(mfp_context ctx);
 

@@ -126,6 +126,8 @@ def load_library():
     lib.mfp_process_name.argtypes = [vp, ctypes.c_uint32]
     lib.mfp_attribute_name.restype = ctypes.c_char_p
     lib.mfp_attribute_name.argtypes = [vp, ctypes.c_uint32]
+    lib.mfp_analysis_counters.restype = ctypes.c_int
+    lib.mfp_analysis_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), sz]
     lib.mfp_analysis_stats.restype = ctypes.c_int
     lib.mfp_analysis_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     lib.mfp_resource_stats.restype = ctypes.c_int
@@ -431,6 +433,16 @@ class Context:
         if self.lib.mfp_analysis_stats(self.h, out) != 0:
             raise MercuryAmdError(_err(self.lib))
         return list(out)
+
+    COUNTER_NAMES = ("classified", "pending", "oversize", "deferred", "lane_priors", "lane_updates", "wave_priors",
+                     "wave_updates")
+
+    def analysis_counters(self):
+        """The last analysis batch's device counters (mfp_analysis_counters) as a dict."""
+        out = (ctypes.c_uint64 * 8)()
+        if self.lib.mfp_analysis_counters(self.h, out, 8) != 0:
+            raise MercuryAmdError(_err(self.lib))
+        return dict(zip(self.COUNTER_NAMES, (int(x) for x in out)))
 
     def profile(self, on=True):
         """Bracket every kernel launch of this context with HIP events (resets the totals)."""

@@ -635,6 +635,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
     const uint64_t ngroups = (P.n + 63) / 64;
     const uint64_t nw = (uint64_t)gridDim.x * AW;
     uint32_t n_an = 0, n_pend = 0;   // per-wave counts, one atomic each at the end
+    uint32_t c_prior = 0, c_upd = 0; // per-lane table entries read by the lane scorer (mfp_analysis_counters)
     for (uint64_t g = (uint64_t)blockIdx.x * AW + wid; g < ngroups; g += nw) {
         const uint64_t i = g * 64 + lane;
         const bool live = i < P.n;
@@ -725,44 +726,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 status = 3;                                                   // unlabeled
             }
         }
-        {   // unknown-TLS sightings of this group: the per-group bitmap, and the
-            // batch table per distinct fingerprint (first / last sighting, count),
-            // one set of atomics per distinct hash per wave
+        {   // unknown-TLS sightings of this group: the per-group bitmap (their
+            // first / last / count per distinct fingerprint: k_seen_scan)
             const uint64_t pm = __ballot(pending);
             if (lane == 0) P.pend_bits[g] = pm;
             n_pend += (uint32_t)__builtin_popcountll(pm);
-#ifdef MFP_PROBE_AN_NOSEEN
-            uint64_t left = 0;
-#else
-            uint64_t left = pm;
-#endif
-            while (left) {
-                const int l0 = __builtin_ctzll(left);
-                const uint64_t h0 = rl64(fh, l0);
-                const uint64_t same = __ballot(pending && fh == h0) & left;
-                left &= ~same;
-                if ((int)lane == l0) {
-                    const uint32_t i_first = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(same));
-                    const uint32_t i_last = (uint32_t)(g * 64 + 63 - (uint64_t)__builtin_clzll(same));
-                    const mfp_seen_tab &T = P.seen;
-                    uint64_t k = h0 & T.mask;
-                    for (uint32_t t = 0; t <= T.mask; t++, k = (k + 1) & T.mask) {
-                        const unsigned long long prev = atomicCAS(&T.slots[k].hash, ~0ull, (unsigned long long)h0);
-                        if (prev == ~0ull) {             // new in this batch: a position in the distinct list
-                            const unsigned int pos = atomicAdd(&T.counters[0], 1u);
-                            if (pos < T.list_cap) T.list[pos] = (uint32_t)k;
-                            else atomicExch(&T.counters[1], 1u);
-                        }
-                        if (prev == ~0ull || prev == h0) {      // (slots start all-ones: min, min of ~last, count - 1)
-                            atomicMin(&T.slots[k].first, i_first);
-                            atomicMin(&T.slots[k].nlast, ~i_last);
-                            atomicAdd(&T.slots[k].count_m1, (unsigned int)__builtin_popcountll(same));
-                            break;
-                        }
-                        if (t == T.mask) atomicExch(&T.counters[1], 1u);   // table full
-                    }
-                }
-            }
         }
 #ifdef MFP_PROBE_AN_STOPB
         if (live) P.out[i] = a;
@@ -913,6 +881,9 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain && !ssh_ua;
 #endif
         if (lanep) {
+            c_prior += np;
+#pragma unroll
+            for (uint32_t f = 0; f < NFEAT; f++) c_upd += hcnt[f] & ~MFP_UPD_SERIAL;
             double *S = scl + lane;                    // S[p * 64]
             for (uint32_t p = 0; p < np; p++) S[p * 64] = D.prior[po + p];
 #pragma unroll
@@ -1027,6 +998,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
     }
     if (lane == 0 && n_an) atomicAdd(&P.stats[0], (unsigned long long)n_an);
     if (lane == 0 && n_pend) atomicAdd(&P.stats[1], (unsigned long long)n_pend);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { c_prior += __shfl_xor(c_prior, d, 64); c_upd += __shfl_xor(c_upd, d, 64); }
+    if (lane == 0 && c_prior) atomicAdd(&P.stats[4], (unsigned long long)c_prior);
+    if (lane == 0 && c_upd) atomicAdd(&P.stats[5], (unsigned long long)c_upd);
 }
 
 // k_analyze_wave: the packets k_analyze deferred (more than PL processes, or a
@@ -1048,6 +1023,7 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
     const mfp_classifier_dev &D = P.D;
     const uint64_t total = P.stats[3];
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
+    uint64_t w_prior = 0, w_upd = 0;   // table entries read (mfp_analysis_counters [6], [7])
     for (uint64_t q = (uint64_t)blockIdx.x * WPB + wid; q < total; q += nw) {
         const Deferred &dq = P.deferred[q];
         const uint32_t i = rfl(dq.i), entry = rfl(dq.entry), slow = rfl(dq.slow_sni);
@@ -1113,6 +1089,9 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
             off[3] = h.off; cnt[3] = h.cnt;
             __builtin_amdgcn_wave_barrier();
         }
+        w_prior += np;
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) w_upd += cnt[f] & ~MFP_UPD_SERIAL;
         // ---- scores: prior, then the six features in the reference's order
         uint32_t anylong = 0;
 #pragma unroll
@@ -1272,6 +1251,8 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
         }
         __builtin_amdgcn_wave_barrier();
     }
+    if (lane == 0 && w_prior) atomicAdd(&P.stats[6], (unsigned long long)w_prior);
+    if (lane == 0 && w_upd) atomicAdd(&P.stats[7], (unsigned long long)w_upd);
 }
 
 
@@ -1291,6 +1272,104 @@ __global__ __launch_bounds__(64) void k_analyze_big(AParams P) {
     __shared__ double sc_lds[1][64 * MAXP_CHUNKS_BIG];
     __shared__ uint8_t fl_lds[1][64 * MAXP_CHUNKS_BIG];
     wave_scorer<MAXP_CHUNKS_BIG, 1>(P, sni_buf, ua_buf, sc_lds, fl_lds);
+}
+
+// k_seen_scan: the batch's unknown-TLS sightings per distinct fingerprint
+// (first and last stream position, count) in the sighting table the host
+// decides from (mfp_prevalence.cpp).  Each block takes a contiguous range of
+// 64-packet groups and aggregates its sightings in an LDS table (one LDS
+// update per distinct fingerprint per group); the block then merges its
+// entries into the global table: one insertion per new fingerprint, a
+// min / max only when it improves the stored one, one count addition.  A few
+// hundred hot fingerprints thus see one global update per block, not one per
+// group (global atomics on a handful of lines serialise at the memory side).
+constexpr int SEEN_LDS = 2048;     // LDS table entries per block (power of two)
+constexpr int SEEN_WPB = 4;        // waves per block
+
+// merge one aggregated entry into the global table (insertion keeps its
+// position in the distinct list for k_seen_export)
+ADEV void seen_merge(const mfp_seen_tab &T, uint64_t h, uint32_t first, uint32_t last, uint32_t cnt) {
+    uint64_t k = h & T.mask;
+    for (uint32_t t = 0; t <= T.mask; t++, k = (k + 1) & T.mask) {
+        mfp_seen_slot &sl = T.slots[k];
+        unsigned long long cur = __hip_atomic_load(&sl.hash, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == ~0ull) {
+            cur = atomicCAS(&sl.hash, ~0ull, (unsigned long long)h);
+            if (cur == ~0ull) {                      // new in this batch: a position in the distinct list
+                const unsigned int pos = atomicAdd(&T.counters[0], 1u);
+                if (pos < T.list_cap) T.list[pos] = (uint32_t)k;
+                else atomicExch(&T.counters[1], 1u);
+                cur = h;
+            }
+        }
+        if (cur == h) {                              // (slots start all-ones: min, min of ~last, count - 1)
+            if (__hip_atomic_load(&sl.first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > first)
+                atomicMin(&sl.first, first);
+            if (__hip_atomic_load(&sl.nlast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > ~last)
+                atomicMin(&sl.nlast, ~last);
+            atomicAdd(&sl.count_m1, cnt);
+            return;
+        }
+    }
+    atomicExch(&T.counters[1], 1u);                  // table full
+}
+
+__global__ __launch_bounds__(64 * SEEN_WPB) void k_seen_scan(AParams P) {
+    __shared__ unsigned long long lh[SEEN_LDS];
+    __shared__ unsigned int lfirst[SEEN_LDS], lnlast[SEEN_LDS], lcnt[SEEN_LDS];
+    const uint32_t lane = lane_id();
+    const uint32_t wid = threadIdx.x >> 6;
+    for (int k = threadIdx.x; k < SEEN_LDS; k += 64 * SEEN_WPB) {
+        lh[k] = ~0ull; lfirst[k] = ~0u; lnlast[k] = ~0u; lcnt[k] = 0;
+    }
+    __syncthreads();
+    const uint64_t ngroups = (P.n + 63) / 64;
+    const uint64_t per = (ngroups + gridDim.x - 1) / gridDim.x;
+    const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = g0 + per < ngroups ? g0 + per : ngroups;
+    // 64 groups per wave round: lane l reads group g + l's bitmap word
+    for (uint64_t gb = g0 + 64 * wid; gb < g1; gb += 64 * SEEN_WPB) {
+        const uint64_t gl = gb + lane;
+        const uint64_t pw = gl < g1 ? P.pend_bits[gl] : 0ull;
+        uint64_t todo = __ballot(pw != 0);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t g = gb + (uint64_t)j;
+            const uint64_t pm = rl64(pw, j);
+            const bool pending = (pm >> lane) & 1;
+            const uint64_t i = g * 64 + lane;
+            uint64_t fh = 0;
+            if (pending) { const mfp_record r = P.rec[i]; fh = fp_key(r, P.fp_arena + r.fp_offset, r.fp_len); }
+            uint64_t left = pm;
+            while (left) {                           // one LDS update per distinct fingerprint of the group
+                const int l0 = __builtin_ctzll(left);
+                const uint64_t h0 = rl64(fh, l0);
+                const uint64_t same = __ballot(pending && fh == h0) & left;
+                left &= ~same;
+                if ((int)lane == l0) {
+                    const uint32_t fi = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(same));
+                    const uint32_t la = (uint32_t)(g * 64 + 63 - (uint64_t)__builtin_clzll(same));
+                    const uint32_t c = (uint32_t)__builtin_popcountll(same);
+                    uint32_t k = (uint32_t)h0 & (SEEN_LDS - 1);
+                    bool done = false;
+                    for (int t = 0; t < 32; t++, k = (k + 1) & (SEEN_LDS - 1)) {
+                        const unsigned long long prev = atomicCAS(&lh[k], ~0ull, (unsigned long long)h0);
+                        if (prev == ~0ull || prev == h0) {
+                            atomicMin(&lfirst[k], fi);
+                            atomicMin(&lnlast[k], ~la);
+                            atomicAdd(&lcnt[k], c);
+                            done = true;
+                            break;
+                        }
+                    }
+                    if (!done) seen_merge(P.seen, h0, fi, la, c);   // the block's table is crowded: straight to HBM
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < SEEN_LDS; k += 64 * SEEN_WPB)
+        if (lh[k] != ~0ull) seen_merge(P.seen, lh[k], lfirst[k], ~lnlast[k], lcnt[k]);
 }
 
 // k_seen_export: the batch's distinct unknown-TLS fingerprints, in the order
@@ -1394,6 +1473,14 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
     hipLaunchKernelGGL(mfpa::k_analyze, dim3((uint32_t)blocks), dim3(64 * mfpa::AW), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
+    {
+        uint64_t sb = (groups + 1023) / 1024;        // about 1024 groups per block, at most 1024 blocks
+        if (sb > 1024) sb = 1024;
+        if (prof) mfp_prof_begin(prof, "k_seen_scan", stream);
+        hipLaunchKernelGGL(mfpa::k_seen_scan, dim3((uint32_t)sb), dim3(64 * mfpa::SEEN_WPB), 0, stream, P);
+        if (prof) mfp_prof_end(prof, stream);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
     if (prof) mfp_prof_begin(prof, "k_analyze_wave", stream);
     hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(1024), dim3(256), 0, stream, P);
     if (D->max_nproc > 64u * mfpa::MAXP_CHUNKS)
