@@ -583,10 +583,18 @@ ADEV float expf_ref(float x) {
 }
 
 // a packet k_analyze hands to k_analyze_wave, with its feature lookups done
+// a packet to score, with its feature lookups done (k_an_features -> k_an_score /
+// k_analyze_wave): slow_sni: domain / SNI lookups still to do (the wave path
+// normalises the name); slow_ua: the SSH user agent; xattr: encrypted_dns,
+// domain_faking, faketls bits found by k_an_features
 struct Deferred {
-    uint32_t i, entry, slow_sni, slow_ua;   // slow_sni: domain / SNI lookups still to do; slow_ua: the SSH user agent
+    uint32_t i, entry, slow_sni, slow_ua;
     uint32_t off[6], cnt[6];
 };
+// a packet k_analyze hands to k_an_features: its fingerprint entry (~0u: none)
+// and what to do (WK_SCORE, WK_XCHECK, WK_PENDING)
+struct WorkItem { uint32_t i, entry, flags, pad; };
+enum { WK_SCORE = 1, WK_XCHECK = 2, WK_PENDING = 4 };
 
 struct AParams {
     mfp_classifier_dev D;
@@ -599,52 +607,72 @@ struct AParams {
     double *attr_prob;           // optional: archive-tag probabilities, MFP_ATTR_DB_TAGS per packet
     uint64_t *pend_bits;         // per group of 64 packets: unknown-TLS sightings (k_analyze_resolve)
     mfp_seen_tab seen;           // this batch's sightings per distinct fingerprint
-    struct Deferred *deferred;   // packets scored by k_analyze_wave
+    struct Deferred *deferred;   // packets scored by k_analyze_wave (per-segment lists)
     uint32_t mode;
-    uint32_t lane_max_p;         // phase L takes fingerprints with P <= min(lane_max_p, PL)
-    unsigned long long *stats;   // [0] analyzed, [1] pending unknown-TLS, [2] over-size P, [3] deferred
+    uint32_t lane_max_p;         // k_an_score takes fingerprints with P <= min(lane_max_p, PL)
+    unsigned long long *stats;   // [0] analyzed, [1] pending unknown-TLS, [2] over-size P, [3] deferred, [4..7] table entries read
+    // the packets to score travel in per-wave segments (k_analyze wave s
+    // writes segment s; the later kernels' wave s reads it): no global
+    // counter, no atomics, dense lanes
+    struct WorkItem *work;       // k_analyze -> k_an_features
+    struct Deferred *lanel;      // k_an_features -> k_an_score
+    uint32_t *seg_n;             // per segment: [0] work items, [1] lane-scored, [2] wave-scored (3 words each)
+    uint32_t nseg, seg_cap;      // segments (k_analyze waves), items per segment
 };
 
 constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.hpp:752-772 order
 
-// k_analyze, in two phases per group of 64 fingerprint records:
-//  A. lane per packet (64 packets in flight per wave): fingerprint hash,
-//     verified fingerprint-table lookup and status, destination context,
-//     ASN, server-name normalisation (plain names; the rest are marked for
-//     phase B) and the six feature-table lookups -> per lane: entry and six
-//     (update list offset, count) pairs;
-//  B. wave per scored packet: prior + update lists loaded lane-parallel,
-//     applied feature by feature as LDS scatters (one update per process per
-//     list, so a feature is one conflict-free scatter and each process sees
-//     the reference's addition order), max / second max, fp32 softmax, result.
+// The classifier's front end, three kernels per batch:
+//  k_analyze      lane per packet, groups of 64 records: verified fingerprint-
+//                 table lookup and status (perform_analysis_common
+//                 analysis.h:1043-1083), the known prevalence set, the
+//                 unknown-TLS bitmap; the analysis record of every packet;
+//                 the packets that need more (scoring, the classifier-agnostic
+//                 attributes, faketls) go to the wave's work segment;
+//  k_an_features  lane per work item, dense: destination context
+//                 (destination_context::init result.h:346), ASN, server-name
+//                 normalisation (plain names), user agent, the six feature-
+//                 table lookups with their byte-exact verification, the
+//                 classifier-agnostic attributes -> lane-scored or wave-scored
+//                 lists;
+//  k_an_score     lane per packet with P <= PL: prior + update lists in lane-
+//                 private LDS rows, max / second max, fp32 softmax, result --
+//                 the reference's own sequential loops (naive_bayes.hpp:752-772,
+//                 compute_score_and_probability analysis.h:222-277, softmax
+//                 softmax.hpp:227-264).
+// Each kernel carries only its stage's state, so none spills, and the later
+// two run on dense lists (no idle lanes for packets without work).
 #ifndef MFP_AN_PL
 #define MFP_AN_PL 16
 #endif
-#ifndef MFP_AN_MINW
-#define MFP_AN_MINW 4      // waves/SIMD: 4 spills 168 B/lane to scratch but hides more latency;
-#endif                     // at 50 M: 37.2 ms vs 39.4 (3), 2 is slower still (profiles/r02u_ab_*)
-constexpr uint32_t PL = MFP_AN_PL;   // phase L: fingerprints with at most PL processes, scored lane per packet
-constexpr int AW = 2;                // waves per k_analyze block (LDS: PL * 512 bytes of score rows per wave)
+constexpr uint32_t PL = MFP_AN_PL;   // k_an_score: fingerprints with at most PL processes, scored lane per packet
+constexpr int AW = 4;                // waves per k_analyze / k_an_features block
+constexpr int SW = 2;                // waves per k_an_score block (LDS: PL * 512 bytes of score rows per wave)
 
-__global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
-    __shared__ double sc_lds[AW][64 * PL];   // per wave: phase L's lane-private score rows S[p][lane]
+ADEV mfp_analysis no_info() {        // analysis_result() (result.h:174-210)
+    mfp_analysis a;
+    a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.status = 0; a.flags = 0;
+    a.proc_slot = MFP_NO_PROCESS; a.reserved = 0;
+    return a;
+}
+
+__global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
-    double *scl = sc_lds[wid];
     const mfp_classifier_dev &D = P.D;
     const uint64_t ngroups = (P.n + 63) / 64;
     const uint64_t nw = (uint64_t)gridDim.x * AW;
+    const uint32_t seg = (uint32_t)(blockIdx.x * AW + wid);
+    WorkItem *wk = P.work + (uint64_t)seg * P.seg_cap;
+    uint32_t n_wk = 0;               // this wave's work items (wave-uniform)
     uint32_t n_an = 0, n_pend = 0;   // per-wave counts, one atomic each at the end
-    uint32_t c_prior = 0, c_upd = 0; // per-lane table entries read by the lane scorer (mfp_analysis_counters)
-    for (uint64_t g = (uint64_t)blockIdx.x * AW + wid; g < ngroups; g += nw) {
+    for (uint64_t g = seg; g < ngroups; g += nw) {
         const uint64_t i = g * 64 + lane;
         const bool live = i < P.n;
         mfp_record r;
         if (live) r = P.rec[i];
         else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; }
-        mfp_analysis a;   // default: no information (analysis_result())
-        a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = 0; a.status = 0; a.flags = 0;
-        a.proc_slot = MFP_NO_PROCESS; a.reserved = 0;
+        mfp_analysis a = no_info();
         // messages whose do_analysis calls the classifier: TLS ClientHello
         // (tls.h:1977), HTTP request (http.cc:571), SSH client KEXINIT
         // (ssh.h:480), QUIC Initial (quic.h:1722), STUN request (stun.h:1021);
@@ -664,24 +692,14 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         }
         n_an += (uint32_t)__builtin_popcountll(am);
 
-        // ================= phase A: lane per packet =================
-        uint32_t status = 0, entry = 0xffffffffu, np = 0, po = 0, mdb = 0, dmz = 0, mbits = 0;
-        bool pending = false;
-        uint32_t hoff[NFEAT], hcnt[NFEAT];
-#pragma unroll
-        for (uint32_t f = 0; f < NFEAT; f++) { hoff[f] = 0; hcnt[f] = 0; }
-        // ---- 1. fingerprint lookup / status (perform_analysis_common, analysis.h:1043-1083):
+        // ---- fingerprint lookup / status (perform_analysis_common, analysis.h:1043-1083):
         // hash and candidate slot per lane, byte-exact check by the wave
         const uint8_t *fp = P.fp_arena + r.fp_offset;
         const uint32_t fl = analyzable ? r.fp_len : 0u;
         uint64_t fh = 0, w0 = 0;
         uint32_t cid = 0xffffffffu, coff = 0;
         if (analyzable) {
-#ifdef MFP_PROBE_AN_NOHASH
-            fh = fl;
-#else
             fh = fp_key(r, fp, fl);
-#endif
             w0 = word_at(fp, fl, 0);
             cid = cand_string_lane(D.fp_slots, D.fp_mask, fh, fl, coff);
         }
@@ -689,11 +707,8 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             const bool ok = wave_verify(cid != 0xffffffffu, fp, (const uint8_t *)D.pool + coff, fl, lane);
             if (cid != 0xffffffffu && !ok) cid = probe_string_lane(D.fp_slots, D.fp_mask, D.pool, fp, fl, fh);
         }
-        entry = cid;
-#ifdef MFP_PROBE_AN_STOP0
-        if (live) P.out[i] = a;
-        continue;
-#endif
+        uint32_t entry = cid, status = 0;
+        bool pending = false;
         const bool tls_unknown = analyzable && entry == 0xffffffffu && fl >= 4 && (uint32_t)w0 == 0x2f736c74u;  // "tls/"
         uint32_t pid = 0xffffffffu, poff = 0;
         if (tls_unknown) pid = cand_string_lane(D.prev_slots, D.prev_mask, fh, fl, poff);
@@ -701,10 +716,6 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             const bool ok = wave_verify(pid != 0xffffffffu, fp, (const uint8_t *)D.pool + poff, fl, lane);
             if (pid != 0xffffffffu && !ok) pid = probe_string_lane(D.prev_slots, D.prev_mask, D.pool, fp, fl, fh);
         }
-#ifdef MFP_PROBE_AN_STOPA
-        if (live) P.out[i] = a;
-        continue;
-#endif
         if (analyzable) {
             if (entry != 0xffffffffu) {
                 status = 1;                                                   // labeled
@@ -732,23 +743,68 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             if (lane == 0) P.pend_bits[g] = pm;
             n_pend += (uint32_t)__builtin_popcountll(pm);
         }
-#ifdef MFP_PROBE_AN_STOPB
-        if (live) P.out[i] = a;
-        continue;
-#endif
-#ifdef MFP_PROBE_AN_STOP1
-        bool scored = false;
-#else
-        bool scored = analyzable && entry != 0xffffffffu;
-#endif
-        if (scored) {
-            const mfp_entry E = D.entry[entry];
-            np = E.nproc; po = E.proc_off; mdb = E.malware_db; dmz = E.generic_dmz; mbits = E.mal_bits;
-            if (np > 64 * MAXP_CHUNKS_BIG) {   // beyond the big scorer: counted, left unscored
-                atomicAdd(&P.stats[2], 1ull);
-                scored = false;
-            }
+        const bool scored = analyzable && entry != 0xffffffffu;
+        if (analyzable) {
+            // no process distribution yet: the scorers fill it in
+            a.flags = MFP_AN_VALID;
+            a.status = (uint8_t)status;
+            if (pending) a.flags |= MFP_AN_PENDING;
+            // analyze_ip_packet: a truncated message reports "unlabeled" and
+            // keeps its classification (pkt_proc.cc:1716-1719)
+            if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED) && !pending) a.status = 3;
         }
+        if (live) P.out[i] = a;   // the status lives in the analysis record only (no 1-byte record rewrite)
+        // the work segment: packets to score, to check for the classifier-
+        // agnostic attributes, or (pending) for faketls
+        const bool work = scored || xcheck || pending;
+        const uint64_t wm = __ballot(work);
+        if (work) {
+            WorkItem w;
+            w.i = (uint32_t)i; w.entry = scored ? entry : 0xffffffffu;
+            w.flags = (scored ? WK_SCORE : 0u) | (xcheck ? WK_XCHECK : 0u) | (pending ? WK_PENDING : 0u);
+            w.pad = 0;
+            wk[n_wk + __builtin_popcountll(wm & ((1ull << lane) - 1))] = w;
+        }
+        n_wk += (uint32_t)__builtin_popcountll(wm);
+    }
+    if (lane == 0) P.seg_n[3 * seg] = n_wk;
+    if (lane == 0 && n_an) atomicAdd(&P.stats[0], (unsigned long long)n_an);
+    if (lane == 0 && n_pend) atomicAdd(&P.stats[1], (unsigned long long)n_pend);
+}
+
+__global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
+    const uint32_t lane = lane_id();
+    const int wid = (int)rfl(threadIdx.x >> 6);
+    const mfp_classifier_dev &D = P.D;
+    const uint32_t seg = (uint32_t)(blockIdx.x * AW + wid);
+    if (seg >= P.nseg) return;
+    const WorkItem *wk = P.work + (uint64_t)seg * P.seg_cap;
+    Deferred *ll = P.lanel + (uint64_t)seg * P.seg_cap, *dl = P.deferred + (uint64_t)seg * P.seg_cap;
+    const uint32_t total = rfl(P.seg_n[3 * seg]);
+    uint32_t n_l = 0, n_d = 0;       // wave-uniform list counts
+    for (uint32_t b0 = 0; b0 < total; b0 += 64) {
+        const bool live = b0 + lane < total;
+        WorkItem w;
+        if (live) w = wk[b0 + lane];
+        else { w.i = 0; w.entry = 0xffffffffu; w.flags = 0; w.pad = 0; }
+        const uint64_t i = w.i;
+        const bool xcheck = w.flags & WK_XCHECK, pending = w.flags & WK_PENDING;
+        bool scored = w.flags & WK_SCORE;
+        const uint32_t entry = w.entry;
+        mfp_record r;
+        if (live) r = P.rec[i];
+        else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; r.fp_offset = 0; r.net = 0; r.msg = 0;
+               r.sni_off = 0; r.sni_len = 0xffff; r.ua_off = 0; r.ua_len = 0xffff; r.dst_port = 0; }
+        const uint8_t *fp = P.fp_arena + r.fp_offset;
+        uint32_t np = 0;
+        if (scored) np = D.entry[entry].nproc;
+        if (scored && np > 64 * MAXP_CHUNKS_BIG) {   // beyond the big scorer: counted, left unscored
+            atomicAdd(&P.stats[2], 1ull);
+            scored = false;
+        }
+        uint32_t hoff[NFEAT], hcnt[NFEAT];
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) { hoff[f] = 0; hcnt[f] = 0; }
         bool plain = false, ssh_ua = false;
         // string features UA, domain, SNI (hoff/hcnt slots 3..5)
         const uint8_t *vs[3] = {nullptr, nullptr, nullptr};
@@ -764,16 +820,8 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
         Dst dd;
         dd.ipv = 0; dd.v4 = 0; dd.hi = 0; dd.lo = 0;
         if (scored || xcheck) dd = dst_of(pkt, r.net);
-#ifdef MFP_PROBE_AN_STOPC
-        if (live) P.out[i] = a;
-        continue;
-#endif
         uint32_t xattr = 0;   // encrypted_dns, domain_faking, faketls
-#ifdef MFP_PROBE_AN_NOXCHECK
-        if (0) {
-#else
         if (xcheck) {
-#endif
             // sn_str: the server name as a C string (strncpy MAX_SNI_LEN, result.h:348)
             const uint32_t sl0 = r.sni_len == 0xffff ? 0u : r.sni_len;
             uint64_t ch = 0;
@@ -781,9 +829,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             if (D.doh_enabled && doh_hit(D, sbase + r.sni_off, cl, ch, dd)) xattr |= 1u << D.doh_idx;
             if (D.faking_enabled && domain_faking(D, sbase + r.sni_off, cl, dd)) xattr |= 1u << D.domain_faking_idx;
         }
-#ifndef MFP_PROBE_AN_NOFAKETLS
-        if (pending && faketls_fp(fp, fl)) xattr |= 1u << D.faketls_idx;   // randomized ClientHellos only
-#endif
+        if (pending && faketls_fp(fp, r.fp_len)) xattr |= 1u << D.faketls_idx;   // randomized ClientHellos only
         if (scored) {
             const uint32_t ipv = dd.ipv;
             uint32_t asn = 0;
@@ -820,12 +866,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
             ul = cstr_hash(up, ul, uh);
             const uint32_t dport = r.dst_port;
 
-            // ---- 3. the six feature lookups
-#ifdef MFP_PROBE_AN_NOFEAT
-            if (0) {
-#else
-            {
-#endif
+            // ---- the six feature lookups
             Hit h;
             h = probe_feature_lane(D, entry, F_ASN, asn, nullptr, 0xffffffffu);
             hoff[0] = h.off; hcnt[0] = h.cnt;
@@ -857,9 +898,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 vs[2] = sp; vl[2] = sl; vk[2] = nh;
                 has[2] = cand_feature_lane(D, entry, F_SNI, nh, sl, vh[2], voff[2]);
             }
-            }
         }
-
 #pragma unroll
         for (int v = 0; v < 3; v++) {
             const bool ok = wave_verify(has[v], vs[v], (const uint8_t *)D.pool + voff[v], vl[v], lane);
@@ -870,26 +909,50 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 hoff[3 + v] = h.off; hcnt[3 + v] = h.cnt;
             }
         }
-
-        // ================= phase L: lane per packet, P <= PL =================
-        // the reference's own sequential loops (naive_bayes.hpp:752-772,
-        // compute_score_and_probability analysis.h:222-277, softmax
-        // softmax.hpp:227-264) on lane-private LDS rows
-#ifdef MFP_PROBE_AN_NOSCORE
-        const bool lanep = false;
-#else
+        // scored: to the lane scorer (small P, plain name) or the wave scorer;
+        // not scored: the attributes go into the record now
         const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain && !ssh_ua;
-#endif
-        if (lanep) {
+        const bool defer = scored && !lanep;
+        if (live && !scored && xattr) P.out[i].attr = (uint16_t)(P.out[i].attr | xattr);
+        Deferred d;
+        d.i = (uint32_t)i; d.entry = entry; d.slow_sni = plain ? 0u : 1u; d.slow_ua = (ssh_ua ? 1u : 0u) | (xattr << 16);
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
+        const uint64_t lm = __ballot(lanep), dm = __ballot(defer);
+        if (lanep) ll[n_l + __builtin_popcountll(lm & ((1ull << lane) - 1))] = d;
+        if (defer) dl[n_d + __builtin_popcountll(dm & ((1ull << lane) - 1))] = d;
+        n_l += (uint32_t)__builtin_popcountll(lm);
+        n_d += (uint32_t)__builtin_popcountll(dm);
+    }
+    if (lane == 0) { P.seg_n[3 * seg + 1] = n_l; P.seg_n[3 * seg + 2] = n_d; }
+    if (lane == 0 && n_d) atomicAdd(&P.stats[3], (unsigned long long)n_d);
+}
+
+__global__ __launch_bounds__(64 * SW) void k_an_score(AParams P) {
+    __shared__ double sc_lds[SW][64 * PL];   // per wave: lane-private score rows S[p][lane]
+    const uint32_t lane = lane_id();
+    const int wid = (int)rfl(threadIdx.x >> 6);
+    double *scl = sc_lds[wid];
+    const mfp_classifier_dev &D = P.D;
+    uint32_t c_prior = 0, c_upd = 0; // per-lane table entries read (mfp_analysis_counters)
+    for (uint32_t seg = blockIdx.x * SW + wid; seg < P.nseg; seg += gridDim.x * SW) {
+        const Deferred *ll = P.lanel + (uint64_t)seg * P.seg_cap;
+        const uint32_t total = rfl(P.seg_n[3 * seg + 1]);
+        for (uint32_t b0 = 0; b0 < total; b0 += 64) {
+            if (b0 + lane >= total) continue;
+            const Deferred d = ll[b0 + lane];
+            const uint64_t i = d.i;
+            const mfp_entry E = D.entry[d.entry];
+            const uint32_t np = E.nproc, po = E.proc_off, mdb = E.malware_db, dmz = E.generic_dmz, mbits = E.mal_bits;
             c_prior += np;
 #pragma unroll
-            for (uint32_t f = 0; f < NFEAT; f++) c_upd += hcnt[f] & ~MFP_UPD_SERIAL;
+            for (uint32_t f = 0; f < NFEAT; f++) c_upd += d.cnt[f] & ~MFP_UPD_SERIAL;
             double *S = scl + lane;                    // S[p * 64]
             for (uint32_t p = 0; p < np; p++) S[p * 64] = D.prior[po + p];
 #pragma unroll
             for (uint32_t f = 0; f < NFEAT; f++) {
-                const uint32_t c = hcnt[f] & ~MFP_UPD_SERIAL;
-                const mfp_update *ul = D.upd + hoff[f];
+                const uint32_t c = d.cnt[f] & ~MFP_UPD_SERIAL;
+                const mfp_update *ul = D.upd + d.off[f];
                 uint32_t k = 0;
                 for (; k + 4 <= c; k += 4) {
                     const mfp_update x0 = ul[k], x1 = ul[k + 1], x2 = ul[k + 2], x3 = ul[k + 3];
@@ -945,59 +1008,22 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_MINW) void k_analyze(AParams P) {
                 for (int k = 0; k < MFP_ATTR_DB_TAGS; k++)
                     if ((tags >> (MFP_ATTR_DB_FIRST + k)) & 1u) o[k] = ssum > 0.0 ? ap[k] / ssum : ap[k];
             }
+            mfp_analysis a = P.out[i];   // status and pending flag from k_analyze
             a.score = max_score;
             a.process = D.proc_id[po + ibest];
             a.proc_slot = po + ibest;
-            a.attr = (uint16_t)(D.proc_attr[po + ibest] | xattr);
+            a.attr = (uint16_t)(D.proc_attr[po + ibest] | (d.slow_ua >> 16));
             a.malware_prob = -1.0;
-            a.flags = MFP_AN_VALID;
+            a.flags = (uint8_t)(MFP_AN_VALID | (a.flags & MFP_AN_PENDING));
             if (mdb) {
                 a.malware_prob = mal;
                 a.flags |= MFP_AN_CLASSIFY_MALWARE;
                 if ((mbits >> ibest) & 1u) a.flags |= MFP_AN_MALWARE;
             }
-            if ((a.flags & MFP_AN_MALWARE) && r.fp_type == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
+            if ((a.flags & MFP_AN_MALWARE) && P.rec[i].fp_type == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
+            P.out[i] = a;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-
-        // ================= the rest: queued for k_analyze_wave =================
-        {
-#ifdef MFP_PROBE_AN_NOLANE
-            const bool defer = false;
-#else
-            const bool defer = scored && !lanep;
-#endif
-            const uint64_t dm = __ballot(defer);
-            if (dm) {
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(&P.stats[3], (unsigned long long)__builtin_popcountll(dm));
-                base = rfl64(base);
-                if (defer) {
-                    Deferred &d = P.deferred[base + __builtin_popcountll(dm & ((1ull << lane) - 1))];
-                    d.i = (uint32_t)i; d.entry = entry; d.slow_sni = plain ? 0u : 1u; d.slow_ua = ssh_ua ? 1u : 0u;
-#pragma unroll
-                    for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
-                }
-            }
-        }
-        if (analyzable) {
-            if (!lanep) {   // no process distribution (yet: k_analyze_wave scores the deferred ones)
-                a.score = 0.0; a.malware_prob = -1.0; a.process = MFP_NO_PROCESS; a.attr = (uint16_t)xattr;
-                a.flags = MFP_AN_VALID; a.proc_slot = MFP_NO_PROCESS;
-            }
-            a.status = (uint8_t)status;
-            if (pending) a.flags |= MFP_AN_PENDING;
-            // analyze_ip_packet: a truncated message reports "unlabeled" and
-            // keeps its classification (pkt_proc.cc:1716-1719)
-            if (P.mode == MFP_MODE_ANALYSIS && (r.flags & MFP_FLAG_TRUNCATED) && !pending) a.status = 3;
-        } else if (xcheck) {
-            a.attr = (uint16_t)xattr;   // unanalyzed type: only the classifier-agnostic attributes
-        }
-        if (live) P.out[i] = a;   // the status lives in the analysis record only (no 1-byte record rewrite)
     }
-    if (lane == 0 && n_an) atomicAdd(&P.stats[0], (unsigned long long)n_an);
-    if (lane == 0 && n_pend) atomicAdd(&P.stats[1], (unsigned long long)n_pend);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) { c_prior += __shfl_xor(c_prior, d, 64); c_upd += __shfl_xor(c_upd, d, 64); }
     if (lane == 0 && c_prior) atomicAdd(&P.stats[4], (unsigned long long)c_prior);
@@ -1021,12 +1047,15 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
     char *nbuf = sni_buf[wid];
     double *scl = sc_lds[wid];
     const mfp_classifier_dev &D = P.D;
-    const uint64_t total = P.stats[3];
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
     uint64_t w_prior = 0, w_upd = 0;   // table entries read (mfp_analysis_counters [6], [7])
-    for (uint64_t q = (uint64_t)blockIdx.x * WPB + wid; q < total; q += nw) {
-        const Deferred &dq = P.deferred[q];
+    for (uint64_t sg = (uint64_t)blockIdx.x * WPB + wid; sg < P.nseg; sg += nw) {
+    const Deferred *dseg = P.deferred + sg * P.seg_cap;
+    const uint32_t total = rfl(P.seg_n[3 * sg + 2]);
+    for (uint32_t q = 0; q < total; q++) {
+        const Deferred &dq = dseg[q];
         const uint32_t i = rfl(dq.i), entry = rfl(dq.entry), slow = rfl(dq.slow_sni);
+        const uint32_t xattr = rfl(dq.slow_ua) >> 16;   // k_an_features' encrypted_dns / domain_faking / faketls
         uint32_t off[NFEAT], cnt[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) { off[f] = rfl(dq.off[f]); cnt[f] = rfl(dq.cnt[f]); }
@@ -1058,7 +1087,7 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
             off[5] = h.off; cnt[5] = h.cnt;
             __builtin_amdgcn_wave_barrier();
         }
-        if (rfl(dq.slow_ua)) {
+        if (rfl(dq.slow_ua) & 1u) {
             // the SSH user agent (ssh_init_packet::do_analysis ssh.h:480-487):
             // protocol then comment into a data_buffer<512> (nulled -- empty --
             // when they do not fit), strncpy 511, NUL stops.  The record's span
@@ -1237,7 +1266,7 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
             a.score = max_score;
             a.process = D.proc_id[po + ibest];
             a.proc_slot = po + ibest;
-            a.attr = (uint16_t)(D.proc_attr[po + ibest] | a.attr);
+            a.attr = (uint16_t)(D.proc_attr[po + ibest] | a.attr | xattr);
             a.malware_prob = -1.0;
             a.flags = (uint8_t)(MFP_AN_VALID | (a.flags & MFP_AN_PENDING));
             if (mdb) {
@@ -1250,6 +1279,7 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
             P.out[i] = a;
         }
         __builtin_amdgcn_wave_barrier();
+    }
     }
     if (lane == 0 && w_prior) atomicAdd(&P.stats[6], (unsigned long long)w_prior);
     if (lane == 0 && w_upd) atomicAdd(&P.stats[7], (unsigned long long)w_upd);
@@ -1459,18 +1489,36 @@ static mfpa::AParams make_params(const mfp_classifier_dev *D, const mfp_seen_tab
     return P;
 }
 
+// the per-wave segments of one batch: k_analyze's waves (segments) and the
+// items a segment holds at most (64 per group a wave can take)
+extern "C" void mfp_analysis_segments(uint64_t n, uint32_t *nseg, uint32_t *seg_cap) {
+    const uint64_t groups = (n + 63) / 64;
+    uint64_t blocks = (groups + mfpa::AW - 1) / mfpa::AW;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    const uint64_t ns = blocks * mfpa::AW;
+    *nseg = (uint32_t)ns;
+    *seg_cap = (uint32_t)(64 * ((groups + ns - 1) / ns));
+}
+
+// scratch: work = nseg * seg_cap WorkItems (16 B), lanel and deferred = nseg *
+// seg_cap Deferred (64 B) each, seg_n = 3 * nseg words
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
-                                   mfp_analysis *out, double *attr_prob, uint32_t *pending, void *deferred,
-                                   unsigned long long *stats, uint32_t mode, uint32_t lane_max_p, hipStream_t stream,
-                                   mfp_prof *prof) {
+                                   mfp_analysis *out, double *attr_prob, uint32_t *pending, void *work, void *lanel,
+                                   void *deferred, uint32_t *seg_n, unsigned long long *stats, uint32_t mode,
+                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof) {
     if (n == 0) return 0;
     mfpa::AParams P = make_params(D, *T, arena, desc, n, rec, fp_arena, out, pending, deferred, stats, mode, lane_max_p);
     P.attr_prob = attr_prob;
-    uint64_t groups = (n + 63) / 64, blocks = (groups + mfpa::AW - 1) / mfpa::AW;
-    if (blocks > 4096) blocks = 4096;
+    P.work = (mfpa::WorkItem *)work;
+    P.lanel = (mfpa::Deferred *)lanel;
+    P.seg_n = seg_n;
+    mfp_analysis_segments(n, &P.nseg, &P.seg_cap);
+    const uint32_t blocks = P.nseg / mfpa::AW;
+    const uint64_t groups = (n + 63) / 64;
     if (prof) mfp_prof_begin(prof, "k_analyze", stream);
-    hipLaunchKernelGGL(mfpa::k_analyze, dim3((uint32_t)blocks), dim3(64 * mfpa::AW), 0, stream, P);
+    hipLaunchKernelGGL(mfpa::k_analyze, dim3(blocks), dim3(64 * mfpa::AW), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
     {
@@ -1481,8 +1529,16 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
         if (prof) mfp_prof_end(prof, stream);
         if (hipGetLastError() != hipSuccess) return -1;
     }
+    if (prof) mfp_prof_begin(prof, "k_an_features", stream);
+    hipLaunchKernelGGL(mfpa::k_an_features, dim3(blocks), dim3(64 * mfpa::AW), 0, stream, P);
+    if (prof) mfp_prof_end(prof, stream);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (prof) mfp_prof_begin(prof, "k_an_score", stream);
+    hipLaunchKernelGGL(mfpa::k_an_score, dim3(blocks < 1024 ? blocks : 1024), dim3(64 * mfpa::SW), 0, stream, P);
+    if (prof) mfp_prof_end(prof, stream);
+    if (hipGetLastError() != hipSuccess) return -1;
     if (prof) mfp_prof_begin(prof, "k_analyze_wave", stream);
-    hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(1024), dim3(256), 0, stream, P);
+    hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(blocks < 1024 ? blocks : 1024), dim3(256), 0, stream, P);
     if (D->max_nproc > 64u * mfpa::MAXP_CHUNKS)
         hipLaunchKernelGGL(mfpa::k_analyze_big, dim3(256), dim3(64), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);

@@ -78,6 +78,25 @@ struct LeStream {
         return v;
     }
 };
+// up to 32 bytes of p[0, len) as eight little-endian 4-byte groups, from the
+// aligned dwords that hold them, all loads issued before any is used (one
+// memory round trip per 32 bytes instead of one per 4); groups past len hold
+// garbage the caller masks.  Only dwords holding requested bytes are read.
+struct LeBlock {
+    uint32_t v[8];
+    DEV void load(const uint8_t *p, long len) {
+        const uintptr_t a = (uintptr_t)p;
+        const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3) * 8;
+        const long nb = len < 32 ? len : 32;
+        const int ndw = (int)(((long)(sh / 8) + nb + 3) / 4);   // 1..9
+        uint32_t w[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) w[k] = k < ndw ? q[k] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = sh ? (w[k] >> sh) | (w[k + 1] << (32 - sh)) : w[k];
+    }
+};
 // 4 bytes (b0 lowest) -> 8 lowercase hex characters, little-endian (b0's high nibble first)
 DEV uint64_t hex4(uint32_t le) {
     uint64_t x = le;
@@ -297,14 +316,20 @@ struct Em {
         for (long i = 0; i < len; i++) push(hex2((uint32_t)i), 2);
         return;
 #endif
-        LeStream st;
-        st.init(p, len);
-        long i = 0;
-        for (; i + 4 <= len; i += 4) push(hex4(st.next()), 8);
-        if (i < len) {
-            const uint64_t v = hex4(st.next());
-            const uint32_t k = (uint32_t)(len - i) * 2;       // 2, 4 or 6 characters
-            push(v & ((1ull << (8 * k)) - 1), k);
+        for (long i0 = 0; i0 < len; i0 += 32) {
+            LeBlock blk;
+            blk.load(p + i0, len - i0);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const long i = i0 + 4 * k;
+                if (i + 4 <= len) {
+                    push(hex4(blk.v[k]), 8);
+                } else if (i < len) {
+                    const uint64_t v = hex4(blk.v[k]);
+                    const uint32_t c = (uint32_t)(len - i) * 2;   // 2, 4 or 6 characters
+                    push(v & ((1ull << (8 * c)) - 1), c);
+                }
+            }
         }
     }
     DEV void hex16s(uint32_t m) { n += 4 * m; last_putc = false; }   // m hex16 appends (length only)
@@ -500,12 +525,18 @@ DEV void hex_degrease(E &b, const uint8_t *p, long len) {   // raw_as_hex_degrea
         if (len >= 2) b.hex16s((uint32_t)(len / 2));
         return;
     }
-    LeStream st;
-    st.init(p, len);
-    for (long i = 0; i < len; i += 4) {
-        const uint32_t v = st.next();             // bytes i..i+3, little-endian
-        b.hex16(degrease16(((v & 0xff) << 8) | ((v >> 8) & 0xff)));
-        if (i + 2 < len) b.hex16(degrease16((((v >> 16) & 0xff) << 8) | (v >> 24)));
+    for (long i0 = 0; i0 < len; i0 += 32) {
+        LeBlock blk;
+        blk.load(p + i0, len - i0);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const long i = i0 + 4 * k;               // bytes i..i+3, little-endian in v[k]
+            if (i < len) {
+                const uint32_t v = blk.v[k];
+                b.hex16(degrease16(((v & 0xff) << 8) | ((v >> 8) & 0xff)));
+                if (i + 2 < len) b.hex16(degrease16((((v >> 16) & 0xff) << 8) | (v >> 24)));
+            }
+        }
     }
 }
 DEV bool is_static_ext(uint32_t t) {                    // static_extension_types tls.h:1000

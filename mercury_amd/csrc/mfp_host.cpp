@@ -22,9 +22,10 @@
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
-                                   mfp_analysis *out, double *attr_prob, uint32_t *pending, void *deferred,
-                                   unsigned long long *stats, uint32_t mode, uint32_t lane_max_p, hipStream_t stream,
-                                   mfp_prof *prof);
+                                   mfp_analysis *out, double *attr_prob, uint32_t *pending, void *work, void *lanel,
+                                   void *deferred, uint32_t *seg_n, unsigned long long *stats, uint32_t mode,
+                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof);
+extern "C" void mfp_analysis_segments(uint64_t n, uint32_t *nseg, uint32_t *seg_cap);
 extern "C" int mfp_launch_seen_export(const mfp_seen_tab *T, uint32_t u, mfp_sighting *out, hipStream_t stream);
 extern "C" int mfp_launch_seen_sequence(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
                                         const mfp_record *rec, const uint8_t *fp_arena, uint32_t *pending,
@@ -259,7 +260,12 @@ struct Slot {
     uint32_t *d_work = nullptr; size_t cap_work = 0;   // bin index lists / fallback list / bin ids
     unsigned long long *d_an_stats = nullptr;
     uint32_t *d_pending = nullptr; size_t cap_pending = 0;   // unknown-TLS sightings (bitmap)
-    uint4 *d_deferred = nullptr; size_t cap_deferred = 0;    // packets for the wave-per-packet scorer (64 B each)
+    // the classifier's per-wave segments (mfp_analysis_segments): work items
+    // (16 B), lane-scored and wave-scored packets (64 B each), counts
+    uint4 *d_work_items = nullptr; size_t cap_work_items = 0;
+    uint4 *d_lanel = nullptr; size_t cap_lanel = 0;
+    uint4 *d_deferred = nullptr; size_t cap_deferred = 0;
+    uint32_t *d_segn = nullptr; size_t cap_segn = 0;
     mfp_analysis *d_an = nullptr; size_t cap_an = 0;
     double *d_ap = nullptr; size_t cap_ap = 0;               // archive-tag probabilities of host batches
     // the unknown-TLS sightings of the batch analysed in this slot (mfp_prevalence)
@@ -294,7 +300,8 @@ struct Slot {
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
-        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_deferred, d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2,
+        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_segn,
+                     d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         if (h_used) (void)hipHostFree(h_used);
@@ -498,15 +505,20 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
                           hipStream_t s) {
     Slot &S = c->slot[slot];
     HIPCHK(hipSetDevice(c->device));
-    if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_deferred, S.cap_deferred, 4 * (n + 1)) ||
-        seen_reserve(S, n, s)) {
+    uint32_t nseg = 0, seg_cap = 0;
+    mfp_analysis_segments(n, &nseg, &seg_cap);
+    const size_t items = (size_t)nseg * seg_cap + 1;
+    if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_work_items, S.cap_work_items, items) ||
+        grow(S.d_lanel, S.cap_lanel, 4 * items) || grow(S.d_deferred, S.cap_deferred, 4 * items) ||
+        grow(S.d_segn, S.cap_segn, 3 * (size_t)nseg + 1) || seen_reserve(S, n, s)) {
         mfp_set_error("device allocation failed");
         return -2;
     }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
     HIPCHK(hipMemsetAsync(S.d_an_stats, 0, 8 * sizeof(unsigned long long), s));
     if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, d_attr_prob,
-                            S.d_pending, S.d_deferred, S.d_an_stats, c->mode, c->an_lane_max_p, s, c->prof) != 0) {
+                            S.d_pending, S.d_work_items, S.d_lanel, S.d_deferred, S.d_segn, S.d_an_stats, c->mode,
+                            c->an_lane_max_p, s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }

@@ -126,7 +126,11 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
     const bool fits = base != ~0ull;
 
     // pass 2: emit
+#ifdef MFP_PROBE_NOPASS2
+    if (0) {
+#else
     if (len && fits) {
+#endif
         Em<true> e;
         e.begin(P.fp_arena + base + excl, out_line[tid]);
         if (plan.ok) {
