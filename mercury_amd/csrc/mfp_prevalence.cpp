@@ -17,12 +17,17 @@
 //     of a fingerprint not in the set is randomized, everything else unlabeled,
 //     and the recency order afterwards is the order of the last sightings;
 //   * sequence: every sighting in stream order, simulated one by one (used
-//     when the distinct form cannot be exact).
+//     when the distinct form cannot be exact).  Long sequences are cut into
+//     chunks decided in parallel: an LRU's content at any point is the
+//     `capacity` most recent distinct keys, so each chunk's starting set is
+//     rebuilt from the sightings before it (lru_at) and the decisions are the
+//     single pass's.
 #include <algorithm>
 #include <cstdint>
 #include <unordered_set>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/mfp.h"
@@ -30,89 +35,104 @@
 
 namespace {
 
-// LRU over 64-bit keys: open-addressing index + intrusive doubly linked list
-// in arrays (node 0 is the list head sentinel)
+// LRU over 64-bit keys: linear-probing index (keys stored in the slots,
+// backward-shift deletion: no tombstones) + intrusive doubly linked list in
+// arrays (node 0 is the list head sentinel; where[n] = node n's slot)
 struct Lru {
+    struct Slot { uint64_t key; uint32_t node; uint32_t pad; };   // node 0: empty
     uint32_t cap;
     std::vector<uint64_t> key;
-    std::vector<uint32_t> prev, next;
-    std::vector<uint32_t> free_nodes;
-    std::vector<uint32_t> slot;     // index: node id + 1, 0 empty, ~0u tombstone
+    std::vector<uint32_t> prev, next, where;
+    std::vector<Slot> slot;
     uint64_t mask;
-    uint32_t size = 0, used_slots = 0;
+    uint32_t size = 0;
 
     explicit Lru(uint32_t c) : cap(c ? c : 1) {
         key.assign((size_t)cap + 1, 0);
         prev.assign((size_t)cap + 1, 0);
         next.assign((size_t)cap + 1, 0);
-        for (uint32_t i = cap; i >= 1; i--) free_nodes.push_back(i);
+        where.assign((size_t)cap + 1, 0);
         uint64_t s = 16;
         while (s < 2ull * cap + 16) s <<= 1;
-        slot.assign(s, 0);
+        slot.assign(s, Slot{0, 0, 0});
         mask = s - 1;
     }
     static uint64_t mix(uint64_t x) {
         x ^= x >> 31; x *= 0x7fb5d329728ea185ull; x ^= x >> 27; x *= 0x81dadef4bc2dd44dull; x ^= x >> 33;
         return x;
     }
-    // index slot of k: its node, or (found = false) the first reusable slot
+    uint64_t home(uint64_t k) const { return mix(k) & mask; }
+    void prefetch(uint64_t k) const { __builtin_prefetch(&slot[home(k)]); }
+    // slot of k (found), or the empty slot that ends its probe
     uint64_t find(uint64_t k, bool &found) const {
-        uint64_t i = mix(k) & mask, tomb = ~0ull;
+        uint64_t i = home(k);
         while (true) {
-            const uint32_t s = slot[i];
-            if (s == 0) { found = false; return tomb != ~0ull ? tomb : i; }
-            if (s == ~0u) { if (tomb == ~0ull) tomb = i; }
-            else if (key[s] == k) { found = true; return i; }
+            const Slot &s = slot[i];
+            if (s.node == 0) { found = false; return i; }
+            if (s.key == k) { found = true; return i; }
             i = (i + 1) & mask;
         }
     }
+    void erase_slot(uint64_t i) {   // backward-shift deletion
+        uint64_t j = i;
+        while (true) {
+            j = (j + 1) & mask;
+            if (slot[j].node == 0) break;
+            const uint64_t h = home(slot[j].key);
+            // slot j's entry may move to i unless its home lies cyclically in (i, j]
+            const bool stay = (i <= j) ? (h > i && h <= j) : (h > i || h <= j);
+            if (!stay) {
+                slot[i] = slot[j];
+                where[slot[i].node] = (uint32_t)i;
+                i = j;
+            }
+        }
+        slot[i].node = 0;
+    }
     void unlink(uint32_t n) { next[prev[n]] = next[n]; prev[next[n]] = prev[n]; }
     void push_front(uint32_t n) { next[n] = next[0]; prev[n] = 0; prev[next[0]] = n; next[0] = n; }
-    void rehash() {   // drop tombstones
-        std::vector<uint32_t> old;
-        old.swap(slot);
-        slot.assign(old.size(), 0);
-        used_slots = 0;
-        for (uint32_t s : old)
-            if (s != 0 && s != ~0u) {
-                uint64_t i = mix(key[s]) & mask;
-                while (slot[i]) i = (i + 1) & mask;
-                slot[i] = s;
-                used_slots++;
-            }
-    }
+    void push_back(uint32_t n) { prev[n] = prev[0]; next[n] = 0; next[prev[0]] = n; prev[0] = n; }
     bool contains(uint64_t k) const { bool f; find(k, f); return f; }
+    uint32_t insert_at(uint64_t i, uint64_t k) {   // i: the empty slot find() returned
+        const uint32_t n = ++size;                 // nodes 1..size are live (evictions reuse theirs)
+        key[n] = k;
+        slot[i] = Slot{k, n, 0};
+        where[n] = (uint32_t)i;
+        return n;
+    }
     // fingerprint_prevalence::update (analysis.h:386-408); returns whether k
     // was in the set (the caller's contains() before the update)
     bool access(uint64_t k) {
         bool found;
-        const uint64_t i = find(k, found);
+        uint64_t i = find(k, found);
         if (found) {
-            const uint32_t n = slot[i];
-            unlink(n);
-            push_front(n);
+            const uint32_t n = slot[i].node;
+            if (next[0] != n) { unlink(n); push_front(n); }
             return true;
         }
-        if (size == cap) {                         // evict the least recently used
+        if (size == cap) {                         // evict the least recently used, reuse its node
             const uint32_t t = prev[0];
             unlink(t);
-            bool f2;
-            const uint64_t j = find(key[t], f2);
-            slot[j] = ~0u;
-            free_nodes.push_back(t);
-            size--;
+            erase_slot(where[t]);
+            i = find(k, found);                    // the shift may have moved k's empty slot
+            key[t] = k;
+            slot[i] = Slot{k, t, 0};
+            where[t] = (uint32_t)i;
+            push_front(t);
+            return false;
         }
-        const uint32_t n = free_nodes.back();
-        free_nodes.pop_back();
-        key[n] = k;
-        push_front(n);
-        bool f3;
-        const uint64_t j = find(k, f3);              // the slot may have moved past a new tombstone
-        if (slot[j] == 0) used_slots++;
-        slot[j] = n;
-        size++;
-        if (used_slots > (mask + 1) / 2) rehash();
+        push_front(insert_at(i, k));
         return false;
+    }
+    // set-up from a recency list: k becomes the least recently used so far
+    // (callers go from most to least recent); false if present or full
+    bool append_lru(uint64_t k) {
+        if (size == cap) return false;
+        bool found;
+        const uint64_t i = find(k, found);
+        if (found) return false;
+        push_back(insert_at(i, k));
+        return true;
     }
     // the keys from least to most recently used
     void export_keys(std::vector<uint64_t> &out) const {
@@ -120,6 +140,15 @@ struct Lru {
         for (uint32_t n = prev[0]; n != 0; n = prev[n]) out.push_back(key[n]);
     }
 };
+
+// The set after the accesses hash[0..end) applied to a set whose keys are
+// `init` (least to most recent): an LRU holds exactly the `cap` most recently
+// accessed distinct keys, in recency order, so it is rebuilt by walking back
+// from end-1 (then into init) until `cap` distinct keys are found.
+void lru_at(Lru &L, const uint64_t *hash, size_t end, const std::vector<uint64_t> &init) {
+    for (size_t i = end; i-- > 0 && L.size < L.cap;) L.append_lru(hash[i]);
+    for (size_t i = init.size(); i-- > 0 && L.size < L.cap;) L.append_lru(init[i]);
+}
 
 }  // namespace
 
@@ -173,7 +202,38 @@ MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t
 MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen) {
     if (!p || (m && (!hash || !seen))) { mfp_set_error("mfp_prevalence_resolve_sequence: bad arguments"); return -1; }
     std::lock_guard<std::mutex> lk(p->mu);
-    for (size_t j = 0; j < m; j++) seen[j] = p->lru.access(hash[j]) ? 1 : 0;
+    Lru &L = p->lru;
+    // chunks of at least 8 x capacity per thread (each chunk's starting set costs a walk back over about
+    // `capacity` distinct keys); up to 16 threads, the per-GPU host share of the target machine
+    const unsigned hw = std::thread::hardware_concurrency();
+    size_t T = m / (8 * (size_t)L.cap);
+    T = std::min<size_t>(T, std::min<size_t>(16, hw ? hw : 1));
+    if (T <= 1) {
+        for (size_t j = 0; j < m; j++) {
+            if (j + 8 < m) L.prefetch(hash[j + 8]);
+            seen[j] = L.access(hash[j]) ? 1 : 0;
+        }
+        return 0;
+    }
+    // chunk t decides hash[s_t..e_t) with its own LRU set up as the shared one
+    // would be at s_t (lru_at): the same decisions as one pass, in parallel
+    std::vector<uint64_t> init;
+    L.export_keys(init);
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; t++)
+        th.emplace_back([&, t]() {
+            const size_t s = m * t / T, e = m * (t + 1) / T;
+            Lru C(L.cap);
+            lru_at(C, hash, s, init);
+            for (size_t j = s; j < e; j++) {
+                if (j + 8 < e) C.prefetch(hash[j + 8]);
+                seen[j] = C.access(hash[j]) ? 1 : 0;
+            }
+        });
+    Lru F(L.cap);                                  // the set after the whole sequence
+    lru_at(F, hash, m, init);
+    for (auto &x : th) x.join();
+    std::swap(L, F);
     return 0;
 }
 

@@ -78,6 +78,35 @@ def test_prevalence_sequence_random(cap, n, span, seed):
     assert np.array_equal(p.resolve_sequence(key_hash(keys)), lru_model(keys.tolist(), cap)[0])
 
 
+@pytest.mark.parametrize("kind", ["few", "near_cap", "wide", "cycle", "bursts"])
+def test_prevalence_sequence_parallel_chunks(kind):
+    """Sequences long enough (>= 2 x 8 x capacity) to be decided in parallel
+    chunks, each starting from the set rebuilt from the sightings before it:
+    the same decisions and the same recency order as the one-pass model,
+    across calls (the set carried over)."""
+    rng = np.random.default_rng(["few", "near_cap", "wide", "cycle", "bursts"].index(kind) + 11)
+    cap = 200
+    p = mercury_amd.Prevalence(cap)
+    allkeys = []
+    for call in range(3):
+        n = 60000 + 777 * call
+        if kind == "few":
+            keys = rng.integers(0, 150, n)             # fewer distinct keys than the capacity
+        elif kind == "near_cap":
+            keys = rng.integers(0, 260, n)
+        elif kind == "wide":
+            keys = rng.integers(0, 5000, n)
+        elif kind == "cycle":
+            keys = np.tile(np.arange(300), n // 300 + 1)[:n] + 1000 * call
+        else:   # bursts of a small working set, now and then a new one
+            keys = (rng.integers(0, 120, n) + 50 * (np.arange(n) // 9000)).astype(np.int64)
+        allkeys += keys.tolist()
+        want, order = lru_model(allkeys, cap)
+        got = p.resolve_sequence(key_hash(keys))
+        assert np.array_equal(got, want[len(allkeys) - n:]), (kind, call)
+        assert np.array_equal(p.keys(), key_hash(order)), (kind, call)
+
+
 def distinct_of(keys, base=0):
     """The batch's distinct list as the device exports it (insertion order)."""
     d, first = [], {}
