@@ -85,11 +85,10 @@ def build_device_batch(torch, n, workload, draw_seed, unique, diverse_tls=0.0):
 
 
 def cpu_threads():
-    """Host threads for the CPU baseline: the cores this process may use (the
-    GPU box sets OMP_NUM_THREADS to its per-GPU CPU share)."""
+    """Host threads for the CPU baseline: one GPU's share of the host's cores
+    (nproc / 8 on an 8-GPU node), within the cores this process may use."""
     aff = len(os.sched_getaffinity(0))
-    env = os.environ.get("OMP_NUM_THREADS")
-    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
+    return max(1, min(aff, (os.cpu_count() or aff) // 8))
 
 
 def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis, resources):
@@ -115,13 +114,27 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis, reso
                                      capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
                 rates[entry] = json.loads(out.decode().strip().splitlines()[-1])
             r = rates["json"]
+            # the same write_json leg on every core this process may use, and on
+            # the box's OMP_NUM_THREADS share, beside the per-GPU-share value
+            points = {}
+            env = os.environ.get("OMP_NUM_THREADS")
+            for tag, th in (("all_cores", len(os.sched_getaffinity(0))),
+                            ("omp_num_threads", int(env) if env and env.isdigit() else None)):
+                if th and th != threads:
+                    out = subprocess.run([ref, "time", path, CONTRACT, resources if analysis else "-", str(th),
+                                          str(seconds / 2), "json"],
+                                         capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
+                    pr = json.loads(out.decode().strip().splitlines()[-1])
+                    points[tag] = {"threads": th, "write_json_mpkt_s": round(pr["pps"] / 1e6, 4)}
             what = "with --analysis (resources loaded)" if analysis else "fingerprint only"
             return {"value": r["pps"] / 1e6, "unit": "Mpkt/s", "cores": threads, "kind": "reference",
                     "entry": "write_json",
                     "get_analysis_context_mpkt_s": round(rates["an"]["pps"] / 1e6, 4),
+                    "other_thread_counts": points,
                     "host": host,
                     "sample": f"{sample_n} {workload} packets looped >= {seconds:.0f} s per entry point, "
-                              f"libmerc {what}, one processor per thread ({threads} threads); write_json "
+                              f"libmerc {what}, one processor per thread ({threads} threads = nproc / 8, "
+                              f"one GPU's share of the node); write_json "
                               f"{r['packets']} packets in {r['seconds']:.1f} s, get_analysis_context "
                               f"{rates['an']['packets']} packets in {rates['an']['seconds']:.1f} s"}
         finally:
@@ -328,9 +341,7 @@ def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
     what the kernel must read and write at least, from the packets' own
     sizes.  k_classify: descriptor + the packet's first 128 bytes + the bin id
     and index; a bin kernel: index + descriptor + the whole packet + record +
-    the fingerprint (+ its 8-byte hash); k_analyze: record + analysis record,
-    plus the fingerprint hash and the packet's address/name bytes of each
-    classified packet (table reads are L2/MALL-resident, not counted)."""
+    the fingerprint (+ its 8-byte hash); the classifier kernels: see below."""
     cap = desc["caplen"].astype(np.int64)
     fl = rec["fp_len"].astype(np.int64)
     hashed = np.where((rec["flags"] & 4) != 0, 8, 0)
@@ -345,25 +356,42 @@ def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
     # only: their mean per-packet bytes stand in for theirs)
     out["k_fingerprint/fallback"] = int(n_fallback * per_pkt.mean()) if len(per_pkt) else 0
     if an is not None:
-        valid = (an["flags"] & 1) != 0
-        sn = np.where(rec["sni_len"] == 0xffff, 0, rec["sni_len"]).astype(np.int64)
-        ua = np.where(rec["ua_len"] == 0xffff, 0, rec["ua_len"]).astype(np.int64)
-        # k_analyze: record in, analysis record out; per classified packet the
-        # string hash, descriptor, address bytes, server name / user agent, the
-        # fingerprint (verified) and SURVEY 8(d)'s table reads: the pool copy of
-        # the string, 8 B per prior and 12 B per update entry of the lane-scored
-        # packets (device counters, mfp_analysis_stats)
+        # the classifier's five kernels (mfp_analysis.hip); per-kernel counts
+        # come from the device counters (mfp_analysis_counters).  Table bytes
+        # are SURVEY 8(d)'s: the pool copy of each verified string, one 32-B
+        # slot per feature lookup, 8 B per prior and 12 B per update entry
         st = an_stats or {}
-        out["k_analyze"] = int(len(rec) * (32 + an.dtype.itemsize) +
-                               (valid * (8 + 16 + 32 + sn + ua + 2 * fl)).sum() +
-                               8 * st.get("lane_priors", 0) + 12 * st.get("lane_updates", 0))
-        # k_analyze_wave: the 64-byte deferred entry, record, priors, update
-        # entries and the analysis record of each wave-scored packet
-        out["k_analyze_wave"] = int(st.get("deferred", 0) * (64 + 32 + 32) + 8 * st.get("wave_priors", 0) +
+        A = an.dtype.itemsize
+        valid = (an["flags"] & 1) != 0
+        scored = valid & (an["process"] != 0xFFFFFFFF)
+        sn = np.where((rec["sni_len"] == 0xffff) | (rec["msg"] == 15), 0, rec["sni_len"]).astype(np.int64)
+        ua = np.where(rec["ua_len"] == 0xffff, 0, rec["ua_len"]).astype(np.int64)
+        ngroups = (len(rec) + 63) // 64
+        # k_analyze: record in, analysis record out; per classified packet the
+        # stored string hash and the fingerprint verified against its pool copy;
+        # the 16-B work item of each packet with more to do; the sighting bitmap
+        out["k_analyze"] = int(len(rec) * (32 + A) + (valid * (8 + 2 * fl)).sum() +
+                               16 * st.get("work_items", 0) + 8 * ngroups)
+        # k_seen_scan: the bitmap, each sighting's record and hash, one 24-B
+        # sighting-slot update per distinct fingerprint per block
+        out["k_seen_scan"] = int(8 * ngroups + st.get("pending", 0) * (32 + 8) + 24 * st.get("seen_merges", 0))
+        # k_an_features: work item, record, descriptor and the 40-B address
+        # window of each work item; server name and user agent with their pool
+        # copies (scored packets); one 32-B slot per feature lookup; the 64-B
+        # entry written to the lane or wave scorer's list
+        out["k_an_features"] = int(st.get("work_items", 0) * (16 + 32 + 16 + 40) + (scored * 2 * (sn + ua)).sum() +
+                                   32 * st.get("feature_slots", 0) +
+                                   64 * (st.get("lane_scored", 0) + st.get("deferred", 0)))
+        # k_an_score: list entry, fingerprint entry, priors, update entries and
+        # the analysis record of each lane-scored packet
+        out["k_an_score"] = int(st.get("lane_scored", 0) * (64 + 32 + A) + 8 * st.get("lane_priors", 0) +
+                                12 * st.get("lane_updates", 0))
+        # k_analyze_wave: the same for each wave-scored packet
+        out["k_analyze_wave"] = int(st.get("deferred", 0) * (64 + 32 + A) + 8 * st.get("wave_priors", 0) +
                                     12 * st.get("wave_updates", 0))
         # k_analyze_resolve: one 8-byte sighting bitmap word per 64 packets, and per
         # pending sighting its record, its sighting-table slot (24 B) and its result
-        out["k_analyze_resolve"] = int(8 * ((len(rec) + 63) // 64) + st.get("pending", 0) * (32 + 24 + 32))
+        out["k_analyze_resolve"] = int(8 * ngroups + st.get("pending", 0) * (32 + 24 + A))
     return out
 
 
@@ -618,10 +646,10 @@ def main():
                    "ms_per_step": round(el2 / steps2 * 1e3, 4),
                    "diverse_tls_fraction": args.diverse_leg,
                    "distinct_fingerprints_per_step": distinct2,
-                   "k_analyze_ms": round(prof2["k_analyze"][1] / steps2, 4) if "k_analyze" in prof2 else None,
-                   "k_analyze_wave_ms": round(prof2["k_analyze_wave"][1] / steps2, 4) if "k_analyze_wave" in prof2 else None,
-                   "k_analyze_resolve_ms": round(prof2["k_analyze_resolve"][1] / steps2, 4)
-                   if "k_analyze_resolve" in prof2 else None,
+                   "classifier_ms": {k: round(v[1] / steps2, 4) for k, v in prof2.items()
+                                     if k.startswith(("k_analyze", "k_an_", "k_seen"))},
+                   "kernel_ms": round(sum(v[1] for v in prof2.values()) / steps2, 4),
+                   "host_ms": round(el2 / steps2 * 1e3 - sum(v[1] for v in prof2.values()) / steps2, 4),
                    "status": {mercury_amd.api.STATUS_NAMES[i]: int(st2[i]) for i in range(5)},
                    "lru_entries": int(ctx.analysis_stats()[3]),
                    "what": "same step, same archive; the unique packets' TLS ClientHellos get random first two "

@@ -422,7 +422,11 @@ MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
  * [1] unknown-TLS sightings, [2] fingerprints with too many processes,
  * [3] packets scored wave-per-packet (k_analyze_wave), [4] / [5] prior and
  * update-list entries read by the lane-per-packet scorer, [6] / [7] the same
- * for the wave scorer (SURVEY 8(d)'s 8*P + 12*U table bytes) */
+ * for the wave scorer (SURVEY 8(d)'s 8*P + 12*U table bytes), [8] work items
+ * k_analyze hands to k_an_features, [9] packets scored lane-per-packet
+ * (k_an_score), [10] feature-table slots read by k_an_features, [11] unknown-
+ * TLS sightings merged into the batch's sighting table by k_seen_scan */
+#define MFP_AN_NCOUNTERS 12
 MFP_EXPORT int mfp_analysis_counters(mfp_context ctx, uint64_t *out, size_t n);
 
 /* bytes of the classifier's device tables in HBM */

@@ -435,12 +435,12 @@ class Context:
         return list(out)
 
     COUNTER_NAMES = ("classified", "pending", "oversize", "deferred", "lane_priors", "lane_updates", "wave_priors",
-                     "wave_updates")
+                     "wave_updates", "work_items", "lane_scored", "feature_slots", "seen_merges")
 
     def analysis_counters(self):
         """The last analysis batch's device counters (mfp_analysis_counters) as a dict."""
-        out = (ctypes.c_uint64 * 8)()
-        if self.lib.mfp_analysis_counters(self.h, out, 8) != 0:
+        out = (ctypes.c_uint64 * len(self.COUNTER_NAMES))()
+        if self.lib.mfp_analysis_counters(self.h, out, len(self.COUNTER_NAMES)) != 0:
             raise MercuryAmdError(_err(self.lib))
         return dict(zip(self.COUNTER_NAMES, (int(x) for x in out)))
 

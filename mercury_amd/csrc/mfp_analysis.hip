@@ -770,6 +770,7 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
     if (lane == 0) P.seg_n[3 * seg] = n_wk;
     if (lane == 0 && n_an) atomicAdd(&P.stats[0], (unsigned long long)n_an);
     if (lane == 0 && n_pend) atomicAdd(&P.stats[1], (unsigned long long)n_pend);
+    if (lane == 0 && n_wk) atomicAdd(&P.stats[8], (unsigned long long)n_wk);
 }
 
 __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
@@ -782,6 +783,7 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
     Deferred *ll = P.lanel + (uint64_t)seg * P.seg_cap, *dl = P.deferred + (uint64_t)seg * P.seg_cap;
     const uint32_t total = rfl(P.seg_n[3 * seg]);
     uint32_t n_l = 0, n_d = 0;       // wave-uniform list counts
+    uint32_t n_look = 0;             // feature-table lookups issued by this lane (mfp_analysis_counters [10])
     for (uint32_t b0 = 0; b0 < total; b0 += 64) {
         const bool live = b0 + lane < total;
         WorkItem w;
@@ -867,6 +869,7 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
             const uint32_t dport = r.dst_port;
 
             // ---- the six feature lookups
+            n_look += 2u + (ipv != 0) + (!ssh_ua) + (plain ? 2u : 0u);
             Hit h;
             h = probe_feature_lane(D, entry, F_ASN, asn, nullptr, 0xffffffffu);
             hoff[0] = h.off; hcnt[0] = h.cnt;
@@ -926,6 +929,10 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
     }
     if (lane == 0) { P.seg_n[3 * seg + 1] = n_l; P.seg_n[3 * seg + 2] = n_d; }
     if (lane == 0 && n_d) atomicAdd(&P.stats[3], (unsigned long long)n_d);
+    if (lane == 0 && n_l) atomicAdd(&P.stats[9], (unsigned long long)n_l);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) n_look += __shfl_xor(n_look, d, 64);
+    if (lane == 0 && n_look) atomicAdd(&P.stats[10], (unsigned long long)n_look);
 }
 
 __global__ __launch_bounds__(64 * SW) void k_an_score(AParams P) {
@@ -1349,6 +1356,7 @@ __global__ __launch_bounds__(64 * SEEN_WPB) void k_seen_scan(AParams P) {
     __shared__ unsigned int lfirst[SEEN_LDS], lnlast[SEEN_LDS], lcnt[SEEN_LDS];
     const uint32_t lane = lane_id();
     const uint32_t wid = threadIdx.x >> 6;
+    uint32_t merges = 0;   // HBM sighting-slot updates (mfp_analysis_counters [11])
     for (int k = threadIdx.x; k < SEEN_LDS; k += 64 * SEEN_WPB) {
         lh[k] = ~0ull; lfirst[k] = ~0u; lnlast[k] = ~0u; lcnt[k] = 0;
     }
@@ -1392,14 +1400,17 @@ __global__ __launch_bounds__(64 * SEEN_WPB) void k_seen_scan(AParams P) {
                             break;
                         }
                     }
-                    if (!done) seen_merge(P.seen, h0, fi, la, c);   // the block's table is crowded: straight to HBM
+                    if (!done) { seen_merge(P.seen, h0, fi, la, c); merges++; }   // the block's table is crowded: straight to HBM
                 }
             }
         }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < SEEN_LDS; k += 64 * SEEN_WPB)
-        if (lh[k] != ~0ull) seen_merge(P.seen, lh[k], lfirst[k], ~lnlast[k], lcnt[k]);
+        if (lh[k] != ~0ull) { seen_merge(P.seen, lh[k], lfirst[k], ~lnlast[k], lcnt[k]); merges++; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) merges += __shfl_xor(merges, d, 64);
+    if (lane == 0 && merges) atomicAdd(&P.stats[11], (unsigned long long)merges);
 }
 
 // k_seen_export: the batch's distinct unknown-TLS fingerprints, in the order

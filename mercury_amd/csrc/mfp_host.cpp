@@ -294,8 +294,8 @@ struct Slot {
     bool init() {
         return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
                hipMalloc(&d_bins, 16 * sizeof(unsigned long long)) == hipSuccess &&
-               hipMalloc(&d_an_stats, 8 * sizeof(unsigned long long)) == hipSuccess &&
-               hipMemset(d_an_stats, 0, 8 * sizeof(unsigned long long)) == hipSuccess &&
+               hipMalloc(&d_an_stats, MFP_AN_NCOUNTERS * sizeof(unsigned long long)) == hipSuccess &&
+               hipMemset(d_an_stats, 0, MFP_AN_NCOUNTERS * sizeof(unsigned long long)) == hipSuccess &&
                hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
@@ -515,7 +515,7 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
         return -2;
     }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
-    HIPCHK(hipMemsetAsync(S.d_an_stats, 0, 8 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(S.d_an_stats, 0, MFP_AN_NCOUNTERS * sizeof(unsigned long long), s));
     if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, d_attr_prob,
                             S.d_pending, S.d_work_items, S.d_lanel, S.d_deferred, S.d_segn, S.d_an_stats, c->mode,
                             c->an_lane_max_p, s, c->prof) != 0) {
@@ -1007,9 +1007,9 @@ extern "C" MFP_EXPORT int mfp_analysis_stats(mfp_context c, uint64_t out[4]) {
 extern "C" MFP_EXPORT int mfp_analysis_counters(mfp_context c, uint64_t *out, size_t n) {
     if (!c || !c->clf || (n && !out)) { mfp_set_error("analysis is not enabled"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    unsigned long long h[8];
+    unsigned long long h[MFP_AN_NCOUNTERS];
     HIPCHK(hipMemcpy(h, c->slot[c->an_slot].d_an_stats, sizeof h, hipMemcpyDeviceToHost));
-    for (size_t k = 0; k < n && k < 8; k++) out[k] = h[k];
+    for (size_t k = 0; k < n && k < MFP_AN_NCOUNTERS; k++) out[k] = h[k];
     return 0;
 }
 

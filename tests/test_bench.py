@@ -44,9 +44,15 @@ def test_kernel_bytes_accounting():
     rec["ua_len"] = 0xffff
     an = np.zeros(3, ANALYSIS_DTYPE)
     an["flags"] = [1, 0, 0]
-    kb = bench.kernel_bytes(rec, desc, an)
+    an["process"] = [7, 0xFFFFFFFF, 0xFFFFFFFF]
+    st = {"work_items": 1, "lane_scored": 1, "feature_slots": 5, "lane_priors": 4, "lane_updates": 10,
+          "pending": 0, "deferred": 0, "seen_merges": 0}
+    kb = bench.kernel_bytes(rec, desc, an, an_stats=st)
     assert kb["k_fingerprint/tls_ch"] == 4 + 16 + 600 + 32 + 300
     assert kb["k_fp_seg/http_req"] == 4 + 16 + 200 + 32 + 100 + 8
     assert kb["k_fingerprint/tcp_syn"] == 4 + 16 + 60 + 32 + 40
     assert kb["k_classify"] == 3 * (16 + 5) + 128 + 128 + 60
-    assert kb["k_analyze"] == 3 * (32 + 32) + (8 + 16 + 32 + 20)   # record + 32-B analysis record
+    assert kb["k_analyze"] == 3 * (32 + 32) + (8 + 2 * 300) + 16 + 8   # record + 32-B analysis record
+    assert kb["k_an_features"] == (16 + 32 + 16 + 40) + 2 * 20 + 32 * 5 + 64
+    assert kb["k_an_score"] == (64 + 32 + 32) + 8 * 4 + 12 * 10
+    assert kb["k_seen_scan"] == 8
