@@ -8,10 +8,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmercury_amd.so")
 OBJ = os.path.join(HERE, "_obj")
 
-SOURCES = ["mfp_kernels.hip", "mfp_analysis.hip", "mfp_compact.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp",
+SOURCES = ["mfp_kernels.hip", "mfp_k_tls.hip", "mfp_k_http.hip", "mfp_k_small.hip", "mfp_k_all.hip", "mfp_analysis.hip", "mfp_compact.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp",
            "mfp_pcap.cpp", "mfp_json.cpp", "mfp_prevalence.cpp", "mfp_quic.hip", "mfp_reassembly.cpp"]
-HEADERS = ["mfp_device.hpp", "mfp_internal.h", "mfp_analysis.h", "mfp_common.hpp", "mfp_cipher_ranges.inc", "mfp_quic_crypto.hpp",
-           "mfp_encap.hpp"]
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 
 
@@ -22,16 +20,29 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _includes(path, seen=None):
+    """`path` and the local headers it includes (#include "..."), transitively."""
+    seen = set() if seen is None else seen
+    path = os.path.normpath(path)
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path, encoding="utf-8", errors="replace") as f:
+        for line in f:
+            t = line.strip()
+            if t.startswith("#include") and '"' in t:
+                _includes(os.path.join(os.path.dirname(path), t.split('"')[1]), seen)
+    return seen
+
+
 def build(verbose=False):
     os.makedirs(OBJ, exist_ok=True)
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", h)
-                                                       for h in ("mfp.h", "mercury_amd_libmerc.h")]
     objs, procs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OBJ, s + ".o")
         objs.append(obj)
-        if _newer(obj, [src] + hdrs):
+        if _newer(obj, sorted(_includes(src))):
             cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
                    "-Wall", "-c", src, "-o", obj]
             if verbose:

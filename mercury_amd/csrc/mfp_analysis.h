@@ -96,6 +96,9 @@ struct mfp_classifier_dev {
     uint32_t *dom_info = nullptr;      // per prefix: [type (1 mapping, 2 exception) | count << 8, byte offset]
     uint8_t *dom_bytes = nullptr;      // mapped domain indices (uint8_t, as the reference stores them)
 };
+// the classifier's per-batch device words: the public counters
+// (mfp_analysis_counters), then [MFP_AN_NCOUNTERS] the wave scorer's segment queue
+#define MFP_AN_STATS_WORDS (MFP_AN_NCOUNTERS + 4)
 #define MFP_DOM_MAPPING 1u
 #define MFP_DOM_EXCEPTION 2u
 

@@ -591,6 +591,19 @@ struct Deferred {
     uint32_t i, entry, slow_sni, slow_ua;
     uint32_t off[6], cnt[6];
 };
+// a packet k_an_features hands to the wave scorers (k_analyze_wave /
+// k_analyze_big): the Deferred fields plus what the scorer would otherwise
+// fetch first (its fingerprint entry, the fingerprint type), so one load of
+// these 20 words -- lane k holds word k -- starts a packet
+struct WItem {
+    uint32_t i, entry, flags, ft;   // flags: bit 0 slow server name, bit 1 SSH user agent, xattr << 16
+    uint32_t po, np, mdb, dmz;      // mfp_entry: proc_off, nproc, malware_db, generic_dmz
+    uint32_t off[6], cnt[6];
+};
+constexpr uint32_t WITEM_WORDS = sizeof(WItem) / 4;
+static_assert(WITEM_WORDS == 20, "WItem layout");
+enum : uint32_t { WI_I = 0, WI_ENTRY = 1, WI_FLAGS = 2, WI_FT = 3, WI_PO = 4, WI_NP = 5, WI_MDB = 6, WI_DMZ = 7,
+                  WI_OFF = 8, WI_CNT = 14 };
 // a packet k_analyze hands to k_an_features: its fingerprint entry (~0u: none)
 // and what to do (WK_SCORE, WK_XCHECK, WK_PENDING)
 struct WorkItem { uint32_t i, entry, flags, pad; };
@@ -607,10 +620,10 @@ struct AParams {
     double *attr_prob;           // optional: archive-tag probabilities, MFP_ATTR_DB_TAGS per packet
     uint64_t *pend_bits;         // per group of 64 packets: unknown-TLS sightings (k_analyze_resolve)
     mfp_seen_tab seen;           // this batch's sightings per distinct fingerprint
-    struct Deferred *deferred;   // packets scored by k_analyze_wave (per-segment lists)
+    struct WItem *deferred;      // packets scored by k_analyze_wave / k_analyze_big (per-segment lists)
     uint32_t mode;
     uint32_t lane_max_p;         // k_an_score takes fingerprints with P <= min(lane_max_p, PL)
-    unsigned long long *stats;   // [0] analyzed, [1] pending unknown-TLS, [2] over-size P, [3] deferred, [4..7] table entries read
+    unsigned long long *stats;   // MFP_AN_STATS_WORDS: the counters of mfp_analysis_counters, then the wave scorer's segment queue
     // the packets to score travel in per-wave segments (k_analyze wave s
     // writes segment s; the later kernels' wave s reads it): no global
     // counter, no atomics, dense lanes
@@ -780,7 +793,8 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
     const uint32_t seg = (uint32_t)(blockIdx.x * AW + wid);
     if (seg >= P.nseg) return;
     const WorkItem *wk = P.work + (uint64_t)seg * P.seg_cap;
-    Deferred *ll = P.lanel + (uint64_t)seg * P.seg_cap, *dl = P.deferred + (uint64_t)seg * P.seg_cap;
+    Deferred *ll = P.lanel + (uint64_t)seg * P.seg_cap;
+    WItem *dl = P.deferred + (uint64_t)seg * P.seg_cap;
     const uint32_t total = rfl(P.seg_n[3 * seg]);
     uint32_t n_l = 0, n_d = 0;       // wave-uniform list counts
     uint32_t n_look = 0;             // feature-table lookups issued by this lane (mfp_analysis_counters [10])
@@ -798,8 +812,10 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
         else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; r.fp_offset = 0; r.net = 0; r.msg = 0;
                r.sni_off = 0; r.sni_len = 0xffff; r.ua_off = 0; r.ua_len = 0xffff; r.dst_port = 0; }
         const uint8_t *fp = P.fp_arena + r.fp_offset;
-        uint32_t np = 0;
-        if (scored) np = D.entry[entry].nproc;
+        mfp_entry E;
+        E.proc_off = 0; E.nproc = 0; E.malware_db = 0; E.generic_dmz = 0;
+        if (scored) E = D.entry[entry];
+        uint32_t np = E.nproc;
         if (scored && np > 64 * MAXP_CHUNKS_BIG) {   // beyond the big scorer: counted, left unscored
             atomicAdd(&P.stats[2], 1ull);
             scored = false;
@@ -902,9 +918,17 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
                 has[2] = cand_feature_lane(D, entry, F_SNI, nh, sl, vh[2], voff[2]);
             }
         }
+        // byte-exact check of the candidates.  Lane by lane: each lane compares
+        // its own (short: server names, user agents) strings with a few wide
+        // loads, all lanes at once; the wave-cooperative check would take one
+        // memory round trip per string of the wave, one after another
 #pragma unroll
         for (int v = 0; v < 3; v++) {
+#ifdef MFP_AN_FEAT_WAVE_VERIFY
             const bool ok = wave_verify(has[v], vs[v], (const uint8_t *)D.pool + voff[v], vl[v], lane);
+#else
+            const bool ok = !has[v] || lane_eq(vs[v], (const uint8_t *)D.pool + voff[v], vl[v]);
+#endif
             if (has[v]) {
                 // a hash collision (ok == false) takes the full probe, which keeps looking
                 const Hit h = ok ? vh[v] : probe_feature_lane(D, entry, v == 0 ? F_UA : v == 1 ? F_DOMAIN : F_SNI, vk[v],
@@ -923,7 +947,15 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
         for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
         const uint64_t lm = __ballot(lanep), dm = __ballot(defer);
         if (lanep) ll[n_l + __builtin_popcountll(lm & ((1ull << lane) - 1))] = d;
-        if (defer) dl[n_d + __builtin_popcountll(dm & ((1ull << lane) - 1))] = d;
+        if (defer) {
+            WItem w;
+            w.i = d.i; w.entry = entry; w.flags = (plain ? 0u : 1u) | (ssh_ua ? 2u : 0u) | (xattr << 16);
+            w.ft = r.fp_type;
+            w.po = E.proc_off; w.np = np; w.mdb = E.malware_db; w.dmz = E.generic_dmz;
+#pragma unroll
+            for (uint32_t f = 0; f < NFEAT; f++) { w.off[f] = hoff[f]; w.cnt[f] = hcnt[f]; }
+            dl[n_d + __builtin_popcountll(dm & ((1ull << lane) - 1))] = w;
+        }
         n_l += (uint32_t)__builtin_popcountll(lm);
         n_d += (uint32_t)__builtin_popcountll(dm);
     }
@@ -1037,101 +1069,390 @@ __global__ __launch_bounds__(64 * SW) void k_an_score(AParams P) {
     if (lane == 0 && c_upd) atomicAdd(&P.stats[5], (unsigned long long)c_upd);
 }
 
-// k_analyze_wave: the packets k_analyze deferred (more than PL processes, or a
-// server name that needs the full normalisation) -- one wavefront per packet,
-// lane i holds process i (up to 64 * MAXP_CHUNKS processes).  Scores live in
-// LDS: the prior and the first 64 updates of every list are loaded in one
-// round trip, then the lists are applied feature by feature as lane-parallel
-// scatters (a list names each process at most once, so every process sees the
-// reference's addition order; lists flagged MFP_UPD_SERIAL go one by one).
-// the scorer, one wave per deferred packet; CH chunks of 64 processes live
-// in registers (sc) and in the wave's LDS rows (scl, fl); WPB waves per block
-template <int CH, int WPB>
-__device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[336], char (*ua_buf)[520],
-                                            double (*sc_lds)[64 * CH], uint8_t (*fl_lds)[64 * CH]) {
+// The wave scorers: the packets k_an_features deferred (more than PL
+// processes, a server name that needs the full normalisation, an SSH user
+// agent) -- one wavefront per packet, lane i holds process i.  Scores live in
+// the wave's LDS row: the prior and the first 64 entries of every update list
+// arrive in one round trip, then the lists are applied feature by feature as
+// lane-parallel scatters (a list names each process at most once, so every
+// process sees the reference's addition order; lists flagged MFP_UPD_SERIAL
+// go one by one); max / second max, the dmz swap, softmax and the sums in the
+// reference's order (naive_bayes.hpp:752-772, analysis.h:222-358,
+// softmax.hpp:227-264).
+
+// the slow feature lookups of a wave-scored packet (WItem flags): the server
+// name normalised on lane 0 into LDS, hashed and verified lane-parallel
+// (strncpy 256, NUL stops); the SSH user agent (ssh_init_packet::do_analysis
+// ssh.h:480-487): protocol then comment into a data_buffer<512> (nulled --
+// empty -- when they do not fit), strncpy 511, NUL stops.  The record's span
+// is "protocol SP comment"; its first space is the delimiter.  Updates
+// off/cnt of features 3 (UA), 4 (domain), 5 (SNI); returns the features changed.
+ADEV uint32_t slow_lookups(const AParams &P, uint32_t i, uint32_t entry, uint32_t flags, char *nbuf, char *ub,
+                           uint32_t (&off)[NFEAT], uint32_t (&cnt)[NFEAT], uint32_t lane) {
+    const mfp_classifier_dev &D = P.D;
+    uint32_t changed = 0;
+    if (flags & 1u) {
+        const mfp_record r = P.rec[i];
+        const uint32_t sni = rfl((uint32_t)r.sni_off | ((uint32_t)r.sni_len << 16));
+        const uint32_t sl = (sni >> 16) == 0xffff ? 0 : (sni >> 16);
+        const uint8_t *sp = ((r.flags & MFP_FLAG_SIDECAR) ? P.fp_arena + r.fp_offset + ((r.fp_len + 7) & ~7u) + 8
+                                                         : P.arena + P.desc[i].offset) + (sni & 0xffff);
+        int nlen = 0;
+        if (lane == 0) nlen = normalize_server_name(sp, (int)sl, nbuf);
+        nlen = (int)rfl((uint32_t)nlen);
+        __builtin_amdgcn_wave_barrier();
+        const int tld = (int)rfl((uint32_t)(lane == 0 ? tld_domain_offset(nbuf, nlen) : 0));
+        const uint8_t *dom = (const uint8_t *)nbuf + tld;
+        Hit h = probe_feature(D, entry, F_DOMAIN, wave_hash(dom, (uint32_t)(nlen - tld), lane), dom,
+                              (uint32_t)(nlen - tld), true, lane);
+        off[4] = h.off; cnt[4] = h.cnt;
+        h = probe_feature(D, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
+                          (const uint8_t *)nbuf, (uint32_t)nlen, true, lane);
+        off[5] = h.off; cnt[5] = h.cnt;
+        __builtin_amdgcn_wave_barrier();
+        changed |= 3u << 4;
+    }
+    if (flags & 2u) {
+        const mfp_record r = P.rec[i];
+        const uint8_t *sp = P.arena + P.desc[i].offset + r.ua_off;
+        const uint32_t L = r.ua_len;
+        int ulen = 0;
+        if (lane == 0) {
+            uint32_t pl = 0;
+            while (pl < L && sp[pl] != ' ') pl++;
+            const uint32_t total = pl < L ? L - 1 : L;
+            uint32_t n = total > 512 ? 0u : (total > 511 ? 511u : total);
+            uint32_t k = 0;
+            for (uint32_t j = 0; k < n && j < L; j++) {
+                if (j == pl) continue;
+                const char c = (char)sp[j];
+                if (c == 0) break;
+                ub[k++] = c;
+            }
+            ulen = (int)k;
+        }
+        ulen = (int)rfl((uint32_t)ulen);
+        __builtin_amdgcn_wave_barrier();
+        const Hit h = probe_feature(D, entry, F_UA, wave_hash((const uint8_t *)ub, (uint32_t)ulen, lane),
+                                    (const uint8_t *)ub, (uint32_t)ulen, true, lane);
+        off[3] = h.off; cnt[3] = h.cnt;
+        __builtin_amdgcn_wave_barrier();
+        changed |= 1u << 3;
+    }
+    return changed;
+}
+
+// one feature's update list applied to the wave's score row; u_idx/u_val:
+// entries 0..63 (lane k: entry k), the rest loaded here
+ADEV void scatter_list(const mfp_classifier_dev &D, double *scl, uint32_t off, uint32_t cntf, uint32_t u_idx,
+                       double u_val, bool anylong, uint32_t lane) {
+    const uint32_t c = cntf & ~MFP_UPD_SERIAL;
+    if (cntf & MFP_UPD_SERIAL) {
+        for (uint32_t k = 0; k < c; k++) {
+            const mfp_update x = k < 64 && !anylong ? mfp_update{(uint32_t)__shfl((int)u_idx, (int)k, 64), 0,
+                                                                __shfl(u_val, (int)k, 64)}
+                                                    : D.upd[off + k];
+            if (lane == 0) scl[x.idx] += x.value;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else {
+        if (lane < c) scl[u_idx] += u_val;
+        for (uint32_t b = 64; b < c; b += 64) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (b + lane < c) { const mfp_update x = D.upd[off + b + lane]; scl[x.idx] += x.value; }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// max, then second max, over the wave's CH chunks (sequential first-index rule)
+template <int CH>
+ADEV void max_two(const double (&sc)[CH], uint32_t np, uint32_t lane, double &mx, uint32_t &imx, uint32_t &isx) {
+    mx = -1.7976931348623157e308;
+    imx = 0xffffffffu;
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+        const uint32_t pi = (uint32_t)c * 64 + lane;
+        if (pi < np && (imx == 0xffffffffu || sc[c] > mx)) { mx = sc[c]; imx = pi; }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const double om = __shfl_xor(mx, d, 64);
+        const uint32_t oi = (uint32_t)__shfl_xor((int)imx, d, 64);
+        if (oi != 0xffffffffu && (imx == 0xffffffffu || om > mx || (om == mx && oi < imx))) { mx = om; imx = oi; }
+    }
+    imx = rfl(imx);
+    mx = __hiloint2double((int)rfl((uint32_t)(__double_as_longlong(mx) >> 32)), (int)rfl((uint32_t)__double_as_longlong(mx)));
+    double sx = -1.7976931348623157e308;
+    isx = 0xffffffffu;
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+        const uint32_t pi = (uint32_t)c * 64 + lane;
+        if (pi < np && pi != imx && (isx == 0xffffffffu || sc[c] > sx)) { sx = sc[c]; isx = pi; }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const double om = __shfl_xor(sx, d, 64);
+        const uint32_t oi = (uint32_t)__shfl_xor((int)isx, d, 64);
+        if (oi != 0xffffffffu && (isx == 0xffffffffu || om > sx || (om == sx && oi < isx))) { sx = om; isx = oi; }
+    }
+    isx = rfl(isx);
+    if (isx == 0xffffffffu) isx = 0;   // P == 1: index_sec stays 0
+}
+
+// the softmax sums in process order, as the reference adds them
+// (softmax.hpp:250-263, analysis.h:268-277), one sum per lane: 0 score_sum,
+// 1 score_sum_without_max, 2 malware_prob, 3.. the archive tags.  Each lane
+// adds e or +0.0 (e >= 0: the same sums), eight row entries per LDS batch.
+ADEV double row_sums(const double *scl, const uint8_t *fl, uint32_t np, uint32_t imx, uint32_t nsum, uint32_t lane) {
+    double acc = 0.0;
+    if (lane < nsum) {
+        const uint32_t sh = lane >= 3 ? lane - 2 : 0;
+        auto take = [&](uint32_t p, uint32_t f) {
+            return lane == 0 ? true : lane == 1 ? p != imx : lane == 2 ? (f & 1u) != 0 : ((f >> sh) & 1u) && !(f & 0x80u);
+        };
+        uint32_t p = 0;
+        for (; p + 8 <= np; p += 8) {
+            double e[8];
+            uint32_t f[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) { e[k] = scl[p + k]; f[k] = fl[p + k]; }
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc += take(p + k, f[k]) ? e[k] : 0.0;
+        }
+        for (; p < np; p++) acc += take(p, fl[p]) ? scl[p] : 0.0;
+    }
+    return acc;
+}
+ADEV double lane_d(double v, uint32_t l) {
+    return __hiloint2double(__builtin_amdgcn_readlane((int)(__double_as_longlong(v) >> 32), (int)l),
+                            __builtin_amdgcn_readlane((int)__double_as_longlong(v), (int)l));
+}
+
+// ---- k_analyze_wave (P <= 64 * MAXP_CHUNKS): software-pipelined over each
+// segment's packets.  Packet q + 1's table rows (update-list heads, priors,
+// process attributes and ids, malware bytes, its analysis-record word) are
+// loaded while packet q is scored, and packet q + 2's WItem one step earlier,
+// so the scoring tail of q runs on LDS and registers only and a packet costs
+// about one memory round trip instead of a chain of them.
+struct WStage {
+    uint32_t uidx[NFEAT];
+    double uval[NFEAT];
+    double pr[MAXP_CHUNKS];
+    uint32_t attr[MAXP_CHUNKS], pid[MAXP_CHUNKS];
+    uint32_t malb[MAXP_CHUNKS];
+    uint32_t outw;               // the analysis record's attr / status / flags word (k_analyze's)
+};
+ADEV uint32_t wf(uint32_t w, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)w, k); }
+ADEV uint32_t wi_load(const WItem *seg, uint32_t q, uint32_t total, uint32_t lane) {
+    return q < total && lane < WITEM_WORDS ? ((const uint32_t *)(seg + q))[lane] : 0u;
+}
+// issue (no use of the results: the loads stay in flight)
+ADEV void stage_issue(const AParams &P, uint32_t w, WStage &st, uint32_t lane) {
+    const mfp_classifier_dev &D = P.D;
+    const uint32_t np = wf(w, WI_NP), po = wf(w, WI_PO), i = wf(w, WI_I);
+    const bool take = np != 0 && np <= 64u * MAXP_CHUNKS;      // a word of zeros past the segment's end
+#pragma unroll
+    for (uint32_t f = 0; f < NFEAT; f++) {
+        const uint32_t c = wf(w, WI_CNT + f) & ~MFP_UPD_SERIAL, o = wf(w, WI_OFF + f);
+        st.uidx[f] = 0; st.uval[f] = 0.0;
+        if (take && lane < c) { st.uidx[f] = D.upd[o + lane].idx; st.uval[f] = D.upd[o + lane].value; }
+    }
+#pragma unroll
+    for (int c = 0; c < MAXP_CHUNKS; c++) {
+        const uint32_t pi = (uint32_t)c * 64 + lane;
+        st.pr[c] = 0.0; st.attr[c] = 0; st.pid[c] = 0; st.malb[c] = 0;
+        if (take && pi < np) {
+            st.pr[c] = D.prior[po + pi];
+            st.attr[c] = D.proc_attr[po + pi];
+            st.pid[c] = D.proc_id[po + pi];
+            st.malb[c] = D.proc_mal[po + pi];
+        }
+    }
+    st.outw = take ? ((const uint32_t *)(P.out + i))[5] : 0u;
+}
+
+__device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_buf)[336], char (*ua_buf)[520],
+                                                 double (*sc_lds)[64 * MAXP_CHUNKS], uint32_t (*at_lds)[64 * MAXP_CHUNKS],
+                                                 uint32_t (*id_lds)[64 * MAXP_CHUNKS], uint8_t (*fl_lds)[64 * MAXP_CHUNKS]) {
+    constexpr int CH = MAXP_CHUNKS;
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
-    char *nbuf = sni_buf[wid];
     double *scl = sc_lds[wid];
+    uint32_t *arow = at_lds[wid], *idrow = id_lds[wid];
+    uint8_t *fl = fl_lds[wid];
     const mfp_classifier_dev &D = P.D;
-    const uint64_t nw = (uint64_t)gridDim.x * WPB;
     uint64_t w_prior = 0, w_upd = 0;   // table entries read (mfp_analysis_counters [6], [7])
-    for (uint64_t sg = (uint64_t)blockIdx.x * WPB + wid; sg < P.nseg; sg += nw) {
-    const Deferred *dseg = P.deferred + sg * P.seg_cap;
+    for (;;) {
+        // segments from a queue: the waves that draw short lists take more of them
+        unsigned long long sgl = 0;
+        if (lane == 0) sgl = atomicAdd(&P.stats[MFP_AN_NCOUNTERS], 1ull);
+        const uint64_t sg = rfl((uint32_t)sgl);
+        if (sg >= P.nseg) break;
+        const WItem *seg = P.deferred + sg * P.seg_cap;
+        const uint32_t total = rfl(P.seg_n[3 * sg + 2]);
+        if (total == 0) continue;
+        uint32_t wc = wi_load(seg, 0, total, lane), wn = wi_load(seg, 1, total, lane);
+        WStage st;
+        stage_issue(P, wc, st, lane);
+        for (uint32_t q = 0; q < total; q++) {
+            const uint32_t i = wf(wc, WI_I), np = wf(wc, WI_NP), po = wf(wc, WI_PO);
+            const uint32_t flags = wf(wc, WI_FLAGS), mdb = wf(wc, WI_MDB), dmz = wf(wc, WI_DMZ), ft = wf(wc, WI_FT);
+            const bool mine = np <= 64u * CH;   // larger: k_analyze_big's
+            uint32_t off[NFEAT], cnt[NFEAT];
+#pragma unroll
+            for (uint32_t f = 0; f < NFEAT; f++) { off[f] = wf(wc, WI_OFF + f); cnt[f] = wf(wc, WI_CNT + f); }
+            uint32_t malbits = 0, outw = 0;
+            if (mine) {
+                // ---- [A] this packet's rows into LDS, the update lists applied
+                if (flags & 3u) {
+                    const uint32_t ch = slow_lookups(P, i, wf(wc, WI_ENTRY), flags, sni_buf[wid], ua_buf[wid], off, cnt, lane);
+#pragma unroll
+                    for (uint32_t f = 3; f < NFEAT; f++)
+                        if ((ch >> f) & 1u) {
+                            st.uidx[f] = 0; st.uval[f] = 0.0;
+                            if (lane < (cnt[f] & ~MFP_UPD_SERIAL)) { st.uidx[f] = D.upd[off[f] + lane].idx; st.uval[f] = D.upd[off[f] + lane].value; }
+                        }
+                }
+                w_prior += np;
+                uint32_t anylong = 0;
+#pragma unroll
+                for (uint32_t f = 0; f < NFEAT; f++) {
+                    w_upd += cnt[f] & ~MFP_UPD_SERIAL;
+                    anylong |= (cnt[f] & ~MFP_UPD_SERIAL) > 64 ? 1u : 0u;
+                }
+#pragma unroll
+                for (int c = 0; c < CH; c++) {
+                    const uint32_t pi = (uint32_t)c * 64 + lane;
+                    if ((uint32_t)c * 64 < np) {
+                        scl[pi] = st.pr[c];
+                        arow[pi] = st.attr[c];
+                        idrow[pi] = st.pid[c];
+                        if (st.malb[c]) malbits |= 1u << c;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (uint32_t f = 0; f < NFEAT; f++) scatter_list(D, scl, off[f], cnt[f], st.uidx[f], st.uval[f], anylong, lane);
+                outw = st.outw;
+            }
+            // ---- [B] the next packet's rows and the WItem after it: in flight
+            // while this packet's scoring tail runs
+            const uint32_t w2 = wi_load(seg, q + 2, total, lane);
+            stage_issue(P, wn, st, lane);
+            if (mine) {
+                // ---- [C] scoring tail: LDS and registers only
+                double sc[CH];
+#pragma unroll
+                for (int c = 0; c < CH; c++) sc[c] = (uint32_t)c * 64 < np ? scl[c * 64 + lane] : 0.0;
+                __builtin_amdgcn_wave_barrier();
+                double mx;
+                uint32_t imx, isx;
+                max_two<CH>(sc, np, lane, mx, imx, isx);
+                const uint32_t mal_isx = (wf(malbits, isx & 63) >> (isx >> 6)) & 1u;
+                const uint32_t mal_imx = (wf(malbits, imx & 63) >> (imx >> 6)) & 1u;
+                // the dmz swap (decided by the ranks alone) and the selected
+                // process's archive tags (analysis.h:258-277)
+                const bool swap = mdb && dmz == imx && !mal_isx;
+                const uint32_t ibest = swap ? isx : imx;
+                const uint32_t abest = rfl(arow[ibest]), pbest = rfl(idrow[ibest]);
+                const uint32_t mal_best = swap ? mal_isx : mal_imx;
+                const uint32_t tags = abest & D.db_tags;
+                // softmax (expf in fp32, stored as double) into LDS, per-process flags
+#pragma unroll
+                for (int c = 0; c < CH; c++) {
+                    const uint32_t pi = (uint32_t)c * 64 + lane;
+                    if (pi < np) {
+                        scl[pi] = (double)expf_ref((float)(sc[c] - mx));
+                        uint32_t f = (malbits >> c) & 1u;
+                        if (tags) f |= ((arow[pi] & tags) >> MFP_ATTR_DB_FIRST) << 1;
+                        if (swap && pi == imx) f |= 0x80u;   // process_score[index_max] = 0 (analysis.h:264)
+                        fl[pi] = (uint8_t)f;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const double acc = row_sums(scl, fl, np, imx, tags ? 3u + MFP_ATTR_DB_TAGS : 3u, lane);
+                double ssum = lane_d(acc, 0), swo = lane_d(acc, 1), mal = lane_d(acc, 2);
+                const double p_imx = scl[imx], p_isx = scl[isx];
+                double ap = 0.0;   // lane k < MFP_ATTR_DB_TAGS: tag k's sum
+                if (tags) {
+#pragma unroll
+                    for (int k = 0; k < MFP_ATTR_DB_TAGS; k++) {
+                        const double v = lane_d(acc, 3 + k);
+                        if ((int)lane == k) ap = v;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                double max_score = p_imx;
+                if (ssum > 0.0 && mdb) mal /= ssum;
+                if (swap) {
+                    ssum = swo;
+                    max_score = p_isx;
+                }
+                if (ssum > 0.0) max_score /= ssum;
+                if (tags && P.attr_prob && lane < MFP_ATTR_DB_TAGS && ((tags >> (MFP_ATTR_DB_FIRST + lane)) & 1u))
+                    P.attr_prob[(uint64_t)i * MFP_ATTR_DB_TAGS + lane] = ssum > 0.0 ? ap / ssum : ap;
+                if (lane == 0) {
+                    // status, pending flag and the additional attributes from k_analyze
+                    mfp_analysis a;
+                    a.score = max_score;
+                    a.process = pbest;
+                    a.proc_slot = po + ibest;
+                    a.attr = (uint16_t)(abest | (outw & 0xffffu) | (flags >> 16));
+                    a.status = (uint8_t)(outw >> 16);
+                    a.malware_prob = -1.0;
+                    a.flags = (uint8_t)(MFP_AN_VALID | ((outw >> 24) & MFP_AN_PENDING));
+                    a.reserved = 0;
+                    if (mdb) {
+                        a.malware_prob = mal;
+                        a.flags |= MFP_AN_CLASSIFY_MALWARE;
+                        if (mal_best) a.flags |= MFP_AN_MALWARE;
+                    }
+                    // encrypted_channel (analysis.h:1161-1163)
+                    if ((a.flags & MFP_AN_MALWARE) && ft == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
+                    P.out[i] = a;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            wc = wn;
+            wn = w2;
+        }
+    }
+    if (lane == 0 && w_prior) atomicAdd(&P.stats[6], (unsigned long long)w_prior);
+    if (lane == 0 && w_upd) atomicAdd(&P.stats[7], (unsigned long long)w_upd);
+}
+
+// ---- k_analyze_big (64 * MAXP_CHUNKS < P <= 64 * MAXP_CHUNKS_BIG, production
+// archives have a few): one wave per block, the CH chunks in registers and in
+// the wave's LDS rows, one packet after another
+template <int CH>
+__device__ __forceinline__ void wave_scorer_big(const AParams &P, char *nbuf, char *ub, double *scl, uint8_t *fl) {
+    const uint32_t lane = lane_id();
+    const mfp_classifier_dev &D = P.D;
+    uint64_t w_prior = 0, w_upd = 0;   // table entries read (mfp_analysis_counters [6], [7])
+    for (uint64_t sg = blockIdx.x; sg < P.nseg; sg += gridDim.x) {
+    const WItem *dseg = P.deferred + sg * P.seg_cap;
     const uint32_t total = rfl(P.seg_n[3 * sg + 2]);
     for (uint32_t q = 0; q < total; q++) {
-        const Deferred &dq = dseg[q];
-        const uint32_t i = rfl(dq.i), entry = rfl(dq.entry), slow = rfl(dq.slow_sni);
-        const uint32_t xattr = rfl(dq.slow_ua) >> 16;   // k_an_features' encrypted_dns / domain_faking / faketls
+        const uint32_t wc = wi_load(dseg, q, total, lane);
+        const uint32_t np = wf(wc, WI_NP);
+        if (np <= 64u * MAXP_CHUNKS) continue;   // k_analyze_wave's
+        const uint32_t i = wf(wc, WI_I), po = wf(wc, WI_PO), mdb = wf(wc, WI_MDB), dmz = wf(wc, WI_DMZ);
+        const uint32_t flags = wf(wc, WI_FLAGS), ft = wf(wc, WI_FT);
         uint32_t off[NFEAT], cnt[NFEAT];
 #pragma unroll
-        for (uint32_t f = 0; f < NFEAT; f++) { off[f] = rfl(dq.off[f]); cnt[f] = rfl(dq.cnt[f]); }
-        const mfp_entry E = D.entry[entry];
-        const uint32_t np = rfl(E.nproc), po = rfl(E.proc_off), mdb = rfl(E.malware_db), dmz = rfl(E.generic_dmz);
-        // each instance takes its own size class: up to 64 * CH
-        // processes here, the rest (up to 64 * MAXP_CHUNKS_BIG) in k_analyze_big
-        if ((CH == MAXP_CHUNKS) != (np <= 64u * MAXP_CHUNKS)) continue;
-        const uint32_t ft = rfl((uint32_t)P.rec[i].fp_type);
-        if (slow) {
-            // server name: full normalisation on lane 0 into LDS, hashed and
-            // verified lane-parallel (strncpy 256, NUL stops)
-            const mfp_record r = P.rec[i];
-            const uint32_t sni = rfl((uint32_t)r.sni_off | ((uint32_t)r.sni_len << 16));
-            const uint32_t sl = (sni >> 16) == 0xffff ? 0 : (sni >> 16);
-            const uint8_t *sp = ((r.flags & MFP_FLAG_SIDECAR) ? P.fp_arena + r.fp_offset + ((r.fp_len + 7) & ~7u) + 8
-                                                             : P.arena + P.desc[i].offset) + (sni & 0xffff);
-            int nlen = 0;
-            if (lane == 0) nlen = normalize_server_name(sp, (int)sl, nbuf);
-            nlen = (int)rfl((uint32_t)nlen);
-            __builtin_amdgcn_wave_barrier();
-            const int tld = (int)rfl((uint32_t)(lane == 0 ? tld_domain_offset(nbuf, nlen) : 0));
-            const uint8_t *dom = (const uint8_t *)nbuf + tld;
-            Hit h = probe_feature(D, entry, F_DOMAIN, wave_hash(dom, (uint32_t)(nlen - tld), lane), dom,
-                                  (uint32_t)(nlen - tld), true, lane);
-            off[4] = h.off; cnt[4] = h.cnt;
-            h = probe_feature(D, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
-                              (const uint8_t *)nbuf, (uint32_t)nlen, true, lane);
-            off[5] = h.off; cnt[5] = h.cnt;
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (rfl(dq.slow_ua) & 1u) {
-            // the SSH user agent (ssh_init_packet::do_analysis ssh.h:480-487):
-            // protocol then comment into a data_buffer<512> (nulled -- empty --
-            // when they do not fit), strncpy 511, NUL stops.  The record's span
-            // is "protocol SP comment"; its first space is the delimiter.
-            const mfp_record r = P.rec[i];
-            const uint8_t *sp = P.arena + P.desc[i].offset + r.ua_off;
-            const uint32_t L = r.ua_len;
-            char *ub = ua_buf[wid];
-            int ulen = 0;
-            if (lane == 0) {
-                uint32_t pl = 0;
-                while (pl < L && sp[pl] != ' ') pl++;
-                const uint32_t total = pl < L ? L - 1 : L;
-                uint32_t n = total > 512 ? 0u : (total > 511 ? 511u : total);
-                uint32_t k = 0;
-                for (uint32_t j = 0; k < n && j < L; j++) {
-                    if (j == pl) continue;
-                    const char c = (char)sp[j];
-                    if (c == 0) break;
-                    ub[k++] = c;
-                }
-                ulen = (int)k;
-            }
-            ulen = (int)rfl((uint32_t)ulen);
-            __builtin_amdgcn_wave_barrier();
-            const Hit h = probe_feature(D, entry, F_UA, wave_hash((const uint8_t *)ub, (uint32_t)ulen, lane),
-                                        (const uint8_t *)ub, (uint32_t)ulen, true, lane);
-            off[3] = h.off; cnt[3] = h.cnt;
-            __builtin_amdgcn_wave_barrier();
-        }
+        for (uint32_t f = 0; f < NFEAT; f++) { off[f] = wf(wc, WI_OFF + f); cnt[f] = wf(wc, WI_CNT + f); }
+        if (flags & 3u) slow_lookups(P, i, wf(wc, WI_ENTRY), flags, nbuf, ub, off, cnt, lane);
         w_prior += np;
-#pragma unroll
-        for (uint32_t f = 0; f < NFEAT; f++) w_upd += cnt[f] & ~MFP_UPD_SERIAL;
-        // ---- scores: prior, then the six features in the reference's order
         uint32_t anylong = 0;
 #pragma unroll
-        for (uint32_t f = 0; f < NFEAT; f++) anylong |= (cnt[f] & ~MFP_UPD_SERIAL) > 64 ? 1u : 0u;
+        for (uint32_t f = 0; f < NFEAT; f++) {
+            w_upd += cnt[f] & ~MFP_UPD_SERIAL;
+            anylong |= (cnt[f] & ~MFP_UPD_SERIAL) > 64 ? 1u : 0u;
+        }
         mfp_update u[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) {
@@ -1150,74 +1471,17 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (uint32_t f = 0; f < NFEAT; f++) {
-            const uint32_t c = cnt[f] & ~MFP_UPD_SERIAL;
-            if (cnt[f] & MFP_UPD_SERIAL) {
-                for (uint32_t k = 0; k < c; k++) {
-                    const mfp_update x = k < 64 && !anylong ? mfp_update{(uint32_t)__shfl((int)u[f].idx, (int)k, 64), 0,
-                                                                        __shfl(u[f].value, (int)k, 64)}
-                                                            : D.upd[off[f] + k];
-                    if (lane == 0) scl[x.idx] += x.value;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                }
-            } else {
-                if (lane < c) scl[u[f].idx] += u[f].value;
-                for (uint32_t b = 64; b < c; b += 64) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    if (b + lane < c) { const mfp_update x = D.upd[off[f] + b + lane]; scl[x.idx] += x.value; }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
+        for (uint32_t f = 0; f < NFEAT; f++) scatter_list(D, scl, off[f], cnt[f], u[f].idx, u[f].value, anylong, lane);
         double sc[CH];
 #pragma unroll
         for (int c = 0; c < CH; c++) sc[c] = (uint32_t)c * 64 < np ? scl[c * 64 + lane] : 0.0;
         __builtin_amdgcn_wave_barrier();
-
-        // ---- max / second max (sequential first-index rule)
-        double mx = -1.7976931348623157e308;
-        uint32_t imx = 0xffffffffu;
-#pragma unroll
-        for (int c = 0; c < CH; c++) {
-            const uint32_t pi = (uint32_t)c * 64 + lane;
-            if (pi < np && (imx == 0xffffffffu || sc[c] > mx)) { mx = sc[c]; imx = pi; }
-        }
-        for (int d = 32; d >= 1; d >>= 1) {
-            const double om = __shfl_xor(mx, d, 64);
-            const uint32_t oi = (uint32_t)__shfl_xor((int)imx, d, 64);
-            if (oi != 0xffffffffu && (imx == 0xffffffffu || om > mx || (om == mx && oi < imx))) { mx = om; imx = oi; }
-        }
-        imx = rfl(imx);
-        mx = __hiloint2double((int)rfl((uint32_t)(__double_as_longlong(mx) >> 32)),
-                              (int)rfl((uint32_t)__double_as_longlong(mx)));
-        double sx = -1.7976931348623157e308;
-        uint32_t isx = 0xffffffffu;
-#pragma unroll
-        for (int c = 0; c < CH; c++) {
-            const uint32_t pi = (uint32_t)c * 64 + lane;
-            if (pi < np && pi != imx && (isx == 0xffffffffu || sc[c] > sx)) { sx = sc[c]; isx = pi; }
-        }
-        for (int d = 32; d >= 1; d >>= 1) {
-            const double om = __shfl_xor(sx, d, 64);
-            const uint32_t oi = (uint32_t)__shfl_xor((int)isx, d, 64);
-            if (oi != 0xffffffffu && (isx == 0xffffffffu || om > sx || (om == sx && oi < isx))) { sx = om; isx = oi; }
-        }
-        isx = rfl(isx);
-        if (isx == 0xffffffffu) isx = 0;   // P == 1: index_sec stays 0
-
-        // ---- the dmz swap (decided by the ranks alone) and the selected
-        // process's archive tags (analysis.h:258-277)
+        double mx;
+        uint32_t imx, isx;
+        max_two<CH>(sc, np, lane, mx, imx, isx);
         const bool swap = mdb && dmz == imx && !D.proc_mal[po + isx];
         const uint32_t ibest = swap ? isx : imx;
         const uint32_t tags = rfl(D.proc_attr[po + ibest] & D.db_tags);
-        // ---- softmax (expf in fp32, stored as double) into LDS; then the
-        // sums in process order, as the reference adds them (softmax.hpp:
-        // 250-263, analysis.h:268-277), one sum per lane: 0 score_sum, 1
-        // score_sum_without_max, 2 malware_prob, 3.. the archive tags
-        uint8_t *fl = fl_lds[wid];
 #pragma unroll
         for (int c = 0; c < CH; c++) {
             const uint32_t pi = (uint32_t)c * 64 + lane;
@@ -1225,36 +1489,20 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
                 scl[pi] = (double)expf_ref((float)(sc[c] - mx));
                 uint32_t f = (uint32_t)((malbits >> c) & 1u);
                 if (tags) f |= ((D.proc_attr[po + pi] & tags) >> MFP_ATTR_DB_FIRST) << 1;
-                if (swap && pi == imx) f |= 0x80u;   // process_score[index_max] = 0 (analysis.h:264)
+                if (swap && pi == imx) f |= 0x80u;
                 fl[pi] = (uint8_t)f;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        double acc = 0.0;
-        const uint32_t nsum = tags ? 3u + MFP_ATTR_DB_TAGS : 3u;
-        if (lane < nsum) {
-            for (uint32_t p = 0; p < np; p++) {
-                const double e = scl[p];
-                const uint32_t f = fl[p];
-                const bool take = lane == 0 ? true
-                                : lane == 1 ? p != imx
-                                : lane == 2 ? (f & 1u) != 0
-                                : ((f >> (lane - 2)) & 1u) && !(f & 0x80u);
-                if (take) acc += e;
-            }
-        }
-        auto lane_d = [&](uint32_t l) {
-            return __hiloint2double(__builtin_amdgcn_readlane((int)(__double_as_longlong(acc) >> 32), (int)l),
-                                    __builtin_amdgcn_readlane((int)__double_as_longlong(acc), (int)l));
-        };
-        double ssum = lane_d(0), swo = lane_d(1), mal = lane_d(2);
+        const double acc = row_sums(scl, fl, np, imx, tags ? 3u + MFP_ATTR_DB_TAGS : 3u, lane);
+        double ssum = lane_d(acc, 0), swo = lane_d(acc, 1), mal = lane_d(acc, 2);
         const double p_imx = scl[imx], p_isx = scl[isx];
-        double ap = 0.0;   // lane k < MFP_ATTR_DB_TAGS: tag k's sum
+        double ap = 0.0;
         if (tags) {
 #pragma unroll
             for (int k = 0; k < MFP_ATTR_DB_TAGS; k++) {
-                const double v = lane_d(3 + k);
+                const double v = lane_d(acc, 3 + k);
                 if ((int)lane == k) ap = v;
             }
         }
@@ -1273,7 +1521,7 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
             a.score = max_score;
             a.process = D.proc_id[po + ibest];
             a.proc_slot = po + ibest;
-            a.attr = (uint16_t)(D.proc_attr[po + ibest] | a.attr | xattr);
+            a.attr = (uint16_t)(D.proc_attr[po + ibest] | a.attr | (flags >> 16));
             a.malware_prob = -1.0;
             a.flags = (uint8_t)(MFP_AN_VALID | (a.flags & MFP_AN_PENDING));
             if (mdb) {
@@ -1281,7 +1529,6 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
                 a.flags |= MFP_AN_CLASSIFY_MALWARE;
                 if (D.proc_mal[po + ibest]) a.flags |= MFP_AN_MALWARE;
             }
-            // encrypted_channel (analysis.h:1161-1163)
             if ((a.flags & MFP_AN_MALWARE) && ft == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
             P.out[i] = a;
         }
@@ -1292,23 +1539,26 @@ __device__ __forceinline__ void wave_scorer(const AParams &P, char (*sni_buf)[33
     if (lane == 0 && w_upd) atomicAdd(&P.stats[7], (unsigned long long)w_upd);
 }
 
-
-__global__ __launch_bounds__(256) void k_analyze_wave(AParams P) {
-    __shared__ char sni_buf[4][336];
-    __shared__ char ua_buf[4][520];
-    __shared__ double sc_lds[4][64 * MAXP_CHUNKS];
-    __shared__ uint8_t fl_lds[4][64 * MAXP_CHUNKS];   // per process: malware (bit 0), archive tags (1-6), swapped out (7)
-    wave_scorer<MAXP_CHUNKS, 4>(P, sni_buf, ua_buf, sc_lds, fl_lds);
+constexpr int WW = 4;   // waves per k_analyze_wave block
+#ifndef MFP_AN_WAVE_MINW
+#define MFP_AN_WAVE_MINW 4
+#endif
+__global__ __launch_bounds__(64 * WW, MFP_AN_WAVE_MINW) void k_analyze_wave(AParams P) {
+    __shared__ char sni_buf[WW][336];
+    __shared__ char ua_buf[WW][520];
+    __shared__ double sc_lds[WW][64 * MAXP_CHUNKS];
+    __shared__ uint32_t at_lds[WW][64 * MAXP_CHUNKS];   // per process: attribute bits
+    __shared__ uint32_t id_lds[WW][64 * MAXP_CHUNKS];   // per process: process id
+    __shared__ uint8_t fl_lds[WW][64 * MAXP_CHUNKS];    // per process: malware (bit 0), archive tags (1-6), swapped out (7)
+    wave_scorer_pipe(P, sni_buf, ua_buf, sc_lds, at_lds, id_lds, fl_lds);
 }
 
-// fingerprints with more than 64 * MAXP_CHUNKS processes (production
-// archives have a few): one wave per block, the wider rows in LDS
 __global__ __launch_bounds__(64) void k_analyze_big(AParams P) {
-    __shared__ char sni_buf[1][336];
-    __shared__ char ua_buf[1][520];
-    __shared__ double sc_lds[1][64 * MAXP_CHUNKS_BIG];
-    __shared__ uint8_t fl_lds[1][64 * MAXP_CHUNKS_BIG];
-    wave_scorer<MAXP_CHUNKS_BIG, 1>(P, sni_buf, ua_buf, sc_lds, fl_lds);
+    __shared__ char sni_buf[336];
+    __shared__ char ua_buf[520];
+    __shared__ double sc_lds[64 * MAXP_CHUNKS_BIG];
+    __shared__ uint8_t fl_lds[64 * MAXP_CHUNKS_BIG];
+    wave_scorer_big<MAXP_CHUNKS_BIG>(P, sni_buf, ua_buf, sc_lds, fl_lds);
 }
 
 // k_seen_scan: the batch's unknown-TLS sightings per distinct fingerprint
@@ -1494,7 +1744,7 @@ static mfpa::AParams make_params(const mfp_classifier_dev *D, const mfp_seen_tab
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.out = out; P.mode = mode;
     P.attr_prob = nullptr;
     P.pend_bits = (uint64_t *)pending;
-    P.deferred = (mfpa::Deferred *)deferred;
+    P.deferred = (mfpa::WItem *)deferred;
     P.lane_max_p = lane_max_p;
     P.stats = stats;
     return P;
@@ -1512,8 +1762,8 @@ extern "C" void mfp_analysis_segments(uint64_t n, uint32_t *nseg, uint32_t *seg_
     *seg_cap = (uint32_t)(64 * ((groups + ns - 1) / ns));
 }
 
-// scratch: work = nseg * seg_cap WorkItems (16 B), lanel and deferred = nseg *
-// seg_cap Deferred (64 B) each, seg_n = 3 * nseg words
+// scratch: work = nseg * seg_cap WorkItems (16 B), lanel = nseg * seg_cap
+// Deferred (64 B), deferred = nseg * seg_cap WItems (80 B), seg_n = 3 * nseg words
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
                                    mfp_analysis *out, double *attr_prob, uint32_t *pending, void *work, void *lanel,

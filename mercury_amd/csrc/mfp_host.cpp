@@ -294,8 +294,8 @@ struct Slot {
     bool init() {
         return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
                hipMalloc(&d_bins, 16 * sizeof(unsigned long long)) == hipSuccess &&
-               hipMalloc(&d_an_stats, MFP_AN_NCOUNTERS * sizeof(unsigned long long)) == hipSuccess &&
-               hipMemset(d_an_stats, 0, MFP_AN_NCOUNTERS * sizeof(unsigned long long)) == hipSuccess &&
+               hipMalloc(&d_an_stats, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
+               hipMemset(d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
@@ -509,13 +509,13 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
     mfp_analysis_segments(n, &nseg, &seg_cap);
     const size_t items = (size_t)nseg * seg_cap + 1;
     if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_work_items, S.cap_work_items, items) ||
-        grow(S.d_lanel, S.cap_lanel, 4 * items) || grow(S.d_deferred, S.cap_deferred, 4 * items) ||
+        grow(S.d_lanel, S.cap_lanel, 4 * items) || grow(S.d_deferred, S.cap_deferred, 5 * items) ||
         grow(S.d_segn, S.cap_segn, 3 * (size_t)nseg + 1) || seen_reserve(S, n, s)) {
         mfp_set_error("device allocation failed");
         return -2;
     }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
-    HIPCHK(hipMemsetAsync(S.d_an_stats, 0, MFP_AN_NCOUNTERS * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(S.d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long), s));
     if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, d_attr_prob,
                             S.d_pending, S.d_work_items, S.d_lanel, S.d_deferred, S.d_segn, S.d_an_stats, c->mode,
                             c->an_lane_max_p, s, c->prof) != 0) {

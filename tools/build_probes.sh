@@ -14,8 +14,14 @@ for spec in "$@"; do
         mercury_amd/_probe/a_$name.o $(ls $OBJ/*.o | grep -v mfp_analysis.hip.o) -lz -lcrypto && echo built $name ) &
     continue
   fi
-  ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/mfp_kernels.hip -o mercury_amd/_probe/k_$name.o &&
-    hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so mercury_amd/_probe/k_$name.o \
-      $(ls $OBJ/*.o | grep -v mfp_kernels.hip.o) -lz -lcrypto && echo built $name ) &
+  (  # fingerprint probes: recompile the walker translation units
+    objs=""
+    for k in mfp_kernels mfp_k_tls mfp_k_http mfp_k_small mfp_k_all; do
+      hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/$k.hip \
+        -o mercury_amd/_probe/k_${name}_$k.o & objs="$objs mercury_amd/_probe/k_${name}_$k.o"
+    done
+    wait
+    hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so $objs \
+      $(ls $OBJ/*.o | grep -v -E "mfp_kernels.hip.o|mfp_k_") -lz -lcrypto && echo built $name ) &
 done
 wait
