@@ -336,6 +336,17 @@ BIN_NAMES = ["tls_ch", "http_req", "tcp_syn", "http_resp", "other", "tls_sh", "s
 MSG_BIN = np.array([4, 0, 5, 5, 6, 6, 1, 3, 2, 2, 7, 7, 7] + [4] * 243, np.int64)
 
 
+def arena_slots(rec, desc):
+    """Fingerprint-arena bytes the device path reserves for these packets:
+    a 64-byte aligned slot holding each string and its 8-byte hash; a TLS
+    ClientHello's slot sized by its bound min(2 * caplen + 64, 8192)."""
+    fl = rec["fp_len"].astype(np.int64)
+    exact = np.where(fl > 0, ((fl + 7) // 8 * 8 + 8 + 63) // 64 * 64, 0)
+    bound = np.minimum(2 * desc["caplen"].astype(np.int64) + 64, 8192)
+    by_bound = ((bound + 7) // 8 * 8 + 8 + 63) // 64 * 64
+    return int(np.where(rec["msg"] == 1, np.maximum(exact, by_bound), exact).sum())
+
+
 def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
     """Algorithmic HBM bytes per step of each kernel:
     what the kernel must read and write at least, from the packets' own
@@ -538,11 +549,12 @@ def main():
         ctx = mercury_amd.Context(cfg, device=local)
     tls_format = mercury_amd.parse_filter(cfg)[1] if not analysis else None
 
-    # size the fp arena from the unique set (exact per replica)
+    # size the fp arena from the unique set: each string's 64-byte slot, the
+    # TLS ClientHellos' slots by their upper bound (k_fp_tls1 reserves before it walks)
     rec_u, fp_u = ctx.process_host(ua, ud)
     distinct_fps = len(set(mercury_amd.fingerprints(rec_u, fp_u)) - {""})
     reps = (n + len(ud) - 1) // len(ud)
-    cap = int(int(rec_u["fp_len"].astype(np.int64).sum() + 16 * len(ud)) * reps * 1.05) + (2 << 30)
+    cap = int(arena_slots(rec_u, ud) * reps * 1.02) + (2 << 30)
     d_rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_fp = torch.empty(cap, dtype=torch.uint8, device="cuda")
     d_used = torch.zeros(4, dtype=torch.int64, device="cuda")

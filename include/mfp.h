@@ -135,8 +135,9 @@ enum {
     MFP_MSG_OPENVPN,  /* openvpn_tcp (openvpn.h:353); sni_off/sni_len: the TCP payload         */
 };
 
-/* TCP reassembly inputs, one per packet (the device walk's view of
- * tcp_packet, tcpip.h:137-173, after set_tcp_protocol pkt_proc.cc:488-572) */
+/* Reassembly inputs, one per packet (the device walk's view of tcp_packet,
+ * tcpip.h:137-173, after set_tcp_protocol pkt_proc.cc:488-572; for DTLS
+ * ClientHello fragments, MFP_SEG_DTLS, of the handshake header) */
 typedef struct {
     uint32_t seq;        /* TCP sequence number (host order)                          */
     uint32_t more;       /* additional_bytes_needed of the message parsed here        */
@@ -153,6 +154,10 @@ enum {
     MFP_SEG_SYN_RST = 16,       /* SYN, SYN/ACK or RST: analyze_ip_packet skips it in reassembly
                                    mode (pkt_proc.cc:1632-1634)                                */
     MFP_SEG_IP = 32,            /* the link layer led to an IP packet: analyze_ip_packet ran    */
+    MFP_SEG_DTLS = 64,          /* a DTLS ClientHello handshake fragment (dtls_client_hello,
+                                   dtls.h:155-175): seq = fragment_offset, more =
+                                   additional_bytes_needed, pay_off / pay_len = the fragment's
+                                   bytes; its message_seq is the 2 bytes at pay_off - 8       */
 };
 
 /* semantics of the reference entry point to follow */
@@ -419,7 +424,7 @@ MFP_EXPORT int mfp_process_os_info(mfp_context ctx, uint32_t proc_slot, uint32_t
 MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
 
 /* the last analysis batch's counters, up to n of: [0] packets classified,
- * [1] unknown-TLS sightings, [2] fingerprints with too many processes,
+ * [1] unknown-TLS sightings, [2] packets whose fingerprint has more than 4096 processes (scored by k_analyze_huge),
  * [3] packets scored wave-per-packet (k_analyze_wave), [4] / [5] prior and
  * update-list entries read by the lane-per-packet scorer, [6] / [7] the same
  * for the wave scorer (SURVEY 8(d)'s 8*P + 12*U table bytes), [8] work items

@@ -173,7 +173,7 @@ ADEV void load_words(const uint8_t *s, uint32_t len, uint32_t j0, uint64_t (&w)[
         w[k] = x;
     }
 }
-constexpr int LB = 8;   // words per batch
+constexpr int LB = 4;   // words per batch (8: more registers than the classifier kernels can spare)
 
 // mfpc::str_hash, one lane
 ADEV uint64_t lane_hash(const uint8_t *s, uint32_t len) {
@@ -195,14 +195,16 @@ ADEV uint64_t fp_key(const mfp_record &r, const uint8_t *fp, uint32_t len) {
     return lane_hash(fp, len);
 }
 
+// B words of each string per round trip (B = 4 where registers are short)
+template <int B = LB>
 ADEV bool lane_eq(const uint8_t *a, const uint8_t *b, uint32_t len) {
-    for (uint32_t j0 = 0; 8 * j0 < len; j0 += LB) {
-        uint64_t x[LB], y[LB];
-        load_words<LB>(a, len, j0, x);
-        load_words<LB>(b, len, j0, y);
+    for (uint32_t j0 = 0; 8 * j0 < len; j0 += B) {
+        uint64_t x[B], y[B];
+        load_words<B>(a, len, j0, x);
+        load_words<B>(b, len, j0, y);
         bool same = true;
 #pragma unroll
-        for (int k = 0; k < LB; k++) same &= x[k] == y[k];
+        for (int k = 0; k < B; k++) same &= x[k] == y[k];
         if (!same) return false;
     }
     return true;
@@ -631,6 +633,8 @@ struct AParams {
     struct Deferred *lanel;      // k_an_features -> k_an_score
     uint32_t *seg_n;             // per segment: [0] work items, [1] lane-scored, [2] wave-scored (3 words each)
     uint32_t nseg, seg_cap;      // segments (k_analyze waves), items per segment
+    double *hrow;                // k_analyze_huge's per-wave score rows (HUGE_WAVES * hstride doubles + as many flag bytes)
+    uint32_t hstride;            // >= the archive's largest P
 };
 
 constexpr uint32_t NFEAT = 6;    // ASN, port, IP, UA, domain, SNI: naive_bayes.hpp:752-772 order
@@ -786,7 +790,10 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
     if (lane == 0 && n_wk) atomicAdd(&P.stats[8], (unsigned long long)n_wk);
 }
 
-__global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
+#ifndef MFP_AN_FEAT_MINW
+#define MFP_AN_FEAT_MINW 4   // 4 waves/SIMD: 10.4 -> 9.0 ms (r03l A/B), no spill
+#endif
+__global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(AParams P) {
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
     const mfp_classifier_dev &D = P.D;
@@ -816,10 +823,7 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
         E.proc_off = 0; E.nproc = 0; E.malware_db = 0; E.generic_dmz = 0;
         if (scored) E = D.entry[entry];
         uint32_t np = E.nproc;
-        if (scored && np > 64 * MAXP_CHUNKS_BIG) {   // beyond the big scorer: counted, left unscored
-            atomicAdd(&P.stats[2], 1ull);
-            scored = false;
-        }
+        if (scored && np > 64 * MAXP_CHUNKS_BIG) atomicAdd(&P.stats[2], 1ull);   // scored by k_analyze_huge
         uint32_t hoff[NFEAT], hcnt[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) { hoff[f] = 0; hcnt[f] = 0; }
@@ -927,7 +931,7 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
 #ifdef MFP_AN_FEAT_WAVE_VERIFY
             const bool ok = wave_verify(has[v], vs[v], (const uint8_t *)D.pool + voff[v], vl[v], lane);
 #else
-            const bool ok = !has[v] || lane_eq(vs[v], (const uint8_t *)D.pool + voff[v], vl[v]);
+            const bool ok = !has[v] || lane_eq<4>(vs[v], (const uint8_t *)D.pool + voff[v], vl[v]);
 #endif
             if (has[v]) {
                 // a hash collision (ok == false) takes the full probe, which keeps looking
@@ -941,15 +945,17 @@ __global__ __launch_bounds__(64 * AW) void k_an_features(AParams P) {
         const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain && !ssh_ua;
         const bool defer = scored && !lanep;
         if (live && !scored && xattr) P.out[i].attr = (uint16_t)(P.out[i].attr | xattr);
-        Deferred d;
-        d.i = (uint32_t)i; d.entry = entry; d.slow_sni = plain ? 0u : 1u; d.slow_ua = (ssh_ua ? 1u : 0u) | (xattr << 16);
-#pragma unroll
-        for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
         const uint64_t lm = __ballot(lanep), dm = __ballot(defer);
-        if (lanep) ll[n_l + __builtin_popcountll(lm & ((1ull << lane) - 1))] = d;
+        if (lanep) {
+            Deferred d;
+            d.i = (uint32_t)i; d.entry = entry; d.slow_sni = 0u; d.slow_ua = xattr << 16;
+#pragma unroll
+            for (uint32_t f = 0; f < NFEAT; f++) { d.off[f] = hoff[f]; d.cnt[f] = hcnt[f]; }
+            ll[n_l + __builtin_popcountll(lm & ((1ull << lane) - 1))] = d;
+        }
         if (defer) {
             WItem w;
-            w.i = d.i; w.entry = entry; w.flags = (plain ? 0u : 1u) | (ssh_ua ? 2u : 0u) | (xattr << 16);
+            w.i = (uint32_t)i; w.entry = entry; w.flags = (plain ? 0u : 1u) | (ssh_ua ? 2u : 0u) | (xattr << 16);
             w.ft = r.fp_type;
             w.po = E.proc_off; w.np = np; w.mdb = E.malware_db; w.dmz = E.generic_dmz;
 #pragma unroll
@@ -1231,17 +1237,19 @@ ADEV double lane_d(double v, uint32_t l) {
 }
 
 // ---- k_analyze_wave (P <= 64 * MAXP_CHUNKS): software-pipelined over each
-// segment's packets.  Packet q + 1's table rows (update-list heads, priors,
-// process attributes and ids, malware bytes, its analysis-record word) are
-// loaded while packet q is scored, and packet q + 2's WItem one step earlier,
-// so the scoring tail of q runs on LDS and registers only and a packet costs
-// about one memory round trip instead of a chain of them.
+// segment's packets.  Packet q + 1's table rows (update-list heads, the first
+// SCH chunks of priors, process attributes and ids, malware bytes, its
+// analysis-record word) are loaded while packet q is scored, and packet q + 2's
+// WItem one step earlier, so the scoring tail of q runs on LDS and registers
+// only and a packet costs about one memory round trip instead of a chain of
+// them.  Chunks SCH.. (P > 64 * SCH, rare) are loaded when the packet starts.
+constexpr int SCH = 4;
 struct WStage {
     uint32_t uidx[NFEAT];
     double uval[NFEAT];
-    double pr[MAXP_CHUNKS];
-    uint32_t attr[MAXP_CHUNKS], pid[MAXP_CHUNKS];
-    uint32_t malb[MAXP_CHUNKS];
+    double pr[SCH];
+    uint32_t attr[SCH], pid[SCH];
+    uint32_t malb[SCH];
     uint32_t outw;               // the analysis record's attr / status / flags word (k_analyze's)
 };
 ADEV uint32_t wf(uint32_t w, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)w, k); }
@@ -1260,7 +1268,7 @@ ADEV void stage_issue(const AParams &P, uint32_t w, WStage &st, uint32_t lane) {
         if (take && lane < c) { st.uidx[f] = D.upd[o + lane].idx; st.uval[f] = D.upd[o + lane].value; }
     }
 #pragma unroll
-    for (int c = 0; c < MAXP_CHUNKS; c++) {
+    for (int c = 0; c < SCH; c++) {
         const uint32_t pi = (uint32_t)c * 64 + lane;
         st.pr[c] = 0.0; st.attr[c] = 0; st.pid[c] = 0; st.malb[c] = 0;
         if (take && pi < np) {
@@ -1323,13 +1331,25 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
                     anylong |= (cnt[f] & ~MFP_UPD_SERIAL) > 64 ? 1u : 0u;
                 }
 #pragma unroll
-                for (int c = 0; c < CH; c++) {
+                for (int c = 0; c < SCH; c++) {
                     const uint32_t pi = (uint32_t)c * 64 + lane;
                     if ((uint32_t)c * 64 < np) {
                         scl[pi] = st.pr[c];
                         arow[pi] = st.attr[c];
                         idrow[pi] = st.pid[c];
                         if (st.malb[c]) malbits |= 1u << c;
+                    }
+                }
+                if (np > 64u * SCH) {
+#pragma unroll
+                    for (int c = SCH; c < CH; c++) {
+                        const uint32_t pi = (uint32_t)c * 64 + lane;
+                        if ((uint32_t)c * 64 < np) {
+                            scl[pi] = pi < np ? D.prior[po + pi] : 0.0;
+                            arow[pi] = pi < np ? D.proc_attr[po + pi] : 0u;
+                            idrow[pi] = pi < np ? D.proc_id[po + pi] : 0u;
+                            if (pi < np && D.proc_mal[po + pi]) malbits |= 1u << c;
+                        }
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1439,7 +1459,7 @@ __device__ __forceinline__ void wave_scorer_big(const AParams &P, char *nbuf, ch
     for (uint32_t q = 0; q < total; q++) {
         const uint32_t wc = wi_load(dseg, q, total, lane);
         const uint32_t np = wf(wc, WI_NP);
-        if (np <= 64u * MAXP_CHUNKS) continue;   // k_analyze_wave's
+        if (np <= 64u * MAXP_CHUNKS || np > 64u * CH) continue;   // k_analyze_wave's / k_analyze_huge's
         const uint32_t i = wf(wc, WI_I), po = wf(wc, WI_PO), mdb = wf(wc, WI_MDB), dmz = wf(wc, WI_DMZ);
         const uint32_t flags = wf(wc, WI_FLAGS), ft = wf(wc, WI_FT);
         uint32_t off[NFEAT], cnt[NFEAT];
@@ -1559,6 +1579,133 @@ __global__ __launch_bounds__(64) void k_analyze_big(AParams P) {
     __shared__ double sc_lds[64 * MAXP_CHUNKS_BIG];
     __shared__ uint8_t fl_lds[64 * MAXP_CHUNKS_BIG];
     wave_scorer_big<MAXP_CHUNKS_BIG>(P, sni_buf, ua_buf, sc_lds, fl_lds);
+}
+
+// ---- k_analyze_huge (P > 64 * MAXP_CHUNKS_BIG, any size): one wave per
+// block, the packet's score row and its per-process flags in a per-wave HBM
+// scratch row (P.hrow: HUGE_WAVES rows of P.hstride doubles, then as many
+// rows of P.hstride flag bytes), the same operations in the same order as the
+// other scorers
+constexpr uint32_t HUGE_WAVES = 128;
+ADEV void row_sync() {   // the wave's global row writes visible to its other lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// max (first index of the largest) over row[0, np) without index `skip`
+ADEV void row_max(const double *row, uint32_t np, uint32_t skip, uint32_t lane, double &mx, uint32_t &im) {
+    mx = -1.7976931348623157e308;
+    im = 0xffffffffu;
+    for (uint32_t p = lane; p < np; p += 64) {
+        const double v = row[p];
+        if (p != skip && (im == 0xffffffffu || v > mx)) { mx = v; im = p; }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const double om = __shfl_xor(mx, d, 64);
+        const uint32_t oi = (uint32_t)__shfl_xor((int)im, d, 64);
+        if (oi != 0xffffffffu && (im == 0xffffffffu || om > mx || (om == mx && oi < im))) { mx = om; im = oi; }
+    }
+    im = rfl(im);
+    mx = __hiloint2double((int)rfl((uint32_t)(__double_as_longlong(mx) >> 32)), (int)rfl((uint32_t)__double_as_longlong(mx)));
+}
+__global__ __launch_bounds__(64) void k_analyze_huge(AParams P) {
+    __shared__ char nbuf[336];
+    __shared__ char ub[520];
+    const uint32_t lane = lane_id();
+    const mfp_classifier_dev &D = P.D;
+    double *row = P.hrow + (uint64_t)blockIdx.x * P.hstride;
+    uint8_t *fl = (uint8_t *)(P.hrow + (uint64_t)HUGE_WAVES * P.hstride) + (uint64_t)blockIdx.x * P.hstride;
+    uint64_t w_prior = 0, w_upd = 0;
+    for (uint64_t sg = blockIdx.x; sg < P.nseg; sg += gridDim.x) {
+    const WItem *dseg = P.deferred + sg * P.seg_cap;
+    const uint32_t total = rfl(P.seg_n[3 * sg + 2]);
+    for (uint32_t q = 0; q < total; q++) {
+        const uint32_t wc = wi_load(dseg, q, total, lane);
+        const uint32_t np = wf(wc, WI_NP);
+        if (np <= 64u * MAXP_CHUNKS_BIG || np > P.hstride) continue;   // the other scorers'
+        const uint32_t i = wf(wc, WI_I), po = wf(wc, WI_PO), mdb = wf(wc, WI_MDB), dmz = wf(wc, WI_DMZ);
+        const uint32_t flags = wf(wc, WI_FLAGS), ft = wf(wc, WI_FT);
+        uint32_t off[NFEAT], cnt[NFEAT];
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) { off[f] = wf(wc, WI_OFF + f); cnt[f] = wf(wc, WI_CNT + f); }
+        if (flags & 3u) slow_lookups(P, i, wf(wc, WI_ENTRY), flags, nbuf, ub, off, cnt, lane);
+        w_prior += np;
+        for (uint32_t p = lane; p < np; p += 64) row[p] = D.prior[po + p];
+        row_sync();
+#pragma unroll
+        for (uint32_t f = 0; f < NFEAT; f++) {
+            const uint32_t c = cnt[f] & ~MFP_UPD_SERIAL;
+            w_upd += c;
+            if (cnt[f] & MFP_UPD_SERIAL) {          // repeated processes: one entry after the other
+                for (uint32_t k = 0; k < c; k++) {
+                    if (lane == 0) { const mfp_update x = D.upd[off[f] + k]; row[x.idx] += x.value; }
+                    row_sync();
+                }
+            } else {                                // a list names each process at most once
+                for (uint32_t b = 0; b < c; b += 64) {
+                    if (b + lane < c) { const mfp_update x = D.upd[off[f] + b + lane]; row[x.idx] += x.value; }
+                    row_sync();
+                }
+            }
+        }
+        double mx, sx;
+        uint32_t imx, isx;
+        row_max(row, np, 0xffffffffu, lane, mx, imx);
+        row_max(row, np, imx, lane, sx, isx);
+        if (isx == 0xffffffffu) isx = 0;
+        const bool swap = mdb && dmz == imx && !D.proc_mal[po + isx];
+        const uint32_t ibest = swap ? isx : imx;
+        const uint32_t tags = rfl(D.proc_attr[po + ibest] & D.db_tags);
+        for (uint32_t p = lane; p < np; p += 64) {
+            const double e = (double)expf_ref((float)(row[p] - mx));
+            uint32_t f = D.proc_mal[po + p] ? 1u : 0u;
+            if (tags) f |= ((D.proc_attr[po + p] & tags) >> MFP_ATTR_DB_FIRST) << 1;
+            if (swap && p == imx) f |= 0x80u;
+            row[p] = e;
+            fl[p] = (uint8_t)f;
+        }
+        row_sync();
+        const double acc = row_sums(row, fl, np, imx, tags ? 3u + MFP_ATTR_DB_TAGS : 3u, lane);
+        double ssum = lane_d(acc, 0), swo = lane_d(acc, 1), mal = lane_d(acc, 2);
+        const double p_imx = row[imx], p_isx = row[isx];
+        double ap = 0.0;
+        if (tags) {
+#pragma unroll
+            for (int k = 0; k < MFP_ATTR_DB_TAGS; k++) {
+                const double v = lane_d(acc, 3 + k);
+                if ((int)lane == k) ap = v;
+            }
+        }
+        double max_score = p_imx;
+        if (ssum > 0.0 && mdb) mal /= ssum;
+        if (swap) {
+            ssum = swo;
+            max_score = p_isx;
+        }
+        if (ssum > 0.0) max_score /= ssum;
+        if (tags && P.attr_prob && lane < MFP_ATTR_DB_TAGS && ((tags >> (MFP_ATTR_DB_FIRST + lane)) & 1u))
+            P.attr_prob[(uint64_t)i * MFP_ATTR_DB_TAGS + lane] = ssum > 0.0 ? ap / ssum : ap;
+        if (lane == 0) {
+            mfp_analysis a = P.out[i];
+            a.score = max_score;
+            a.process = D.proc_id[po + ibest];
+            a.proc_slot = po + ibest;
+            a.attr = (uint16_t)(D.proc_attr[po + ibest] | a.attr | (flags >> 16));
+            a.malware_prob = -1.0;
+            a.flags = (uint8_t)(MFP_AN_VALID | (a.flags & MFP_AN_PENDING));
+            if (mdb) {
+                a.malware_prob = mal;
+                a.flags |= MFP_AN_CLASSIFY_MALWARE;
+                if (D.proc_mal[po + ibest]) a.flags |= MFP_AN_MALWARE;
+            }
+            if ((a.flags & MFP_AN_MALWARE) && ft == 1) a.attr |= (uint16_t)(1u << D.enc_channel_idx);
+            P.out[i] = a;
+        }
+        row_sync();   // the row is rewritten by the next packet
+    }
+    }
+    if (lane == 0 && w_prior) atomicAdd(&P.stats[6], (unsigned long long)w_prior);
+    if (lane == 0 && w_upd) atomicAdd(&P.stats[7], (unsigned long long)w_upd);
 }
 
 // k_seen_scan: the batch's unknown-TLS sightings per distinct fingerprint
@@ -1747,7 +1894,17 @@ static mfpa::AParams make_params(const mfp_classifier_dev *D, const mfp_seen_tab
     P.deferred = (mfpa::WItem *)deferred;
     P.lane_max_p = lane_max_p;
     P.stats = stats;
+    P.hrow = nullptr;
+    P.hstride = 0;
     return P;
+}
+
+// bytes of k_analyze_huge's scratch rows for an archive whose largest
+// fingerprint has max_nproc processes (0: the kernel is not needed)
+extern "C" size_t mfp_analysis_huge_bytes(uint32_t max_nproc) {
+    if (max_nproc <= 64u * mfpa::MAXP_CHUNKS_BIG) return 0;
+    const size_t stride = (max_nproc + 63u) & ~63u;
+    return (size_t)mfpa::HUGE_WAVES * stride * 9;
 }
 
 // the per-wave segments of one batch: k_analyze's waves (segments) and the
@@ -1768,7 +1925,7 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
                                    mfp_analysis *out, double *attr_prob, uint32_t *pending, void *work, void *lanel,
                                    void *deferred, uint32_t *seg_n, unsigned long long *stats, uint32_t mode,
-                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof) {
+                                   uint32_t lane_max_p, void *huge_rows, hipStream_t stream, mfp_prof *prof) {
     if (n == 0) return 0;
     mfpa::AParams P = make_params(D, *T, arena, desc, n, rec, fp_arena, out, pending, deferred, stats, mode, lane_max_p);
     P.attr_prob = attr_prob;
@@ -1802,6 +1959,12 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
     hipLaunchKernelGGL(mfpa::k_analyze_wave, dim3(blocks < 1024 ? blocks : 1024), dim3(256), 0, stream, P);
     if (D->max_nproc > 64u * mfpa::MAXP_CHUNKS)
         hipLaunchKernelGGL(mfpa::k_analyze_big, dim3(256), dim3(64), 0, stream, P);
+    if (D->max_nproc > 64u * mfpa::MAXP_CHUNKS_BIG) {
+        if (!huge_rows) return -1;
+        P.hrow = (double *)huge_rows;
+        P.hstride = (D->max_nproc + 63u) & ~63u;
+        hipLaunchKernelGGL(mfpa::k_analyze_huge, dim3(mfpa::HUGE_WAVES), dim3(64), 0, stream, P);
+    }
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -172,20 +172,33 @@ DEV uint64_t swar_alpha(uint64_t w) {                  // isalpha (ASCII)
     const uint64_t x = (w | 0x2020202020202020ull) & 0x7f7f7f7f7f7f7f7full;
     return (x + 0x1f1f1f1f1f1f1f1full) & ~(x + 0x0505050505050505ull) & ~w & 0x8080808080808080ull;
 }
-// first byte of [p, e) whose class flag is set, or e; one aligned 8-byte
-// load per 8 bytes (a lane scanning its own packet), words inside the range only
+// first byte of [p, e) whose class flag is set, or e.  A lane scanning its
+// own packet: SWB aligned 8-byte loads issued together per memory round trip
+// (words inside the range only), then the flags checked in order
+#ifndef MFP_SWB
+#define MFP_SWB 4
+#endif
 template <class F>
 DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag) {
     if (!p || p >= e) return e;
+    const uintptr_t ee = (uintptr_t)e;
     uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
-    uint64_t m = flag(*(const uint64_t *)a) & (~0ull << (8 * ((uintptr_t)p & 7)));
+    uint64_t m0 = ~0ull << (8 * ((uintptr_t)p & 7));   // bytes before p in the first word
     while (true) {
-        const uintptr_t in = (uintptr_t)e - a;         // bytes of this word inside the range
-        if (in < 8) m &= (1ull << (8 * in)) - 1;
-        if (m) return (const uint8_t *)(a + (__builtin_ctzll(m) >> 3));
-        a += 8;
-        if (a >= (uintptr_t)e) return e;
-        m = flag(*(const uint64_t *)a);
+        uint64_t w[MFP_SWB];
+#pragma unroll
+        for (int k = 0; k < MFP_SWB; k++) w[k] = a + 8 * k < ee ? *(const uint64_t *)(a + 8 * k) : 0ull;
+#pragma unroll
+        for (int k = 0; k < MFP_SWB; k++) {
+            const uintptr_t ak = a + 8 * k;
+            if (ak >= ee) return e;
+            uint64_t m = flag(w[k]) & (k == 0 ? m0 : ~0ull);
+            const uintptr_t in = ee - ak;                  // bytes of this word inside the range
+            if (in < 8) m &= (1ull << (8 * in)) - 1;
+            if (m) return (const uint8_t *)(ak + (__builtin_ctzll(m) >> 3));
+        }
+        a += 8 * MFP_SWB;
+        m0 = ~0ull;
     }
 }
 DEV void cparse_to_delim(Cur &dst, Cur &r, uint8_t delim) {   // datum::parse_up_to_delim datum.h:313
@@ -1781,6 +1794,13 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
             long bl = clen(body);
             if (flen <= len && bl >= 0 && (uint64_t)bl <= len) more = len - (uint64_t)bl;
         }
+    }
+    if (msg == MFP_MSG_DTLS_CH && cfg.seg && cnotempty(body)) {
+        // offset-reassembly inputs of the fragment (dtls_client_hello
+        // dtls.h:155-175, process_udp_offset_reassembly reassembly.hpp:1036)
+        o.seg_kind |= MFP_SEG_DTLS;
+        o.seq = (uint32_t)foff; o.more = (uint32_t)more;
+        o.pay_off = (uint32_t)(body.d - base); o.pay_len = (uint32_t)clen(body);
     }
     if (msg == MFP_MSG_DTLS_CH) {
         if ((uint32_t)more) o.flags |= MFP_FLAG_TRUNCATED;

@@ -24,7 +24,8 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
                                    const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, const uint8_t *fp_arena,
                                    mfp_analysis *out, double *attr_prob, uint32_t *pending, void *work, void *lanel,
                                    void *deferred, uint32_t *seg_n, unsigned long long *stats, uint32_t mode,
-                                   uint32_t lane_max_p, hipStream_t stream, mfp_prof *prof);
+                                   uint32_t lane_max_p, void *huge_rows, hipStream_t stream, mfp_prof *prof);
+extern "C" size_t mfp_analysis_huge_bytes(uint32_t max_nproc);
 extern "C" void mfp_analysis_segments(uint64_t n, uint32_t *nseg, uint32_t *seg_cap);
 extern "C" int mfp_launch_seen_export(const mfp_seen_tab *T, uint32_t u, mfp_sighting *out, hipStream_t stream);
 extern "C" int mfp_launch_seen_sequence(const mfp_classifier_dev *D, const mfp_seen_tab *T, uint64_t n,
@@ -265,6 +266,7 @@ struct Slot {
     uint4 *d_work_items = nullptr; size_t cap_work_items = 0;
     uint4 *d_lanel = nullptr; size_t cap_lanel = 0;
     uint4 *d_deferred = nullptr; size_t cap_deferred = 0;
+    uint4 *d_huge = nullptr; size_t cap_huge = 0;     // k_analyze_huge's score rows (archives with P > 4096)
     uint32_t *d_segn = nullptr; size_t cap_segn = 0;
     mfp_analysis *d_an = nullptr; size_t cap_an = 0;
     double *d_ap = nullptr; size_t cap_ap = 0;               // archive-tag probabilities of host batches
@@ -300,7 +302,7 @@ struct Slot {
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
-        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_segn,
+        void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
                      d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
@@ -352,10 +354,11 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     std::string resources;
     bool analysis = false, reassembly = false;
     if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly)) return nullptr;
-    if (reassembly && (sel & (SEL_QUIC | SEL_DTLS))) {
-        // process_udp_data's reassembly (QUIC CRYPTO frames, DTLS fragments,
-        // pkt_proc.cc:926-944) is not on the device path: refuse, do not diverge
-        mfp_set_error("reassembly covers TCP only here; remove quic and dtls from the selection");
+    if (reassembly && (sel & SEL_QUIC)) {
+        // process_udp_data's QUIC CRYPTO-frame reassembly (pkt_proc.cc:926-933,
+        // reassembly.hpp:895-1030) is not on the device path: refuse, do not
+        // diverge (TCP messages and DTLS ClientHello fragments are reassembled)
+        mfp_set_error("reassembly covers TCP and DTLS here; remove quic from the selection");
         return nullptr;
     }
     int ndev = 0;
@@ -515,10 +518,15 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
         return -2;
     }
     mfp_classifier_dev *D = mfp_classifier_device_mut(c->clf);
+    const size_t huge = mfp_analysis_huge_bytes(D->max_nproc);
+    if (huge && grow(S.d_huge, S.cap_huge, (huge + 15) / 16)) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
     HIPCHK(hipMemsetAsync(S.d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long), s));
     if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, d_attr_prob,
                             S.d_pending, S.d_work_items, S.d_lanel, S.d_deferred, S.d_segn, S.d_an_stats, c->mode,
-                            c->an_lane_max_p, s, c->prof) != 0) {
+                            c->an_lane_max_p, S.d_huge, s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
@@ -674,11 +682,17 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
 static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                             size_t n, size_t fp_cap, bool analysis, bool attr_prob) {
     Slot &S = c->slot[slot];
-    uint64_t lo = UINT64_MAX, hi = 0;
+    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
     for (size_t i = 0; i < n; i++) {
         lo = std::min<uint64_t>(lo, desc[i].offset);
         hi = std::max<uint64_t>(hi, desc[i].offset + desc[i].caplen);
+        total += desc[i].caplen;
     }
+    // the device arena holds the strings at their reserved slots (the TLS
+    // ClientHello bin reserves by an upper bound, k_fp_tls1): sized by the
+    // bound, whatever the caller's dense capacity; the callers check that the
+    // packed strings fit theirs
+    const size_t dcap = std::max(fp_cap, mfp_fp_arena_bound(n, total));
     if (n == 0) lo = hi = 0;   // (a capture ring hands packets in arena order; this scan is a few ms per 1M)
     lo &= ~(uint64_t)255;
     if (hi > arena_len) { mfp_set_error("descriptor past the end of the arena"); return -1; }
@@ -686,7 +700,7 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     // 64 bytes of padding after the span: the kernels read the aligned block
     // that holds a packet's last byte
     if (grow(S.d_arena, S.cap_arena, span + 64) || grow(S.d_desc, S.cap_desc, n + 1) || grow(S.d_rec, S.cap_rec, n + 1) ||
-        grow(S.d_fp, S.cap_fp, fp_cap + 64) || grow(S.d_fp2, S.cap_fp2, fp_cap + 64) ||
+        grow(S.d_fp, S.cap_fp, dcap + 64) || grow(S.d_fp2, S.cap_fp2, dcap + 64) ||
         (analysis && grow(S.d_an, S.cap_an, n + 1)) ||
         (analysis && attr_prob && grow(S.d_ap, S.cap_ap, MFP_ATTR_DB_TAGS * (n + 1)))) {
         mfp_set_error("device allocation failed");
@@ -696,7 +710,7 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     if (copy) HIPCHK(hipMemcpyAsync(S.d_arena, arena + lo, copy, hipMemcpyHostToDevice, S.stream));
     if (n) HIPCHK(hipMemcpyAsync(S.d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, S.stream));
     const uint8_t *d_base = S.d_arena - lo;
-    int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, fp_cap, (uint64_t *)S.d_used, S.stream);
+    int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, dcap, (uint64_t *)S.d_used, S.stream);
     if (r) return r;
     if (analysis) {
         r = analyze_locked(c, slot, d_base, S.d_desc, n, S.d_rec, S.d_fp, S.d_an, attr_prob ? S.d_ap : nullptr, S.stream);
@@ -737,7 +751,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
     const unsigned long long used = S.h_used[2];   // dense bytes
-    if (S.h_used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
     if (used) HIPCHK(hipMemcpy(fp_arena, S.d_fp2, used, hipMemcpyDeviceToHost));
     return (long long)used;
 }
@@ -760,7 +774,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_seg(mfp_context c, const 
     HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
     const unsigned long long used = S.h_used[2];
-    if (S.h_used[1]) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
     if (used) HIPCHK(hipMemcpy(fp_arena, S.d_fp2, used, hipMemcpyDeviceToHost));
     return (long long)used;
 }

@@ -31,6 +31,9 @@ constexpr int TILE = 256;
 #ifndef MFP_LANE_MINW
 #define MFP_LANE_MINW 4      // 4 waves per SIMD: measured best for the TLS CH and mixed bins
 #endif
+#ifndef MFP_TLS_PLAN_ONLY
+#define MFP_TLS_PLAN_ONLY 1
+#endif
 #ifndef MFP_TLS_MINW
 #define MFP_TLS_MINW 3       // the TLS parser wants ~200 VGPRs: 3 waves/SIMD measured best (4: spills, 2: latency)
 #endif
@@ -69,6 +72,10 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
             if (e.valid()) len = e.n;
             else o.fp_type = 0;       // fingerprint::final drops truncated fingerprints
         }
+        // the TLS lane kernel emits from a ClientHello plan only: a fingerprint
+        // without one (server messages, extension lists the plan cannot hold)
+        // goes to the fallback lane, so this kernel carries no second walker
+        if (FAM == FAM_TLS && MFP_TLS_PLAN_ONLY && live && len && !plan.ok) { punt = true; len = 0; }
     }
     {
         // a parser this instance lacks: the fallback lane; QUIC and OpenVPN
@@ -141,7 +148,7 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
         e.begin(P.fp_arena + base + excl, out_line[tid]);
         if (plan.ok) {
             tls_ch_emit(e, plan);
-        } else {
+        } else if constexpr (!(FAM == FAM_TLS && MFP_TLS_PLAN_ONLY)) {
             Out o2;
             packet_walk<FAM>(e, P.cfg, o2, data, dsc.caplen, dsc.linktype);
         }
@@ -168,6 +175,134 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
             write_seg(P, i, o);
     }
     __syncthreads();   // tile_base / wave_tot reuse
+    }
+}
+
+// k_fp_tls1 -- the TLS ClientHello bin in one pass.  Each string's slot is
+// reserved BEFORE the walk, from an upper bound on its length: 2 characters
+// per byte of the frame plus 64 (hex doubles the bytes it prints; the
+// ClientHello's unprinted headers, random and session id outweigh the
+// parentheses), at most 8192.  So a lane emits its fingerprint from the plan
+// right after building it, while the ClientHello's bytes are still in the
+// cache, instead of after the tile's scan of exact lengths.  Strings are spaced
+// by their bound, not packed (within mfp_fp_arena_bound).  A string longer than
+// its bound, or one without a plan, goes to the fallback lane.
+#ifndef MFP_TLS_ONEPASS
+#define MFP_TLS_ONEPASS 1
+#endif
+template <int = 0>
+__global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
+    __shared__ uint32_t wave_tot[TILE / 64];
+    __shared__ uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
+    __shared__ unsigned long long tile_base;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
+        const uint64_t t = tile * TILE + tid;
+        const bool live = t < count;
+        const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
+        mfp_pkt_desc dsc;
+        if (live) dsc = P.desc[i];
+        else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
+        const uint8_t *data = P.arena + dsc.offset;
+
+        // reservation from the bound: one atomic per tile
+        const uint32_t bound = live ? (2 * dsc.caplen + 64 < FP_MAX ? 2 * dsc.caplen + 64 : FP_MAX) : 0u;
+        const uint32_t slot = bound ? (((bound + 7) & ~7u) + 8 + 63) & ~63u : 0u;
+        uint32_t incl = slot;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) wave_tot[wid] = incl;
+        __syncthreads();
+        uint32_t wbase = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < TILE / 64; w++) {
+            const uint32_t tt = wave_tot[w];
+            if (w < wid) wbase += tt;
+            total += tt;
+        }
+        const uint32_t excl = wbase + incl - slot;
+        if (tid == 0) {
+            unsigned long long b = total ? atomicAdd(&P.fp_used[0], (unsigned long long)total) : 0ull;
+            if (b + total > P.fp_cap) { atomicExch(&P.fp_used[1], 1ull); b = ~0ull; }
+            tile_base = b;
+        }
+        __syncthreads();
+        const unsigned long long base = tile_base;
+        const bool fits = base != ~0ull;
+
+        // walk + plan
+        Out o;
+        uint32_t len = 0;
+        bool punt = false;
+        TlsPlan plan;
+        plan.ok = false;
+        {
+            Em<false> e;
+            e.plan = &plan;
+            packet_walk<FAM_TLS>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+            punt = live && e.punt;
+            if (o.fp_type && !punt) {
+                if (e.valid()) len = e.n;
+                else o.fp_type = 0;       // fingerprint::final drops truncated fingerprints
+            }
+            if (live && len && (!plan.ok || ((len + 7) & ~7u) + 8 > slot)) { punt = true; len = 0; }
+        }
+        {
+            const bool to_quic = punt && (o.msg == MFP_MSG_QUIC || o.msg == MFP_MSG_OPENVPN);
+            const bool to_fb = punt && !to_quic;
+            const uint64_t pm = __ballot(to_fb);
+            if (pm) {
+                uint32_t b = 0;
+                if (lane == 0) b = (uint32_t)atomicAdd(&P.fp_used[3], (unsigned long long)__builtin_popcountll(pm));
+                b = (uint32_t)__shfl((int)b, 0, 64);
+                if (to_fb) fallback[b + __builtin_popcountll(pm & ((1ull << lane) - 1))] = (uint32_t)i;
+            }
+            const uint64_t qm = __ballot(to_quic);
+            if (qm) {
+                uint32_t b = 0;
+                if (lane == 0) b = (uint32_t)atomicAdd(P.quic_count, (unsigned long long)__builtin_popcountll(qm));
+                b = (uint32_t)__shfl((int)b, 0, 64);
+                if (to_quic) P.quic_idx[b + __builtin_popcountll(qm & ((1ull << lane) - 1))] = (uint32_t)i;
+            }
+        }
+        // emit from the plan, the ClientHello still in the cache
+        if (len && fits) {
+            Em<true> e;
+            e.begin(P.fp_arena + base + excl, out_line[tid]);
+            tls_ch_emit(e, plan);
+            e.finish();
+            *(uint64_t *)(P.fp_arena + base + excl + ((len + 7) & ~7u)) = e.hash();
+        }
+        {   // bytes written (fp_used[2]): the exact lengths
+            uint32_t lsum = fits ? len : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) lsum += __shfl_xor(lsum, d, 64);
+            if (lane == 0 && lsum) atomicAdd(&P.fp_used[2], (unsigned long long)lsum);
+        }
+        if (live && !punt) {
+            mfp_record r;
+            r.fp_offset = fits ? base + excl : 0;
+            r.fp_len = fits ? len : 0;
+            r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
+            r.msg = (uint8_t)o.msg;
+            r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
+            r.status = 0;
+            r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
+            r.sni_len = (uint16_t)o.sni_len;
+            r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);
+            r.ua_len = (uint16_t)o.ua_len;
+            r.src_port = (uint16_t)o.src_port;
+            r.dst_port = (uint16_t)o.dst_port;
+            r.net = o.net;
+            P.rec[i] = r;
+            write_seg(P, i, o);
+        }
+        __syncthreads();   // tile_base / wave_tot reuse
     }
 }
 
@@ -530,8 +665,14 @@ template <uint32_t FAM>
 int launch_bin(const KParams &P, uint32_t *fallback, bool lds, const char *name, uint32_t lblocks, uint32_t fblocks,
                hipStream_t stream, mfp_prof *prof) {
     if (prof) mfp_prof_begin(prof, name, stream);
-    if (lds) hipLaunchKernelGGL((k_fp_lds<false, MFP_LDS_STAGE, FAM>), dim3(lblocks), dim3(64), 0, stream, P, fallback);
-    else hipLaunchKernelGGL(k_fingerprint<FAM>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback);
+    if (lds) {
+        hipLaunchKernelGGL((k_fp_lds<false, MFP_LDS_STAGE, FAM>), dim3(lblocks), dim3(64), 0, stream, P, fallback);
+    } else {
+        if constexpr (FAM == FAM_TLS && MFP_TLS_ONEPASS)   // (bin kernels always have a fallback list)
+            hipLaunchKernelGGL(k_fp_tls1<>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback);
+        else
+            hipLaunchKernelGGL(k_fingerprint<FAM>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback);
+    }
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

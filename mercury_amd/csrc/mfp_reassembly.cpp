@@ -109,15 +109,17 @@ uint32_t ssh_more(const uint8_t *p, size_t n) {
 
 struct FlowKey {
     uint8_t v;            // 4 or 6
+    uint8_t proto;        // 6 TCP, 17 UDP (struct key's protocol)
     uint8_t src[16], dst[16];
     uint16_t sport, dport;
     bool operator==(const FlowKey &o) const {
-        return v == o.v && sport == o.sport && dport == o.dport && !memcmp(src, o.src, 16) && !memcmp(dst, o.dst, 16);
+        return v == o.v && proto == o.proto && sport == o.sport && dport == o.dport && !memcmp(src, o.src, 16) &&
+               !memcmp(dst, o.dst, 16);
     }
 };
 struct FlowKeyHash {
     size_t operator()(const FlowKey &k) const {
-        uint64_t h = 1469598103934665603ull ^ k.v;
+        uint64_t h = 1469598103934665603ull ^ k.v ^ (uint64_t)k.proto << 8;
         auto mix = [&](const uint8_t *p, size_t n) { for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; } };
         mix(k.src, 16); mix(k.dst, 16);
         h ^= (uint64_t)k.sport << 16 | k.dport; h *= 1099511628211ull;
@@ -132,6 +134,8 @@ struct Flow {
     uint64_t init_time = 0;
     uint32_t init_seq = 0, init_seg_len = 0, total_needed = 0;
     bool ssh_type = false;           // reassembly_type::ssh (indefinite)
+    uint8_t cid[2] = {0, 0};         // UDP offset reassembly: the DTLS message_seq (get_cid_datum)
+    uint32_t cid_len = 0;
     size_t contiguous = 0;
     size_t seg_count = 0;
     std::vector<std::pair<uint32_t, uint32_t>> segs;   // [first, second] relative sequence numbers
@@ -255,10 +259,10 @@ extern "C" MFP_EXPORT const uint8_t *mfp_reassembler_frames(mfp_reassembler r, s
     return r && !r->frames.empty() ? r->frames.data() : nullptr;
 }
 
-static bool flow_key(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, FlowKey &k) {
+static bool flow_key(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, FlowKey &k, uint8_t proto = 6) {
     const uint32_t ip = r.net & 0xffff, v = (r.net >> 16) & 15;
     memset(&k, 0, sizeof k);
-    k.v = (uint8_t)v; k.sport = r.src_port; k.dport = r.dst_port;
+    k.v = (uint8_t)v; k.proto = proto; k.sport = r.src_port; k.dport = r.dst_port;
     if (v == 4 && ip + 20 <= caplen) { memcpy(k.src, pkt + ip + 12, 4); memcpy(k.dst, pkt + ip + 16, 4); return true; }
     if (v == 6 && ip + 40 <= caplen) { memcpy(k.src, pkt + ip + 8, 16); memcpy(k.dst, pkt + ip + 24, 16); return true; }
     return false;
@@ -278,7 +282,28 @@ static uint32_t rebuild(std::vector<uint8_t> &out, const uint8_t *pkt, uint32_t 
     const bool levels = (r.flags & MFP_FLAG_ENCAP) && mfpe::walk(pkt, caplen, linktype, ip, chain);
     if (!levels) start = ip;                                // the inner IP header on its own (LINKTYPE_RAW)
     const size_t at = out.size();
-    out.insert(out.end(), pkt + start, pkt + s.pay_off);
+    const bool dtls = s.kind & MFP_SEG_DTLS;
+    if (!dtls) {
+        out.insert(out.end(), pkt + start, pkt + s.pay_off);
+    } else {
+        // a DTLS ClientHello: the datagram's headers up to its first record,
+        // then that record's header and the handshake header of the whole
+        // message (fragment_offset 0, fragment_length = its length), so the
+        // re-walk parses the reassembled body as dtls_client_hello's
+        // reparse_from_buf does (dtls.h:170-173)
+        const uint32_t rec_off = s.pay_off - 25, udp_off = rec_off - 8;
+        out.insert(out.end(), pkt + start, pkt + rec_off + 11);            // ..., record type, version, epoch, sequence
+        const uint32_t L = (uint32_t)len;
+        const uint8_t hs[14] = {(uint8_t)((12 + L) >> 8), (uint8_t)(12 + L),   // record length
+                                pkt[s.pay_off - 12],                          // msg_type
+                                (uint8_t)(L >> 16), (uint8_t)(L >> 8), (uint8_t)L,
+                                pkt[s.pay_off - 8], pkt[s.pay_off - 7],       // message_seq
+                                0, 0, 0, (uint8_t)(L >> 16), (uint8_t)(L >> 8), (uint8_t)L};
+        out.insert(out.end(), hs, hs + 14);
+        const uint32_t ul = 8 + 25 + L;                                      // the UDP length
+        out[at + (udp_off - start) + 4] = (uint8_t)(ul >> 8);
+        out[at + (udp_off - start) + 5] = (uint8_t)ul;
+    }
     out.insert(out.end(), data, data + len);
     const uint32_t flen = (uint32_t)(out.size() - at);
     auto patch = [&](uint32_t off, uint32_t v) {            // ipv4 tot_len (ip.h:124-137) / ipv6 payload_len (:448-474)
@@ -313,6 +338,77 @@ static void drop(mfp_reassembler R, decltype(R->table)::iterator it) {
     R->table.erase(it);
 }
 
+// a flow whose state is final: its buffer rebuilt as a frame for the
+// device's re-walk (in the completing packet i's place), the flow consumed
+static void complete(mfp_reassembler R, size_t i, const uint8_t *pkt, const mfp_pkt_desc &d, const mfp_record &r,
+                     const mfp_tcp_seg &s, decltype(R->table)::iterator it, bool an_path) {
+    Flow &f = it->second.f;
+    R->who.push_back(i);
+    R->who_props.push_back((uint16_t)(1u | (uint32_t)f.flags << 1 | (uint32_t)f.ovl << 8));
+    mfp_pkt_desc d2;
+    d2.offset = R->frames.size();
+    const uint32_t fl = rebuild(R->frames, pkt, d.caplen, d.linktype, r, s, f.buf, f.contiguous);
+    d2.caplen = fl & 0x7fffffffu;
+    d2.linktype = (fl >> 31) ? d.linktype : (uint16_t)101;   // the packet's, or LINKTYPE_RAW
+    d2.flags = 0;
+    R->desc2.push_back(d2);
+    drop(R, it);                                              // consumed, then clean_curr_flow
+    if (an_path) R->more_state = false;                       // finalize_reassembly_flow (reassembly.hpp:1218-1228)
+}
+
+// one DTLS ClientHello fragment (process_udp_data pkt_proc.cc:896-945 ->
+// process_udp_offset_reassembly reassembly.hpp:1036-1100 ->
+// tcp_reassembler::process_udp_data_pkt :748-783): the first fragment of a
+// message opens a flow keyed by the 5-tuple and the message_seq; later ones
+// fill it by fragment_offset; a complete (or truncated) buffer is
+// fingerprinted in the completing packet's place; the fragments before write
+// no record.  Fragments that cannot take part are fingerprinted on their own.
+template <class NoRecord>
+static void dtls_fragment(mfp_reassembler R, size_t i, const uint8_t *arena, const mfp_pkt_desc *desc,
+                          const uint64_t *ts_ns, mfp_record *rec, bool an_path, NoRecord &no_record) {
+    const mfp_tcp_seg &s = R->seg[i];
+    const mfp_record &r = rec[i];
+    const uint8_t *pkt = arena + desc[i].offset;
+    const uint32_t frag_len = s.pay_len, frag_off = s.seq, more_bytes = s.more;
+    if (frag_len > kMaxData || frag_len == 0) return;
+    if (frag_off == 0 && !more_bytes) return;                        // a complete message
+    if ((uint64_t)frag_len + more_bytes > kMaxData) return;         // beyond the buffer
+    if (s.pay_off < 33 || (uint64_t)s.pay_off + frag_len > desc[i].caplen) return;
+    FlowKey k;
+    if (!flow_key(pkt, desc[i].caplen, r, k, 17)) return;
+    const uint8_t cid[2] = {pkt[s.pay_off - 8], pkt[s.pay_off - 7]};   // message_seq, big-endian (dtls.h:119)
+    const uint64_t sec = ts_ns ? ts_ns[i] / 1000000000ull : 0;
+    auto cid_ok = [&](const Flow &f) { return f.cid_len == 0 || !memcmp(f.cid, cid, 2); };
+    housekeeping(R, sec);                                            // check_flow (reassembly.hpp:669-692)
+    auto it = R->table.find(k);
+    if (it != R->table.end() && !cid_ok(it->second.f)) return;      // another message on this 5-tuple: standalone
+    if (it == R->table.end() && !more_bytes) return;                 // a later fragment without a flow: standalone
+    const bool first = it == R->table.end();                         // udp_segment{init_seg = true} (:1071-1080)
+    housekeeping(R, sec);                                            // process_udp_data_pkt's own check_flow
+    it = R->table.find(k);
+    if (it != R->table.end() && !cid_ok(it->second.f)) { no_record(i); return; }
+    const uint8_t *data = pkt + s.pay_off;
+    if (it == R->table.end()) {                                      // init_reassembly
+        R->age.push_back(k);
+        auto &e = R->table[k];
+        e.age = std::prev(R->age.end());
+        e.f.init(frag_len, frag_off, first ? more_bytes : 0, false, sec, data, frag_len);
+        e.f.cid[0] = cid[0]; e.f.cid[1] = cid[1]; e.f.cid_len = 2;
+        it = R->table.find(k);
+    } else {
+        Flow &f = it->second.f;
+        if (sec - f.init_time >= kTimeout) { f.state = S_TRUNCATED; f.flags |= 1u << F_TIMEOUT; }   // set_expired
+        else f.add(frag_len, frag_off, data, frag_len);
+    }
+    const Flow &f = it->second.f;
+    if (f.state == S_SUCCESS || f.state == S_TRUNCATED) {
+        complete(R, i, pkt, desc[i], r, s, it, an_path);
+    } else {
+        no_record(i);
+        if (an_path) R->more_state = true;                          // in_progress (pkt_proc.cc:1659-1661)
+    }
+}
+
 // the flow table over one batch, in stream order (process_tcp_data
 // pkt_proc.cc:773-893).  an_path: the analysis_context path
 // (analyze_ip_packet pkt_proc.cc:1624-1646): SYN, SYN/ACK and RST are skipped
@@ -345,6 +441,11 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
             }
         }
         if (more) more[i] = R->more_state;
+        if (s.kind & MFP_SEG_DTLS) {
+            dtls_fragment(R, i, arena, desc, ts_ns, rec, an_path, no_record);
+            if (more) more[i] = R->more_state;
+            continue;
+        }
         if (!(s.kind & MFP_SEG_DATA)) {
             if (an_path && (s.kind & MFP_SEG_TCP)) no_record(i);   // empty data: process_tcp_data returns false
             continue;
@@ -384,17 +485,7 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
         }
         Flow &f = it->second.f;
         if (f.state == S_SUCCESS || f.state == S_TRUNCATED) {   // is_ready: fingerprint the buffer
-            R->who.push_back(i);
-            R->who_props.push_back((uint16_t)(1u | (uint32_t)f.flags << 1 | (uint32_t)f.ovl << 8));
-            mfp_pkt_desc d2;
-            d2.offset = R->frames.size();
-            const uint32_t fl = rebuild(R->frames, pkt, desc[i].caplen, desc[i].linktype, r, s, f.buf, f.contiguous);
-            d2.caplen = fl & 0x7fffffffu;
-            d2.linktype = (fl >> 31) ? desc[i].linktype : (uint16_t)101;   // the packet's, or LINKTYPE_RAW
-            d2.flags = 0;
-            R->desc2.push_back(d2);
-            drop(R, it);                                    // consumed, then clean_curr_flow
-            if (an_path) R->more_state = false;             // finalize_reassembly_flow (reassembly.hpp:1218-1228)
+            complete(R, i, pkt, desc[i], r, s, it, an_path);
         } else {
             no_record(i);                                   // no record for this segment
             if (an_path) R->more_state = true;              // in_progress (pkt_proc.cc:1636-1638)

@@ -163,3 +163,25 @@ def test_classifier_more_than_512_processes():
     bad = test_analysis.compare(ref, rec, an, names)
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
     assert m["valid_big_p"] > 50
+
+
+@pytest.mark.gpu
+def test_classifier_more_than_4096_processes():
+    """Fingerprints with 4097..9000 processes (k_analyze_huge: one wave per
+    packet, the score row in HBM scratch) equal the reference
+    (tests/golden/make_golden_hugep.py); none is left unscored."""
+    m = json.load(open(os.path.join(GOLD, "hugep_manifest.json")))
+    arena, desc, sources = load()
+    cfg = f"select=stun;resources={os.path.join(GOLD, 'hugep_resources.tgz')};analysis"
+    ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+    try:
+        rec, fp, an = ctx.process_host_analysis(arena, desc)
+        names = [ctx.process_name(int(p)) for p in an["process"]]
+        counters = ctx.analysis_counters()
+    finally:
+        ctx.close()
+    ref = test_analysis.load_ref_an("hugep_an.tsv.gz")
+    bad = test_analysis.compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+    assert m["valid_huge_p"] > 100
+    assert counters["oversize"] >= m["valid_huge_p"]   # every one of them went through k_analyze_huge

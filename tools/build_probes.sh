@@ -1,6 +1,8 @@
 #!/bin/bash
 # profiling variants of libmercury_amd.so (never shipped: mercury_amd/_probe/)
 # usage: tools/build_probes.sh NAME:MACRO[,MACRO] ...
+#   an_*: mfp_analysis.hip only; tls_* / http_*: that family's walker TU only;
+#   anything else: every walker TU
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p mercury_amd/_probe
@@ -16,12 +18,15 @@ for spec in "$@"; do
   fi
   (  # fingerprint probes: recompile the walker translation units
     objs=""
-    for k in mfp_kernels mfp_k_tls mfp_k_http mfp_k_small mfp_k_all; do
+    tus="mfp_kernels mfp_k_tls mfp_k_http mfp_k_small mfp_k_all"
+    case $name in tls_*) tus=mfp_k_tls ;; http_*) tus=mfp_k_http ;; esac   # probes of one family
+    for k in $tus; do
       hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/$k.hip \
         -o mercury_amd/_probe/k_${name}_$k.o & objs="$objs mercury_amd/_probe/k_${name}_$k.o"
     done
     wait
     hipcc --offload-arch=gfx950 -shared -fPIC -o mercury_amd/_probe/libmercury_amd_$name.so $objs \
-      $(ls $OBJ/*.o | grep -v -E "mfp_kernels.hip.o|mfp_k_") -lz -lcrypto && echo built $name ) &
+      $(for o in $OBJ/*.o; do b=$(basename $o .hip.o); case " $tus " in *" $b "*) ;; *) echo $o ;; esac; done) \
+      -lz -lcrypto && echo built $name ) &
 done
 wait
