@@ -628,6 +628,11 @@ def main():
     total_pkts = n * world
     value = total_pkts * args.steps / elapsed / 1e6
     an_counters = ctx.analysis_counters() if analysis else None
+    if analysis and os.environ.get("MFP_REPORT_PHASES"):   # probe builds (MFP_AN_PHASES): k_analyze_wave clock sums
+        import ctypes
+        words = (ctypes.c_uint64 * 21)()
+        ctx.lib.mfp_analysis_counters(ctx.h, words, 21)
+        an_counters["wave_phase_clocks"] = [int(x) for x in words[13:21]]
     kbytes = kernel_bytes(rec, desc, an if analysis else None, n_fallback, an_counters)
     diverse = None
     if analysis and args.diverse_leg > 0 and world == 1:

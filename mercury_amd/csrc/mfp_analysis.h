@@ -98,7 +98,8 @@ struct mfp_classifier_dev {
 };
 // the classifier's per-batch device words: the public counters
 // (mfp_analysis_counters), then [MFP_AN_NCOUNTERS] the wave scorer's segment queue
-#define MFP_AN_STATS_WORDS (MFP_AN_NCOUNTERS + 4)
+// (+1..8: per-phase clock sums of k_analyze_wave in MFP_AN_PHASES probe builds)
+#define MFP_AN_STATS_WORDS (MFP_AN_NCOUNTERS + 12)
 #define MFP_DOM_MAPPING 1u
 #define MFP_DOM_EXCEPTION 2u
 

@@ -1214,9 +1214,12 @@ ADEV void max_two(const double (&sc)[CH], uint32_t np, uint32_t lane, double &mx
 ADEV double row_sums(const double *scl, const uint8_t *fl, uint32_t np, uint32_t imx, uint32_t nsum, uint32_t lane) {
     double acc = 0.0;
     if (lane < nsum) {
-        const uint32_t sh = lane >= 3 ? lane - 2 : 0;
+        // which entries this lane adds, as masks (no branches per entry)
+        const bool l_all = lane == 0, l_wo = lane == 1;
+        const uint32_t m = lane == 2 ? 1u : lane >= 3 ? 1u << (lane - 2) : 0u;
+        const uint32_t x80 = lane >= 3 ? 0x80u : 0u;   // the swapped-out maximum counts 0 for the tags
         auto take = [&](uint32_t p, uint32_t f) {
-            return lane == 0 ? true : lane == 1 ? p != imx : lane == 2 ? (f & 1u) != 0 : ((f >> sh) & 1u) && !(f & 0x80u);
+            return l_all | (l_wo & (p != imx)) | (((f & m) != 0u) & ((f & x80) == 0u));
         };
         uint32_t p = 0;
         for (; p + 8 <= np; p += 8) {
@@ -1281,6 +1284,13 @@ ADEV void stage_issue(const AParams &P, uint32_t w, WStage &st, uint32_t lane) {
     st.outw = take ? ((const uint32_t *)(P.out + i))[5] : 0u;
 }
 
+// MFP_AN_PHASES (probe builds): clock sums per phase of the pipelined scorer
+// into stats[MFP_AN_NCOUNTERS + 1 + k]
+#ifdef MFP_AN_PHASES
+#define PH_MARK(k) do { const uint64_t t_ = clock64(); ph[k] += t_ - ph_t; ph_t = t_; } while (0)
+#else
+#define PH_MARK(k) do { } while (0)
+#endif
 __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_buf)[336], char (*ua_buf)[520],
                                                  double (*sc_lds)[64 * MAXP_CHUNKS], uint32_t (*at_lds)[64 * MAXP_CHUNKS],
                                                  uint32_t (*id_lds)[64 * MAXP_CHUNKS], uint8_t (*fl_lds)[64 * MAXP_CHUNKS]) {
@@ -1292,6 +1302,10 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
     uint8_t *fl = fl_lds[wid];
     const mfp_classifier_dev &D = P.D;
     uint64_t w_prior = 0, w_upd = 0;   // table entries read (mfp_analysis_counters [6], [7])
+#ifdef MFP_AN_PHASES
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t ph_t = clock64();
+#endif
     for (;;) {
         // segments from a queue: the waves that draw short lists take more of them
         unsigned long long sgl = 0;
@@ -1312,6 +1326,7 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
 #pragma unroll
             for (uint32_t f = 0; f < NFEAT; f++) { off[f] = wf(wc, WI_OFF + f); cnt[f] = wf(wc, WI_CNT + f); }
             uint32_t malbits = 0, outw = 0;
+            PH_MARK(0);
             if (mine) {
                 // ---- [A] this packet's rows into LDS, the update lists applied
                 if (flags & 3u) {
@@ -1354,14 +1369,17 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                PH_MARK(1);
 #pragma unroll
                 for (uint32_t f = 0; f < NFEAT; f++) scatter_list(D, scl, off[f], cnt[f], st.uidx[f], st.uval[f], anylong, lane);
                 outw = st.outw;
+                PH_MARK(2);
             }
             // ---- [B] the next packet's rows and the WItem after it: in flight
             // while this packet's scoring tail runs
             const uint32_t w2 = wi_load(seg, q + 2, total, lane);
             stage_issue(P, wn, st, lane);
+            PH_MARK(3);
             if (mine) {
                 // ---- [C] scoring tail: LDS and registers only
                 double sc[CH];
@@ -1371,6 +1389,7 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
                 double mx;
                 uint32_t imx, isx;
                 max_two<CH>(sc, np, lane, mx, imx, isx);
+                PH_MARK(4);
                 const uint32_t mal_isx = (wf(malbits, isx & 63) >> (isx >> 6)) & 1u;
                 const uint32_t mal_imx = (wf(malbits, imx & 63) >> (imx >> 6)) & 1u;
                 // the dmz swap (decided by the ranks alone) and the selected
@@ -1394,9 +1413,11 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                PH_MARK(5);
                 const double acc = row_sums(scl, fl, np, imx, tags ? 3u + MFP_ATTR_DB_TAGS : 3u, lane);
                 double ssum = lane_d(acc, 0), swo = lane_d(acc, 1), mal = lane_d(acc, 2);
                 const double p_imx = scl[imx], p_isx = scl[isx];
+                PH_MARK(6);
                 double ap = 0.0;   // lane k < MFP_ATTR_DB_TAGS: tag k's sum
                 if (tags) {
 #pragma unroll
@@ -1436,6 +1457,7 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
                     P.out[i] = a;
                 }
                 __builtin_amdgcn_wave_barrier();
+                PH_MARK(7);
             }
             wc = wn;
             wn = w2;
@@ -1443,6 +1465,10 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
     }
     if (lane == 0 && w_prior) atomicAdd(&P.stats[6], (unsigned long long)w_prior);
     if (lane == 0 && w_upd) atomicAdd(&P.stats[7], (unsigned long long)w_upd);
+#ifdef MFP_AN_PHASES
+    if (lane == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&P.stats[MFP_AN_NCOUNTERS + 1 + k], (unsigned long long)ph[k]);
+#endif
 }
 
 // ---- k_analyze_big (64 * MAXP_CHUNKS < P <= 64 * MAXP_CHUNKS_BIG, production
