@@ -292,10 +292,6 @@ struct Slot {
     char *d_fp2 = nullptr; size_t cap_fp2 = 0;   // dense (compacted) fingerprints of a host batch
     unsigned long long *h_used = nullptr;   // pinned copy of d_used
     hipStream_t stream = nullptr;
-    // a second stream for half of a large host-to-device copy: two copies in
-    // flight use two DMA engines (one engine tops out near 30 GB/s)
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_in = nullptr, ev_out = nullptr;
 
     bool init() {
         return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
@@ -303,25 +299,7 @@ struct Slot {
                hipMalloc(&d_an_stats, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipMemset(d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
-               hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
-               hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_in, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_out, hipEventDisableTiming) == hipSuccess;
-    }
-    // host -> device copy of `len` bytes on `stream`; a large one is split
-    // over `stream` and `aux` (ordered after the stream's earlier work, and
-    // the stream's later work after both halves)
-    hipError_t copy_in(void *dst, const void *src, size_t len) {
-        static const bool split = !getenv("MFP_COPY_SPLIT") || atoi(getenv("MFP_COPY_SPLIT")) != 0;   // A/B switch
-        if (!split || len < ((size_t)64 << 20)) return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, stream);
-        const size_t h = (len / 2 + 4095) & ~(size_t)4095;
-        hipError_t e;
-        if ((e = hipEventRecord(ev_in, stream)) != hipSuccess || (e = hipStreamWaitEvent(aux, ev_in, 0)) != hipSuccess ||
-            (e = hipMemcpyAsync(dst, src, h, hipMemcpyHostToDevice, stream)) != hipSuccess ||
-            (e = hipMemcpyAsync((char *)dst + h, (const char *)src + h, len - h, hipMemcpyHostToDevice, aux)) != hipSuccess ||
-            (e = hipEventRecord(ev_out, aux)) != hipSuccess)
-            return e;
-        return hipStreamWaitEvent(stream, ev_out, 0);
+               hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
     }
     void release() {
         void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
@@ -329,9 +307,6 @@ struct Slot {
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         if (h_used) (void)hipHostFree(h_used);
-        if (ev_in) (void)hipEventDestroy(ev_in);
-        if (ev_out) (void)hipEventDestroy(ev_out);
-        if (aux) (void)hipStreamDestroy(aux);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -732,7 +707,7 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
         return -2;
     }
     const uint64_t copy = std::min<uint64_t>(span + 16, arena_len - lo);
-    if (copy) HIPCHK(S.copy_in(S.d_arena, arena + lo, copy));
+    if (copy) HIPCHK(hipMemcpyAsync(S.d_arena, arena + lo, copy, hipMemcpyHostToDevice, S.stream));
     if (n) HIPCHK(hipMemcpyAsync(S.d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, S.stream));
     const uint8_t *d_base = S.d_arena - lo;
     int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, dcap, (uint64_t *)S.d_used, S.stream);
