@@ -633,6 +633,14 @@ def main():
         words = (ctypes.c_uint64 * 21)()
         ctx.lib.mfp_analysis_counters(ctx.h, words, 21)
         an_counters["wave_phase_clocks"] = [int(x) for x in words[13:21]]
+    if os.environ.get("MFP_REPORT_PHASES"):   # probe builds (MFP_K_PHASES): walker phase clock sums
+        import ctypes
+        for tu in ("tls", "http"):
+            fn = getattr(ctx.lib, f"mfp_probe_read_{tu}", None)
+            if fn is not None:
+                words = (ctypes.c_uint64 * 8)()
+                if fn(words) == 0:
+                    (an_counters if an_counters is not None else {})[f"{tu}_phase_clocks"] = [int(x) for x in words[:5]]
     kbytes = kernel_bytes(rec, desc, an if analysis else None, n_fallback, an_counters)
     diverse = None
     if analysis and args.diverse_leg > 0 and world == 1:

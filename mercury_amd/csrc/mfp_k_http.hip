@@ -16,3 +16,5 @@ MFP_BIN_LAUNCHER(seg) {
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+KPH_READER(http)

@@ -5,3 +5,5 @@
 MFP_BIN_LAUNCHER(tls) {
     return mfp::launch_bin<mfp::FAM_TLS>(*P, fallback, lds != 0, name, lblocks, fblocks, stream, prof);
 }
+
+KPH_READER(tls)

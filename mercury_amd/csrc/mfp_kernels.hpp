@@ -20,6 +20,23 @@
 #include "mfp_device.hpp"
 #include "mfp_internal.h"
 
+// MFP_K_PHASES (probe builds): clock sums per phase of k_fp_tls1 / k_fp_seg in
+// this translation unit's mfp_kphase[] (read by mfp_probe_read_<tu>)
+#ifdef MFP_K_PHASES
+static __device__ unsigned long long mfp_kphase[8];
+#define KPH_DECL uint64_t kph_t = clock64(); uint64_t kph[5] = {0, 0, 0, 0, 0};
+#define KPH(k) do { const uint64_t t_ = clock64(); kph[k] += t_ - kph_t; kph_t = t_; } while (0)
+#define KPH_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 5; k_++) atomicAdd(&mfp_kphase[k_], (unsigned long long)kph[k_]); } while (0)
+#define KPH_READER(suffix) \
+    extern "C" MFP_EXPORT int mfp_probe_read_##suffix(unsigned long long *out) { \
+        return hipMemcpyFromSymbol(out, HIP_SYMBOL(mfp_kphase), sizeof(mfp_kphase)) == hipSuccess ? 0 : -1; }
+#else
+#define KPH_DECL
+#define KPH(k) do { } while (0)
+#define KPH_FLUSH() do { } while (0)
+#define KPH_READER(suffix)
+#endif
+
 namespace mfp {
 
 constexpr int TILE = 256;
@@ -198,6 +215,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    KPH_DECL
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
         const uint64_t t = tile * TILE + tid;
         const bool live = t < count;
@@ -234,6 +252,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         __syncthreads();
         const unsigned long long base = tile_base;
         const bool fits = base != ~0ull;
+        KPH(0);
 
         // walk + plan
         Out o;
@@ -252,6 +271,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
             }
             if (live && len && (!plan.ok || ((len + 7) & ~7u) + 8 > slot)) { punt = true; len = 0; }
         }
+        KPH(1);
         {
             const bool to_quic = punt && (o.msg == MFP_MSG_QUIC || o.msg == MFP_MSG_OPENVPN);
             const bool to_fb = punt && !to_quic;
@@ -270,6 +290,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
                 if (to_quic) P.quic_idx[b + __builtin_popcountll(qm & ((1ull << lane) - 1))] = (uint32_t)i;
             }
         }
+        KPH(2);
         // emit from the plan, the ClientHello still in the cache
         if (len && fits) {
             Em<true> e;
@@ -278,6 +299,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
             e.finish();
             *(uint64_t *)(P.fp_arena + base + excl + ((len + 7) & ~7u)) = e.hash();
         }
+        KPH(3);
         {   // bytes written (fp_used[2]): the exact lengths
             uint32_t lsum = fits ? len : 0u;
 #pragma unroll
@@ -303,7 +325,9 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
             write_seg(P, i, o);
         }
         __syncthreads();   // tile_base / wave_tot reuse
+        KPH(4);
     }
+    KPH_FLUSH();
 }
 
 // k_fp_seg -- the HTTP bins: lane-per-packet walk (the lane walker's SWAR
@@ -334,6 +358,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
     }
     __syncthreads();
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    KPH_DECL
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
         const uint64_t t = tile * TILE + tid;
         const bool live = t < count;
@@ -353,6 +378,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             if (e.valid()) len = e.n;
             else o.fp_type = 0;
         }
+        KPH(0);
 
         // reservation: 16-byte aligned slots holding string + hash
         const uint32_t slot = len ? (len + 8 + 15) & ~15u : 0u;
@@ -399,12 +425,33 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             if (fb) fallback[b + __builtin_popcountll(fbm & ((1ull << lane) - 1))] = (uint32_t)i;
         }
 
+        KPH(1);
         // wave-cooperative expansion, one packet at a time
         uint64_t todo = fits ? __ballot(len != 0) : 0ull;
 #ifdef MFP_PROBE_SEG_NOEXPAND
         todo = 0;
 #endif
         const uint64_t dptr = (uint64_t)(uintptr_t)data;
+        // packet j's 16-byte blocks (up to SEG_STAGE bytes: two per lane),
+        // loaded into registers while the packet before it is expanded, then
+        // written to the wave's LDS stage: the stage's memory round trip is
+        // off the per-packet critical path
+        constexpr uint32_t SPL = SEG_STAGE / 16 / 64;   // blocks per lane
+        uint4 pre[SPL];
+        auto stage_load = [&](int j) {
+            const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dptr, j) |
+                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dptr >> 32), j) << 32);
+            const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)dsc.caplen, j);
+            const uint32_t a16 = (uint32_t)(src & 15);
+            const uint32_t nvec = a16 + cl <= SEG_STAGE ? (a16 + cl + 15) >> 4 : 0u;
+            const uint4 *s16 = (const uint4 *)(uintptr_t)(src - a16);
+#pragma unroll
+            for (uint32_t k = 0; k < SPL; k++) {
+                const uint32_t v = k * 64 + lane;
+                pre[k] = v < nvec ? s16[v] : make_uint4(0, 0, 0, 0);
+            }
+        };
+        if (todo) stage_load(__builtin_ctzll(todo));
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -414,25 +461,26 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dptr, j) |
                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dptr >> 32), j) << 32);
             uint8_t *out = P.fp_arena + base + ex;
-            // stage the packet in LDS (one coalesced 16-byte load per lane):
-            // the expansion's byte reads then cost an LDS round trip, not a
-            // dependent L2 round trip per character group
+            // the packet from the LDS stage (expansion's byte reads are LDS
+            // round trips, not dependent L2 round trips); a packet larger than
+            // the stage is read where it lies
             const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)dsc.caplen, j);
             const uint8_t *pk = (const uint8_t *)(uintptr_t)src;
             const uint32_t a16 = (uint32_t)(src & 15);
+            __builtin_amdgcn_wave_barrier();
             if (a16 + cl <= SEG_STAGE) {
-                const uint32_t nvec = (a16 + cl + 15) >> 4;
-                const uint4 *s16 = (const uint4 *)(uintptr_t)(src - a16);
-                __builtin_amdgcn_wave_barrier();
-                for (uint32_t v = lane; v < nvec; v += 64) stage[wid][v] = s16[v];
-                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (uint32_t k = 0; k < SPL; k++) stage[wid][k * 64 + lane] = pre[k];
                 pk = (const uint8_t *)&stage[wid][0] + a16;
             }
+            __builtin_amdgcn_wave_barrier();
+            if (todo) stage_load(__builtin_ctzll(todo));   // the next packet, in flight during this expansion
             uint64_t h = seg_expand(segs + (wid * 64 + j) * SEG_STRIDE, ns, pk, T, out, pool, lane);
             h = wave_xor64(h);
             if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
         }
 
+        KPH(2);
         if (live && !fb) {
             mfp_record r;
             r.fp_offset = fits ? base + excl : 0;
@@ -452,7 +500,9 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             write_seg(P, i, o);
         }
         __syncthreads();   // tile_base / wave_tot / segs reuse
+        KPH(3);
     }
+    KPH_FLUSH();
 }
 
 

@@ -24,10 +24,11 @@ o = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 ks = {k: v["ms_per_step"] for k, v in o["kernels"].items()}
 top = sorted(ks.items(), key=lambda x: -x[1])[:7]
 print(f"{sys.argv[1]:14s} {o['value']:8.1f} Mpkt/s {o['ms_per_step']:8.2f} ms  " + "  ".join(f"{k}={v:.2f}" for k, v in top))
-ph = (o.get("analysis_counters") or {}).get("wave_phase_clocks")
-if ph:
-    t = sum(ph) or 1
-    print("   k_analyze_wave phases (% of clocks): " + " ".join(f"{k}:{100 * v / t:.1f}" for k, v in enumerate(ph)))
+for key in ("wave_phase_clocks", "tls_phase_clocks", "http_phase_clocks"):
+    ph = (o.get("analysis_counters") or {}).get(key)
+    if ph:
+        t = sum(ph) or 1
+        print(f"   {key} (% of clocks): " + " ".join(f"{k}:{100 * v / t:.1f}" for k, v in enumerate(ph)))
 PY
 done
 echo done
