@@ -361,7 +361,7 @@ def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
     out = {"k_classify": int((16 + np.minimum(cap, 128) + 5).sum())}
     sums = np.bincount(b, weights=per_pkt, minlength=8)
     for k, nm in enumerate(BIN_NAMES):
-        for kern in ("k_fingerprint/", "k_fp_seg/", "k_wave_fp/", "k_fp_lds/"):
+        for kern in ("k_fingerprint/", "k_fp_seg/", "k_fp_tls1/", "k_fp_lds/"):
             out[kern + nm] = int(sums[k])
     # the fallback lane re-walks the packets the bin kernels hand back (count
     # only: their mean per-packet bytes stand in for theirs)

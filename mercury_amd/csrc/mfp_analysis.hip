@@ -1872,11 +1872,15 @@ __global__ __launch_bounds__(256) void k_seen_sequence(AParams P, const uint32_t
 //   else per sighting in stream order: seen_seq[group_off[g] + rank] == 0.
 __global__ __launch_bounds__(256) void k_analyze_resolve(AParams P, const uint8_t *seen_pos, const uint32_t *group_off,
                                                          const uint8_t *seen_seq) {
+    // lane per packet: a wave takes one group of 64, its sightings side by
+    // side (the sequence path's position = the group's offset + the
+    // sighting's rank in the group)
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t ngroups = (P.n + 63) / 64;
-    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += (uint64_t)gridDim.x * 256) {
-    uint32_t r = seen_pos ? 0u : group_off[g];
-    for (uint64_t w = P.pend_bits[g]; w; w &= w - 1) {
-        const uint32_t i = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(w));
+    for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ngroups; g += (uint64_t)gridDim.x * 4) {
+        const uint64_t w = P.pend_bits[g];
+        if (!((w >> lane) & 1)) continue;
+        const uint32_t i = (uint32_t)(g * 64 + lane);
         mfp_analysis a = P.out[i];
         const mfp_record rc = P.rec[i];
         bool seen;
@@ -1890,7 +1894,7 @@ __global__ __launch_bounds__(256) void k_analyze_resolve(AParams P, const uint8_
                 if (sl.hash == ~0ull) break;
             }
         } else {
-            seen = seen_seq[r++] != 0;
+            seen = seen_seq[group_off[g] + (uint32_t)__builtin_popcountll(w & ((1ull << lane) - 1))] != 0;
         }
         a.flags &= (uint8_t)~MFP_AN_PENDING;
         if (seen) {   // unlabeled: no process, no faketls; encrypted_dns / domain_faking stay
@@ -1901,7 +1905,6 @@ __global__ __launch_bounds__(256) void k_analyze_resolve(AParams P, const uint8_
         }
         if (P.mode == MFP_MODE_ANALYSIS && (rc.flags & MFP_FLAG_TRUNCATED)) a.status = 3;   // pkt_proc.cc:1716-1719
         P.out[i] = a;
-    }
     }
 }
 
@@ -2022,8 +2025,8 @@ extern "C" int mfp_launch_analysis_resolve(const mfp_classifier_dev *D, const mf
     if (n == 0) return 0;
     mfpa::AParams P = make_params(D, *T, nullptr, nullptr, n, (mfp_record *)rec, fp_arena, out, pending, nullptr,
                                   nullptr, mode, 0);
-    uint64_t groups = (n + 63) / 64, blocks = (groups + 255) / 256;
-    if (blocks > 1024) blocks = 1024;
+    uint64_t groups = (n + 63) / 64, blocks = (groups + 3) / 4;   // a wave per group of 64 packets
+    if (blocks > 8192) blocks = 8192;
     if (prof) mfp_prof_begin(prof, "k_analyze_resolve", stream);
     hipLaunchKernelGGL(mfpa::k_analyze_resolve, dim3((uint32_t)blocks), dim3(256), 0, stream, P, seen_pos, group_off,
                        seen_seq);

@@ -186,7 +186,10 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
         P.count = bin_count + b;
         const bool seg = bin_seg_mask & (1u << b);
         const bool lds = bin_lds_mask & (1u << b);
-        const char *nm = lds ? lds_name[b] : seg ? seg_name[b] : lane_name[b];
+        // (the TLS bins' lane walker is the one-pass k_fp_tls1: its own name in the profiles)
+        const char *nm = lds ? lds_name[b] : seg ? seg_name[b]
+                       : (MFP_TLS_ONEPASS && (b == 0 || b == 5)) ? (b == 0 ? "k_fp_tls1/tls_ch" : "k_fp_tls1/tls_sh")
+                                                                  : lane_name[b];
         const uint32_t lb = (uint32_t)lblocks, fb = (uint32_t)fblocks;
         int rc;
         if (seg) rc = mfp_launch_bin_seg(&P, fallback, lds, nm, lb, fb, stream, prof);

@@ -48,7 +48,7 @@ def test_kernel_bytes_accounting():
     st = {"work_items": 1, "lane_scored": 1, "feature_slots": 5, "lane_priors": 4, "lane_updates": 10,
           "pending": 0, "deferred": 0, "seen_merges": 0}
     kb = bench.kernel_bytes(rec, desc, an, an_stats=st)
-    assert kb["k_fingerprint/tls_ch"] == 4 + 16 + 600 + 32 + 300
+    assert kb["k_fp_tls1/tls_ch"] == 4 + 16 + 600 + 32 + 300
     assert kb["k_fp_seg/http_req"] == 4 + 16 + 200 + 32 + 100 + 8
     assert kb["k_fingerprint/tcp_syn"] == 4 + 16 + 60 + 32 + 40
     assert kb["k_classify"] == 3 * (16 + 5) + 128 + 128 + 60
