@@ -293,22 +293,6 @@ struct Em {
     }
     DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
         if (EMIT) {
-#ifdef MFP_EM_BRANCHLESS
-            // the word so far and the overflow, computed unconditionally; the
-            // LDS line takes the word at every push (the next push overwrites
-            // it unless the word was complete), so lanes only branch to flush
-            const uint32_t sh = 8 * nacc;
-            const uint64_t lo = acc | (v << sh);
-            const uint64_t hi = sh ? (v >> (64 - sh)) : 0ull;
-            const uint32_t tot = nacc + k;
-            const bool full = tot >= 8;
-            line[nw] = lo;
-            h ^= full ? mfpc::word_term(lo, wi) : 0ull;
-            wi += full; nw += full;
-            acc = full ? hi : lo;
-            nacc = full ? tot - 8 : tot;
-            if (nw == 8) { flush_line(8); out += 64; nw = 0; }
-#else
             const uint32_t room = 8 - nacc;
             if (k < room) {
                 acc |= v << (8 * nacc);
@@ -320,7 +304,6 @@ struct Em {
                 acc = rest ? (v >> (8 * room)) : 0;
                 nacc = rest;
             }
-#endif
         }
         n += k;
     }
