@@ -36,8 +36,16 @@ typedef struct {
     uint64_t offset;
     uint32_t caplen;
     uint16_t linktype;
-    uint16_t flags;      /* reserved, 0 */
+    uint16_t flags;      /* 0, or MFP_DESC_* */
 } mfp_pkt_desc;
+enum {
+    /* a QUIC Initial whose ClientHello was reassembled across datagrams (the
+     * reassembler's frames, mfp_reassembler_frames): the packet's caplen bytes,
+     * zero padding to a multiple of 8, a little-endian u32 length L, 4 zero
+     * bytes, then the L bytes of reassembled CRYPTO data the ClientHello is
+     * parsed from (quic_init::reparse_crypto_buf quic.h:1593-1598) */
+    MFP_DESC_QUIC_CRYPTO = 1,
+};
 
 /* Per-packet result (32 bytes). */
 typedef struct {
@@ -118,7 +126,9 @@ enum {
                                   decrypted payload (sni/ua spans index the sidecar); contexts in
                                   MFP_MODE_WRITE_JSON add at json_off what the JSON writer prints
                                   (the plaintext, the handshake bytes, the cc frame's place, the
-                                  salt).  Packed host arenas keep it. */
+                                  salt); with reassembly inputs requested an Initial whose CRYPTO
+                                  data may need reassembly has the block too (its plaintext).
+                                  Packed host arenas keep it. */
 };
 /* For MFP_MSG_TLS_SH / MFP_MSG_TLS_CERT records sni_off/sni_len hold the
  * certificate_list datum (tls.h:275-296), the bytes the JSON writer's
@@ -158,6 +168,10 @@ enum {
                                    dtls.h:155-175): seq = fragment_offset, more =
                                    additional_bytes_needed, pay_off / pay_len = the fragment's
                                    bytes; its message_seq is the 2 bytes at pay_off - 8       */
+    MFP_SEG_QUIC = 128,         /* a QUIC Initial (quic_init): more = additional_bytes_needed,
+                                   pay_off / pay_len = the UDP payload; when its CRYPTO data
+                                   may take part in reassembly the record's sidecar carries the
+                                   plaintext (JSON block flag bit 2)                          */
 };
 
 /* semantics of the reference entry point to follow */

@@ -354,13 +354,6 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     std::string resources;
     bool analysis = false, reassembly = false;
     if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly)) return nullptr;
-    if (reassembly && (sel & SEL_QUIC)) {
-        // process_udp_data's QUIC CRYPTO-frame reassembly (pkt_proc.cc:926-933,
-        // reassembly.hpp:895-1030) is not on the device path: refuse, do not
-        // diverge (TCP messages and DTLS ClientHello fragments are reassembled)
-        mfp_set_error("reassembly covers TCP and DTLS here; remove quic from the selection");
-        return nullptr;
-    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         mfp_set_error("no HIP device available: the mercury_amd fingerprint path runs only on the GPU");
@@ -684,8 +677,19 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     Slot &S = c->slot[slot];
     uint64_t lo = UINT64_MAX, hi = 0, total = 0;
     for (size_t i = 0; i < n; i++) {
+        uint64_t end = desc[i].offset + desc[i].caplen;
+        if (desc[i].flags & MFP_DESC_QUIC_CRYPTO) {
+            // the reassembled CRYPTO data behind the packet travels with it
+            const uint64_t at = desc[i].offset + ((desc[i].caplen + 7) & ~7ull);
+            if (at + 8 > arena_len) { mfp_set_error("reassembled QUIC data past the end of the arena"); return -1; }
+            const uint32_t L = (uint32_t)arena[at] | (uint32_t)arena[at + 1] << 8 | (uint32_t)arena[at + 2] << 16 |
+                               (uint32_t)arena[at + 3] << 24;
+            if (L > 8192) { mfp_set_error("reassembled QUIC data longer than the 8192-byte buffer"); return -1; }
+            end = at + 8 + L;
+            total += 8 + L;
+        }
         lo = std::min<uint64_t>(lo, desc[i].offset);
-        hi = std::max<uint64_t>(hi, desc[i].offset + desc[i].caplen);
+        hi = std::max<uint64_t>(hi, end);
         total += desc[i].caplen;
     }
     // the device arena holds the strings at their reserved slots (the TLS

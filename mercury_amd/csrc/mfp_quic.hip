@@ -365,6 +365,9 @@ struct QRes {
     Cur hs;                 // the bytes the handshake was parsed from
     const uint8_t *cc;      // the cc frame's type byte in `plain`, or null
     uint32_t salt;          // salt of the decryption (0..5), 0xff none
+    // reassembly inputs (process_quic_reassembly reassembly.hpp:895-1033)
+    uint32_t more;          // additional_bytes_needed (quic.h:1628-1630)
+    uint32_t min_off;       // get_min_crypto_offset (quic.h:1644-1646), ~0u without CRYPTO data
 };
 
 // quic_init ctor (quic.h:1513-1591)
@@ -373,6 +376,7 @@ DEV QRes quic_process(Cur pay, uint8_t *pt, uint8_t *cb, const uint32_t *te, uin
     r.flags = 0; r.hello = false; r.pre = false; r.ver = nullptr;
     cset_null(r.ch.version); cset_null(r.ch.ciphers); cset_null(r.ch.compression); cset_null(r.ch.extensions);
     cset_null(r.plain); cset_null(r.hs); r.cc = nullptr; r.salt = 0xff;
+    r.more = 0; r.min_off = ~0u;
     const QHdr h = quic_hdr(pay);
     if (!h.valid) return r;
     r.ver = h.ver;
@@ -400,6 +404,7 @@ DEV QRes quic_process(Cur pay, uint8_t *pt, uint8_t *cb, const uint32_t *te, uin
     r.cc = s.cc;
     r.flags = MFP_FLAG_EMIT;                    // is_not_empty(): the header parsed (quic.h:1623)
     if (s.buf_len == 0) return r;               // crypto_buffer.is_valid()
+    r.min_off = (uint32_t)s.min_off;
     Cur d;
     if ((uint64_t)s.total == s.max_off + s.max_len - s.min_off) {   // no missing frames (quic.h:1267-1272)
         d = cmk(cb, cb + s.buf_len);
@@ -415,7 +420,8 @@ DEV QRes quic_process(Cur pay, uint8_t *pt, uint8_t *cb, const uint32_t *te, uin
     }
     r.hs = d;
     const Hs hs = tls_hs_parse(d);
-    if ((uint32_t)hs.more) r.flags |= MFP_FLAG_TRUNCATED;   // more_bytes_needed (uint32_t)
+    r.more = (uint32_t)hs.more;                 // more_bytes_needed (uint32_t)
+    if (r.more) r.flags |= MFP_FLAG_TRUNCATED;
     r.ch = tls_ch_parse(hs.body);
     r.hello = cnotempty(r.ch.compression);
     return r;
@@ -607,11 +613,25 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             packet_walk(e, c, o, data, dsc.caplen, dsc.linktype);
         }
         QRes q;
-        q.flags = 0; q.hello = false; q.pre = false; q.ver = nullptr;
+        q.flags = 0; q.hello = false; q.pre = false; q.ver = nullptr; q.more = 0; q.min_off = ~0u;
         const bool ovpn = live && o.msg == MFP_MSG_OPENVPN;
         OvRes v; v.present = false; v.hello = false;
         if (live && o.msg == MFP_MSG_QUIC)
             q = quic_process(cmk(data + o.pay_off, data + o.pay_off + o.pay_len), pt, cb, s_te, s_gh, (uint32_t)tid);
+        // a reassembled Initial (include/mfp.h MFP_DESC_QUIC_CRYPTO): the
+        // ClientHello is parsed again from the reassembled CRYPTO data the
+        // host put behind the packet (reparse_crypto_buf quic.h:1593-1598);
+        // the pre-decrypted path keeps its own hello (get_tls_client_hello
+        // quic.h:1655-1660), the packet's header, plaintext and truncation stay
+        if (live && o.msg == MFP_MSG_QUIC && (dsc.flags & MFP_DESC_QUIC_CRYPTO) && (q.flags & MFP_FLAG_EMIT) && !q.pre) {
+            const uint8_t *rb = data + ((dsc.caplen + 7) & ~7u);
+            const uint32_t rl = (uint32_t)ld(rb) | (uint32_t)ld(rb + 1) << 8 | (uint32_t)ld(rb + 2) << 16 | (uint32_t)ld(rb + 3) << 24;
+            Cur d = cmk(rb + 8, rb + 8 + (rl > Q_CB ? Q_CB : rl));
+            q.hs = d;
+            const Hs hs = tls_hs_parse(d);
+            q.ch = tls_ch_parse(hs.body);
+            q.hello = cnotempty(q.ch.compression);
+        }
         if (ovpn) {
             v = ovpn_process(cmk(data + o.pay_off, data + o.pay_off + o.pay_len), pt);
             q.flags = v.present ? MFP_FLAG_EMIT : 0;
@@ -635,8 +655,14 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         // classifier inputs, and on the write_json path the bytes the JSON
         // writer needs for the record's "tls" and "quic" objects (quic.h:1662-1690),
         // present also when there is no fingerprint
-        const bool json = live && o.msg == MFP_MSG_QUIC && (q.flags & MFP_FLAG_EMIT) && P.cfg.mode == MFP_MODE_WRITE_JSON;
-        const uint32_t pt_n = json ? span_len(q.plain) : 0u, hs_n = json && q.hello ? span_len(q.hs) : 0u;
+        const bool quic = live && o.msg == MFP_MSG_QUIC && (q.flags & MFP_FLAG_EMIT);
+        // with reassembly inputs requested: the plaintext of an Initial whose
+        // CRYPTO data may take part in reassembly (its frames are walked again
+        // by the host's flow table, mfp_reassembly.cpp quic_initial)
+        const bool reasm = quic && P.seg != nullptr && cnotempty(q.plain) && q.min_off != ~0u && (q.more || q.min_off);
+        const bool json = quic && (P.cfg.mode == MFP_MODE_WRITE_JSON || reasm);
+        const uint32_t pt_n = json ? span_len(q.plain) : 0u;
+        const uint32_t hs_n = json && q.hello && P.cfg.mode == MFP_MODE_WRITE_JSON ? span_len(q.hs) : 0u;
         const uint32_t meta = len && !ovpn ? span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
         const uint32_t jlen = json ? 16 + pt_n + hs_n : 0u;
         const uint32_t side = (len && !ovpn) || json ? 8 + meta + jlen : 0u;
@@ -712,7 +738,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
                 const uint32_t cco = q.cc && cnotempty(q.plain) ? (uint32_t)(q.cc - q.plain.d) : 0xffffu;
                 const uint32_t hv[5] = {o.pay_off, o.pay_len, pt_n, hs_n, cco};
                 for (int k = 0; k < 5; k++) { hdr[2 * k] = (uint8_t)hv[k]; hdr[2 * k + 1] = (uint8_t)(hv[k] >> 8); }
-                hdr[10] = (uint8_t)((q.pre ? 1u : 0u) | (q.hello ? 2u : 0u));
+                hdr[10] = (uint8_t)((q.pre ? 1u : 0u) | (q.hello ? 2u : 0u) | (reasm ? 4u : 0u));
                 hdr[11] = (uint8_t)q.salt;
                 hdr[12] = hdr[13] = hdr[14] = hdr[15] = 0;
                 for (int k = 0; k < 16; k++) sc[at + k] = hdr[k];
@@ -744,6 +770,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             r.dst_port = (uint16_t)o.dst_port;
             r.net = o.net;
             P.rec[i] = r;
+            if (quic) { o.seg_kind |= MFP_SEG_QUIC; o.more = q.more; }
             write_seg(P, i, o);
         }
         __syncthreads();   // tile_base / wave_tot reuse

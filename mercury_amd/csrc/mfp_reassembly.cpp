@@ -1,5 +1,6 @@
-// mfp_reassembly.cpp -- TCP reassembly of multi-segment messages (SURVEY
-// §8(f) rank 4) around the device fingerprint path.
+// mfp_reassembly.cpp -- reassembly of multi-segment messages (SURVEY §8(f)
+// rank 4) around the device fingerprint path: TCP messages, DTLS ClientHello
+// fragments, QUIC ClientHellos spread over several Initials.
 //
 // The reference's write_json path with "reassembly" configured
 // (stateful_pkt_proc::process_tcp_data pkt_proc.cc:773-893 over
@@ -134,8 +135,8 @@ struct Flow {
     uint64_t init_time = 0;
     uint32_t init_seq = 0, init_seg_len = 0, total_needed = 0;
     bool ssh_type = false;           // reassembly_type::ssh (indefinite)
-    uint8_t cid[2] = {0, 0};         // UDP offset reassembly: the DTLS message_seq (get_cid_datum)
-    uint32_t cid_len = 0;
+    uint8_t cid[20] = {};            // UDP reassembly: the DTLS message_seq, the QUIC connection id
+    uint32_t cid_len = 0;            // (get_cid_datum, max_cid_len 20)
     size_t contiguous = 0;
     size_t seg_count = 0;
     std::vector<std::pair<uint32_t, uint32_t>> segs;   // [first, second] relative sequence numbers
@@ -231,6 +232,34 @@ struct Flow {
     }
 };
 
+// quic_init's cryptographic_buffer (quic.h:1203-1294) for one packet
+struct QCrypto {
+    uint8_t buf[kMaxData];                        // zero for every packet (a new quic_init)
+    uint64_t buf_len = 0, min_off = ~0ull, min_len = ~0ull, max_off = 0, max_len = 0;
+    uint32_t total = 0, count = 0, first = 0xffff; // first_frame_index (invalid_first_frame_index)
+    uint64_t foff[20], flen[20];                  // crypto_frames: offset, length
+    uint32_t min_crypto_offset = 0xffffffffu;     // quic_init::min_crypto_offset
+    void reset() {
+        memset(buf, 0, sizeof buf);
+        buf_len = 0; min_off = ~0ull; min_len = ~0ull; max_off = 0; max_len = 0;
+        total = 0; count = 0; first = 0xffff; min_crypto_offset = 0xffffffffu;
+    }
+    // extend + update_crypto_frames + the min offset (quic.h:1226-1265, 1541-1548)
+    void add(uint64_t off, uint64_t len, const uint8_t *data) {
+        if (off > kMaxData || len > kMaxData || off + len > kMaxData) return;
+        memcpy(buf + off, data, len);
+        if (off + len > buf_len) buf_len = off + len;
+        if (off == 0) first = count;
+        if (off <= min_off) { min_off = off; min_len = len; }
+        if (off >= max_off) { max_off = off; max_len = len; }
+        total += (uint32_t)len;
+        if (count < 20) { foff[count] = off; flen[count] = len; count++; }
+        if (off <= min_crypto_offset) min_crypto_offset = (uint32_t)off;
+    }
+    bool missing() const { return (uint64_t)total != max_off + max_len - min_off; }   // quic.h:1267-1272
+    bool has_first() const { return first != 0xffff && first < count; }
+};
+
 }  // namespace
 
 struct mfp_reassembler_s {
@@ -249,6 +278,7 @@ struct mfp_reassembler_s {
     std::vector<uint8_t> quiet;                     // 1: a segment that writes no record (return false)
     std::vector<uint8_t> merged;                    // arena ++ frames (the classifier pass)
     std::vector<mfp_pkt_desc> desc3;
+    QCrypto qc;                                     // the current QUIC Initial's crypto buffer
 };
 
 extern "C" MFP_EXPORT mfp_reassembler mfp_reassembler_create(void) { return new mfp_reassembler_s; }
@@ -323,6 +353,14 @@ static uint32_t rebuild(std::vector<uint8_t> &out, const uint8_t *pkt, uint32_t 
 // are dropped (active_reap), otherwise up to two expired ones (passive_reap).
 // The reference walks its unordered_map from a persistent iterator; here the
 // two oldest flows are the candidates.
+// check_flow's connection-id test (reassembly.hpp:679-688): a flow without one
+// matches any; otherwise the incoming id, cut to 20 bytes, must equal it
+// (datum::cmp: same bytes and length)
+static bool cid_matches(const Flow &f, const uint8_t *cid, uint32_t n) {
+    if (n > 20) n = 20;
+    return f.cid_len == 0 || (f.cid_len == n && !memcmp(f.cid, cid, n));
+}
+
 static void housekeeping(mfp_reassembler R, uint64_t sec) {
     const bool active = R->table.size() >= kMaxFlows;
     for (int d = 0; d < 2 && !R->age.empty(); d++) {
@@ -347,10 +385,27 @@ static void complete(mfp_reassembler R, size_t i, const uint8_t *pkt, const mfp_
     R->who_props.push_back((uint16_t)(1u | (uint32_t)f.flags << 1 | (uint32_t)f.ovl << 8));
     mfp_pkt_desc d2;
     d2.offset = R->frames.size();
-    const uint32_t fl = rebuild(R->frames, pkt, d.caplen, d.linktype, r, s, f.buf, f.contiguous);
-    d2.caplen = fl & 0x7fffffffu;
-    d2.linktype = (fl >> 31) ? d.linktype : (uint16_t)101;   // the packet's, or LINKTYPE_RAW
-    d2.flags = 0;
+    if (s.kind & MFP_SEG_QUIC) {
+        // a QUIC Initial: the packet itself, then the reassembled CRYPTO data
+        // its ClientHello is parsed from (include/mfp.h MFP_DESC_QUIC_CRYPTO)
+        std::vector<uint8_t> &o = R->frames;
+        o.insert(o.end(), pkt, pkt + d.caplen);
+        while (o.size() % 8) o.push_back(0);
+        const uint32_t L = (uint32_t)f.contiguous;
+        const uint8_t hdr[8] = {(uint8_t)L, (uint8_t)(L >> 8), (uint8_t)(L >> 16), (uint8_t)(L >> 24), 0, 0, 0, 0};
+        o.insert(o.end(), hdr, hdr + 8);
+        o.insert(o.end(), f.buf, f.buf + L);
+        while (o.size() % 8) o.push_back(0);
+        o.resize(o.size() + 16, 0);
+        d2.caplen = d.caplen;
+        d2.linktype = d.linktype;
+        d2.flags = MFP_DESC_QUIC_CRYPTO;
+    } else {
+        const uint32_t fl = rebuild(R->frames, pkt, d.caplen, d.linktype, r, s, f.buf, f.contiguous);
+        d2.caplen = fl & 0x7fffffffu;
+        d2.linktype = (fl >> 31) ? d.linktype : (uint16_t)101;   // the packet's, or LINKTYPE_RAW
+        d2.flags = 0;
+    }
     R->desc2.push_back(d2);
     drop(R, it);                                              // consumed, then clean_curr_flow
     if (an_path) R->more_state = false;                       // finalize_reassembly_flow (reassembly.hpp:1218-1228)
@@ -378,7 +433,7 @@ static void dtls_fragment(mfp_reassembler R, size_t i, const uint8_t *arena, con
     if (!flow_key(pkt, desc[i].caplen, r, k, 17)) return;
     const uint8_t cid[2] = {pkt[s.pay_off - 8], pkt[s.pay_off - 7]};   // message_seq, big-endian (dtls.h:119)
     const uint64_t sec = ts_ns ? ts_ns[i] / 1000000000ull : 0;
-    auto cid_ok = [&](const Flow &f) { return f.cid_len == 0 || !memcmp(f.cid, cid, 2); };
+    auto cid_ok = [&](const Flow &f) { return cid_matches(f, cid, 2); };
     housekeeping(R, sec);                                            // check_flow (reassembly.hpp:669-692)
     auto it = R->table.find(k);
     if (it != R->table.end() && !cid_ok(it->second.f)) return;      // another message on this 5-tuple: standalone
@@ -406,6 +461,186 @@ static void dtls_fragment(mfp_reassembler R, size_t i, const uint8_t *arena, con
     } else {
         no_record(i);
         if (an_path) R->more_state = true;                          // in_progress (pkt_proc.cc:1659-1661)
+    }
+}
+
+// ---- QUIC Initials whose ClientHello spans datagrams
+// (process_udp_data pkt_proc.cc:933-939 -> process_quic_reassembly
+// reassembly.hpp:895-1033 over the same flow table, keyed by the 5-tuple and
+// the connection id)
+
+// variable_length_integer (quic_vli.hpp), as k_quic reads it: a short read
+// nulls the cursor and yields what was read
+static uint64_t hvli(HC &c) {
+    uint64_t b = 0;
+    hrd(c, 1, b);
+    const int len = (b & 0xc0) == 0xc0 ? 8 : (b & 0xc0) == 0x80 ? 4 : (b & 0xc0) == 0x40 ? 2 : 1;
+    uint64_t v = b & 0x3f;
+    for (int k = 1; k < len; k++) { uint64_t x = 0; hrd(c, 1, x); v = v * 256 + x; }
+    return v;
+}
+
+// the frame loop (quic_init quic.h:1532-1552; strict: quic_init_decry::parse
+// quic.h:1369-1390), the same walk as k_quic's quic_frames over the plaintext
+// the device decrypted
+static bool quic_frames_host(HC p, bool strict, QCrypto &q) {
+    while (p.d && p.d < p.e) {
+        uint64_t t = 0;
+        hrd(p, 1, t);
+        bool crypto = false;
+        uint64_t off = 0, len = 0;
+        HC data{nullptr, nullptr};
+        if (t == 0x06) {
+            off = hvli(p); len = hvli(p);
+            hparse(data, p, (long)len);
+            crypto = true;
+        } else if (t == 0x1c) {
+            hvli(p); hvli(p);
+            const uint64_t rl = hvli(p);
+            HC r; hparse(r, p, (long)rl);
+        } else if (t == 0x02 || t == 0x03) {
+            hvli(p); hvli(p);
+            const uint64_t rc = hvli(p);
+            hvli(p);
+            if (rc > 1000) hnull(p);
+            else for (uint64_t k = 0; k < rc && p.d && p.d < p.e; k++) { hvli(p); hvli(p); }
+            if (t == 0x03) { hvli(p); hvli(p); hvli(p); }
+        } else if (t != 0x00 && t != 0x01) {
+            return !strict;
+        }
+        if (strict && !p.d) return false;
+        if (crypto && data.d && data.d < data.e) q.add(off, len, data.d);
+    }
+    return true;
+}
+
+// the long header's connection ids (quic_initial_packet::parse quic.h:421-522);
+// get_cid: the DCID when not empty, else the SCID (quic.h:1611-1617)
+static bool quic_cid(const uint8_t *pay, uint32_t n, const uint8_t *&cid, uint32_t &cid_len) {
+    HC d{pay, pay + n};
+    uint64_t v;
+    hrd(d, 1, v);
+    HC ver; hparse(ver, d, 4);
+    hrd(d, 1, v);
+    if (v > 20 || !d.d) return false;
+    HC dcid; hparse(dcid, d, (long)v);
+    hrd(d, 1, v);
+    if (v > 20 || !d.d) return false;
+    HC scid; hparse(scid, d, (long)v);
+    if (!dcid.d || !scid.d) return false;
+    if (dcid.e > dcid.d) { cid = dcid.d; cid_len = (uint32_t)(dcid.e - dcid.d); }
+    else { cid = scid.d; cid_len = (uint32_t)(scid.e - scid.d); }
+    return true;
+}
+
+// one QUIC Initial through process_quic_reassembly: its CRYPTO data opens or
+// feeds the flow of its 5-tuple and connection id; a complete (or truncated)
+// buffer is fingerprinted in the completing packet's place, the Initials
+// before it write no record, the rest are taken on their own
+template <class NoRecord>
+static void quic_initial(mfp_reassembler R, size_t i, const uint8_t *arena, const mfp_pkt_desc *desc,
+                         const uint64_t *ts_ns, mfp_record *rec, const char *fp_arena, bool an_path,
+                         NoRecord &no_record) {
+    const mfp_tcp_seg &s = R->seg[i];
+    const mfp_record &r = rec[i];
+    const uint8_t *pkt = arena + desc[i].offset;
+    const uint32_t more_bytes = s.more;                      // udp_pkt.additional_bytes_needed()
+    if (more_bytes > kMaxData) return;                       // pkt_proc.cc:935-937
+    // the plaintext from the record's sidecar (JSON block flag bit 2)
+    if (!(r.flags & MFP_FLAG_SIDECAR)) return;
+    const uint8_t *sc = (const uint8_t *)fp_arena + r.fp_offset + ((r.fp_len + 7) & ~7u) + 8;
+    const uint32_t jo = (uint32_t)sc[6] | (uint32_t)sc[7] << 8;
+    if (!jo) return;
+    const uint8_t *j = sc + jo;
+    if (!(j[10] & 4)) return;                                // no CRYPTO data that could need reassembly
+    const uint32_t pt_len = (uint32_t)j[4] | (uint32_t)j[5] << 8;
+    const bool pre = j[10] & 1;
+    QCrypto &q = R->qc;
+    q.reset();
+    quic_frames_host(HC{j + 16, j + 16 + pt_len}, pre, q);
+    // get_crypto_buf (quic.h:1600-1609): the bytes from the smallest CRYPTO offset
+    const uint32_t crypto_offset = q.min_crypto_offset;
+    const uint32_t crypto_len = (!q.buf_len || crypto_offset == 0xffffffffu || crypto_offset > q.buf_len)
+                                    ? 0u : (uint32_t)(q.buf_len - crypto_offset);
+    if (crypto_len > kMaxData) return;
+    if (!crypto_len || (!crypto_offset && !more_bytes)) return;          // a complete Initial
+    if ((uint64_t)crypto_len + more_bytes > kMaxData) return;
+    if (s.pay_off + (uint64_t)s.pay_len > desc[i].caplen) return;
+    const uint8_t *cid = nullptr;
+    uint32_t cid_len = 0;
+    if (!quic_cid(pkt + s.pay_off, s.pay_len, cid, cid_len)) return;
+    FlowKey k;
+    if (!flow_key(pkt, desc[i].caplen, r, k, 17)) return;
+    const uint64_t sec = ts_ns ? ts_ns[i] / 1000000000ull : 0;
+    const bool missing = q.missing();
+    // check_flow (reassembly.hpp:669-692)
+    housekeeping(R, sec);
+    auto it = R->table.find(k);
+    if (it != R->table.end() && !cid_matches(it->second.f, cid, cid_len)) return;   // another connection: standalone
+    const bool fresh = it == R->table.end();
+    if (fresh && !more_bytes) return;
+    // process_udp_data_pkt (reassembly.hpp:748-783) for one segment of the
+    // packet's crypto buffer: open the flow, or add to it while in progress
+    bool lost = false;                                       // curr_flow reset by a connection-id mismatch
+    auto segment = [&](bool init, uint64_t off, uint64_t len) {
+        housekeeping(R, sec);
+        auto f = R->table.find(k);
+        if (f != R->table.end() && !cid_matches(f->second.f, cid, cid_len)) { lost = true; return; }
+        lost = false;
+        const uint8_t *data = q.buf + off;
+        if (f == R->table.end()) {                           // init_reassembly (UDP ctor reassembly.hpp:224-275)
+            R->age.push_back(k);
+            auto &e = R->table[k];
+            e.age = std::prev(R->age.end());
+            e.f.init((uint32_t)len, (uint32_t)off, init ? more_bytes : 0, false, sec, data, (uint32_t)len);
+            e.f.cid_len = cid_len;
+            memcpy(e.f.cid, cid, cid_len);
+        } else if (f->second.f.state == S_PROGRESS) {        // continue_reassembly
+            Flow &fl = f->second.f;
+            if (sec - fl.init_time >= kTimeout) { fl.state = S_TRUNCATED; fl.flags |= 1u << F_TIMEOUT; }
+            else fl.add((uint32_t)len, (uint32_t)off, data, (uint32_t)len);
+        }
+    };
+    const uint64_t max_end = (uint64_t)crypto_offset + crypto_len;
+    auto usable = [&](uint32_t x) {
+        return q.flen[x] && q.foff[x] + q.flen[x] <= max_end && q.foff[x] <= 0xffffffffu && q.flen[x] <= 0xffffffffu;
+    };
+    if (fresh) {
+        if (!missing) {
+            segment(true, crypto_offset, crypto_len);
+        } else {
+            if (q.count == 0 || q.first == 0xffff) return;
+            if (q.first >= q.count) return;                  // frames[first_frame_idx] past the list: not restated
+            const uint32_t ff = q.first;
+            if (q.flen[ff] < 10) {                           // min_crypto_data (quic.h:1571-1578)
+                const uint64_t fo = q.foff[ff];
+                if (fo < max_end && fo <= 0xffffffffu) {
+                    uint64_t sl = 10;
+                    if (max_end - fo < sl) sl = max_end - fo;
+                    if (sl) segment(true, fo, sl);
+                }
+            } else if (usable(ff)) {
+                segment(true, q.foff[ff], q.flen[ff]);
+            }
+            for (uint32_t x = 0; x < q.count; x++)
+                if (x != ff && usable(x)) segment(false, q.foff[x], q.flen[x]);
+        }
+    } else {
+        if (it->second.f.state != S_PROGRESS) { no_record(i); return; }   // success / truncated: return false
+        if (!missing) {
+            segment(false, crypto_offset, crypto_len);
+        } else {
+            if (q.count == 0) return;
+            for (uint32_t x = 0; x < q.count; x++)
+                if (usable(x)) segment(false, q.foff[x], q.flen[x]);
+        }
+    }
+    it = R->table.find(k);
+    if (!lost && it != R->table.end() && (it->second.f.state == S_SUCCESS || it->second.f.state == S_TRUNCATED)) {
+        complete(R, i, pkt, desc[i], r, s, it, an_path);     // reparse_crypto_buf, set_completed
+    } else {
+        no_record(i);
+        if (an_path && !lost && it != R->table.end()) R->more_state = true;   // in_progress (pkt_proc.cc:1660-1662)
     }
 }
 
@@ -443,6 +678,11 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
         if (more) more[i] = R->more_state;
         if (s.kind & MFP_SEG_DTLS) {
             dtls_fragment(R, i, arena, desc, ts_ns, rec, an_path, no_record);
+            if (more) more[i] = R->more_state;
+            continue;
+        }
+        if (s.kind & MFP_SEG_QUIC) {
+            quic_initial(R, i, arena, desc, ts_ns, rec, fp_arena, an_path, no_record);
             if (more) more[i] = R->more_state;
             continue;
         }
@@ -506,7 +746,7 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
         for (size_t j = 0; j < m; j++) {
             const size_t i = R->who[j];
             mfp_record r2 = R->rec2[j];
-            if (r2.fp_type) r2.fp_offset += (uint64_t)used;
+            if (r2.fp_type || (r2.flags & MFP_FLAG_SIDECAR)) r2.fp_offset += (uint64_t)used;
             // the reassembler's own "reassembly_properties" replace {"truncated":true}
             // (write_reassembly_properties reassembly.hpp:1231-1247)
             if (!an_path) r2.flags &= (uint8_t)~MFP_FLAG_TRUNCATED;

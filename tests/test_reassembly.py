@@ -128,12 +128,6 @@ def test_reassembly_across_batches():
 
 
 @pytest.mark.gpu
-def test_reassembly_refusals():
-    with pytest.raises(mercury_amd.MercuryAmdError):
-        mercury_amd.Context("select=tls,quic;reassembly", device=0)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("key", ["r0", "r1"])
 def test_reassembly_json_vs_reference(key):
     """The whole JSON line of every packet (mfp_write_json_batch_reassembly over
