@@ -24,15 +24,12 @@
 //      device fingerprints them in one more batch; their records replace the
 //      completing packets' records.
 // State persists across batches in the mfp_reassembler (the processor's
-// tcp_reassembler).  Deviations, by construction: the reference reaps expired
-// flows in unordered_map iteration order (passive_reap, active_reap at 10000
-// flows, reassembly.hpp:597-640); here an expired flow is found expired when
-// its next segment arrives, and at 10000 flows the oldest ones are dropped.
+// tcp_reassembler), in the reference's container with its hash, reaped from a
+// persistent iterator exactly as passive_reap / active_reap do.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstring>
-#include <list>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -118,13 +115,30 @@ struct FlowKey {
                !memcmp(dst, o.dst, 16);
     }
 };
+// std::hash<key> (flow_key.h:257-286, 313-317): the flow table's bucket of a
+// key, and so its iteration order (the reaping order), follow from it
 struct FlowKeyHash {
     size_t operator()(const FlowKey &k) const {
-        uint64_t h = 1469598103934665603ull ^ k.v ^ (uint64_t)k.proto << 8;
-        auto mix = [&](const uint8_t *p, size_t n) { for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; } };
-        mix(k.src, 16); mix(k.dst, 16);
-        h ^= (uint64_t)k.sport << 16 | k.dport; h *= 1099511628211ull;
-        return (size_t)h;
+        const uint64_t m = 2862933555777941757ull;
+        uint64_t x;
+        const uint16_t sp = k.sport, dp = k.dport;
+        const uint8_t pr = k.proto;
+        if (k.v == 4) {
+            uint32_t sa, da;                            // addr.ipv4: network order, read as stored
+            memcpy(&sa, k.src, 4); memcpy(&da, k.dst, 4);
+            x = (uint64_t)sp * da + (uint64_t)dp * sa;
+            x *= m;
+            x += (uint32_t)(sa + da + sp + dp + pr);    // unsigned int arithmetic
+            x *= m;
+        } else {
+            uint64_t sa[2], da[2];
+            memcpy(sa, k.src, 16); memcpy(da, k.dst, 16);
+            x = (uint64_t)sp * da[0] * da[1] + (uint64_t)dp * sa[0] * sa[1];
+            x *= m;
+            x += sa[0] + sa[1] + da[0] + da[1] + sp + dp + pr;
+            x *= m;
+        }
+        return (size_t)x;
     }
 };
 
@@ -263,11 +277,12 @@ struct QCrypto {
 }  // namespace
 
 struct mfp_reassembler_s {
-    // flows in reassembly, and their keys in insertion order (the reaping order
-    // here; each flow holds its position, so a consumed flow leaves the list)
-    struct Entry { Flow f; std::list<FlowKey>::iterator age; };
+    // the flows in reassembly (tcp_reassembler::table, reassembly.hpp:549-568):
+    // the same container, hash and reserved size as the reference, so its
+    // iteration order -- which the reaping iterator walks -- is the reference's
+    struct Entry { Flow f; };
     std::unordered_map<FlowKey, Entry, FlowKeyHash> table;
-    std::list<FlowKey> age;
+    decltype(table)::iterator reap_it;              // reassembly.hpp:555
     bool more_state = false;                        // analysis_context::flow_state_pkts_needed (sticky)
     std::vector<mfp_tcp_seg> seg;
     std::vector<mfp_record> rec2;
@@ -279,6 +294,7 @@ struct mfp_reassembler_s {
     std::vector<uint8_t> merged;                    // arena ++ frames (the classifier pass)
     std::vector<mfp_pkt_desc> desc3;
     QCrypto qc;                                     // the current QUIC Initial's crypto buffer
+    mfp_reassembler_s() { table.reserve(kMaxFlows); reap_it = table.end(); }
 };
 
 extern "C" MFP_EXPORT mfp_reassembler mfp_reassembler_create(void) { return new mfp_reassembler_s; }
@@ -349,10 +365,6 @@ static uint32_t rebuild(std::vector<uint8_t> &out, const uint8_t *pkt, uint32_t 
     return flen | (levels ? 0x80000000u : 0u);
 }
 
-// check_flow's housekeeping (reassembly.hpp:645-655): at max_entries flows two
-// are dropped (active_reap), otherwise up to two expired ones (passive_reap).
-// The reference walks its unordered_map from a persistent iterator; here the
-// two oldest flows are the candidates.
 // check_flow's connection-id test (reassembly.hpp:679-688): a flow without one
 // matches any; otherwise the incoming id, cut to 20 bytes, must equal it
 // (datum::cmp: same bytes and length)
@@ -361,19 +373,25 @@ static bool cid_matches(const Flow &f, const uint8_t *cid, uint32_t n) {
     return f.cid_len == 0 || (f.cid_len == n && !memcmp(f.cid, cid, n));
 }
 
+// check_flow's housekeeping (reassembly.hpp:596-655): at max_entries flows two
+// are dropped (active_reap), otherwise up to two expired ones (passive_reap),
+// from the persistent reaping iterator over the table
+static void reap_step(mfp_reassembler R) {                 // increment_reap_iterator
+    if (R->reap_it != R->table.end()) ++R->reap_it;
+    else R->reap_it = R->table.begin();
+}
 static void housekeeping(mfp_reassembler R, uint64_t sec) {
     const bool active = R->table.size() >= kMaxFlows;
-    for (int d = 0; d < 2 && !R->age.empty(); d++) {
-        auto it = R->table.find(R->age.front());
-        if (!active && sec - it->second.f.init_time < kTimeout) break;   // reassembly_flow_context::is_expired
-        R->age.pop_front();
-        R->table.erase(it);
+    for (int d = 0; d < 2; d++) {
+        reap_step(R);
+        if (R->reap_it != R->table.end() &&
+            (active || sec - R->reap_it->second.f.init_time >= kTimeout))   // reassembly_flow_context::is_expired
+            R->reap_it = R->table.erase(R->reap_it);
     }
 }
 
-static void drop(mfp_reassembler R, decltype(R->table)::iterator it) {
-    R->age.erase(it->second.age);
-    R->table.erase(it);
+static void drop(mfp_reassembler R, decltype(R->table)::iterator it) {   // clean_curr_flow (reassembly.hpp:830-835)
+    R->reap_it = R->table.erase(it);
 }
 
 // a flow whose state is final: its buffer rebuilt as a frame for the
@@ -444,9 +462,7 @@ static void dtls_fragment(mfp_reassembler R, size_t i, const uint8_t *arena, con
     if (it != R->table.end() && !cid_ok(it->second.f)) { no_record(i); return; }
     const uint8_t *data = pkt + s.pay_off;
     if (it == R->table.end()) {                                      // init_reassembly
-        R->age.push_back(k);
         auto &e = R->table[k];
-        e.age = std::prev(R->age.end());
         e.f.init(frag_len, frag_off, first ? more_bytes : 0, false, sec, data, frag_len);
         e.f.cid[0] = cid[0]; e.f.cid[1] = cid[1]; e.f.cid_len = 2;
         it = R->table.find(k);
@@ -589,9 +605,7 @@ static void quic_initial(mfp_reassembler R, size_t i, const uint8_t *arena, cons
         lost = false;
         const uint8_t *data = q.buf + off;
         if (f == R->table.end()) {                           // init_reassembly (UDP ctor reassembly.hpp:224-275)
-            R->age.push_back(k);
             auto &e = R->table[k];
-            e.age = std::prev(R->age.end());
             e.f.init((uint32_t)len, (uint32_t)off, init ? more_bytes : 0, false, sec, data, (uint32_t)len);
             e.f.cid_len = cid_len;
             memcpy(e.f.cid, cid, cid_len);
@@ -701,25 +715,31 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
         FlowKey k;
         if (!flow_key(pkt, desc[i].caplen, r, k)) continue;
         const uint64_t sec = ts_ns ? ts_ns[i] / 1000000000ull : 0;
-        housekeeping(R, sec);
+        housekeeping(R, sec);                               // check_flow (pkt_proc.cc:840)
         auto it = R->table.find(k);
         const uint8_t *data = pkt + s.pay_off;
         const uint32_t avail = s.pay_off + (uint64_t)data_len <= desc[i].caplen ? data_len : 0;
-        if (it == R->table.end()) {
+        const bool had = it != R->table.end();
+        if (!had) {
             if (supp) continue;                             // not in reassembly: taken as complete
             if (!more_bytes) { no_record(i); continue; }
-            R->age.push_back(k);
+        }
+        // 0: in order, after the flow's contiguous bytes (pkt_proc.cc:856-861)
+        const uint32_t seq = had && !s.seq ? (uint32_t)it->second.f.contiguous : s.seq;
+        // process_tcp_data_pkt (reassembly.hpp:717-746): its own check_flow, then
+        // open the flow (again, if that check reaped it) or continue it
+        housekeeping(R, sec);
+        it = R->table.find(k);
+        if (it == R->table.end()) {
             auto &e = R->table[k];
-            e.age = std::prev(R->age.end());
-            e.f.init(data_len, s.seq, more_bytes, (s.kind & MFP_SEG_SSH) != 0, sec, data, avail);
+            e.f.init(data_len, seq, had ? 0 : more_bytes, (s.kind & MFP_SEG_SSH) != 0, sec, data, avail);
             it = R->table.find(k);
-        } else {
+        } else if (it->second.f.state == S_PROGRESS) {
             Flow &f = it->second.f;
             if (sec - f.init_time >= kTimeout) {            // continue_reassembly: set_expired
                 f.state = S_TRUNCATED;
                 f.flags |= 1u << F_TIMEOUT;
             } else {
-                const uint32_t seq = s.seq ? s.seq : (uint32_t)f.contiguous;   // 0: in order (pkt_proc.cc:857-861)
                 f.add(data_len, seq, data, avail);
             }
         }

@@ -311,3 +311,41 @@ def tunnel_scenarios(seed=0x5EED0011):
                 inner_ip = T.ip6(l4, 6) if v6_inner else T.ip4(l4, 6, src=0x0a000105, dst=0x5db8d822)
                 out.append((f"tun_{kind}{r}.{j}", wrap(kind, inner_ip, v6_inner)))
     return out
+
+
+def reap_scenarios(seed=0x5EED0018, t0=1700000000, n_active=10150, n_stall=64, n_new=8):
+    """(phase, frame, capture time in seconds) for the reaping-order fixture
+    (tests/golden/make_golden_reap.py): the flow table filled past its 10 000
+    entries with ClientHellos whose first segment says more bytes follow
+    (active_reap drops two flows per new one), their second segments (the
+    survivors complete, active reaping goes on), then flows stalled past the
+    15 s timeout reaped by passive_reap while new flows arrive, and the
+    stalled flows' second segments."""
+    rng = np.random.default_rng(seed)
+    hello = synth.client_hello(rng, "openssl", "reap.example.com")
+    cut = 60
+    out = []
+
+    def flow(k, sport_base):
+        # distinct source addresses and ports: the flow keys spread over the buckets
+        return Flow(sport_base + k % 20000, src=0x0a000000 + (k * 2654435761 & 0xffffff), dst=0x0d59b21b)
+
+    flows = [flow(k, 20000) for k in range(n_active)]
+    for f in flows:                                   # phase A: first segments
+        out.append(("fill", f.pkt(hello[:cut], 0), t0))
+    for f in flows:                                   # phase B: second segments
+        out.append(("finish", f.pkt(hello[cut:], cut), t0 + 1))
+    t1 = t0 + 100
+    stalled = [flow(k + 500000, 30000) for k in range(n_stall)]
+    cut2 = len(hello) - 8                             # a timed-out buffer still holds a ClientHello
+    for f in stalled:                                 # phase C: flows that stall
+        out.append(("stall", f.pkt(hello[:cut2], 0), t1))
+    fresh = [flow(k + 900000, 40000) for k in range(n_new)]
+    for f in fresh:                                   # phase D: new flows after the timeout (passive reaping)
+        out.append(("new", f.pkt(hello[:cut], 0), t1 + 20))
+    order = list(rng.permutation(n_stall))
+    for j in order:                                   # phase E: the stalled flows' second segments
+        out.append(("late", stalled[j].pkt(hello[cut2:], cut2), t1 + 21))
+    for f in fresh:                                   # phase F: the new flows complete
+        out.append(("done", f.pkt(hello[cut:], cut), t1 + 22))
+    return out
