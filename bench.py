@@ -84,6 +84,93 @@ def build_device_batch(torch, n, workload, draw_seed, unique, diverse_tls=0.0):
     return ua, ud, d_arena, desc, d_desc
 
 
+def replicate_npz(torch, path, n):
+    """The packets of a committed fixture (tests/golden/*.npz: arena + desc),
+    replicated on the device to n packets."""
+    z = np.load(path)
+    ua, ud = z["arena"], z["desc"]
+    u = len(ud)
+    span = int((ud["offset"].astype(np.int64) + ud["caplen"]).max())
+    stride = (span + 64 + 255) // 256 * 256
+    reps = (n + u - 1) // u
+    host = np.zeros(stride, dtype=np.uint8)
+    host[:span] = ua[:span]
+    d_arena = torch.from_numpy(host).cuda().repeat(reps)
+    desc = np.tile(ud, reps)[:n].copy()
+    desc["offset"] += (np.arange(reps, dtype=np.uint64) * np.uint64(stride)).repeat(u)[:n]
+    return d_arena, desc, torch.from_numpy(desc.view(np.uint8)).cuda()
+
+
+def other_paths(torch, steps):
+    """The paths config 4 does not exercise, timed on their own batches: QUIC
+    Initials (k_quic: key derivation, header protection, AES-GCM, CRYPTO
+    frames, fingerprint), STUN + OpenVPN-over-TCP, and the reassembly path
+    (device walk, host flow table in stream order, the rebuilt messages'
+    device pass) over the TCP / DTLS / QUIC reassembly streams."""
+    import mercury_amd
+    gold = os.path.join(ROOT, "tests", "golden")
+    out = {}
+    for name, npz, sel, n in (("quic_initials", "quic_packets.npz", "select=quic", 2_000_000),
+                              ("stun_openvpn", "stun_ovpn_packets.npz", "select=stun,openvpn_tcp", 4_000_000)):
+        d_arena, desc, d_desc = replicate_npz(torch, os.path.join(gold, npz), n)
+        ctx = mercury_amd.Context(sel, device=0)
+        cap = ctx.fp_arena_bound(desc)
+        d_rec = torch.empty(n * mercury_amd.RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        d_fp = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        d_used = torch.zeros(4, dtype=torch.int64, device="cuda")
+        stream = torch.cuda.current_stream()
+
+        def step():
+            ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(), cap,
+                               d_used.data_ptr(), stream.cuda_stream)
+        step()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        prof = ctx.profile_read()
+        ctx.profile(False)
+        rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
+        ctx.close()
+        byts = int(desc["caplen"].astype(np.int64).sum())
+        kms = {k: round(v[1] / steps, 4) for k, v in prof.items()}
+        out[name] = {"value": round(n * steps / el / 1e6, 3), "unit": "Mpkt/s", "packets": n, "steps": steps,
+                     "ms_per_step": round(el / steps * 1e3, 4), "gb_per_s": round(byts * steps / el / 1e9, 3),
+                     "fingerprints_per_step": int((rec["fp_type"] > 0).sum()), "kernel_ms": kms,
+                     "what": f"{npz} (reference pcaps + synthetic) replicated on the device, {sel}"}
+        del d_arena, d_desc, d_rec, d_fp
+        torch.cuda.empty_cache()
+    # the reassembly path: one host batch of the three reassembly streams,
+    # repeated (the flows reopen on each repetition)
+    parts = []
+    for npz in ("reasm_packets.npz", "dtls_reasm_packets.npz", "quic_reasm_packets.npz"):
+        z = np.load(os.path.join(gold, npz))
+        parts.append((z["arena"], z["desc"]))
+    reps = 40
+    arena = np.concatenate([a for a, _ in parts])
+    base = np.cumsum([0] + [len(a) for a, _ in parts[:-1]])
+    one = np.concatenate([d.copy() for _, d in parts])
+    off = np.concatenate([np.full(len(d), b, np.uint64) for (_, d), b in zip(parts, base)])
+    one["offset"] += off
+    desc = np.tile(one, reps)
+    ctx = mercury_amd.Context("select=tls,ssh,http,dtls,quic;reassembly", device=0)
+    ts = np.full(len(desc), 1700000000 * 10**9, np.uint64)
+    ctx.process_host_reassembly(arena, desc[:len(one)], ts_ns=ts[:len(one)])
+    t0 = time.perf_counter()
+    rec, fp, props, _, _ = ctx.process_host_reassembly(arena, desc, ts_ns=ts)
+    el = time.perf_counter() - t0
+    ctx.close()
+    out["reassembly"] = {"value": round(len(desc) / el / 1e6, 3), "unit": "Mpkt/s", "packets": len(desc),
+                         "ms": round(el * 1e3, 3), "reassembled": int((props & 1).sum()),
+                         "what": "host batch (pageable memory): the TCP, DTLS and QUIC reassembly streams "
+                                 f"(tests/golden reasm/dtls_reasm/quic_reasm packets) x {reps}, "
+                                 "device walk + host flow table + the rebuilt messages' device pass"}
+    return out
+
+
 def cpu_threads():
     """Host threads for the CPU baseline: one GPU's share of the host's cores
     (nproc / 8 on an 8-GPU node), within the cores this process may use."""
@@ -477,6 +564,8 @@ def main():
     ap.add_argument("--diverse-leg", type=float, default=1.0,
                     help="fraction of TLS ClientHellos with per-packet cipher suites in the realistic-diversity "
                          "leg (reported beside value; 0 = skip)")
+    ap.add_argument("--no-other-paths", action="store_true",
+                    help="skip the QUIC / STUN+OpenVPN / reassembly legs")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check without a GPU: ranks start, join the gloo group, report, exit")
     args = ap.parse_args()
@@ -690,6 +779,12 @@ def main():
             log(f"[rank {rank}] end-to-end leg failed: {e}")
             if tdist:
                 raise
+    others = None
+    if world == 1 and not args.no_other_paths:
+        try:
+            others = other_paths(torch, max(1, min(args.steps, 5)))
+        except Exception as e:   # reported beside the headline, never instead of it
+            log(f"other-paths legs failed: {e}")
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -775,6 +870,7 @@ def main():
             "diversity": diverse,
             "analysis_counters": an_counters,
             "end_to_end": e2e,
+            "other_paths": others,
         }
         print(json.dumps(out), flush=True)
     ctx.close()
