@@ -110,8 +110,8 @@ def other_paths(torch, steps):
     import mercury_amd
     gold = os.path.join(ROOT, "tests", "golden")
     out = {}
-    for name, npz, sel, n in (("quic_initials", "quic_packets.npz", "select=quic", 2_000_000),
-                              ("stun_openvpn", "stun_ovpn_packets.npz", "select=stun,openvpn_tcp", 4_000_000)):
+    for name, npz, sel, n in (("quic_initials", "quic_packets.npz", "quic", 2_000_000),
+                              ("stun_openvpn", "stun_ovpn_packets.npz", "stun,openvpn_tcp", 4_000_000)):
         d_arena, desc, d_desc = replicate_npz(torch, os.path.join(gold, npz), n)
         ctx = mercury_amd.Context(sel, device=0)
         cap = ctx.fp_arena_bound(desc)

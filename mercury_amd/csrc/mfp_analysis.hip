@@ -1740,7 +1740,9 @@ __global__ __launch_bounds__(64) void k_analyze_huge(AParams P) {
 // 64-packet groups and aggregates its sightings in an LDS table (one LDS
 // update per distinct fingerprint per group); the block then merges its
 // entries into the global table: one insertion per new fingerprint, a
-// min / max only when it improves the stored one, one count addition.  A few
+// min / max only when it improves the stored one, one count addition.  The
+// distinct fingerprints of a group are found with ballots first, then their
+// leader lanes update the table together.  A few
 // hundred hot fingerprints thus see one global update per block, not one per
 // group (global atomics on a handful of lines serialise at the memory side).
 constexpr int SEEN_LDS = 2048;     // LDS table entries per block (power of two)
@@ -1801,30 +1803,39 @@ __global__ __launch_bounds__(64 * SEEN_WPB) void k_seen_scan(AParams P) {
             const uint64_t i = g * 64 + lane;
             uint64_t fh = 0;
             if (pending) { const mfp_record r = P.rec[i]; fh = fp_key(r, P.fp_arena + r.fp_offset, r.fp_len); }
+            // the group's distinct fingerprints: the lowest lane of each is its
+            // leader and carries first / last / count (ballots only) ...
             uint64_t left = pm;
-            while (left) {                           // one LDS update per distinct fingerprint of the group
+            bool lead = false;
+            uint32_t fi = 0, la = 0, c = 0;
+            while (left) {
                 const int l0 = __builtin_ctzll(left);
                 const uint64_t h0 = rl64(fh, l0);
                 const uint64_t same = __ballot(pending && fh == h0) & left;
                 left &= ~same;
                 if ((int)lane == l0) {
-                    const uint32_t fi = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(same));
-                    const uint32_t la = (uint32_t)(g * 64 + 63 - (uint64_t)__builtin_clzll(same));
-                    const uint32_t c = (uint32_t)__builtin_popcountll(same);
-                    uint32_t k = (uint32_t)h0 & (SEEN_LDS - 1);
-                    bool done = false;
-                    for (int t = 0; t < 32; t++, k = (k + 1) & (SEEN_LDS - 1)) {
-                        const unsigned long long prev = atomicCAS(&lh[k], ~0ull, (unsigned long long)h0);
-                        if (prev == ~0ull || prev == h0) {
-                            atomicMin(&lfirst[k], fi);
-                            atomicMin(&lnlast[k], ~la);
-                            atomicAdd(&lcnt[k], c);
-                            done = true;
-                            break;
-                        }
-                    }
-                    if (!done) { seen_merge(P.seen, h0, fi, la, c); merges++; }   // the block's table is crowded: straight to HBM
+                    lead = true;
+                    fi = (uint32_t)(g * 64 + (uint64_t)__builtin_ctzll(same));
+                    la = (uint32_t)(g * 64 + 63 - (uint64_t)__builtin_clzll(same));
+                    c = (uint32_t)__builtin_popcountll(same);
                 }
+            }
+            // ... then the leaders update the LDS table side by side (one update
+            // per distinct fingerprint of the group, their latencies overlapped)
+            if (lead) {
+                uint32_t k = (uint32_t)fh & (SEEN_LDS - 1);
+                bool done = false;
+                for (int t = 0; t < 32; t++, k = (k + 1) & (SEEN_LDS - 1)) {
+                    const unsigned long long prev = atomicCAS(&lh[k], ~0ull, (unsigned long long)fh);
+                    if (prev == ~0ull || prev == fh) {
+                        atomicMin(&lfirst[k], fi);
+                        atomicMin(&lnlast[k], ~la);
+                        atomicAdd(&lcnt[k], c);
+                        done = true;
+                        break;
+                    }
+                }
+                if (!done) { seen_merge(P.seen, fh, fi, la, c); merges++; }   // the block's table is crowded: straight to HBM
             }
         }
     }
