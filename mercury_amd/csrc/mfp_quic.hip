@@ -140,6 +140,27 @@ DEV void expand(const mfpq::Hmac &m, const LabelMsg &a, const LabelMsg &b, bool 
     mfpq::hmac_short(m, w, use_b ? b.len : a.len, out);
 }
 
+// len bytes src -> dst (disjoint, any alignment) with 8-byte stores at dst's
+// alignment, each word funnel-shifted from two aligned 8-byte loads of src
+// (byte-wise moves of a lane's own scratch slot are one memory transaction per
+// byte per lane); src may be read up to 7 bytes past its end
+DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t len) {
+    uint32_t j = 0;
+    while (j < len && (((uintptr_t)(dst + j)) & 7)) { dst[j] = src[j]; j++; }
+    if (j + 8 <= len) {
+        const uintptr_t a = (uintptr_t)(src + j);
+        const uint64_t *q = (const uint64_t *)(a & ~(uintptr_t)7);
+        const uint32_t sh = (uint32_t)(a & 7) * 8;
+        uint64_t cur = q[0];
+        for (; j + 8 <= len; j += 8) {
+            const uint64_t nxt = *++q;
+            *(uint64_t *)(dst + j) = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+            cur = nxt;
+        }
+    }
+    for (; j < len; j++) dst[j] = src[j];
+}
+
 // big-endian word of packet bytes p[0..n) (n <= 4), zero-padded
 DEV uint32_t be_bytes(const uint8_t *p, uint32_t n) {
     return n == 0 ? 0u : ld_be32n(p, (int)n) << (8 * (4 - n));
@@ -257,13 +278,25 @@ DEV int quic_decrypt(const QHdr &h, uint8_t *pt, const uint32_t *te, uint64_t *g
     }
     // ciphertext: GHASH over it, CTR keystream from counter 2 (J0 = iv || 1)
     const uint32_t nct = (uint32_t)ct_len;
+    // the ciphertext through aligned 8-byte loads (two per block, the third
+    // carried to the next block), bytes past ct_len masked off
+    const uint64_t *cq = (const uint64_t *)((uintptr_t)ct & ~(uintptr_t)7);
+    const uint32_t csh = (uint32_t)((uintptr_t)ct & 7) * 8;
+    uint64_t cx0 = nct ? cq[0] : 0ull;
     for (uint32_t b0 = 0, ctr = 2; b0 < nct; b0 += 16, ctr++) {
         const uint32_t left = nct - b0;
-        uint32_t c[4];
+        const uint64_t cx1 = cq[b0 / 8 + 1], cx2 = cq[b0 / 8 + 2];
+        const uint64_t lo = csh ? (cx0 >> csh) | (cx1 << (64 - csh)) : cx0;
+        const uint64_t hi = csh ? (cx1 >> csh) | (cx2 << (64 - csh)) : cx1;
+        cx0 = cx2;
+        uint32_t c[4] = {__builtin_bswap32((uint32_t)lo), __builtin_bswap32((uint32_t)(lo >> 32)),
+                         __builtin_bswap32((uint32_t)hi), __builtin_bswap32((uint32_t)(hi >> 32))};
+        if (left < 16) {
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t o = 4 * k;
-            c[k] = o < left ? be_bytes(ct + b0 + o, left - o < 4 ? left - o : 4u) : 0u;
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t o = 4 * k, n = o < left ? (left - o < 4 ? left - o : 4u) : 0u;
+                c[k] &= n == 0 ? 0u : 0xffffffffu << (8 * (4 - n));
+            }
         }
         ghash_block(gh, lane, xh, xl, c[0], c[1], c[2], c[3]);
         const uint32_t cb[4] = {iv[0], iv[1], iv[2], ctr};
@@ -308,7 +341,7 @@ DEV void cs_reset(CState &s) {
 DEV void cb_extend(CState &s, uint64_t off, uint64_t len, Cur data, uint8_t *cb, uint32_t &hw) {
     if (off > Q_CB || len > Q_CB || off + len > Q_CB) return;
     for (uint32_t j = hw; j < (uint32_t)off; j++) cb[j] = 0;
-    for (uint32_t j = 0; j < (uint32_t)len; j++) cb[off + j] = (uint8_t)ld(data.d + j);
+    copy_bytes(cb + off, data.d, (uint32_t)len);
     if (off + len > hw) hw = (uint32_t)(off + len);
     if (off + len > s.buf_len) s.buf_len = off + len;
     if (off == 0) { s.first_ok = s.count < 20; s.first = data; }
@@ -317,6 +350,23 @@ DEV void cb_extend(CState &s, uint64_t off, uint64_t len, Cur data, uint8_t *cb,
     s.total += (uint32_t)len;
     if (s.count < 20) s.count++;
 }
+// the end of a run of zero bytes from d (at most e): four aligned 8-byte
+// loads per step, so an Initial's PADDING (hundreds of one-byte frames) costs a
+// few dependent loads, not one per byte; may read up to 31 bytes past e
+DEV const uint8_t *skip_zeros(const uint8_t *d, const uint8_t *e) {
+    while (d < e && ((uintptr_t)d & 7)) { if (ld(d)) return d; d++; }
+    while (d < e) {
+        const uint64_t *q = (const uint64_t *)d;
+        const uint64_t w[4] = {q[0], q[1], q[2], q[3]};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (w[k]) { const uint8_t *r = d + 8 * k + (__builtin_ctzll(w[k]) >> 3); return r < e ? r : e; }
+        }
+        d += 32;
+    }
+    return e;
+}
+
 // the frame loop: strict = quic_init_decry::parse (quic.h:1369-1390: an invalid
 // frame or a null cursor fails the whole payload), otherwise quic_init's loop
 // (quic.h:1532-1552: stop at the first invalid frame).  Returns strict validity.
@@ -324,6 +374,10 @@ DEV bool quic_frames(Cur p, bool strict, CState &s, uint8_t *cb, uint32_t &hw) {
     while (cnotempty(p)) {
         const uint8_t *at = p.d;
         const uint32_t t = rd_u8(p);            // quic_frame ctor quic.h:1131-1152
+        if (t == 0x00) {                        // PADDING: the zero bytes that follow are PADDING frames too
+            p.d = skip_zeros(p.d, p.e);
+            continue;
+        }
         bool crypto = false;
         uint64_t off = 0, len = 0;
         Cur data; cset_null(data);

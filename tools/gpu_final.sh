@@ -15,7 +15,7 @@ tail -1 $O/smoke.log
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 head -c 300 $O/bench.json; echo
 TAG=$T BENCH="--diverse-leg 0" bash tools/gpu_traffic.sh || exit 1
-B="python3 bench.py --packets 10000000 --steps 3 --warmup 1 --no-cpu-baseline --e2e-total 0 --diverse-leg 0"
+B="python3 bench.py --packets 10000000 --steps 3 --warmup 1 --no-cpu-baseline --e2e-total 0 --diverse-leg 0 --no-other-paths"
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_INSTS_SMEM -f csv -d $O/p1 -o p1 -- $B > $O/p1.out 2>&1 || { tail -5 $O/p1.out; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS -f csv -d $O/p2 -o p2 -- $B > $O/p2.out 2>&1 || { tail -5 $O/p2.out; exit 1; }
 python tools/pmc_summary.py $O > $O/pmc_summary.txt 2>&1 || true

@@ -27,7 +27,7 @@ for s in ${STEPS:-tests}; do
       timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py ${BENCH:-} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
       head -c 600 $O/bench.json; echo ;;
     prof)
-      B="python3 bench.py --packets ${PK:-50000000} --steps 4 --warmup 1 --no-cpu-baseline --e2e-total 0 ${BENCH:-}"
+      B="python3 bench.py --packets ${PK:-50000000} --steps 4 --warmup 1 --no-cpu-baseline --e2e-total 0 --no-other-paths ${BENCH:-}"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o kt -- $B > $O/kt.out 2>&1 || { tail -20 $O/kt.out; exit 1; }
       head -12 $O/kt/kt_kernel_stats.csv | cut -c1-160 ;;
     *) echo "unknown step $s"; exit 2 ;;

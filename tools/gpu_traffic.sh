@@ -10,7 +10,7 @@ T=${TAG:-r02t}
 O=gpurun_out/$T
 mkdir -p $O
 PKN=${PK:-50000000}
-B="python3 bench.py --packets $PKN --steps 4 --warmup 1 --no-cpu-baseline --e2e-total 0 ${BENCH:-}"
+B="python3 bench.py --packets $PKN --steps 4 --warmup 1 --no-cpu-baseline --e2e-total 0 --no-other-paths ${BENCH:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o kt -- $B > $O/kt.out 2>&1 || { tail -20 $O/kt.out; exit 1; }
 echo "kernel-trace done"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o fetch -- $B > $O/fetch.out 2>&1 || { tail -5 $O/fetch.out; exit 1; }
