@@ -350,6 +350,10 @@ DEV void cb_extend(CState &s, uint64_t off, uint64_t len, Cur data, uint8_t *cb,
     s.total += (uint32_t)len;
     if (s.count < 20) s.count++;
 }
+// PADDING runs skipped word-wide in quic_frames (pending a GPU run: off)
+#ifndef MFP_QUIC_PADSKIP
+#define MFP_QUIC_PADSKIP 0
+#endif
 // the end of a run of zero bytes from d (at most e): four aligned 8-byte
 // loads per step, so an Initial's PADDING (hundreds of one-byte frames) costs a
 // few dependent loads, not one per byte; may read up to 31 bytes past e
@@ -374,10 +378,12 @@ DEV bool quic_frames(Cur p, bool strict, CState &s, uint8_t *cb, uint32_t &hw) {
     while (cnotempty(p)) {
         const uint8_t *at = p.d;
         const uint32_t t = rd_u8(p);            // quic_frame ctor quic.h:1131-1152
+#if MFP_QUIC_PADSKIP
         if (t == 0x00) {                        // PADDING: the zero bytes that follow are PADDING frames too
             p.d = skip_zeros(p.d, p.e);
             continue;
         }
+#endif
         bool crypto = false;
         uint64_t off = 0, len = 0;
         Cur data; cset_null(data);
