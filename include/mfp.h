@@ -461,6 +461,15 @@ MFP_EXPORT int mfp_resource_stats_ex(const char *path, const uint8_t *enc_key, u
  * normalisation the device applies to server names); returns the length */
 MFP_EXPORT int mfp_normalize_server_name(const char *name, size_t len, char *out, size_t cap);
 
+/* host only (tests): the archive's subnet tries (pyasn.db, domain mappings)
+ * built exactly as the device gets them -- the reference's LC-tries
+ * (lctrie/lctrie.hpp) -- and queried with the device's lct_find: per
+ * "dst_ip<TAB>server_name" line of `queries`, asn[i] = get_asn_info(dst_ip)
+ * and fake[i] = is_domain_faking(server_name, dst_ip) (addr.cc:172-208,
+ * 707-792; no name: 0).  Returns the lines answered (<= cap), -1 on error. */
+MFP_EXPORT long long mfp_lpm_query(const char *resources, const char *queries, uint32_t *asn, int8_t *fake,
+                                   size_t cap);
+
 /* ---- per-kernel timing (bench.py's roofline; the rocprofv3 cross-check) ----
  * on != 0: from now on every kernel launch of this context is bracketed by
  * HIP events recorded on its launch stream (totals reset); on == 0: off. */

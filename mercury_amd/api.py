@@ -132,6 +132,8 @@ def load_library():
     lib.mfp_analysis_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     lib.mfp_resource_stats.restype = ctypes.c_int
     lib.mfp_resource_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+    lib.mfp_lpm_query.restype = ctypes.c_longlong
+    lib.mfp_lpm_query.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, sz]
     lib.mfp_normalize_server_name.restype = ctypes.c_int
     lib.mfp_normalize_server_name.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
     lib.mfp_parse_filter.restype = ctypes.c_int
@@ -593,6 +595,22 @@ def resource_stats(path, enc_key=None):
     keys = ["fingerprints", "entries", "processes", "updates", "known_prevalence", "asn_prefixes", "disabled",
             "process_names"]
     return dict(zip(keys, list(out)))
+
+
+def lpm_query(resources, queries):
+    """Host-only: the archive's subnet LC-tries built as the device gets them
+    and queried with the device's lookup; queries = [(dst_ip, server_name)].
+    Returns [(asn, domain_faking)] (subnet_data::get_asn_info /
+    is_domain_faking, addr.cc:172-208, 707-792)."""
+    lib = load_library()
+    text = "".join(f"{ip}\t{name}\n" for ip, name in queries).encode("latin-1")
+    n = len(queries)
+    asn = np.zeros(max(n, 1), np.uint32)
+    fake = np.zeros(max(n, 1), np.int8)
+    got = lib.mfp_lpm_query(resources.encode(), text, asn.ctypes.data, fake.ctypes.data, n)
+    if got < 0:
+        raise MercuryAmdError(_err(lib))
+    return [(int(asn[i]), int(fake[i])) for i in range(got)]
 
 
 def normalize_server_name(name):

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/mfp.h"
+#include "mfp_lctrie.hpp"
 
 // open-addressing string table slot (fingerprint DB, known-prevalence set)
 struct mfp_fp_slot {
@@ -43,8 +44,6 @@ struct mfp_update {     // class update (naive_bayes.hpp:21-41)
     double value;
 };
 
-struct mfp_asn4 { uint32_t lo, hi, asn, pad; };             // host-order address interval
-struct mfp_asn6 { uint64_t lo_hi, lo_lo, hi_hi, hi_lo; uint32_t asn, pad; };   // 128-bit host-order interval
 
 // one batch's unknown-TLS sightings, per distinct fingerprint hash (the
 // adaptive part of fingerprint_prevalence is decided on the host,
@@ -75,9 +74,9 @@ struct mfp_classifier_dev {
     mfp_feat_slot *feat_slots = nullptr; uint64_t feat_mask = 0;
     mfp_update *upd = nullptr;
     char *pool = nullptr;
-    mfp_asn4 *asn4 = nullptr; uint32_t n_asn4 = 0;
-    uint32_t *asn4_bucket = nullptr;   // 65537 entries: first interval with hi >= b << 16 (narrows the search)
-    mfp_asn6 *asn6 = nullptr; uint32_t n_asn6 = 0;
+    // pyasn.db as the reference's LC-tries (mfp_lctrie.hpp); n_* = node count, 0: no table
+    mfp_lct_node *asn4_node = nullptr; mfp_lct_net4 *asn4_net = nullptr; uint32_t n_asn4 = 0;
+    mfp_lct_node *asn6_node = nullptr; mfp_lct_net6 *asn6_net = nullptr; uint32_t n_asn6 = 0;
     uint32_t types_mask = 0;           // analyzable fingerprint types (fp_types)
     uint32_t max_nproc = 0;            // the largest process count of an entry (k_analyze_big when > 512)
     uint32_t enc_channel_idx = 7, faketls_idx = 9, doh_idx = 6, domain_faking_idx = 8;
@@ -91,8 +90,9 @@ struct mfp_classifier_dev {
     uint32_t *doh_v4 = nullptr; uint32_t n_doh_v4 = 0;               // sorted IPv4 (parse_ipv4 values)
     uint64_t *doh_v6 = nullptr; uint32_t n_doh_v6 = 0;               // sorted (hi, lo) pairs
     mfp_fp_slot *dom_slots = nullptr; uint64_t dom_mask = 0;         // mapped domain -> domain index (id)
-    mfp_asn4 *dom4 = nullptr; uint32_t n_dom4 = 0;                   // prefix intervals, asn = info + 1
-    mfp_asn6 *dom6 = nullptr; uint32_t n_dom6 = 0;                   // 0: no IPv6 mappings
+    // domain-mapping LC-tries; a subnet's val = its dom_info index + 1; n_* = node count, 0: no table
+    mfp_lct_node *dom4_node = nullptr; mfp_lct_net4 *dom4_net = nullptr; uint32_t n_dom4 = 0;
+    mfp_lct_node *dom6_node = nullptr; mfp_lct_net6 *dom6_net = nullptr; uint32_t n_dom6 = 0;
     uint32_t *dom_info = nullptr;      // per prefix: [type (1 mapping, 2 exception) | count << 8, byte offset]
     uint8_t *dom_bytes = nullptr;      // mapped domain indices (uint8_t, as the reference stores them)
 };

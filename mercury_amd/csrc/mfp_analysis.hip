@@ -92,31 +92,6 @@ ADEV Hit probe_feature(const mfp_classifier_dev &D, uint32_t entry, uint32_t kin
     }
 }
 
-ADEV uint32_t asn_v4(const mfp_classifier_dev &D, uint32_t addr_host) {
-    int lo = 0, hi = (int)D.n_asn4 - 1;
-    while (lo <= hi) {
-        int mid = (lo + hi) >> 1;
-        const uint32_t a = rfl(D.asn4[mid].lo), b = rfl(D.asn4[mid].hi);
-        if (addr_host < a) hi = mid - 1;
-        else if (addr_host > b) lo = mid + 1;
-        else return rfl(D.asn4[mid].asn);
-    }
-    return 0;
-}
-ADEV bool le128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) { return ah < bh || (ah == bh && al <= bl); }
-ADEV uint32_t asn_v6(const mfp_classifier_dev &D, uint64_t xh, uint64_t xl) {
-    int lo = 0, hi = (int)D.n_asn6 - 1;
-    while (lo <= hi) {
-        int mid = (lo + hi) >> 1;
-        const mfp_asn6 r = D.asn6[mid];
-        const uint64_t ah = rfl64(r.lo_hi), al = rfl64(r.lo_lo), bh = rfl64(r.hi_hi), bl = rfl64(r.hi_lo);
-        if (!le128(ah, al, xh, xl)) hi = mid - 1;
-        else if (!le128(xh, xl, bh, bl)) lo = mid + 1;
-        else return rfl(r.asn);
-    }
-    return 0;
-}
-
 // apply one feature's update list to the per-lane scores
 ADEV void apply(const mfp_classifier_dev &D, Hit h, double (&sc)[MAXP_CHUNKS], uint32_t lane) {
     const uint32_t cnt = h.cnt & ~MFP_UPD_SERIAL;   // applied in list order either way
@@ -331,31 +306,17 @@ ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_
     }
 }
 
+// subnet_data::get_asn_info (addr.cc:172-208): lct_find on the reference's
+// tries (mfp_lctrie.hpp), the subnet's ASN or 0
 ADEV uint32_t asn_v4_lane(const mfp_classifier_dev &D, uint32_t addr_host) {
-    // the bucket index narrows ~17 dependent probes of the whole table to the
-    // few intervals that can hold an address of this /16
-    const uint32_t b = addr_host >> 16;
-    int lo = (int)D.asn4_bucket[b], hi = (int)D.asn4_bucket[b + 1];
-    if (hi > (int)D.n_asn4 - 1) hi = (int)D.n_asn4 - 1;
-    while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        const mfp_asn4 r = D.asn4[mid];
-        if (addr_host < r.lo) hi = mid - 1;
-        else if (addr_host > r.hi) lo = mid + 1;
-        else return r.asn;
-    }
-    return 0;
+    if (!D.n_asn4) return 0;
+    const uint32_t s = lct_find4(D.asn4_node, D.asn4_net, addr_host);
+    return s == MFP_LCT_NIL ? 0 : D.asn4_net[s].val;
 }
 ADEV uint32_t asn_v6_lane(const mfp_classifier_dev &D, uint64_t xh, uint64_t xl) {
-    int lo = 0, hi = (int)D.n_asn6 - 1;
-    while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        const mfp_asn6 r = D.asn6[mid];
-        if (!le128(r.lo_hi, r.lo_lo, xh, xl)) hi = mid - 1;
-        else if (!le128(xh, xl, r.hi_hi, r.hi_lo)) lo = mid + 1;
-        else return r.asn;
-    }
-    return 0;
+    if (!D.n_asn6) return 0;
+    const uint32_t s = lct_find6(D.asn6_node, D.asn6_net, xh, xl);
+    return s == MFP_LCT_NIL ? 0 : D.asn6_net[s].val;
 }
 
 // ---------------------------------------------------------------------------
@@ -420,27 +381,15 @@ ADEV bool domain_faking(const mfp_classifier_dev &D, const uint8_t *sn, uint32_t
     if (d.ipv == 4) {
         const uint32_t v = d.v4;   // ipv4_address::get_addr_type private_use (ip_address.hpp:119-123)
         if ((v & 0xff) == 0x0a || (v & 0xf0ff) == 0x10ac || (v & 0xffff) == 0xa8c0) return false;
-        const uint32_t h = __builtin_bswap32(v);
-        int lo = 0, hi = (int)D.n_dom4 - 1;
-        while (lo <= hi) {
-            const int mid = (lo + hi) >> 1;
-            const mfp_asn4 r = D.dom4[mid];
-            if (h < r.lo) hi = mid - 1;
-            else if (h > r.hi) lo = mid + 1;
-            else { info = r.asn; break; }
-        }
+        if (!D.n_dom4) return true;    // no IPv4 mappings: nothing holds it
+        const uint32_t sub = lct_find4(D.dom4_node, D.dom4_net, __builtin_bswap32(v));
+        if (sub != MFP_LCT_NIL) info = D.dom4_net[sub].val;
     } else if (d.ipv == 6 && D.n_dom6) {
         // is_private_address (ipv6_lctrie.h:255): the first byte in memory of
         // the host-order high half, i.e. address byte 7
         if ((d.hi & 0xff) == 0xfc || (d.hi & 0xff) == 0xfd) return false;
-        int lo = 0, hi = (int)D.n_dom6 - 1;
-        while (lo <= hi) {
-            const int mid = (lo + hi) >> 1;
-            const mfp_asn6 r = D.dom6[mid];
-            if (!le128(r.lo_hi, r.lo_lo, d.hi, d.lo)) hi = mid - 1;
-            else if (!le128(d.hi, d.lo, r.hi_hi, r.hi_lo)) lo = mid + 1;
-            else { info = r.asn; break; }
-        }
+        const uint32_t sub = lct_find6(D.dom6_node, D.dom6_net, d.hi, d.lo);
+        if (sub != MFP_LCT_NIL) info = D.dom6_net[sub].val;
     } else {
         return false;
     }
@@ -827,7 +776,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
         uint32_t hoff[NFEAT], hcnt[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) { hoff[f] = 0; hcnt[f] = 0; }
-        bool plain = false, ssh_ua = false;
+        bool plain = false, ssh_ua = false, stun_ua = false;
         // string features UA, domain, SNI (hoff/hcnt slots 3..5)
         const uint8_t *vs[3] = {nullptr, nullptr, nullptr};
         uint32_t vl[3] = {0, 0, 0}, voff[3] = {0, 0, 0};
@@ -880,8 +829,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             // the ALPN list); QUIC's is transport parameter 0x3129 (tls.h:1346-1355)
             // SSH (protocol + comment, the delimiting space dropped) is built and
             // probed by k_analyze_wave
+            // STUN's SOFTWARE goes through utf8_safe_string (stun.h:1024): the
+            // wave scorer escapes it into LDS (slow_lookups)
             ssh_ua = r.msg == MFP_MSG_SSH_INIT && r.ua_len != 0xffff;
-            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH || ssh_ua ? 0u : r.ua_len;
+            stun_ua = r.msg == MFP_MSG_STUN;
+            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH || ssh_ua || stun_ua ? 0u : r.ua_len;
             if (ul > 511) ul = 511;
             const uint8_t *up = sbase + r.ua_off;
             uint64_t uh = 0;
@@ -889,7 +841,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             const uint32_t dport = r.dst_port;
 
             // ---- the six feature lookups
-            n_look += 2u + (ipv != 0) + (!ssh_ua) + (plain ? 2u : 0u);
+            n_look += 2u + (ipv != 0) + (!ssh_ua && !stun_ua) + (plain ? 2u : 0u);
             Hit h;
             h = probe_feature_lane(D, entry, F_ASN, asn, nullptr, 0xffffffffu);
             hoff[0] = h.off; hcnt[0] = h.cnt;
@@ -914,7 +866,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             }
             // string features: candidate slots here, byte-exact check by the wave below
             vs[0] = up; vl[0] = ul; vk[0] = uh;
-            has[0] = !ssh_ua && cand_feature_lane(D, entry, F_UA, uh, ul, vh[0], voff[0]);
+            has[0] = !ssh_ua && !stun_ua && cand_feature_lane(D, entry, F_UA, uh, ul, vh[0], voff[0]);
             if (plain) {   // else k_analyze_wave normalises the name (wave, LDS)
                 vs[1] = sp + tld; vl[1] = sl - tld; vk[1] = lane_hash(sp + tld, sl - tld);
                 has[1] = cand_feature_lane(D, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
@@ -942,7 +894,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
         }
         // scored: to the lane scorer (small P, plain name) or the wave scorer;
         // not scored: the attributes go into the record now
-        const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain && !ssh_ua;
+        const bool lanep = scored && np <= PL && np <= P.lane_max_p && plain && !ssh_ua && !stun_ua;
         const bool defer = scored && !lanep;
         if (live && !scored && xattr) P.out[i].attr = (uint16_t)(P.out[i].attr | xattr);
         const uint64_t lm = __ballot(lanep), dm = __ballot(defer);
@@ -955,7 +907,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
         }
         if (defer) {
             WItem w;
-            w.i = (uint32_t)i; w.entry = entry; w.flags = (plain ? 0u : 1u) | (ssh_ua ? 2u : 0u) | (xattr << 16);
+            w.i = (uint32_t)i; w.entry = entry; w.flags = (plain ? 0u : 1u) | (ssh_ua ? 2u : 0u) | (stun_ua ? 4u : 0u) | (xattr << 16);
             w.ft = r.fp_type;
             w.po = E.proc_off; w.np = np; w.mdb = E.malware_db; w.dmz = E.generic_dmz;
 #pragma unroll
@@ -1091,8 +1043,10 @@ __global__ __launch_bounds__(64 * SW) void k_an_score(AParams P) {
 // (strncpy 256, NUL stops); the SSH user agent (ssh_init_packet::do_analysis
 // ssh.h:480-487): protocol then comment into a data_buffer<512> (nulled --
 // empty -- when they do not fit), strncpy 511, NUL stops.  The record's span
-// is "protocol SP comment"; its first space is the delimiter.  Updates
-// off/cnt of features 3 (UA), 4 (domain), 5 (SNI); returns the features changed.
+// is "protocol SP comment"; its first space is the delimiter.  The STUN
+// SOFTWARE value (flag 4) as utf8_safe_string<512> makes it (stun.h:1024,
+// mfpc::utf8_safe_512).  Updates off/cnt of features 3 (UA), 4 (domain), 5
+// (SNI); returns the features changed.
 ADEV uint32_t slow_lookups(const AParams &P, uint32_t i, uint32_t entry, uint32_t flags, char *nbuf, char *ub,
                            uint32_t (&off)[NFEAT], uint32_t (&cnt)[NFEAT], uint32_t lane) {
     const mfp_classifier_dev &D = P.D;
@@ -1118,12 +1072,14 @@ ADEV uint32_t slow_lookups(const AParams &P, uint32_t i, uint32_t entry, uint32_
         __builtin_amdgcn_wave_barrier();
         changed |= 3u << 4;
     }
-    if (flags & 2u) {
+    if (flags & 6u) {
         const mfp_record r = P.rec[i];
         const uint8_t *sp = P.arena + P.desc[i].offset + r.ua_off;
         const uint32_t L = r.ua_len;
         int ulen = 0;
-        if (lane == 0) {
+        if (lane == 0 && (flags & 4u)) {
+            ulen = L == 0xffff ? 0 : (int)mfpc::utf8_safe_512(sp, L, ub);
+        } else if (lane == 0) {
             uint32_t pl = 0;
             while (pl < L && sp[pl] != ' ') pl++;
             const uint32_t total = pl < L ? L - 1 : L;
@@ -1329,7 +1285,7 @@ __device__ __forceinline__ void wave_scorer_pipe(const AParams &P, char (*sni_bu
             PH_MARK(0);
             if (mine) {
                 // ---- [A] this packet's rows into LDS, the update lists applied
-                if (flags & 3u) {
+                if (flags & 7u) {
                     const uint32_t ch = slow_lookups(P, i, wf(wc, WI_ENTRY), flags, sni_buf[wid], ua_buf[wid], off, cnt, lane);
 #pragma unroll
                     for (uint32_t f = 3; f < NFEAT; f++)
@@ -1491,7 +1447,7 @@ __device__ __forceinline__ void wave_scorer_big(const AParams &P, char *nbuf, ch
         uint32_t off[NFEAT], cnt[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) { off[f] = wf(wc, WI_OFF + f); cnt[f] = wf(wc, WI_CNT + f); }
-        if (flags & 3u) slow_lookups(P, i, wf(wc, WI_ENTRY), flags, nbuf, ub, off, cnt, lane);
+        if (flags & 7u) slow_lookups(P, i, wf(wc, WI_ENTRY), flags, nbuf, ub, off, cnt, lane);
         w_prior += np;
         uint32_t anylong = 0;
 #pragma unroll
@@ -1654,7 +1610,7 @@ __global__ __launch_bounds__(64) void k_analyze_huge(AParams P) {
         uint32_t off[NFEAT], cnt[NFEAT];
 #pragma unroll
         for (uint32_t f = 0; f < NFEAT; f++) { off[f] = wf(wc, WI_OFF + f); cnt[f] = wf(wc, WI_CNT + f); }
-        if (flags & 3u) slow_lookups(P, i, wf(wc, WI_ENTRY), flags, nbuf, ub, off, cnt, lane);
+        if (flags & 7u) slow_lookups(P, i, wf(wc, WI_ENTRY), flags, nbuf, ub, off, cnt, lane);
         w_prior += np;
         for (uint32_t p = lane; p < np; p += 64) row[p] = D.prior[po + p];
         row_sync();

@@ -36,6 +36,7 @@
 #include "mfp_analysis.h"
 #include "mfp_common.hpp"
 #include "mfp_internal.h"
+#include "mfp_lctrie.hpp"
 
 namespace {
 
@@ -569,28 +570,28 @@ void process_fp_db_line(mfp_classifier_s &c, const std::string &line) {
     if (used) c.entries.push_back(std::move(e));
 }
 
-// pyasn.db line "a.b.c.d/len<ws>asn" (lct_subnet_set_from_string)
+// pyasn.db line: a '.' makes it IPv4 (analysis.h:896-905); parsed as
+// lct_subnet_set_from_string does (lctrie_bgp.hpp:23-98): sscanf with "%hhu"
+// octets (taken modulo 256) or an IPv6 text of at most 45 characters, a
+// length in 1..32 / 1..128 and an ASN -- anything else is skipped
 void process_asn_line(mfp_classifier_s &c, const std::string &line) {
-    size_t sl = line.find('/');
-    if (sl == std::string::npos) return;
-    std::string addr = line.substr(0, sl);
-    char *end = nullptr;
-    long len = strtol(line.c_str() + sl + 1, &end, 10);
-    while (end && (*end == ' ' || *end == '\t')) end++;
-    unsigned long asn = end ? strtoul(end, nullptr, 10) : 0;
-    if (addr.find('.') != std::string::npos) {
-        int pos = 0;
-        uint32_t v;
-        if (!mfpc::parse_ipv4((const uint8_t *)addr.data(), (int)addr.size(), pos, v) || len < 0 || len > 32) return;
-        uint32_t be = (v & 0xff) << 24 | (v >> 8 & 0xff) << 16 | (v >> 16 & 0xff) << 8 | (v >> 24);
-        uint32_t mask = len == 0 ? 0 : (0xffffffffu << (32 - len));
-        c.asn4.push_back({(uint64_t)(be & mask) << 8 | (uint64_t)len, (uint32_t)asn});
+    uint8_t len = 0;
+    unsigned asn = 0;
+    if (line.find('.') != std::string::npos) {
+        uint32_t addr = 0;
+        unsigned char *dq = (unsigned char *)&addr;   // host order, as the reference fills it
+        if (sscanf(line.c_str(), "%hhu.%hhu.%hhu.%hhu/%hhu\t%u", dq + 3, dq + 2, dq + 1, dq, &len, &asn) != 6) return;
+        if (len == 0 || len > 32) return;
+        c.asn4.push_back({(uint64_t)addr << 8 | (uint64_t)len, (uint32_t)asn});
     } else {
+        char a[46];
+        if (sscanf(line.c_str(), "%45[^/]/%hhu\t%u", a, &len, &asn) != 3) return;
+        if (len == 0 || len > 128) return;
         int pos = 0;
-        uint8_t a[16];
-        if (!mfpc::parse_ipv6((const uint8_t *)addr.data(), (int)addr.size(), pos, a) || len < 0 || len > 128) return;
-        for (int b = (int)len; b < 128; b++) a[b / 8] &= (uint8_t)~(0x80u >> (b % 8));
-        std::string k((const char *)a, 16);
+        uint8_t b[16];
+        const int al = (int)strlen(a);
+        if (!mfpc::parse_ipv6((const uint8_t *)a, al, pos, b) || pos != al) return;
+        std::string k((const char *)b, 16);   // masked when the trie is built (subnet_mask_v6)
         k.push_back((char)len);
         c.asn6.push_back({k, (uint32_t)asn});
     }
@@ -840,6 +841,224 @@ uint64_t pow2_at_least(uint64_t n) {
     return p;
 }
 
+
+// ---------------------------------------------------------------------------
+// the reference's LC-trie, built as it builds it (lctrie/lctrie.hpp,
+// lctrie_ip.hpp, ipv6_lctrie.h), for a W-bit key (32: IPv4 in a1's low word;
+// 128: IPv6 as (a0, a1) = (high, low) 64-bit halves, ip_address.hpp:775-814)
+// ---------------------------------------------------------------------------
+struct LNet {
+    uint64_t a0 = 0, a1 = 0;
+    uint8_t type = 0, len = 0;           // IP_BASE 0 / IP_PREFIX 1 / IP_PREFIX_FULL 2
+    uint32_t prefix = MFP_LCT_NIL;
+    uint32_t val = 0;
+};
+struct LTrie {
+    std::vector<mfp_lct_node> node;      // empty: no table (lookups find nothing)
+    std::vector<LNet> net;
+};
+
+template <int W> uint64_t l_ext(uint32_t pos, uint32_t num, const LNet &k) {
+    if constexpr (W == 32) return lct_ext4(pos, num, (uint32_t)k.a1);
+    else return lct_ext6(pos, num, k.a0, k.a1);
+}
+template <int W> uint64_t l_ext_idx(uint32_t pos, uint32_t num, const LNet &k) {
+    if constexpr (W == 32) return lct_ext4(pos, num, (uint32_t)k.a1);
+    else return lct_ext6_idx(pos, num, k.a0, k.a1);
+}
+// REMOVE (common.hpp:98-101, ipv6_lctrie.h:196-212)
+template <int W> LNet l_remove(uint32_t p, const LNet &k) {
+    LNet r;
+    if constexpr (W == 32) {
+        r.a1 = lct_shr32(lct_shl32((uint32_t)k.a1, p), p);
+    } else if (p < 64) {
+        r.a0 = lct_shr64(lct_shl64(k.a0, p), p); r.a1 = k.a1;
+    } else {
+        r.a1 = lct_shr64(lct_shl64(k.a1, p - 64), p - 64);
+    }
+    return r;
+}
+bool l_less(const LNet &x, const LNet &y) { return x.a0 != y.a0 ? x.a0 < y.a0 : x.a1 < y.a1; }
+
+// subnet_isprefix (lctrie_ip.hpp:427-434)
+template <int W> bool l_isprefix(const LNet &s, const LNet &t) {
+    return s.len == 0 || (s.len <= t.len && l_ext<W>(0, s.len, s) == l_ext<W>(0, s.len, t));
+}
+
+// compute_skip (lctrie.hpp:87-109)
+template <int W> uint8_t l_skip(const LTrie &T, const std::vector<uint32_t> &bases, uint32_t prefix, uint32_t first,
+                                uint32_t num, uint32_t *newprefix) {
+    if (prefix == 0 && first == 0) return 0;
+    const LNet lo = l_remove<W>(prefix, T.net[bases[first]]), hi = l_remove<W>(prefix, T.net[bases[first + num - 1]]);
+    uint32_t i = prefix;
+    while (i < 2u * W && l_ext<W>(i, 1, lo) == l_ext<W>(i, 1, hi)) i++;
+    *newprefix = i;
+    return (uint8_t)(*newprefix - prefix);
+}
+
+// compute_branch (lctrie.hpp:111-159); FILLFACT 50, ROOT_BRANCH 16
+template <int W> uint8_t l_branch(const LTrie &T, const std::vector<uint32_t> &bases, uint32_t prefix, uint32_t first,
+                                  uint32_t num, uint32_t newprefix) {
+    if (num == 2) return 1;
+    if (prefix == 0 && first == 0) return 16;
+    size_t bits = 1, count = 0;
+    do {
+        bits++;
+        if (num < ((50u * (1u << bits)) / 100u) || (newprefix + bits) > (size_t)W) break;
+        size_t i = first;
+        count = 0;
+        const uint64_t maxpat = (uint64_t)1 << bits;
+        for (uint64_t pat = 0; pat < maxpat; pat++) {
+            bool found = false;
+            while (i < first + num && pat == l_ext<W>(newprefix, (uint32_t)bits, T.net[bases[i]])) { i++; found = true; }
+            if (found) count++;
+        }
+    } while (count >= ((50u * (1u << bits)) / 100u));
+    return (uint8_t)(bits - 1);
+}
+
+// build_inner (lctrie.hpp:161-248); node indices grow as the reference's do
+template <int W> void l_build_inner(LTrie &T, const std::vector<uint32_t> &bases, uint32_t &ncount, uint32_t prefix,
+                                    uint32_t first, uint32_t num, uint32_t pos) {
+    if (T.node.size() < (size_t)ncount) T.node.resize(ncount);
+    mfp_lct_node &nd0 = T.node[pos];
+    if (num == 1) {
+        nd0.branch = 0; nd0.skip = 0; nd0.index = first;
+        return;
+    }
+    uint32_t newprefix = 0;
+    const uint8_t skip = l_skip<W>(T, bases, prefix, first, num, &newprefix);
+    const uint8_t branch = l_branch<W>(T, bases, prefix, first, num, newprefix);
+    const uint32_t idx = ncount;
+    T.node[pos].skip = skip; T.node[pos].branch = branch; T.node[pos].index = idx;
+    ncount += 1u << branch;
+    T.node.resize(ncount);
+    // an empty slot's pattern compared through the 32-bit EXTRACT overload
+    // (common.hpp:86): the uint64_t bit pattern does not convert to
+    // ipv6_addr_lct (explicit constructor), so IPv6 builds take it too
+    auto slot_bits = [&](uint64_t bitpat, uint32_t n) -> uint64_t {
+        return lct_ext4((uint32_t)W - branch, n, (uint32_t)bitpat);
+    };
+    auto chain_match = [&](uint32_t base, uint64_t bitpat) -> uint32_t {
+        uint32_t prep = T.net[base].prefix;
+        while (prep != MFP_LCT_NIL) {
+            const uint32_t len = T.net[prep].len;
+            if (len > newprefix && l_ext_idx<W>(newprefix, len - newprefix, T.net[base]) == slot_bits(bitpat, len - newprefix))
+                return len;
+            prep = T.net[prep].prefix;
+        }
+        return 0;
+    };
+    size_t p = first;
+    for (uint64_t bitpat = 0; bitpat < ((uint64_t)1 << branch); ++bitpat) {
+        size_t k = 0;
+        while (p + k < first + num && l_ext_idx<W>(newprefix, branch, T.net[bases[p + k]]) == bitpat) ++k;
+        if (k == 0) {
+            const uint32_t match1 = p > first ? chain_match(bases[p - 1], bitpat) : 0;
+            const uint32_t match2 = p < first + num ? chain_match(bases[p], bitpat) : 0;
+            if ((match1 > match2 && p > first) || p == first + num)
+                l_build_inner<W>(T, bases, ncount, newprefix + branch, (uint32_t)p - 1, 1, idx + (uint32_t)bitpat);
+            else
+                l_build_inner<W>(T, bases, ncount, newprefix + branch, (uint32_t)p, 1, idx + (uint32_t)bitpat);
+        } else if (k == 1 && (uint32_t)(T.net[bases[p]].len - newprefix) < (uint32_t)branch) {
+            const size_t bits = branch - T.net[bases[p]].len + newprefix;
+            for (uint32_t i = (uint32_t)bitpat; i < bitpat + (1u << bits); i++)
+                l_build_inner<W>(T, bases, ncount, newprefix + branch, (uint32_t)p, 1, idx + i);
+            bitpat = bitpat + (1u << bits) - 1;
+        } else {
+            l_build_inner<W>(T, bases, ncount, newprefix + branch, (uint32_t)p, (uint32_t)k, idx + (uint32_t)bitpat);
+        }
+        p += k;
+    }
+}
+
+// subnet_data::process_final / process_final_v6 / process_domain_mappings_final[_v6]
+// (addr.cc:460-705) over (address, length, value) entries in file order:
+// subnet_mask_v4/_v6, qsort by (address, length) -- glibc's qsort is a stable
+// merge sort here -- subnet_dedup kept literally (of two adjacent equal
+// prefixes the first stays and the loop steps past the survivor), subnet_prefix
+// with its UINT64_MAX size cap, the full-prefix check that abandons the table,
+// then lct_build
+template <int W> LTrie l_build(std::vector<LNet> v) {
+    LTrie T;
+    if (v.empty()) return T;
+    for (auto &s : v) {
+        if constexpr (W == 32) {
+            const uint32_t mask = s.len >= 32 ? 0xffffffffu : ~(0xffffffffu >> s.len);
+            s.a1 = (uint32_t)s.a1 & mask;
+        } else {
+            const u128 a = (u128)s.a0 << 64 | s.a1;
+            const u128 mask = s.len >= 128 ? ~(u128)0 : ~(~(u128)0 >> s.len);
+            s.a0 = (uint64_t)((a & mask) >> 64); s.a1 = (uint64_t)(a & mask);
+        }
+    }
+    std::stable_sort(v.begin(), v.end(), [](const LNet &x, const LNet &y) {
+        if (l_less(x, y)) return true;
+        if (l_less(y, x)) return false;
+        return x.len < y.len;
+    });
+    size_t size = v.size();
+    for (size_t i = 0, j = 1; j < size; ++i, ++j)
+        if (v[i].a0 == v[j].a0 && v[i].a1 == v[j].a1 && v[i].len == v[j].len) {
+            v.erase(v.begin() + (long)j);
+            --size;
+        }
+    // subnet_prefix (lctrie_ip.hpp:440-585)
+    const size_t n = v.size();
+    std::vector<uint64_t> sz(n), used(n, 0);
+    for (size_t i = 0; i < n; ++i) v[i].prefix = MFP_LCT_NIL;
+    for (size_t i = 0; i < n; ++i) {
+        const size_t j = i + 1;
+        if (j < n && l_isprefix<W>(v[i], v[j])) {
+            v[j].prefix = (uint32_t)i;
+            for (size_t k = j + 1; k < n && l_isprefix<W>(v[i], v[k]); ++k) v[k].prefix = (uint32_t)i;
+            v[i].type = 1;
+        } else {
+            v[i].type = 0;
+        }
+        const unsigned host_bits = W - v[i].len;
+        sz[i] = host_bits >= 64 ? UINT64_MAX : (uint64_t)1 << host_bits;
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (v[i].prefix != MFP_LCT_NIL) used[v[i].prefix] += sz[i];
+    for (size_t i = 0; i < n; ++i)
+        if (used[i] == sz[i]) v[i].type = 2;
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t pr = v[i].prefix;
+        if (pr != MFP_LCT_NIL && v[pr].type == 2) v[i].prefix = v[pr].prefix;
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (v[i].prefix != MFP_LCT_NIL && v[v[i].prefix].type == 2) return T;   // the reference returns unbuilt
+    // lct_build (lctrie.hpp:262-319)
+    std::vector<uint32_t> bases;
+    for (size_t i = 0; i < n; ++i)
+        if (v[i].type == 0) bases.push_back((uint32_t)i);
+    if (bases.empty()) return T;
+    T.net = std::move(v);
+    T.node.assign(1, mfp_lct_node{0, 0, 0, 0});
+    uint32_t ncount = 1;
+    l_build_inner<W>(T, bases, ncount, 0, 0, (uint32_t)bases.size(), 0);
+    T.node.resize(ncount);
+    for (auto &nd : T.node)
+        if (nd.branch == 0) nd.index = bases[nd.index];   // leaves hold the net index
+    return T;
+}
+
+LNet lnet4(uint32_t addr_host, int len, uint32_t val) { LNet s; s.a1 = addr_host; s.len = (uint8_t)len; s.val = val; return s; }
+LNet lnet6(u128 addr, int len, uint32_t val) {
+    LNet s; s.a0 = (uint64_t)(addr >> 64); s.a1 = (uint64_t)addr; s.len = (uint8_t)len; s.val = val; return s;
+}
+std::vector<mfp_lct_net4> dev_nets4(const LTrie &T) {
+    std::vector<mfp_lct_net4> o;
+    for (auto &s : T.net) o.push_back(mfp_lct_net4{(uint32_t)s.a1, s.prefix, s.val, s.len});
+    return o;
+}
+std::vector<mfp_lct_net6> dev_nets6(const LTrie &T) {
+    std::vector<mfp_lct_net6> o;
+    for (auto &s : T.net) o.push_back(mfp_lct_net6{s.a0, s.a1, s.prefix, s.val, s.len, 0});
+    return o;
+}
+
 struct HostTables {
     std::vector<mfp_fp_slot> fp_slots;
     std::vector<mfp_entry> entry;
@@ -851,77 +1070,15 @@ struct HostTables {
     std::vector<mfp_update> upd;
     std::vector<char> pool;
     std::vector<mfp_fp_slot> prev_slots;   // known prevalence set
-    std::vector<mfp_asn4> asn4;
-    std::vector<mfp_asn6> asn6;
+    LTrie asn4, asn6;                    // pyasn.db (subnet_data's ipv4/ipv6_subnet_trie)
     // additional attributes
     std::vector<mfp_fp_slot> doh_names, dom_slots;
     std::vector<uint32_t> doh_v4;
     std::vector<uint64_t> doh_v6;
-    std::vector<mfp_asn4> dom4;
-    std::vector<mfp_asn6> dom6;
+    LTrie dom4, dom6;                    // domain-mappings.db (ipv4/ipv6_domain_trie)
     std::vector<uint32_t> dom_info;
     std::vector<uint8_t> dom_bytes;
 };
-
-// a prefix for the longest-match sweep: [lo, hi], its value, its length
-struct Pfx { u128 lo, hi; uint32_t val; int len; };
-struct Iv { u128 lo, hi; uint32_t val; };
-
-// lctrie preparation (addr.cc:460-518 / 584-705): masked prefixes sorted by
-// (address, length) -- glibc's qsort is a stable merge sort -- then
-// subnet_dedup (lctrie_ip.hpp:383-420), kept literally: of two adjacent equal
-// prefixes the first stays, and the loop steps past the survivor, so a third
-// copy is compared with the one after it
-void sort_dedup(std::vector<Pfx> &v) {
-    std::stable_sort(v.begin(), v.end(), [](const Pfx &a, const Pfx &b) { return a.lo != b.lo ? a.lo < b.lo : a.len < b.len; });
-    size_t size = v.size();
-    for (size_t i = 0, j = 1; j < size; ++i, ++j)
-        if (v[i].lo == v[j].lo && v[i].len == v[j].len) {
-            v.erase(v.begin() + (long)j);
-            --size;
-        }
-}
-
-// lct_find (lctrie.hpp:348) as disjoint intervals: the prefixes are nested
-// or disjoint, so one sweep in (start, length) order with a stack of open
-// prefixes gives every address range its innermost (longest) prefix
-std::vector<Iv> lpm_intervals(const std::vector<Pfx> &ps) {
-    std::vector<Iv> out;
-    std::vector<Pfx> st;
-    u128 cursor = 0;
-    bool wrapped = false;   // the cursor passed the top of the space
-    auto emit = [&](u128 lo, u128 hi, uint32_t v) { if (!wrapped && lo <= hi) out.push_back(Iv{lo, hi, v}); };
-    auto close_top = [&]() {
-        const Pfx b = st.back();
-        emit(std::max(cursor, b.lo), b.hi, b.val);
-        if (b.hi == ~(u128)0) wrapped = true;
-        else cursor = std::max(cursor, b.hi + 1);
-        st.pop_back();
-    };
-    for (auto &p : ps) {
-        while (!st.empty() && st.back().hi < p.lo) close_top();
-        if (!st.empty() && p.lo > 0) emit(std::max(cursor, st.back().lo), p.lo - 1, st.back().val);
-        cursor = std::max(cursor, p.lo);
-        st.push_back(p);
-    }
-    while (!st.empty()) close_top();
-    return out;
-}
-
-Pfx pfx(u128 addr, int len, int bits, uint32_t val) {
-    const u128 span = len == 0 ? (bits == 128 ? ~(u128)0 : (((u128)1 << bits) - 1)) : (((u128)1 << (bits - len)) - 1);
-    const u128 lo = addr & ~span;
-    return Pfx{lo, lo + span, val, len};
-}
-
-mfp_asn4 iv4(const Iv &v) { mfp_asn4 r; r.lo = (uint32_t)v.lo; r.hi = (uint32_t)v.hi; r.asn = v.val; r.pad = 0; return r; }
-mfp_asn6 iv6(const Iv &v) {
-    mfp_asn6 r;
-    r.lo_hi = (uint64_t)(v.lo >> 64); r.lo_lo = (uint64_t)v.lo;
-    r.hi_hi = (uint64_t)(v.hi >> 64); r.hi_lo = (uint64_t)v.hi;
-    r.asn = v.val; r.pad = 0;
-    return r;
-}
 
 uint32_t pool_add(HostTables &t, const std::string &s) {
     uint32_t off = (uint32_t)t.pool.size();
@@ -942,7 +1099,43 @@ void insert_string_slot(std::vector<mfp_fp_slot> &slots, uint64_t h, uint32_t id
 
 }  // namespace
 
-static mfp_asn4 mk4(uint32_t lo, uint32_t hi, uint32_t asn) { mfp_asn4 r; r.lo = lo; r.hi = hi; r.asn = asn; r.pad = 0; return r; }
+
+namespace {
+
+// the four LC-tries of subnet_data (addr.cc:460-705): pyasn.db IPv4 / IPv6
+// (subnet_data::get_asn_info addr.cc:172-208) and the domain mappings
+// (is_domain_faking addr.cc:707-792; a subnet's value = 1 + its dom_info index)
+void build_tries(const mfp_classifier_s &cs, HostTables &t) {
+    const mfp_classifier_s *c = &cs;
+    {
+        std::vector<LNet> v;
+        for (auto &p : c->asn4) v.push_back(lnet4((uint32_t)(p.first >> 8), (int)(p.first & 0xff), p.second));
+        t.asn4 = l_build<32>(std::move(v));
+        v.clear();
+        for (auto &p : c->asn6) {
+            u128 a = 0;
+            for (int k = 0; k < 16; k++) a = a << 8 | (uint8_t)p.first[k];
+            v.push_back(lnet6(a, (uint8_t)p.first[16], p.second));
+        }
+        t.asn6 = l_build<128>(std::move(v));
+    }
+    for (int fam = 0; fam < 2; fam++) {
+        const std::vector<DomPrefix> &src = fam == 0 ? c->dom4 : c->dom6;
+        std::vector<LNet> v;
+        for (size_t k = 0; k < src.size(); k++)
+            v.push_back(fam == 0 ? lnet4((uint32_t)src[k].addr, src[k].len, (uint32_t)k) : lnet6(src[k].addr, src[k].len, (uint32_t)k));
+        LTrie T = fam == 0 ? l_build<32>(std::move(v)) : l_build<128>(std::move(v));
+        for (auto &s : T.net) {   // value: 1 + the subnet's dom_info index
+            const DomPrefix &dp = src[s.val];
+            s.val = (uint32_t)t.dom_info.size() / 2 + 1;
+            t.dom_info.push_back(dp.type | (uint32_t)dp.idx.size() << 8);
+            t.dom_info.push_back((uint32_t)t.dom_bytes.size());
+            t.dom_bytes.insert(t.dom_bytes.end(), dp.idx.begin(), dp.idx.end());
+        }
+        (fam == 0 ? t.dom4 : t.dom6) = std::move(T);
+    }
+}
+}  // namespace
 
 int mfp_classifier_upload(mfp_classifier *c, int device) {
     HostTables t;
@@ -1010,22 +1203,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
                 put_feat(eid, k, mfpc::str_hash((const uint8_t *)kv.first.data(), 16), kv.second, &kv.first);
         }
     }
-    // ASN (subnet_data::get_asn_info addr.cc:172-208): longest-prefix match
-    // over the deduplicated prefixes, as disjoint intervals
-    {
-        std::vector<Pfx> ps;
-        for (auto &p : c->asn4) ps.push_back(pfx((u128)(p.first >> 8), (int)(p.first & 0xff), 32, p.second));
-        sort_dedup(ps);
-        for (auto &v : lpm_intervals(ps)) t.asn4.push_back(iv4(v));
-        ps.clear();
-        for (auto &p : c->asn6) {
-            u128 lo = 0;
-            for (int k = 0; k < 16; k++) lo = lo << 8 | (uint8_t)p.first[k];
-            ps.push_back(pfx(lo, (uint8_t)p.first[16], 128, p.second));
-        }
-        sort_dedup(ps);
-        for (auto &v : lpm_intervals(ps)) t.asn6.push_back(iv6(v));
-    }
+    build_tries(*c, t);
     // encrypted_dns watchlist: names (hash table), addresses (sorted sets)
     t.doh_names.assign(pow2_at_least(2 * c->doh_names.size() + 2), mfp_fp_slot{0, 0xffffffffu, 0, 0});
     for (auto &nm : c->doh_names)
@@ -1047,45 +1225,23 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     for (auto &kv : c->dom_idx)
         insert_string_slot(t.dom_slots, mfpc::str_hash((const uint8_t *)kv.first.data(), (uint32_t)kv.first.size()),
                            kv.second, pool_add(t, kv.first), (uint32_t)kv.first.size());
-    for (int fam = 0; fam < 2; fam++) {
-        const std::vector<DomPrefix> &src = fam == 0 ? c->dom4 : c->dom6;
-        std::vector<Pfx> ps;
-        for (size_t k = 0; k < src.size(); k++) ps.push_back(pfx(src[k].addr, src[k].len, fam == 0 ? 32 : 128, (uint32_t)k));
-        sort_dedup(ps);
-        for (auto &v : lpm_intervals(ps)) {
-            const DomPrefix &dp = src[v.val];
-            const uint32_t info = (uint32_t)t.dom_info.size() / 2;
-            t.dom_info.push_back(dp.type | (uint32_t)dp.idx.size() << 8);
-            t.dom_info.push_back((uint32_t)t.dom_bytes.size());
-            t.dom_bytes.insert(t.dom_bytes.end(), dp.idx.begin(), dp.idx.end());
-            Iv w = v;
-            w.val = info + 1;
-            if (fam == 0) t.dom4.push_back(iv4(w)); else t.dom6.push_back(iv6(w));
-        }
-    }
     if (t.pool.empty()) t.pool.push_back(0);
     if (t.upd.empty()) t.upd.push_back(mfp_update{0, 0, 0});
     if (t.prior.empty()) { t.prior.push_back(0); t.proc_id.push_back(0); t.proc_mal.push_back(0); t.proc_attr.push_back(0); }
     if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0, 0, {0, 0, 0}});
-    if (t.asn4.empty()) t.asn4.push_back(mk4(1, 0, 0));
-    if (t.asn6.empty()) { mfp_asn6 r{}; r.lo_lo = 1; t.asn6.push_back(r); }
     if (t.doh_v4.empty()) t.doh_v4.push_back(0);
     if (t.doh_v6.empty()) { t.doh_v6.push_back(0); t.doh_v6.push_back(0); }
-    if (t.dom4.empty()) t.dom4.push_back(mk4(1, 0, 0));
-    if (t.dom6.empty()) { mfp_asn6 r{}; r.lo_lo = 1; t.dom6.push_back(r); }
     if (t.dom_info.empty()) { t.dom_info.push_back(0); t.dom_info.push_back(0); }
     if (t.dom_bytes.empty()) t.dom_bytes.push_back(0);
 
-    // ASN bucket index: bucket[b] = first interval whose end reaches b << 16;
-    // the interval holding an address of bucket b lies in [bucket[b], bucket[b + 1]]
-    std::vector<uint32_t> asn4_bucket(65537);
-    {
-        size_t i = 0;
-        for (uint64_t b = 0; b <= 65536; b++) {
-            while (i < t.asn4.size() && (uint64_t)t.asn4[i].hi < (b << 16)) i++;
-            asn4_bucket[b] = (uint32_t)i;
-        }
-    }
+    // device copies of the tries (a table the reference leaves unbuilt gets
+    // one placeholder node and no lookups: n_* = 0)
+    auto nodes = [](const LTrie &T) { return T.node.empty() ? std::vector<mfp_lct_node>(1, mfp_lct_node{0, 0, 0, 0}) : T.node; };
+    auto nets4 = [](const LTrie &T) { return T.net.empty() ? std::vector<mfp_lct_net4>(1, mfp_lct_net4{0, 0, 0, 0}) : dev_nets4(T); };
+    auto nets6 = [](const LTrie &T) { return T.net.empty() ? std::vector<mfp_lct_net6>(1, mfp_lct_net6{0, 0, 0, 0, 0, 0}) : dev_nets6(T); };
+    const auto asn4_node = nodes(t.asn4), asn6_node = nodes(t.asn6), dom4_node = nodes(t.dom4), dom6_node = nodes(t.dom6);
+    const auto asn4_net = nets4(t.asn4), dom4_net = nets4(t.dom4);
+    const auto asn6_net = nets6(t.asn6), dom6_net = nets6(t.dom6);
     mfp_classifier_dev &d = c->dev;
     mfp_classifier_free_device(d);
     if (hipSetDevice(device) != hipSuccess) return -1;
@@ -1098,23 +1254,25 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     bool ok = up(d.fp_slots, t.fp_slots) && up(d.prev_slots, t.prev_slots) && up(d.entry, t.entry) &&
               up(d.prior, t.prior) && up(d.proc_id, t.proc_id) && up(d.proc_mal, t.proc_mal) &&
               up(d.proc_attr, t.proc_attr) && up(d.feat_slots, t.feat_slots) && up(d.upd, t.upd) && up(d.pool, t.pool) &&
-              up(d.asn4, t.asn4) && up(d.asn4_bucket, asn4_bucket) && up(d.asn6, t.asn6) && up(d.doh_names, t.doh_names) &&
+              up(d.asn4_node, asn4_node) && up(d.asn4_net, asn4_net) && up(d.asn6_node, asn6_node) &&
+              up(d.asn6_net, asn6_net) && up(d.doh_names, t.doh_names) &&
               up(d.doh_v4, t.doh_v4) && up(d.doh_v6, t.doh_v6) && up(d.dom_slots, t.dom_slots) &&
-              up(d.dom4, t.dom4) && up(d.dom6, t.dom6) && up(d.dom_info, t.dom_info) && up(d.dom_bytes, t.dom_bytes);
+              up(d.dom4_node, dom4_node) && up(d.dom4_net, dom4_net) && up(d.dom6_node, dom6_node) &&
+              up(d.dom6_net, dom6_net) && up(d.dom_info, t.dom_info) && up(d.dom_bytes, t.dom_bytes);
     if (!ok) { mfp_set_error("classifier device upload failed"); return -2; }
     {
         auto nb = [](const auto &v) { return (uint64_t)(v.size() * sizeof(v[0])); };
         c->device_bytes = nb(t.fp_slots) + nb(t.prev_slots) + nb(t.entry) + nb(t.prior) + nb(t.proc_id) +
-                          nb(t.proc_mal) + nb(t.proc_attr) + nb(t.feat_slots) + nb(t.upd) + nb(t.pool) + nb(t.asn4) +
-                          nb(asn4_bucket) +
-                          nb(t.asn6) + nb(t.doh_names) + nb(t.doh_v4) + nb(t.doh_v6) + nb(t.dom_slots) + nb(t.dom4) +
-                          nb(t.dom6) + nb(t.dom_info) + nb(t.dom_bytes);
+                          nb(t.proc_mal) + nb(t.proc_attr) + nb(t.feat_slots) + nb(t.upd) + nb(t.pool) + nb(asn4_node) +
+                          nb(asn4_net) + nb(asn6_node) + nb(asn6_net) + nb(t.doh_names) + nb(t.doh_v4) + nb(t.doh_v6) +
+                          nb(t.dom_slots) + nb(dom4_node) + nb(dom4_net) + nb(dom6_node) + nb(dom6_net) +
+                          nb(t.dom_info) + nb(t.dom_bytes);
     }
     d.fp_mask = t.fp_slots.size() - 1;
     d.prev_mask = t.prev_slots.size() - 1;
     d.feat_mask = t.feat_slots.size() - 1;
-    d.n_asn4 = (uint32_t)t.asn4.size();
-    d.n_asn6 = c->asn6.empty() ? 0 : (uint32_t)t.asn6.size();
+    d.n_asn4 = (uint32_t)t.asn4.node.size();
+    d.n_asn6 = (uint32_t)t.asn6.node.size();
     const char *rnd[3] = {"tls/randomized", "tls/1/randomized", "tls/2/randomized"};
     for (int k = 0; k < 3; k++) {
         auto it = c->fpdb.find(rnd[k]);
@@ -1136,15 +1294,89 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     d.n_doh_v6 = (uint32_t)(c->doh_v6.empty() ? 0 : t.doh_v6.size() / 2);
     d.faking_enabled = c->faking_enabled;
     d.dom_mask = t.dom_slots.size() - 1;
-    d.n_dom4 = (uint32_t)t.dom4.size();
-    d.n_dom6 = c->dom6.empty() ? 0 : (uint32_t)t.dom6.size();
+    d.n_dom4 = (uint32_t)t.dom4.node.size();
+    d.n_dom6 = (uint32_t)t.dom6.node.size();
     return 0;
+}
+
+// Test hook (CPU): the four subnet tries built exactly as the device gets
+// them and queried on the host with the device's lookup (mfp_lctrie.hpp),
+// for subnet_data::get_asn_info and is_domain_faking (addr.cc:172-208,
+// 707-792).  queries: "dst_ip<TAB>server_name" lines (no name: no faking
+// check); returns the number of queries answered, -1 on a load error.
+extern "C" MFP_EXPORT long long mfp_lpm_query(const char *resources, const char *queries, uint32_t *asn, int8_t *fake,
+                                              size_t cap) {
+    mfp_classifier *c = mfp_classifier_load(resources);
+    if (!c) return -1;
+    HostTables t;
+    build_tries(*c, t);
+    auto find4 = [](const LTrie &T, uint32_t k) -> const LNet * {
+        if (T.node.empty()) return nullptr;
+        const std::vector<mfp_lct_net4> nets = dev_nets4(T);
+        const uint32_t s = lct_find4(T.node.data(), nets.data(), k);
+        return s == MFP_LCT_NIL ? nullptr : &T.net[s];
+    };
+    auto find6 = [](const LTrie &T, uint64_t k0, uint64_t k1) -> const LNet * {
+        if (T.node.empty()) return nullptr;
+        const std::vector<mfp_lct_net6> nets = dev_nets6(T);
+        const uint32_t s = lct_find6(T.node.data(), nets.data(), k0, k1);
+        return s == MFP_LCT_NIL ? nullptr : &T.net[s];
+    };
+    auto dom_match = [&](const LNet *sub, uint32_t didx) -> bool {   // false: not faking
+        if (!sub) return true;
+        const uint32_t ty = t.dom_info[2 * (sub->val - 1)], off = t.dom_info[2 * (sub->val - 1) + 1];
+        if ((ty & 0xff) == MFP_DOM_EXCEPTION) return false;
+        for (uint32_t k = 0; k < (ty >> 8); k++)
+            if ((uint32_t)t.dom_bytes[off + k] == didx) return false;
+        return true;
+    };
+    long long n = 0;
+    const char *q = queries;
+    while (*q && (size_t)n < cap) {
+        const char *e = strchr(q, '\n');
+        std::string line = e ? std::string(q, e - q) : std::string(q);
+        q = e ? e + 1 : q + line.size();
+        const size_t tab = line.find('\t');
+        const std::string ip = line.substr(0, tab), name = tab == std::string::npos ? "" : line.substr(tab + 1);
+        uint8_t d[4];
+        const bool v4 = sscanf(ip.c_str(), "%hhu.%hhu.%hhu.%hhu", d, d + 1, d + 2, d + 3) == 4;
+        const uint32_t k4 = (uint32_t)d[0] << 24 | (uint32_t)d[1] << 16 | (uint32_t)d[2] << 8 | d[3];
+        uint64_t k0 = 0, k1 = 0;
+        bool v6 = false;
+        if (!v4) {
+            uint8_t b[16];
+            int pos = 0;
+            v6 = mfpc::parse_ipv6((const uint8_t *)ip.data(), (int)ip.size(), pos, b) && pos == (int)ip.size();
+            for (int k = 0; k < 8; k++) { k0 = k0 << 8 | b[k]; k1 = k1 << 8 | b[8 + k]; }
+        }
+        const LNet *a = v4 ? find4(t.asn4, k4) : v6 ? find6(t.asn6, k0, k1) : nullptr;
+        asn[n] = a ? a->val : 0;
+        int8_t f = 0;
+        if (!name.empty()) {
+            const std::string nm = name.compare(0, 4, "www.") == 0 ? name.substr(4) : name;
+            auto it = c->dom_idx.find(nm);
+            if (it != c->dom_idx.end()) {
+                if (v4) {
+                    const bool priv = d[0] == 10 || (d[0] == 172 && (d[1] & 0xf0) == 16) || (d[0] == 192 && d[1] == 168);
+                    f = !priv && dom_match(find4(t.dom4, k4), it->second);
+                } else if (v6 && !t.dom6.node.empty()) {
+                    const uint8_t b7 = (uint8_t)k0;   // is_private_address: the first byte in memory of a[0]
+                    f = !(b7 == 0xfc || b7 == 0xfd) && dom_match(find6(t.dom6, k0, k1), it->second);
+                }
+            }
+        }
+        fake[n] = f;
+        n++;
+    }
+    mfp_classifier_free(c);
+    return n;
 }
 
 void mfp_classifier_free_device(mfp_classifier_dev &d) {
     void *ptrs[] = {d.fp_slots, d.prev_slots, d.entry, d.prior, d.proc_id, d.proc_mal, d.proc_attr,
-                    d.feat_slots, d.upd, d.pool, d.asn4, d.asn4_bucket, d.asn6, d.doh_names, d.doh_v4, d.doh_v6,
-                    d.dom_slots, d.dom4, d.dom6, d.dom_info, d.dom_bytes};
+                    d.feat_slots, d.upd, d.pool, d.asn4_node, d.asn4_net, d.asn6_node, d.asn6_net, d.doh_names,
+                    d.doh_v4, d.doh_v6, d.dom_slots, d.dom4_node, d.dom4_net, d.dom6_node, d.dom6_net, d.dom_info,
+                    d.dom_bytes};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = mfp_classifier_dev{};
 }

@@ -50,6 +50,87 @@ MFP_HD uint64_t feat_slot_hash(uint32_t entry, uint32_t kind, uint64_t key) {
 enum FeatureKind : uint32_t { F_ASN = 0, F_PORT = 1, F_IPV4 = 2, F_IPV6 = 3, F_UA = 4, F_DOMAIN = 5, F_SNI = 6 };
 
 // ---------------------------------------------------------------------------
+// utf8_safe_string<512> (utf8.hpp:1059-1088) as stun::message::do_analysis
+// hands the SOFTWARE value to the classifier (stun.h:1021-1036): the text of
+// utf8_string::write (utf8.hpp:200-340: JSON escapes, \uXXXX for control
+// characters and every non-ASCII codepoint, surrogate pairs above U+FFFF) in a
+// 512-byte output_buffer, then strncpy 511.  The buffer's datum is null --
+// the user agent empty -- when the input is not valid UTF-8 (write returns
+// false) or the text does not fit: append_putc keeps one byte for the NUL
+// (buffer_stream.h:134-157) and the four hex digits go through append_memcpy,
+// whose bound is strict (doff < dlen - 1 - 4, buffer_stream.h:159-176).
+// Writes at most 511 bytes to out; returns the length (0: empty).
+// ---------------------------------------------------------------------------
+MFP_HD uint32_t utf8_safe_512(const uint8_t *x, uint32_t len, char *out) {
+    const char hex[] = "0123456789abcdef";
+    uint32_t k = 0;
+    bool ok = true;
+    auto putc = [&](char c) { if (k < 511) out[k++] = c; else ok = false; };
+    auto cp4 = [&](uint32_t c) {
+        putc('\\'); putc('u');
+        if (ok && k < 507) {
+            out[k] = hex[(c >> 12) & 15]; out[k + 1] = hex[(c >> 8) & 15];
+            out[k + 2] = hex[(c >> 4) & 15]; out[k + 3] = hex[c & 15];
+            k += 4;
+        } else {
+            ok = false;
+        }
+    };
+    auto cont = [](uint32_t b) { return (b & 0xc0) == 0x80; };
+    uint32_t j = 0;
+    while (j < len && ok) {
+        const uint32_t b0 = x[j];
+        if (b0 >= 0x80) {
+            if (b0 < 0xc2) return 0;                         // invalid lead byte
+            uint32_t cp = 0, n = 0;
+            if (b0 >= 0xf0 && b0 <= 0xf4) n = 4;
+            else if (b0 >= 0xe0 && b0 <= 0xef) n = 3;
+            else if (b0 < 0xe0) n = 2;
+            else return 0;                                   // 0xf5..0xff
+            if (len - j < n) return 0;                       // sequence too short
+            const uint32_t b1 = x[j + 1];
+            bool second;                                     // is_second_byte_valid (RFC 3629)
+            switch (b0) {
+            case 0xe0: second = b1 >= 0xa0 && b1 <= 0xbf; break;
+            case 0xed: second = b1 >= 0x80 && b1 <= 0x9f; break;
+            case 0xf0: second = b1 >= 0x90 && b1 <= 0xbf; break;
+            case 0xf4: second = b1 >= 0x80 && b1 <= 0x8f; break;
+            default: second = cont(b1);
+            }
+            if (!second) return 0;
+            if (n == 2) cp = ((b0 & 0x1f) << 6) | (b1 & 0x3f);
+            else if (n == 3) {
+                if (!cont(x[j + 2])) return 0;
+                cp = ((b0 & 0x0f) << 12) | ((b1 & 0x3f) << 6) | (x[j + 2] & 0x3f);
+            } else {
+                if (!cont(x[j + 2]) || !cont(x[j + 3])) return 0;
+                cp = ((b0 & 0x07) << 18) | ((b1 & 0x3f) << 12) | ((uint32_t)(x[j + 2] & 0x3f) << 6) | (x[j + 3] & 0x3f);
+            }
+            if (cp == 0) return 0;
+            if ((cp >= 0xe000 && cp <= 0xf8ff) || (cp >= 0xf0000 && cp <= 0xffffd) || (cp >= 0x100000 && cp <= 0x10fffd) ||
+                (cp >= 0xd800 && cp <= 0xdfff))
+                return 0;                                    // private use, surrogate half
+            if (cp > 0xffff) {
+                cp -= 0x10000;
+                cp4((cp >> 10) + 0xd800);
+                cp4((cp & 0x3ff) + 0xdc00);
+            } else {
+                cp4(cp);
+            }
+            j += n;
+        } else {
+            if (b0 < 0x20 || b0 == 0x7f) cp4(b0);
+            else {
+                if (b0 == '"' || b0 == '\\') putc('\\');
+                putc((char)b0);
+            }
+            j++;
+        }
+    }
+    return ok ? k : 0;
+}
+
+// ---------------------------------------------------------------------------
 // server_identifier::get_normalized_domain_name(detail::on)
 // input: the server name as the reference's C string sees it (destination
 // context strncpy: at most MAX_SNI_LEN-1 = 256 bytes, stops at NUL)

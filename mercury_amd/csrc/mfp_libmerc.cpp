@@ -14,6 +14,7 @@
 
 #include "../../include/mercury_amd_libmerc.h"
 #include "../../include/mfp.h"
+#include "mfp_common.hpp"
 #include "mfp_internal.h"
 
 struct mercury {
@@ -190,6 +191,10 @@ static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *p
         }
         if (u.size() > 512) u.clear();
         copy_cstr(ac.ua, sizeof ac.ua, (const uint8_t *)u.data(), u.size());
+    } else if (rec.msg == MFP_MSG_STUN) {
+        // utf8_safe_string<512> of the SOFTWARE value (stun.h:1024-1027)
+        const uint32_t n = rec.ua_len == 0xffff ? 0 : mfpc::utf8_safe_512(pkt + rec.ua_off, rec.ua_len, ac.ua);
+        ac.ua[n] = 0;
     } else {
         copy_cstr(ac.ua, sizeof ac.ua, sb + rec.ua_off, rec.ua_len == 0xffff || hello ? 0 : rec.ua_len);
     }

@@ -255,6 +255,11 @@ struct QCrypto {
     uint32_t min_crypto_offset = 0xffffffffu;     // quic_init::min_crypto_offset
     void reset() {
         memset(buf, 0, sizeof buf);
+        reset_meta();
+    }
+    // cryptographic_buffer::reset (quic.h:1283-1292): the bookkeeping only,
+    // the bytes stay
+    void reset_meta() {
         buf_len = 0; min_off = ~0ull; min_len = ~0ull; max_off = 0; max_len = 0;
         total = 0; count = 0; first = 0xffff; min_crypto_offset = 0xffffffffu;
     }
@@ -530,6 +535,34 @@ static bool quic_frames_host(HC p, bool strict, QCrypto &q) {
     return true;
 }
 
+// quic_init's ctor (quic.h:1513-1528) before it decrypts: an Initial whose
+// protected first byte has zero reserved bits is first parsed as already
+// decrypted (quic_init_decry::parse, strict), over the payload after the
+// packet-number length the protected byte names; when that parse fails, the
+// CRYPTO frames it read stay in the buffer (crypto_buffer.reset() keeps the
+// bytes) and show through the gaps the decrypted frames leave.  The header is
+// quic_initial_packet::parse (quic.h:421-522), as k_quic's quic_hdr reads it.
+static void quic_stale_bytes(const uint8_t *pay, uint32_t n, QCrypto &q) {
+    if (n < 1184) return;                                     // min_len_pdu quic.h:525
+    HC d{pay, pay + n};
+    uint64_t ci = 0, v = 0;
+    hrd(d, 1, ci);
+    HC x; hparse(x, d, 4);
+    hrd(d, 1, v);
+    if (v > 20 || !d.d) return;
+    hparse(x, d, (long)v);
+    hrd(d, 1, v);
+    if (v > 20 || !d.d) return;
+    hparse(x, d, (long)v);
+    const uint64_t tl = hvli(d);
+    hparse(x, d, (long)tl);
+    const uint64_t len = hvli(d);
+    if (!d.d || (uint64_t)(d.e - d.d) < len || len < 64) return;   // min_len_pn_and_payload quic.h:524
+    HC payload; hparse(payload, d, (long)len);
+    if (!payload.d || payload.d >= payload.e || (ci & 0x0c)) return;
+    quic_frames_host(HC{payload.d + (ci & 3) + 1, payload.e}, true, q);
+}
+
 // the long header's connection ids (quic_initial_packet::parse quic.h:421-522);
 // get_cid: the DCID when not empty, else the SCID (quic.h:1611-1617)
 static bool quic_cid(const uint8_t *pay, uint32_t n, const uint8_t *&cid, uint32_t &cid_len) {
@@ -573,6 +606,10 @@ static void quic_initial(mfp_reassembler R, size_t i, const uint8_t *arena, cons
     const bool pre = j[10] & 1;
     QCrypto &q = R->qc;
     q.reset();
+    if (!pre) {                                              // the failed already-decrypted parse's bytes
+        quic_stale_bytes(pkt + s.pay_off, s.pay_len, q);
+        q.reset_meta();
+    }
     quic_frames_host(HC{j + 16, j + 16 + pt_len}, pre, q);
     // get_crypto_buf (quic.h:1600-1609): the bytes from the smallest CRYPTO offset
     const uint32_t crypto_offset = q.min_crypto_offset;

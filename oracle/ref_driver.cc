@@ -28,6 +28,8 @@
 // Mode "time": run write_json (or, with a trailing "an", the analysis_context
 // entry) with T threads (one processor per thread over contiguous shards),
 // print packets/s.
+// Mode "lpm" (lpm <pyasn.db> <domain mappings> <queries>): the reference's
+// subnet_data LC-tries queried directly (see lpm_mode).
 //
 // Uses the reference's public C API (libmerc.h:211-736) plus the processor's
 // analysis context (pkt_proc.h:132), exactly as the reference's own unit-test
@@ -44,6 +46,7 @@
 #include <unistd.h>
 #include "libmerc.h"
 #include "pkt_proc.h"
+#include "addr.h"
 
 struct pkt { const uint8_t *data; uint32_t len; uint16_t linktype; };
 
@@ -106,8 +109,68 @@ static int sni_mode(const char *path) {
     return 0;
 }
 
+// mode "lpm": the reference's subnet_data (addr.cc) built from a pyasn.db
+// text file and a domain-mapping file (one "subnet<TAB>tag" line per entry,
+// the pairs classifier::process_domain_mapping_line analysis.h:765-819 makes:
+// the tag is the type for proxy/sinkhole), finalised as the classifier does
+// (analysis.h:961-964); then for each query line "dst_ip<TAB>server_name":
+//   dst_ip  server_name  get_asn_info(dst_ip)  is_domain_faking(server_name, dst_ip)
+static std::vector<std::string> lines_of(const char *path) {
+    std::vector<std::string> out;
+    if (!path || strcmp(path, "-") == 0) return out;
+    FILE *f = fopen(path, "rb");
+    if (!f) { perror(path); exit(1); }
+    char line[8192];
+    while (fgets(line, sizeof line, f)) {
+        size_t n = strlen(line);
+        if (n && line[n - 1] == '\n') line[--n] = 0;
+        out.emplace_back(line, n);
+    }
+    fclose(f);
+    return out;
+}
+
+static int lpm_mode(const char *asn_path, const char *dom_path, const char *q_path) {
+    fflush(stdout);
+    int saved = dup(1), devnull = open("/dev/null", O_WRONLY);   // subnet_dedup prints
+    if (devnull >= 0) dup2(devnull, 1);
+    subnet_data sd;
+    {
+        std::vector<std::string> v4, v6;   // the split of analysis.h:896-905
+        for (auto &l : lines_of(asn_path)) (l.find('.') != std::string::npos ? v4 : v6).push_back(l);
+        sd.process_asn_subnets(v4);
+        sd.process_asn_subnets_v6(v6);
+        std::vector<std::pair<std::string, std::string>> d4, d6;
+        for (auto &l : lines_of(dom_path)) {
+            size_t t = l.find('\t');
+            if (t == std::string::npos) continue;
+            std::string sub = l.substr(0, t), tag = l.substr(t + 1);
+            (sub.find('.') != std::string::npos ? d4 : d6).push_back({sub, tag});
+        }
+        sd.process_domain_mapping_subnets(d4);
+        sd.process_domain_mapping_subnets_v6(d6);
+        sd.process_final();
+        sd.process_final_v6();
+        sd.process_domain_mappings_final();
+        sd.process_domain_mappings_final_v6();
+    }
+    fflush(stdout);
+    if (saved >= 0) { dup2(saved, 1); close(saved); }
+    if (devnull >= 0) close(devnull);
+    for (auto &q : lines_of(q_path)) {
+        size_t t = q.find('\t');
+        std::string ip = t == std::string::npos ? q : q.substr(0, t);
+        std::string name = t == std::string::npos ? "" : q.substr(t + 1);
+        const uint32_t asn = sd.get_asn_info(ip.c_str());
+        const int fake = name.empty() ? 0 : (int)sd.is_domain_faking(name.c_str(), ip.c_str());
+        printf("%s\t%s\t%u\t%d\n", ip.c_str(), name.c_str(), asn, fake);
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc == 3 && std::string(argv[1]) == "sni") return sni_mode(argv[2]);
+    if (argc == 5 && std::string(argv[1]) == "lpm") return lpm_mode(argv[2], argv[3], argv[4]);
     if (argc < 4) {
         fprintf(stderr, "usage: %s fp|an|json|time <input> <config-string> [resources] [threads] [seconds] [json|an]\n", argv[0]);
         return 2;

@@ -66,9 +66,9 @@ def build(seed=0x5EED0A1C):
         "VERSION": "2026.01.01; 2.0.dual\n",
         "fingerprint_db.json": "\n".join(lines) + "\n",
         "fp_prevalence_tls.txt": "",
-        # no nested IPv6 prefixes: the reference's IPv6 LC-trie does not fall
-        # back to an enclosing prefix reliably (known deviations)
-        "pyasn.db": "\n".join(x for x in synth_db.ASN_LINES if not x.startswith("2607:f8b0::/48")) + "\n",
+        # 2607:f8b0::/32 holds one /48: the reference's IPv6 LC-trie finds no
+        # ASN in the /32 outside the /48 (tests/test_lpm.py), as the device does
+        "pyasn.db": "\n".join(synth_db.ASN_LINES) + "\n",
         "doh-watchlist.txt": "quic.tech\nwww.example.com\n13.89.178.27\n",
         "domain-mappings.db": "".join(json.dumps(x) + "\n" for x in [
             {"subnet": "13.89.0.0/16", "type": "domain_mapping", "tag": "example.net"},

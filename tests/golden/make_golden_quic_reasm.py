@@ -7,7 +7,7 @@ built by oracle/Makefile.ref, driven by oracle/_ref/merc_ref_drv) with
 One packet stream, processed in order by one reference processor: the
 reference's multi-datagram QUIC pcaps (unit_tests/pcaps/quic_fragmented,
 quic_reordered_frames, quic-crypto-packets, quic_init.capture2), then the
-synthetic streams of tests/quic_reasm_synth.py.
+synthetic streams of tests/quic_reasm_synth.py (scenarios, then stale_scenarios).
 
 Outputs (committed):
   quic_reasm_packets.npz       the whole stream (pcap + synthetic packets)
@@ -47,7 +47,7 @@ def main():
     pk = []
     for name in PCAPS:
         pk += pcaplib.read_pcap(os.path.join("/root/reference/unit_tests/pcaps", name))[:PER_PCAP]
-    syn = quic_reasm_synth.scenarios()
+    syn = quic_reasm_synth.scenarios() + quic_reasm_synth.stale_scenarios()
     pkts = pk + [(1, p) for _, p in syn]
     arena, desc = pcaplib.make_batch(pkts)
     sources = [f"pcap.{i}" for i in range(len(pk))] + [lab for lab, _ in syn]

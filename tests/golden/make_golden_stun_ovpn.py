@@ -36,6 +36,8 @@ sys.path.insert(0, ROOT)
 from tests import pcaplib, stun_ovpn_synth, synth  # noqa: E402
 from oracle.compare_ref import REF  # noqa: E402
 
+ESCAPED = []   # filled in main(): utf8_safe() of the fixture's SOFTWARE values
+
 PCAPS_ALL = ["stun.pcap", "stun_classic.pcap", "openvpn_tcp_single.pcap", "openvpn_tcp_multi.pcap"]
 PCAPS_EMIT = ["emix.pcap", "surfshark.pcap"]
 CONFIGS = {
@@ -47,6 +49,45 @@ CONFIGS = {
 
 def ref(mode, path, cfg, res="-"):
     return subprocess.run([REF, mode, path, cfg, res], capture_output=True, check=True).stdout
+
+
+def utf8_safe(b):
+    """The text utf8_safe_string<512> gives the classifier for SOFTWARE value b
+    (utf8.hpp:200-340, 1059-1088; stun.h:1024), "" when null: test
+    infrastructure only, to key the archive's user agents; checked below
+    against the reference's own JSON text for the same values."""
+    out = []
+    try:
+        t = b.decode("utf-8", errors="strict")
+    except UnicodeDecodeError:
+        return ""
+    for ch in t:
+        c = ord(ch)
+        if 0xd800 <= c <= 0xdfff or 0xe000 <= c <= 0xf8ff or 0xf0000 <= c <= 0xffffd or 0x100000 <= c <= 0x10fffd:
+            return ""
+        if c < 0x20 or c == 0x7f or c >= 0x80:
+            if c > 0xffff:
+                c -= 0x10000
+                out.append("\\u%04x\\u%04x" % ((c >> 10) + 0xd800, (c & 0x3ff) + 0xdc00))
+            else:
+                out.append("\\u%04x" % c)
+        elif ch in '"\\':
+            out.append("\\" + ch)
+        else:
+            out.append(ch)
+    # fit: 511 bytes, a \uXXXX's hex digits only below offset 507 (append_memcpy's strict bound)
+    k = 0
+    for piece in out:
+        if piece.startswith("\\u"):
+            for j in range(0, len(piece), 6):
+                if k + 2 > 511 or k + 2 >= 507:
+                    return ""
+                k += 6
+        else:
+            if k + len(piece) > 511:
+                return ""
+            k += len(piece)
+    return "".join(out)
 
 
 def make_archive(fps):
@@ -63,6 +104,9 @@ def make_archive(fps):
             e = synth_db._proc_entry(rng, str(rng.choice(synth_db.PROC_NAMES)), int(rng.integers(1, 500)), [], [],
                                      uas, rng.random() < 0.2, {a: rng.random() < 0.2 for a in synth_db.ATTRS}, False)
             e["classes_port_port"] = {"3478": e["count"], "19302": max(1, e["count"] // 4)}
+            # every escaped SOFTWARE value of the fixture is a user agent of every process
+            for u in ESCAPED:
+                e["classes_user_agent"][u] = int(rng.integers(1, e["count"] + 1))
             e["classes_ip_ip"] = {"3.132.228.249": int(rng.integers(1, e["count"] + 1)),
                                   "13.89.178.27": int(rng.integers(1, e["count"] + 1))}
             procs.append(e)
@@ -86,6 +130,7 @@ def make_archive(fps):
 
 
 def main():
+    ESCAPED[:] = sorted({utf8_safe(b) for b in stun_ovpn_synth.SOFTWARE_ESCAPES} - {""})
     keep, sources = [], []
     for name in PCAPS_ALL:
         for i, p in enumerate(pcaplib.read_pcap(os.path.join("/root/reference/unit_tests/pcaps", name))):
@@ -128,9 +173,21 @@ def main():
             for i, r in enumerate(rows):
                 if r[2] == b"16":
                     stun_fps.setdefault(r[4].decode("latin-1"), i)
-    # archive: about 60 % of the distinct STUN fingerprints
+    # the escaped SOFTWARE values against the reference's JSON "stun" text
+    # (the same utf8_string::write), for the values it accepts
+    js_stun = ref("json", tmp, "stun").decode("latin-1")
+    for b in stun_ovpn_synth.SOFTWARE_ESCAPES:
+        e = utf8_safe(b)
+        assert not e or ('"' + e + '"') in js_stun, b
+    # archive: about 60 % of the distinct STUN fingerprints, and those of the
+    # SOFTWARE scenarios
     rng = np.random.default_rng(0x5EED000E)
-    chosen = [fp for fp in sorted(stun_fps) if rng.random() < 0.6]
+    sw_fps = set()
+    rows_stun = [l.split(b"\t") for l in ref("fp", tmp, "stun").splitlines()]
+    for i, src in enumerate(sources):
+        if src.startswith("synth:software") and rows_stun[i][2] == b"16":
+            sw_fps.add(rows_stun[i][4].decode("latin-1"))
+    chosen = [fp for fp in sorted(stun_fps) if rng.random() < 0.6 or fp in sw_fps]
     uas = ["libjingle", "WebRTC", "first", "second", "Coturn-4.5.2 'dan Eider'", "v6 agent", "x" * 37]
     arch = make_archive([(fp, uas) for fp in chosen])
     apath = os.path.join(HERE, "stun_resources.tgz")

@@ -183,6 +183,85 @@ def scenarios(seed=0x5EED0016):
     return out
 
 
+def _vli(b, p):
+    if p >= len(b):
+        return None, p
+    n = 1 << (b[p] >> 6)
+    if p + n > len(b):
+        return None, p
+    v = b[p] & 0x3f
+    for k in range(1, n):
+        v = v * 256 + b[p + k]
+    return v, p + n
+
+
+def _strict_crypto_writes(raw):
+    """quic_init_decry::parse (quic.h:1369-1390) over raw bytes: the CRYPTO
+    frames it writes into the buffer (extend: within 8 KiB) before it fails,
+    and whether it failed."""
+    p, writes = 0, []
+    while p < len(raw):
+        t = raw[p]
+        p += 1
+        data = None
+        if t == 0x06:
+            off, p = _vli(raw, p)
+            ln, p = _vli(raw, p) if off is not None else (None, p)
+            if ln is None or p + ln > len(raw):
+                return writes, True
+            data, p = (off, raw[p:p + ln]), p + ln
+        elif t == 0x1c:
+            for _ in range(2):
+                v, p = _vli(raw, p)
+                if v is None:
+                    return writes, True
+            rl, p = _vli(raw, p)
+            if rl is None or p + rl > len(raw):
+                return writes, True
+            p += rl
+        elif t in (0x02, 0x03):
+            return writes, True           # (an ACK in ciphertext: skipped by the search)
+        elif t not in (0x00, 0x01):
+            return writes, True
+        if data and data[1] and data[0] <= 8192 and data[0] + len(data[1]) <= 8192:
+            writes.append(data)
+    return writes, False
+
+
+def stale_scenarios(seed=0x5EED0C0C, n=3, gap=(60, 70)):
+    """Initials whose crypto buffer shows the bytes of the failed
+    already-decrypted parse (quic.h:1513-1528: crypto_buffer.reset() keeps
+    the bytes): the protected first byte's reserved bits are zero, the
+    ciphertext read as frames writes a CRYPTO frame over [gap), the decrypted
+    frames cover [0, 970) but that gap, overlapping so the frame check sees
+    no missing frame (total == span, quic.h:1267-1272); a second datagram
+    completes the ClientHello.  Found by searching DCIDs."""
+    rng = np.random.default_rng(seed)
+    out = []
+    found = 0
+    while found < n:
+        ch = big_hello(rng, 2000)
+        a, b = gap
+        f1 = crypto(ch, 0, a - 20) + crypto(ch, a - 30, 30) + crypto(ch, b, 970 - b)
+        for _ in range(400000):
+            c = Conn(rng, 57000 + found)
+            c.pn = int(rng.integers(0, 1000))
+            q = qs.initial(c.version, c.dcid, c.scid, b"", c.pn + 1, 2, f1)
+            if q[0] & 0x0c:
+                continue
+            hl = 1 + 4 + 1 + len(c.dcid) + 1 + len(c.scid) + 1 + 2
+            raw = q[hl + (q[0] & 3) + 1:]
+            writes, failed = _strict_crypto_writes(raw)
+            if failed and any(o < b and o + len(d) > a for o, d in writes):
+                break
+        else:
+            raise RuntimeError("no stale-byte Initial found")
+        out.append((f"stale.{found}.0", c.datagram(f1)))
+        out.append((f"stale.{found}.1", c.datagram(crypto(ch, 970, len(ch) - 970))))
+        found += 1
+    return out
+
+
 def timed_scenarios(seed=0x5EED0017, t0=1700000000):
     """(label, frame, capture time in seconds): connections that stall past the timeout."""
     rng = np.random.default_rng(seed)

@@ -60,9 +60,19 @@ def tcp_frame(payload, sport=51089, dport=1194, v6=False):
     return synth.frame(synth.tcp(payload, sport=sport, dport=dport), 6, v6=v6)
 
 
+SOFTWARE_ESCAPES = [b'quote " backslash \\ slash /', b"tab\tnewline\n ctl\x01 del\x7f", "ünïcode ✓ 😀".encode(),
+                    b"\xff\xfe invalid", b"\xc0\x80 overlong", b"\xed\xa0\x80 surrogate", "\ue000 private".encode(),
+                    b"x" * 505 + "é".encode(), b"x" * 504 + "é".encode(), b"x" * 511, b"x" * 512, b"nul\x00inside",
+                    "😀".encode() * 42, "😀".encode() * 43, b"\xe2\x82", "€uro".encode()]
+
+
 def stun_scenarios(rng):
     out = []
     sw = [b"libjingle", b"Coturn-4.5.2 'dan Eider'", b"WebRTC", b"x" * 37, "ünïcode".encode()]
+    # SOFTWARE values the classifier sees through utf8_safe_string<512>
+    # (stun.h:1024): JSON escapes, non-ASCII, invalid UTF-8 (null: empty user
+    # agent), and the 511-byte bound around a \uXXXX escape
+    sw += SOFTWARE_ESCAPES
     fp_types = [0x0006, 0x0008, 0x0020, 0x8007, 0x8008, 0x8022, 0x8028, 0xc003, 0xc057, 0xdaba]
     other = [0x0001, 0x0003, 0x0024, 0x0025, 0x8029, 0x802a, 0x000c, 0x000d, 0x0019, 0x0013, 0xc001]
     for cls in (0x0000, 0x0010, 0x0100, 0x0110):

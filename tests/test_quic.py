@@ -146,8 +146,12 @@ def test_quic_replicated_batch():
 # QUIC format (pkt_proc.h:97-99)
 # ---------------------------------------------------------------------------
 def load_attr():
+    return load_attr_file("quic_attr.tsv.gz")
+
+
+def load_attr_file(name):
     rows = []
-    with gzip.open(os.path.join(GOLD, "quic_attr.tsv.gz"), "rt", encoding="latin-1") as f:
+    with gzip.open(os.path.join(GOLD, name), "rt", encoding="latin-1") as f:
         for line in f:
             p = line.rstrip("\n").split("\t")
             attrs = {}
