@@ -143,6 +143,9 @@ enum {
     MFP_MSG_DTLS_HVR, MFP_MSG_QUIC,
     MFP_MSG_STUN,     /* stun::message (stun.h:783); sni_off/sni_len: the STUN message, ua: SOFTWARE */
     MFP_MSG_OPENVPN,  /* openvpn_tcp (openvpn.h:353); sni_off/sni_len: the TCP payload         */
+    MFP_MSG_OTHER,    /* identified as a protocol the selection names but this path does not
+                         parse ("all", or e.g. "dns": traffic_selector proto_identify.h:620-895):
+                         no record; counted (mercury_packet_processor_* log it once)             */
 };
 
 /* Reassembly inputs, one per packet (the device walk's view of tcp_packet,
@@ -235,9 +238,18 @@ MFP_EXPORT size_t mfp_fp_arena_bound(size_t n, size_t total_caplen);
 /* Parse a packet_filter_cfg string exactly as mfp_init does (host only, no
  * device needed): *select receives the MFP selection bits, *tls_format the TLS
  * format (0/1/2) in bits 0-7 and the QUIC format (0/1) in bits 8-15.
- * Returns 0, or -1 with mfp_last_error() set.  Mirrors global_config's
- * parser (global_config.h:143-153,246-275,348-368). */
+ * Mirrors global_config's parser (global_config.h:55-121, 143-153, 246-276;
+ * config_generator.cc:115-162), including what it only logs: an unknown
+ * protocol name ends the list, an unknown format keeps the default.  Returns
+ * 0; 1 when the reference would have logged such a problem (the text is in
+ * mfp_last_error()); -1 on error. */
 MFP_EXPORT int mfp_parse_filter(const char *packet_filter_cfg, uint32_t *select, uint32_t *tls_format);
+/* as mfp_parse_filter, and *other = the protocols the selection names outside
+ * this path whose identification comes first (bit set of mfp_device.hpp's
+ * BLK_*; "all" sets all of them): their messages write no record
+ * (MFP_MSG_OTHER). */
+MFP_EXPORT int mfp_parse_filter_ex(const char *packet_filter_cfg, uint32_t *select, uint32_t *tls_format,
+                                   uint32_t *other);
 
 /* ---- --analysis: the process classifier (classifier, analysis.h) ----
  * Enabled by mfp_init when packet_filter_cfg holds "resources=<archive.tgz>"

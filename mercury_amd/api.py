@@ -31,7 +31,8 @@ FP_TYPE_NAMES = ["unknown", "tls", "tls_server", "http", "http_server", "ssh", "
                  "ssh_init", "ssh_server", "ssh_kex_server", "ssh_init_server"]
 MSG_NAMES = ["none", "tls.client_hello", "tls.server_hello", "tls.certificate", "ssh.init", "ssh.kex",
              "http.request", "http.response", "tcp.syn", "tcp.syn_ack", "dtls.client_hello",
-             "dtls.server_hello", "dtls.hello_verify_request", "quic.initial", "stun", "openvpn_tcp"]
+             "dtls.server_hello", "dtls.hello_verify_request", "quic.initial", "stun", "openvpn_tcp",
+             "other"]   # MFP_MSG_OTHER: a selected protocol outside the path (no record)
 
 # mfp_tcp_seg (include/mfp.h): reassembly inputs per packet
 SEG_DTYPE = np.dtype([("seq", "<u4"), ("more", "<u4"), ("pay_off", "<u4"), ("pay_len", "<u2"), ("kind", "u1"),
@@ -138,6 +139,9 @@ def load_library():
     lib.mfp_normalize_server_name.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
     lib.mfp_parse_filter.restype = ctypes.c_int
     lib.mfp_parse_filter.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    lib.mfp_parse_filter_ex.restype = ctypes.c_int
+    lib.mfp_parse_filter_ex.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]
     lib.mfp_process_pipelined.restype = ctypes.c_longlong
     lib.mfp_process_pipelined.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp, vp, sz]
     lib.mfp_profile_enable.restype = ctypes.c_int
@@ -628,9 +632,21 @@ def parse_filter(cfg):
     """packet_filter_cfg -> (selection bits, tls format); host only."""
     lib = load_library()
     sel, fmt = ctypes.c_uint32(0), ctypes.c_uint32(0)
-    if lib.mfp_parse_filter(None if cfg is None else cfg.encode(), ctypes.byref(sel), ctypes.byref(fmt)) != 0:
+    if lib.mfp_parse_filter(None if cfg is None else cfg.encode(), ctypes.byref(sel), ctypes.byref(fmt)) < 0:
         raise MercuryAmdError(_err(lib))
     return sel.value, fmt.value
+
+
+def parse_filter_ex(cfg):
+    """packet_filter_cfg -> (selection bits, bits of the selected protocols
+    outside the path that are identified first); host only."""
+    lib = load_library()
+    sel, fmt, other = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_uint32(0)
+    rc = lib.mfp_parse_filter_ex(None if cfg is None else cfg.encode(), ctypes.byref(sel), ctypes.byref(fmt),
+                                 ctypes.byref(other))
+    if rc < 0:
+        raise MercuryAmdError(_err(lib))
+    return sel.value, other.value, (_err(lib) if rc > 0 else "")
 
 
 def fingerprints(rec, fp_arena):

@@ -1351,6 +1351,26 @@ struct Cfg {
     uint32_t select, tls_format, mode;
     uint32_t classify;   // stop after protocol identification (o.msg), emit nothing
     uint32_t seg;        // the caller wants the reassembly inputs (KParams::seg)
+    uint32_t block;      // BLK_*: selected protocols outside this path that are identified first
+};
+// Protocols the selection may name ("all" names every one) that this path does
+// not parse, but whose matchers or ports the reference consults before one of
+// this path's (traffic_selector proto_identify.h:620-895; get_tcp_msg_type
+// :936-942, get_udp_msg_type :944-968, the port tables :970-1075): a packet
+// they claim writes no record here (MFP_MSG_OTHER), whatever this path would
+// have made of it.  Mirrored in mfp_host.cpp (parse_select).
+enum : uint32_t {
+    BLK_SMTP = 1u << 0, BLK_DNS_TCP = 1u << 1, BLK_DNS_UDP = 1u << 2, BLK_SMB = 1u << 3, BLK_BT = 1u << 4,
+    BLK_MYSQL = 1u << 5, BLK_SOCKS = 1u << 6, BLK_IEC = 1u << 7, BLK_DNP3 = 1u << 8, BLK_LDAP = 1u << 9,
+    BLK_NBSS = 1u << 10, BLK_FTP_RESP = 1u << 11, BLK_TACACS = 1u << 12, BLK_RDP = 1u << 13, BLK_KRB5 = 1u << 14,
+    BLK_REDIS_REQ = 1u << 15, BLK_REDIS_RESP = 1u << 16, BLK_IMAP_REQ = 1u << 17, BLK_IMAP_RESP = 1u << 18,
+    BLK_TELNET = 1u << 19, BLK_IPSEC = 1u << 20, BLK_WIREGUARD = 1u << 21, BLK_SSDP = 1u << 22, BLK_NBDS = 1u << 23,
+    BLK_TFTP = 1u << 24, BLK_SNMP = 1u << 25, BLK_SYSLOG = 1u << 26,
+    BLK_TCP = BLK_SMTP | BLK_DNS_TCP | BLK_SMB | BLK_BT | BLK_MYSQL | BLK_SOCKS | BLK_IEC | BLK_DNP3 | BLK_LDAP |
+              BLK_NBSS | BLK_FTP_RESP | BLK_TACACS | BLK_RDP | BLK_KRB5 | BLK_REDIS_REQ | BLK_REDIS_RESP |
+              BLK_IMAP_REQ | BLK_IMAP_RESP | BLK_TELNET,
+    BLK_UDP_PORTS = BLK_IPSEC | BLK_NBDS | BLK_TFTP | BLK_KRB5 | BLK_SNMP | BLK_SYSLOG,
+    BLK_UDP = BLK_DNS_UDP | BLK_BT | BLK_WIREGUARD | BLK_SSDP | BLK_UDP_PORTS,
 };
 // parser families compiled into a walker instance (template argument FAM):
 // a bin kernel carries only its protocol's parser, so its code and register
@@ -1458,6 +1478,87 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
     return true;
 }
 
+// the TCP matchers of selected protocols outside this path, consulted only
+// when this path's matchers found nothing (they come after them in the tcp
+// table; the 4-byte ones, with their length checks, are the tcp4 table that
+// follows it): smtp_server "250-" (smtp.h:282), dns_packet::tcp_matcher
+// (dns.h:1152), smb1 / smb2 (smb1.h:311, smb2.h:856), bittorrent_handshake
+// (bittorrent.h:422), mysql_server_greet at offset 3 (mysql.hpp:577; the
+// reference's bound check, (length + offset) < 8, lets it read past a short
+// payload: read here as zero bytes), iec60870_5_104 (iec60870_5_104.h:538-549),
+// dnp3 (dnp3.h:501-512), socks4_req / socks5_hello / socks5_req_resp
+// (socks.h:90-110, 219-229, 490-505)
+DEV bool tcp_other_matcher(Cur p, uint32_t blk) {
+    const long n = clen(p);
+    if (!p.d || n < 4) return false;                                  // protocol_identifier::get_msg_type
+    if (n >= 8) {
+        if ((blk & BLK_SMTP) && m8(p, LE8(0xff, 0xff, 0xff, 0xff, 0, 0, 0, 0), LE8('2', '5', '0', '-', 0, 0, 0, 0)))
+            return true;
+        if ((blk & BLK_DNS_TCP) && m8(p, LE8(0, 0, 0, 0, 0x10, 0x48, 0xff, 0), 0)) return true;
+        if ((blk & BLK_SMB) && (m8(p, LE8(0, 0, 0, 0, 0xff, 0xff, 0xff, 0xff), LE8(0, 0, 0, 0, 0xff, 'S', 'M', 'B')) ||
+                                m8(p, LE8(0, 0, 0, 0, 0xff, 0xff, 0xff, 0xff), LE8(0, 0, 0, 0, 0xfe, 'S', 'M', 'B'))))
+            return true;
+        if ((blk & BLK_BT) && m8(p, ~0ull, LE8(0x13, 'B', 'i', 't', 'T', 'o', 'r', 'r'))) return true;
+    }
+    if (blk & BLK_MYSQL) {
+        uint64_t w = 0;
+        for (int i = 0; i < 8; i++) w |= (uint64_t)(3 + i < n ? ld(p.d + 3 + i) : 0u) << (8 * i);
+        if ((w & LE8(0xf8, 0xff, 0xf0, 0xff, 0xf0, 0xe0, 0xe0, 0)) == LE8(0, 0x0a, 0x30, 0x2e, 0x30, 0x20, 0x20, 0))
+            return true;
+    }
+    const uint32_t b0 = ld(p.d), b1 = ld(p.d + 1), b2 = ld(p.d + 2), b3 = ld(p.d + 3);
+    if ((blk & BLK_IEC) && b0 == 0x68 && (long)(b1 + 2) == n) return true;
+    if ((blk & BLK_DNP3) && b0 == 0x05 && b1 == 0x64 &&
+        (long)(3 + b2 + 2 + (b2 % 16 ? b2 / 16 + 1 : b2 / 16) * 2) == n)
+        return true;
+    if (blk & BLK_SOCKS) {
+        if (b0 == 0x04 && (b1 & 0xfc) == 0 && n > 8) {
+            const uint32_t f = ld(p.d + 8);
+            if ((n == 9 && f == 0) || ((f >= 32 || f == 0) && ld(p.e - 2) >= 32 && ld(p.e - 1) == 0)) return true;
+        }
+        if (b0 == 0x05 && (b1 & 0xf0) == 0 && (long)(2 + b1) == n) return true;
+        if (b0 == 0x05 && (b1 & 0xf0) == 0 && b2 == 0 && (b3 & 0xf8) == 0) {
+            const long dom = n > 4 ? (long)ld(p.d + 4) : 0;
+            if (n == 10 || n == 22 || n == 7 + dom) return true;
+        }
+    }
+    return false;
+}
+// get_tcp_msg_type_from_ports (proto_identify.h:1015-1075): the ports checked
+// before OpenVPN's 1194 (ldap, nbss) and after it (the rest), all before the
+// keyword matchers that find HTTP
+DEV bool tcp_other_port_first(uint32_t sp, uint32_t dp, uint32_t blk) {
+    return ((blk & BLK_LDAP) && (sp == 389 || dp == 389)) || ((blk & BLK_NBSS) && (sp == 139 || dp == 139));
+}
+DEV bool tcp_other_port(uint32_t sp, uint32_t dp, uint32_t blk) {
+    return ((blk & BLK_FTP_RESP) && sp == 21) || ((blk & BLK_TACACS) && (sp == 49 || dp == 49)) ||
+           ((blk & BLK_RDP) && (sp == 3389 || dp == 3389)) || ((blk & BLK_MYSQL) && (sp == 3306 || dp == 3306)) ||
+           ((blk & BLK_KRB5) && (sp == 88 || dp == 88)) || ((blk & BLK_REDIS_REQ) && dp == 6379) ||
+           ((blk & BLK_REDIS_RESP) && sp == 6379) || ((blk & BLK_IMAP_REQ) && dp == 143) ||
+           ((blk & BLK_IMAP_RESP) && sp == 143) || ((blk & BLK_TELNET) && (sp == 23 || dp == 23));
+}
+// the UDP matchers of the udp table that precede QUIC's (and so every 16- and
+// 4-byte matcher): dns_packet::matcher (dns.h:1141; also for nbns / mdns),
+// wireguard (wireguard.h:52), ssdp (ssdp.h:153), bittorrent DHT and LSD
+// (bittorrent.h:66, 257); ESP/IKE on port 4500 before any of them (:946-953)
+DEV bool udp_other_first(Cur p, uint32_t sp, uint32_t dp, uint32_t blk) {
+    if ((blk & BLK_IPSEC) && (sp == 4500 || dp == 4500)) return true;
+    if (!p.d || clen(p) < 8) return false;
+    return ((blk & BLK_DNS_UDP) && m8(p, LE8(0, 0, 0x10, 0x48, 0xff, 0, 0xff, 0x80), 0)) ||
+           ((blk & BLK_WIREGUARD) && m8(p, LE8(0xff, 0xff, 0xff, 0xff, 0, 0, 0, 0), LE8(1, 0, 0, 0, 0, 0, 0, 0))) ||
+           ((blk & BLK_SSDP) && m8(p, LE8(0xe8, 0x84, 0xf0, 0xe0, 0, 0x90, 0, 0), LE8(0x48, 0x04, 0x50, 0x40, 0, 0x10, 0, 0))) ||
+           ((blk & BLK_BT) && (m8(p, LE8(0xff, 0xff, 0xff, 0x8c, 0xff, 0xff, 0xff, 0xff), LE8('d', '1', ':', 0, 'd', '2', ':', 'i')) ||
+                               m8(p, ~0ull, LE8('B', 'T', '-', 'S', 'E', 'A', 'R', 'C'))));
+}
+// get_udp_msg_type_from_ports (proto_identify.h:970-1013): the ports checked
+// before VXLAN / Geneve / GRE over UDP (the encapsulation walk uses the same
+// table, pkt_proc.cc:1000-1018)
+DEV bool udp_other_port(uint32_t sp, uint32_t dp, uint32_t blk) {
+    return ((blk & BLK_IPSEC) && (sp == 500 || dp == 500)) || ((blk & BLK_NBDS) && sp == 138 && dp == 138) ||
+           ((blk & BLK_TFTP) && (sp == 69 || dp == 69)) || ((blk & BLK_KRB5) && (sp == 88 || dp == 88)) ||
+           ((blk & BLK_SNMP) && (sp == 161 || sp == 162 || dp == 161 || dp == 162)) || ((blk & BLK_SYSLOG) && dp == 514);
+}
+
 // set_tcp_protocol pkt_proc.cc:488 (selection subset)
 template <uint32_t FAM, class E>
 DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, const uint8_t *base) {
@@ -1476,6 +1577,19 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
                  m8(pkt, LE8(0xff, 0xff, 0xf0, 0, 0, 0xff, 0, 0), LE8(0, 0, 0, 0, 0, 0x14, 0, 0)))
             msg = MFP_MSG_SSH_KEX;
     }
+    // a selected protocol outside this path claims the payload first: the
+    // walkers that parse HTTP decide it (they carry the checks), the others
+    // hand the packet to the fallback lane, which does
+    const bool blk = msg == 0 && (cfg.block & BLK_TCP) && !cfg.classify;
+    if (blk) {
+        if constexpr (!(FAM & FAM_HTTP)) {
+            b.punt_pkt();
+            return;
+        } else if (tcp_other_matcher(pkt, cfg.block) || tcp_other_port_first(sport, dport, cfg.block)) {
+            o.msg = MFP_MSG_OTHER;
+            return;
+        }
+    }
     // tcp_msg_type_from_ports (proto_identify.h:1028-1030): OpenVPN over TCP
     // on port 1194, before the keyword matchers.  k_quic parses it (the
     // ClientHello may span several control records, openvpn.h:388-403).
@@ -1484,6 +1598,10 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         o.pay_off = (uint32_t)(pkt.d - base);
         o.pay_len = (uint32_t)clen(pkt);
         if (!cfg.classify) b.punt_pkt();
+        return;
+    }
+    if (blk && tcp_other_port(sport, dport, cfg.block)) {
+        o.msg = MFP_MSG_OTHER;
         return;
     }
     if (msg == 0) {
@@ -1745,6 +1863,16 @@ DEV void stun_msg(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
 // set_udp_protocol pkt_proc.cc:677 (selection subset: QUIC, DTLS, STUN)
 template <uint32_t FAM, class E>
 DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
+    // a selected protocol outside this path claims the datagram first: only
+    // the fallback lane (every family) carries the checks
+    if ((cfg.block & BLK_UDP) && !cfg.classify) {
+        if constexpr (FAM != FAM_ALL) {
+            b.punt_pkt();
+            return;
+        } else {
+            if (udp_other_first(pkt, o.src_port, o.dst_port, cfg.block)) { o.msg = MFP_MSG_OTHER; return; }
+        }
+    }
     // 8-byte matchers before 16-byte ones (get_udp_msg_type proto_identify.h:955-960):
     // the QUIC long header (quic_initial_packet::matcher quic.h:544).  Only
     // k_quic (mfp_quic.hip) parses QUIC; every other walker hands it over.
@@ -1770,6 +1898,8 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
     if (!msg) {                                        // udp4: STUN's length matcher
         if ((cfg.select & SEL_STUN) && 20 + ((ld(pkt.d + 2) << 8) | ld(pkt.d + 3)) == (uint32_t)clen(pkt))
             stun_msg<FAM>(b, cfg, o, pkt, base);
+        else if ((cfg.block & BLK_UDP_PORTS) && !cfg.classify && udp_other_port(o.src_port, o.dst_port, cfg.block))
+            o.msg = MFP_MSG_OTHER;
         return;
     }
     o.msg = msg;
@@ -1974,7 +2104,10 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
             Cur u = pkt;
             const uint8_t *uh = cget_ptr(u, 8);
             const uint32_t dport = uh ? (ld(uh + 2) << 8) | ld(uh + 3) : 0u;
-            if ((cfg.select & SEL_VXLAN) && dport == 4789) {            // vxlan.hpp
+            const uint32_t sport = uh ? (ld(uh) << 8) | ld(uh + 1) : 0u;
+            if ((cfg.block & BLK_UDP_PORTS) && udp_other_port(sport, dport, cfg.block)) {
+                break;                                                  // a port-table protocol first
+            } else if ((cfg.select & SEL_VXLAN) && dport == 4789) {     // vxlan.hpp
                 pkt = u;
                 const uint32_t fl = rd_u8(pkt);
                 Cur t; cparse(t, pkt, 3); cparse(t, pkt, 3); cparse(t, pkt, 1);

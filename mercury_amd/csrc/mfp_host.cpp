@@ -37,7 +37,8 @@ extern "C" int mfp_launch_analysis_resolve(const mfp_classifier_dev *D, const mf
                                            const uint32_t *group_off, const uint8_t *seen_seq, hipStream_t stream,
                                            mfp_prof *prof);
 
-extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
+extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t tls_format, uint32_t mode,
+                                      const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, mfp_tcp_seg *seg,
                                       uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
@@ -87,24 +88,35 @@ static std::string trim(const std::string &s) {
     return s.substr(a, b - a);
 }
 
-// global_config::set_protocols (global_config.h:246) restricted to the
-// protocols of this path; the reference's traffic_selector turns the map
-// into matchers (proto_identify.h:620-895)
-static bool parse_select(const std::string &list, uint32_t &sel) {
-    // "all" (and the empty selection, which the reference reads as "all",
-    // global_config.h:248) selects ~45 protocols this path does not parse
-    // (DNS, SMTP, ...): the reference would write records the device
-    // cannot, so it is refused rather than silently diverging
-    if (strip(list).empty() || strip(list) == "all") {
-        mfp_set_error("protocol selection \"%s\" includes protocols outside the device path; select from: tls, "
-                      "tls.client_hello, tls.server_hello, tls.server_certificate, ssh, ssh.client, ssh.server, "
-                      "http, http.request, http.response, tcp, tcp.syn_ack, dtls, quic, stun, openvpn_tcp, gre, vxlan, "
-                      "geneve, none",
-                      list.empty() ? "" : list.c_str());
-        return false;
-    }
-    const std::string &s = list;
-    std::map<std::string, uint32_t> known = {
+// global_config::set_protocols (global_config.h:246-276) over the reference's
+// protocol names (global_config.h:163-227).  This path's protocols set
+// `sel`; the others write no record, and those whose matchers or ports the
+// reference consults before one of this path's set their BLK_* bits in
+// `block` (traffic_selector proto_identify.h:620-895; mirrored in
+// mfp_device.hpp).  "all" sets everything; "none" clears everything
+// (proto_identify.h:623-627); a name the reference does not know is refused,
+// as set_protocols refuses it.
+enum : uint32_t {
+    BLK_SMTP = 1u << 0, BLK_DNS_TCP = 1u << 1, BLK_DNS_UDP = 1u << 2, BLK_SMB = 1u << 3, BLK_BT = 1u << 4,
+    BLK_MYSQL = 1u << 5, BLK_SOCKS = 1u << 6, BLK_IEC = 1u << 7, BLK_DNP3 = 1u << 8, BLK_LDAP = 1u << 9,
+    BLK_NBSS = 1u << 10, BLK_FTP_RESP = 1u << 11, BLK_TACACS = 1u << 12, BLK_RDP = 1u << 13, BLK_KRB5 = 1u << 14,
+    BLK_REDIS_REQ = 1u << 15, BLK_REDIS_RESP = 1u << 16, BLK_IMAP_REQ = 1u << 17, BLK_IMAP_RESP = 1u << 18,
+    BLK_TELNET = 1u << 19, BLK_IPSEC = 1u << 20, BLK_WIREGUARD = 1u << 21, BLK_SSDP = 1u << 22, BLK_NBDS = 1u << 23,
+    BLK_TFTP = 1u << 24, BLK_SNMP = 1u << 25, BLK_SYSLOG = 1u << 26, BLK_ALL = (1u << 27) - 1,
+};
+struct SelState {
+    uint32_t sel = 0, block = 0;
+    bool none = false;          // protocols["none"]: cleared at the end (proto_identify.h:623-627)
+    std::string warn;           // what the reference logs (printf_err) and goes on from
+};
+static void add_warning(SelState &st, const std::string &w) { st.warn += (st.warn.empty() ? "" : "; ") + w; }
+
+// set_protocols (global_config.h:246-276), literally: the list is split at
+// ','; every token but the last has its spaces removed (the last keeps them:
+// the function strips the rest of the string, not the token); the first
+// unknown token is logged and ends the list, what was set stays
+static void parse_select(const std::string &data, SelState &st) {
+    static const std::map<std::string, uint32_t> known = {
         {"none", 0},
         {"tls", SEL_TLS_CH | SEL_TLS_SH | SEL_TLS_CERT}, {"tls.client_hello", SEL_TLS_CH},
         {"tls.server_hello", SEL_TLS_SH}, {"tls.server_certificate", SEL_TLS_CERT},
@@ -114,89 +126,129 @@ static bool parse_select(const std::string &list, uint32_t &sel) {
         {"gre", SEL_GRE}, {"vxlan", SEL_VXLAN}, {"geneve", SEL_GENEVE},
         {"stun", SEL_STUN}, {"openvpn_tcp", SEL_OPENVPN},
     };
-    bool none = false;
+    static const std::map<std::string, uint32_t> other = {
+        {"arp", 0}, {"bittorrent", BLK_BT}, {"cdp", 0}, {"dhcp", 0}, {"dnp3", BLK_DNP3},
+        {"dns", BLK_DNS_TCP | BLK_DNS_UDP}, {"icmp", 0}, {"iec", BLK_IEC}, {"kerberos", BLK_KRB5}, {"ldap", BLK_LDAP},
+        {"imap", BLK_IMAP_REQ | BLK_IMAP_RESP}, {"imap.request", BLK_IMAP_REQ}, {"imap.response", BLK_IMAP_RESP},
+        {"ipsec", BLK_IPSEC}, {"lldp", 0}, {"mdns", BLK_DNS_UDP}, {"nbns", BLK_DNS_UDP}, {"nbds", BLK_NBDS},
+        {"nbss", BLK_NBSS}, {"ospf", 0}, {"rdp", BLK_RDP}, {"rfb", 0}, {"sctp", 0}, {"smb", BLK_SMB}, {"smtp", BLK_SMTP},
+        {"snmp", BLK_SNMP}, {"ssdp", BLK_SSDP}, {"syslog", BLK_SYSLOG}, {"tacacs", BLK_TACACS}, {"tcp.message", 0},
+        {"telnet", BLK_TELNET}, {"tftp", BLK_TFTP}, {"wireguard", BLK_WIREGUARD}, {"mysql", BLK_MYSQL},
+        {"tofsee", 0}, {"socks", BLK_SOCKS}, {"ftp", BLK_FTP_RESP}, {"ftp.response", BLK_FTP_RESP},
+        {"ftp.request", 0}, {"redis", BLK_REDIS_REQ | BLK_REDIS_RESP}, {"redis.request", BLK_REDIS_REQ},
+        {"redis.response", BLK_REDIS_RESP},
+    };
+    const std::string list = data.empty() ? std::string("all") : data;   // global_config.h:248
     size_t pos = 0;
     while (true) {
-        size_t c = s.find(',', pos);
-        std::string tok = strip(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
-        auto it = known.find(tok);
-        if (it == known.end()) {
-            mfp_set_error("protocol selection \"%s\" is not supported by the device path", tok.c_str());
-            return false;
-        }
-        if (tok == "none") none = true;
-        sel |= it->second;
-        if (c == std::string::npos) break;
-        pos = c + 1;
-    }
-    if (none) sel = 0;   // proto_identify.h:611-615
-    return true;
-}
-
-// fingerprint_format::set_fingerprint_format (global_config.h:55-121); the
-// result packs the TLS format in bits 0-7 and the QUIC format in bits 8-15
-static bool parse_format(const std::string &s, uint32_t &tls_format) {
-    size_t pos = 0;
-    while (pos <= s.size()) {
-        size_t c = s.find(',', pos);
-        std::string tok = strip(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
-        if (!tok.empty()) {
-            size_t sl = tok.find('/');
-            std::string proto = tok.substr(0, sl), ver = sl == std::string::npos ? "" : tok.substr(sl + 1);
-            if (proto == "tls") {
-                if (ver == "") tls_format = tls_format & ~0xffu;
-                else if (ver == "1") tls_format = (tls_format & ~0xffu) | 1u;
-                else if (ver == "2") tls_format = (tls_format & ~0xffu) | 2u;
-                else { mfp_set_error("unknown fingerprint format %s", tok.c_str()); return false; }
-            } else if (proto == "quic") {
-                if (ver == "") tls_format &= ~0xff00u;
-                else if (ver == "1") tls_format = (tls_format & ~0xff00u) | (1u << 8);
-                else { mfp_set_error("unknown fingerprint format %s", tok.c_str()); return false; }
-            } else {
-                mfp_set_error("unknown fingerprint format %s", tok.c_str());
-                return false;
-            }
+        const size_t c = list.find(',', pos);
+        const std::string tok = c == std::string::npos ? list.substr(pos) : strip(list.substr(pos, c - pos));
+        if (tok == "all") {
+            st.sel |= SEL_ALL;
+            st.block |= BLK_ALL;
+        } else if (auto it = known.find(tok); it != known.end()) {
+            if (tok == "none") st.none = true;
+            st.sel |= it->second;
+        } else if (auto jt = other.find(tok); jt != other.end()) {
+            st.block |= jt->second;
+        } else {
+            add_warning(st, "unrecognized filter command \"" + tok + "\"");
+            return;
         }
         if (c == std::string::npos) break;
         pos = c + 1;
     }
-    return true;
 }
 
+// fingerprint_format::set_fingerprint_format (global_config.h:55-121),
+// literally: a token is substr(start, current_pos) -- a count, not an end --
+// with its spaces removed, the last token keeps its spaces; an unknown format
+// is logged and ends the list ("using default instead").  The result packs
+// the TLS format in bits 0-7 and the QUIC format in bits 8-15.
+static void parse_format(const std::string &s, uint32_t &tls_format, SelState &st) {
+    auto one = [&](const std::string &tok) -> bool {
+        const size_t sl = tok.find('/');
+        const std::string proto = tok.substr(0, sl), ver = sl == std::string::npos ? "" : tok.substr(sl + 1);
+        if (proto == "tls" && (ver == "" || ver == "1" || ver == "2")) {
+            tls_format = (tls_format & ~0xffu) | (ver == "" ? 0u : ver == "1" ? 1u : 2u);
+            return true;
+        }
+        if (proto == "quic" && (ver == "" || ver == "1")) {
+            tls_format = (tls_format & ~0xff00u) | (ver == "1" ? 1u << 8 : 0u);
+            return true;
+        }
+        add_warning(st, "unknown fingerprint format: " + tok + "; using default instead");
+        return false;
+    };
+    if (s.empty()) return;
+    size_t start = 0, cur;
+    while ((cur = s.find(',', start)) != std::string::npos) {
+        const std::string tok = strip(s.substr(start, cur));
+        start = cur + 1;
+        if (!one(tok)) return;
+    }
+    if (start < s.size()) one(s.substr(start));
+}
+
+// global_config(const libmerc_config&) (global_config.h:143-153): a string
+// without ';' is the protocol list; otherwise parse_additional_options
+// (config_generator.cc:115-162): ';'-separated tokens, trimmed, key=value or a
+// bare key; a key no option recognises is taken as a protocol list.  Warnings
+// (what the reference logs and goes on from) land in *warn.
 bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
-                      bool *reassembly) {
-    sel = 0; tls_format = 0;
+                      bool *reassembly, uint32_t *block_out, std::string *warn) {
+    tls_format = 0;
+    SelState st;
     std::string s = cfg ? cfg : "";
-    if (s.find(';') == std::string::npos) return parse_select(s, sel);   // global_config.h:148-152
-    // key=value;... (config_generator.cc parse_tokens); without select=
-    // nothing is selected, as in the reference
-    size_t pos = 0;
-    while (pos <= s.size()) {
-        size_t c = s.find(';', pos);
-        std::string tok = trim(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
-        if (!tok.empty()) {
-            size_t eq = tok.find('=');
-            std::string key = trim(tok.substr(0, eq)), val = eq == std::string::npos ? "" : trim(tok.substr(eq + 1));
-            if (key == "select") { if (!parse_select(val, sel)) return false; }
-            else if (key == "format") { if (!parse_format(val, tls_format)) return false; }
-            else if (key == "resources") { if (resources) *resources = val; }
-            else if (key == "analysis") { if (analysis) *analysis = val.empty() || val == "1"; }
-            else if (key == "reassembly" || key == "tcp-reassembly") {   // global_config.h:354-355
-                if (reassembly) *reassembly = true;
+    if (s.find(';') == std::string::npos) {
+        parse_select(s, st);
+    } else {
+        static const char *const ignored[] = {   // recognised options that do not affect this path's output
+            "quic-trial-decryption", "stats-blocking", "raw-features", "crypto-assess", "minimize-ram",
+            "network-behavioral-detections", "exposed-creds", "http-headers", "http-body-max", "dns-json",
+            "certs-json", "metadata", "stats", "report_os", "nonselected-tcp-data", "nonselected-udp-data",
+            "fp_proc_threshold", "proc_dst_threshold", "max_stats_entries"};
+        size_t pos = 0;
+        while (pos <= s.size()) {
+            size_t c = s.find(';', pos);
+            std::string tok = trim(s.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
+            if (!tok.empty()) {
+                size_t eq = tok.find('=');
+                std::string key = trim(tok.substr(0, eq)), val = eq == std::string::npos ? "" : trim(tok.substr(eq + 1));
+                if (key == "select" || key == "-s" || key == "--select") parse_select(val, st);
+                else if (key == "format") parse_format(val, tls_format, st);
+                else if (key == "resources") { if (resources) *resources = val; }
+                else if (key == "analysis" || key == "-a" || key == "--analysis") {
+                    if (analysis) *analysis = val.empty() || val == "1";
+                } else if (key == "reassembly" || key == "tcp-reassembly") {   // global_config.h:354-355
+                    if (reassembly) *reassembly = true;
+                } else if (std::find(std::begin(ignored), std::end(ignored), key) == std::end(ignored)) {
+                    parse_select(key, st);   // config_generator.cc:156-160
+                }
             }
-            // other keys (metadata, stats, ...) do not affect fingerprints
+            if (c == std::string::npos) break;
+            pos = c + 1;
         }
-        if (c == std::string::npos) break;
-        pos = c + 1;
     }
+    sel = st.none ? 0 : st.sel;
+    if (block_out) *block_out = st.none ? 0 : st.block;
+    if (warn) *warn = st.warn;
     return true;
 }
 
 extern "C" MFP_EXPORT int mfp_parse_filter(const char *cfg, uint32_t *select, uint32_t *tls_format) {
-    uint32_t sel = 0, fmt = 0;
-    if (!mfp_parse_config(cfg, sel, fmt, nullptr, nullptr, nullptr)) return -1;
+    return mfp_parse_filter_ex(cfg, select, tls_format, nullptr);
+}
+
+extern "C" MFP_EXPORT int mfp_parse_filter_ex(const char *cfg, uint32_t *select, uint32_t *tls_format,
+                                              uint32_t *other) {
+    uint32_t sel = 0, fmt = 0, blk = 0;
+    std::string warn;
+    if (!mfp_parse_config(cfg, sel, fmt, nullptr, nullptr, nullptr, &blk, &warn)) return -1;
     if (select) *select = sel;
     if (tls_format) *tls_format = fmt;
+    if (other) *other = blk;
+    if (!warn.empty()) { mfp_set_error("%s", warn.c_str()); return 1; }
     return 0;
 }
 
@@ -314,6 +366,7 @@ struct Slot {
 struct mfp_context_s {
     int device = 0;
     uint32_t select = SEL_ALL, tls_format = 0, mode = 0;
+    uint32_t block = 0;                  // BLK_*: selected protocols outside this path (mfp_device.hpp)
     uint32_t quic_format = 0;            // fingerprint_format::quic_fingerprint_format (global_config.h:41)
     uint32_t quic_grid = 512;            // k_quic workgroups (x 128 lanes, each with a scratch slot)
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|lane (A/B, debugging)
@@ -350,10 +403,10 @@ extern "C" MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int de
 
 extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int device, int mode,
                                                const uint8_t *enc_key) {
-    uint32_t sel, fmt;
+    uint32_t sel, fmt, blk = 0;
     std::string resources;
     bool analysis = false, reassembly = false;
-    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly)) return nullptr;
+    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly, &blk)) return nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         mfp_set_error("no HIP device available: the mercury_amd fingerprint path runs only on the GPU");
@@ -361,7 +414,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     }
     if (device < 0 || device >= ndev) { mfp_set_error("bad device %d", device); return nullptr; }
     auto *c = new mfp_context_s;
-    c->device = device; c->select = sel; c->tls_format = fmt & 0xff; c->quic_format = (fmt >> 8) & 0xff; c->mode = mode;
+    c->device = device; c->select = sel; c->block = blk; c->tls_format = fmt & 0xff; c->quic_format = (fmt >> 8) & 0xff; c->mode = mode;
     c->reassembly = reassembly;
     const char *st = getenv("MFP_STRATEGY");
     if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
@@ -462,7 +515,7 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
         if (grow(S.d_seg, S.cap_seg, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
         d_seg = S.d_seg;
     }
-    if (mfp_launch_fingerprint(c->select, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, d_seg, (uint8_t *)d_fp_arena,
+    if (mfp_launch_fingerprint(c->select, c->block, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, d_seg, (uint8_t *)d_fp_arena,
                                fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
                                c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
                                c->prof) != 0) {

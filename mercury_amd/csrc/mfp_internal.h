@@ -11,7 +11,7 @@
 
 void mfp_set_error(const char *fmt, ...);
 bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
-                      bool *reassembly);
+                      bool *reassembly, uint32_t *block = nullptr, std::string *warn = nullptr);
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode);
 uint32_t mfp_context_mode(mfp_context c);   // MFP_MODE_*
 

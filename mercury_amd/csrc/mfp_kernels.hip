@@ -76,6 +76,10 @@ __global__ __launch_bounds__(TILE) void k_classify(KParams P, uint32_t *bins, ui
             c.seg = 0;
             packet_walk(e, c, o, (const uint8_t *)&win[tid][0] + sh, take, dsc.linktype);
             bin = msg_bin(o.msg);
+            // selected protocols outside this path may claim a QUIC, OpenVPN
+            // or DTLS packet first (Cfg::block): k_quic and the DTLS walker do
+            // not decide that, the "other" bin's walker does
+            if (P.cfg.block && (bin == QUIC_BIN || (bin == 7 && (P.cfg.block & BLK_UDP)))) bin = 4;
             cls[i] = (uint8_t)bin;
         }
 #pragma unroll
@@ -120,7 +124,8 @@ extern "C" int mfp_launch_quic(const void *kparams, uint8_t *scratch, uint32_t q
                                hipStream_t stream, mfp_prof *prof);
 
 // launchers used by the host library (mfp_host.cpp)
-extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint32_t mode, const uint8_t *arena,
+extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t tls_format, uint32_t mode,
+                                      const uint8_t *arena,
                                       const mfp_pkt_desc *desc, uint64_t n, mfp_record *rec, mfp_tcp_seg *seg,
                                       uint8_t *fp_arena,
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
@@ -137,6 +142,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t tls_format, uint
     mfp::KParams P;
     P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0;
     P.cfg.seg = seg ? 1u : 0u;
+    P.cfg.block = block;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
     P.fp_used = fp_used;
     P.seg = seg;

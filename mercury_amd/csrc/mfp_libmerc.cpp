@@ -4,6 +4,7 @@
 // interface is the batch API.  File:line cites are relative to
 // /root/reference/src/libmerc/.
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -28,6 +29,10 @@ struct mercury {
     mfp_prevalence prev = nullptr;
     uint8_t enc_key[16] = {0};    // libmerc_config.enc_key (encrypted resource archive)
     bool keyed = false;
+    // packets identified as a selected protocol outside the device path
+    // (MFP_MSG_OTHER, e.g. under "all"): they write no record; counted, and
+    // logged once per context
+    std::atomic<uint64_t> other{0};
 };
 
 struct analysis_context {       // the fields libmerc's accessors read (result.h:174-420)
@@ -79,6 +84,19 @@ static void log_error(const char *fmt, ...) {
     g_printf_err(log_err, fmt, ap);
     va_end(ap);
 }
+static void log_warn(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    g_printf_err(log_warning, fmt, ap);
+    va_end(ap);
+}
+// a message of a selected protocol this path does not parse: no record
+static void note_other(mercury *m, const mfp_record &rec) {
+    if (rec.msg != MFP_MSG_OTHER) return;
+    if (m->other.fetch_add(1, std::memory_order_relaxed) == 0)
+        log_warn("the selection names protocols outside the MI355X device path (tls, dtls, ssh, http, tcp, "
+                    "quic, stun, openvpn_tcp, gre, vxlan, geneve); their messages write no record\n");
+}
 
 #ifndef MFP_GIT_COMMIT
 #define MFP_GIT_COMMIT "commit unknown"   // libmerc.cc:29-36
@@ -118,11 +136,13 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
     m->cfg = cfg;
     // validate now, so a bad configuration fails at init as in the reference
     uint32_t sel, fmt;
-    if (mfp_parse_filter(cfg.c_str(), &sel, &fmt) != 0) {
+    const int prc = mfp_parse_filter(cfg.c_str(), &sel, &fmt);
+    if (prc < 0) {
         log_error("%s\n", mfp_last_error());
         delete m;
         return nullptr;
     }
+    if (prc > 0) log_error("%s\n", mfp_last_error());   // printf_err(log_err, ...) as set_protocols does, and go on
     return m;
 }
 
@@ -278,6 +298,7 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
         const uint8_t *fr = mfp_reassembler_frames(p->reasm, &flen);
         if (d2.offset >= len + 16 && fr) p->arena.insert(p->arena.end(), fr, fr + flen);
         fill_context(ctx, p->ac, p->arena.data() + d2.offset, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+        note_other(p->mc, rec);
         n = want_an ? mfp_write_json_batch_reassembly_analysis(ctx, p->arena.data(), &d2, 1, &rec, p->fp.data(), &props,
                                                                &an, ap, &t, (char *)buffer, buffer_size, &end, &skipped, 1)
                     : mfp_write_json_batch_reassembly(p->arena.data(), &d2, 1, &rec, p->fp.data(), &props, &t,
@@ -287,6 +308,7 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
                                                    cap, want_an ? &an : nullptr, want_an ? ap : nullptr);
         if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
         fill_context(ctx, p->ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+        note_other(p->mc, rec);
         n = want_an ? mfp_write_json_batch_analysis(ctx, p->arena.data(), &d, 1, &rec, p->fp.data(), &an, ap, &t,
                                                     (char *)buffer, buffer_size, &end, &skipped, 1)
                     : mfp_write_json_batch(p->arena.data(), &d, 1, &rec, p->fp.data(), &t, (char *)buffer,
@@ -352,6 +374,7 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
     }
     analysis_context &ac = p->ac;
     fill_context(ctx, ac, base, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+    note_other(p->mc, rec);
     if (!want_an) return nullptr;   // no classifier: analysis result never valid
     return (an.flags & MFP_AN_VALID) ? &ac : nullptr;
 }

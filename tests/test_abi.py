@@ -57,17 +57,47 @@ def test_only_declared_symbols_are_exported():
     ("select=tls.client_hello;format=tls/2", oracle.SEL["tls.client_hello"], 2),
     ("select=ssh.client;", oracle.SEL["ssh.client"], 0),
     ("format=tls/1;", 0, 1),          # key=value form without select= selects nothing
-    ("tls,none", 0, 0),              # proto_identify.h:611-615
+    ("tls,none", 0, 0),              # proto_identify.h:623-627
 ])
 def test_parse_filter(cfg, sel, fmt):
     assert mercury_amd.parse_filter(cfg) == (sel, fmt)
 
 
-@pytest.mark.parametrize("cfg", ["select=tls", "quic,dns", "tls,dns", "select=tls;format=tls/9",
-                                 None, "", "all", " all ", "select=all;format=tls/1", "tls,all"])
-def test_parse_filter_rejects(cfg):
-    with pytest.raises(mercury_amd.MercuryAmdError):
-        mercury_amd.parse_filter(cfg)
+# what the reference only logs (set_protocols / set_fingerprint_format return
+# false, and mercury_init goes on, global_config.h:55-121, 246-276): an unknown
+# protocol name ends the list, an unknown format keeps the default
+@pytest.mark.parametrize("cfg,sel,fmt", [
+    ("select=tls", 0, 0),                                  # a bare list: "select=tls" is one unknown name
+    ("tls,bogus,http", oracle.SEL["tls"], 0),              # the list ends at the unknown name
+    ("tls, http", oracle.SEL["tls"], 0),                   # the last token keeps its space
+    ("select=tls;format=tls/9", oracle.SEL["tls"], 0),
+    ("select=tls;format=tls/1, quic/1", oracle.SEL["tls"], 1),   # " quic/1" keeps its space
+    ("tls,,http", oracle.SEL["tls"], 0),
+])
+def test_parse_filter_logged(cfg, sel, fmt):
+    assert mercury_amd.parse_filter(cfg) == (sel, fmt)
+    assert mercury_amd.api.parse_filter_ex(cfg)[2]        # the reference logs it
+
+
+# "all" (also the empty and the missing selection, global_config.h:248) and
+# lists naming protocols outside the path: this path's protocols run, the
+# others write no record; those whose matchers or ports come first are
+# recorded in the "other" bits (mfp_device.hpp BLK_*); in the ';' form a key no
+# option recognises is a protocol list (config_generator.cc:156-160)
+BLK_ALL = (1 << 27) - 1
+SEL_EVERY = (1 << 16) - 1
+
+
+@pytest.mark.parametrize("cfg,sel,other", [
+    ("all", SEL_EVERY, BLK_ALL), ("", SEL_EVERY, BLK_ALL), (None, SEL_EVERY, BLK_ALL),
+    ("select=all;format=tls/1", SEL_EVERY, BLK_ALL), ("tls,all", SEL_EVERY, BLK_ALL),
+    ("all;format=tls/1;reassembly", SEL_EVERY, BLK_ALL), ("select=;format=tls/1", SEL_EVERY, BLK_ALL),
+    ("tls,dns", oracle.SEL["tls"], (1 << 1) | (1 << 2)), ("quic,mdns", 1 << 10, 1 << 2),
+    ("tls,arp,icmp,tofsee", oracle.SEL["tls"], 0), ("http,rdp,telnet", oracle.SEL["http"], (1 << 13) | (1 << 19)),
+    ("all,none", 0, 0), ("tls;metadata;none", 0, 0), ("format=tls/1", 0, 0),
+])
+def test_parse_filter_other_protocols(cfg, sel, other):
+    assert mercury_amd.api.parse_filter_ex(cfg)[:2] == (sel, other)
 
 
 def test_no_cpu_fallback():
