@@ -12,9 +12,9 @@
  * reference's own libmerc (oracle/_ref/libmerc_ref.so, on the dev host) --
  * the second run pins the expected numbers to the reference.  The pcaps are
  * the reference's test pcaps, written back from tests/golden/ref_packets.npz
- * by tests/test_libmerc_fixture.py.  Test-case configurations that select
- * "all" use the protocols in scope here ("tls" / "tls,http,dtls"); every other
- * setting is the reference test's.  Prints one line per case and exits
+ * by tests/test_libmerc_fixture.py.  Every configuration is the reference
+ * test's, "all" included (its protocols outside the device path write no
+ * record, tests/test_all.py).  Prints one line per case and exits
  * non-zero when a count differs from the reference test's expectation.
  */
 #include <dlfcn.h>
@@ -118,10 +118,10 @@ static const struct tcase cases[] = {
      fingerprint_type_http, NULL, 1, 0},
     /* "test http with analysis and linktype raw" */
     {"http raw IP with analysis", "http_rawip.pcap", "http", 1, AC_TYPE, fingerprint_type_http, NULL, 9, 101},
-    /* "test linux sll2" / "test linux sll[2] with analysis" ("all" -> "tls") */
-    {"linux sll2 lines", "sll2_tls.pcap", "tls", 0, JSON_COUNT, 0, NULL, 1, 276},
-    {"linux sll2 with analysis", "sll2_tls.pcap", "tls", 1, AC_TYPE, fingerprint_type_tls, NULL, 1, 276},
-    {"linux sll with analysis", "sll_tls.pcap", "tls", 1, AC_TYPE, fingerprint_type_tls, NULL, 1, 113},
+    /* "test linux sll2" / "test linux sll[2] with analysis" */
+    {"linux sll2 lines", "sll2_tls.pcap", "all", 0, JSON_COUNT, 0, NULL, 1, 276},
+    {"linux sll2 with analysis", "sll2_tls.pcap", "all", 1, AC_TYPE, fingerprint_type_tls, NULL, 1, 276},
+    {"linux sll with analysis", "sll_tls.pcap", "all", 1, AC_TYPE, fingerprint_type_tls, NULL, 1, 113},
     /* "test SGT encapsulated TLS with analysis" */
     {"SGT TLS with analysis", "tls_sgt.pcap", "tls.client_hello", 1, AC_TYPE, fingerprint_type_tls, NULL, 58, 0},
     {"SGT TLS lines", "tls_sgt.pcap", "tls.client_hello", 1, JSON_COUNT, 0, NULL, 58, 0},
@@ -132,11 +132,11 @@ static const struct tcase cases[] = {
      fingerprint_type_dtls, "\"dtls\"", 1, 0},
     {"dtls partial fragment truncated", "dtls_fragmented_client_hello_partial.pcap", "dtls", 0, FIRST_JSON_HAS, 0,
      "\"reassembly_properties\":{\"truncated\":true", 1, 0},
-    /* "test attribute detection with analysis" ("all" -> "tls,http,dtls") */
-    {"malware_tls attributes", "malware_tls.pcap", "tls,http,dtls", 1, ATTR_COUNT, 0, NULL, 2, 0},
-    {"ipv6 domain_faking", "ipv6-domain-faking.pcap", "tls,http,dtls", 1, CHECK_ATTR, 0, "domain_faking", 1, 0},
-    {"faketls", "faketls_potatovpn.pcap", "tls,http,dtls", 1, CHECK_ATTR, 0, "faketls", 1, 0},
-    {"faketls domain_faking", "faketls_potatovpn.pcap", "tls,http,dtls", 1, CHECK_ATTR, 0, "domain_faking", 1, 0},
+    /* "test attribute detection with analysis" */
+    {"malware_tls attributes", "malware_tls.pcap", "all", 1, ATTR_COUNT, 0, NULL, 2, 0},
+    {"ipv6 domain_faking", "ipv6-domain-faking.pcap", "all", 1, CHECK_ATTR, 0, "domain_faking", 1, 0},
+    {"faketls", "faketls_potatovpn.pcap", "all", 1, CHECK_ATTR, 0, "faketls", 1, 0},
+    {"faketls domain_faking", "faketls_potatovpn.pcap", "all", 1, CHECK_ATTR, 0, "domain_faking", 1, 0},
 };
 
 static char out[1 << 16];
