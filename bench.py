@@ -171,6 +171,49 @@ def other_paths(torch, steps):
     return out
 
 
+def per_packet_shim(seconds=2.0):
+    """The libmerc per-packet API as embedders drive it (tests/c/per_packet_bench:
+    T threads, one processor each, one call per packet): write_json and
+    get_analysis_context through libmercury_amd.so at 1, 8 and 32 threads
+    (concurrent calls are combined into device batches,
+    mercury_amd/csrc/mfp_libmerc.cpp submit()), and the reference libmerc
+    beside it at 1 and 32 threads when oracle/_ref is present."""
+    from tests import pcaplib, synth
+    prog = os.path.join(ROOT, "tests", "c", "per_packet_bench")
+    if not os.path.exists(prog):
+        return None
+    a, d = synth.batch(20_000, seed=TEMPLATE_SEED["mixed"], workload="mixed", n_templates=N_TEMPLATES)
+    pk = [a[int(x["offset"]):int(x["offset"]) + int(x["caplen"])].tobytes() for x in d]
+    res = os.path.join(ROOT, "tests", "golden", "synth_resources.tgz")
+    out = {"what": "20 000 mixed packets (tests/synth.py), one processor per thread, one call per packet, "
+                   f"{seconds:.0f} s per point; analysis entry with tests/golden/synth_resources.tgz",
+           "points": []}
+    with tempfile.NamedTemporaryFile(suffix=".pcap", delete=False) as t:
+        path = t.name
+    pcaplib.write_pcap(path, pk, linktype=1)
+    try:
+        libs = [("mercury_amd", os.path.join(ROOT, "mercury_amd", "libmercury_amd.so"), (1, 8, 32))]
+        ref = os.path.join(ROOT, "oracle", "_ref", "libmerc_ref.so")
+        if os.path.exists(ref):
+            libs.append(("reference", ref, (1, 32)))
+        for name, lib, ths in libs:
+            for entry in ("json", "an"):
+                for th in ths:
+                    r = subprocess.run([prog, lib, path, CONTRACT, res if entry == "an" else "-", str(th), str(seconds),
+                                        entry], capture_output=True, timeout=seconds * 6 + 120)
+                    if r.returncode != 0:
+                        out["points"].append({"lib": name, "entry": entry, "threads": th,
+                                              "error": r.stderr.decode(errors="replace")[-300:]})
+                        continue
+                    x = json.loads(r.stdout.decode().strip().splitlines()[-1])
+                    out["points"].append({"lib": name, "entry": x["entry"], "threads": th,
+                                          "kpkt_s": round(x["pps"] / 1e3, 2), "lat_us_p50": x["lat_us_p50"],
+                                          "lat_us_p99": x["lat_us_p99"]})
+    finally:
+        os.unlink(path)
+    return out
+
+
 def cpu_threads():
     """Host threads for the CPU baseline: one GPU's share of the host's cores
     (nproc / 8 on an 8-GPU node), within the cores this process may use."""
@@ -779,6 +822,12 @@ def main():
             log(f"[rank {rank}] end-to-end leg failed: {e}")
             if tdist:
                 raise
+    shim = None
+    if world == 1 and not args.no_other_paths:
+        try:
+            shim = per_packet_shim()
+        except Exception as e:   # reported beside the headline, never instead of it
+            log(f"per-packet shim leg failed: {e}")
     others = None
     if world == 1 and not args.no_other_paths:
         try:
@@ -871,6 +920,7 @@ def main():
             "analysis_counters": an_counters,
             "end_to_end": e2e,
             "other_paths": others,
+            "per_packet_shim": shim,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -993,12 +993,17 @@ extern "C" MFP_EXPORT int mfp_analysis_resolve(mfp_context c, const mfp_sighting
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
     if (u && !d) { mfp_set_error("mfp_analysis_resolve: null decisions"); return -1; }
-    {   // one decision per distinct entry of the pending batch (the resolve kernel indexes them by position)
-        std::vector<mfp_sighting> have;
-        const long long cnt = slot_distinct(c, *S, have);
-        if (cnt < 0) return (int)cnt;
-        if ((size_t)cnt != u) {
-            mfp_set_error("mfp_analysis_resolve: %zu decisions, the batch has %lld distinct fingerprints", u, cnt);
+    {   // one decision per distinct entry of the pending batch (the resolve kernel
+        // indexes them by position): the sighting table's counters say how many
+        unsigned int cnt[4];
+        HIPCHK(hipMemcpyAsync(cnt, S->seen.counters, sizeof cnt, hipMemcpyDeviceToHost, S->pend.stream));
+        HIPCHK(hipStreamSynchronize(S->pend.stream));
+        if (cnt[1] || cnt[0] > S->seen.list_cap) {
+            mfp_set_error("mfp_analysis_resolve: the batch's sighting table overflowed (use the sequence form)");
+            return -3;
+        }
+        if ((size_t)cnt[0] != u) {
+            mfp_set_error("mfp_analysis_resolve: %zu decisions, the batch has %u distinct fingerprints", u, cnt[0]);
             return -1;
         }
     }

@@ -5,6 +5,7 @@
 // /root/reference/src/libmerc/.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -33,6 +34,9 @@ struct mercury {
     // (MFP_MSG_OTHER, e.g. under "all"): they write no record; counted, and
     // logged once per context
     std::atomic<uint64_t> other{0};
+    // concurrent per-packet calls on this context are combined into one device
+    // batch per entry point (see submit())
+    struct Combiner *comb[2] = {nullptr, nullptr};
 };
 
 struct analysis_context {       // the fields libmerc's accessors read (result.h:174-420)
@@ -74,7 +78,8 @@ static int stderr_err(enum log_level level, const char *format, va_list args) {
     const int s = std::vfprintf(stderr, format, args);
     return s < 0 ? s : r + s;
 }
-static int silent_err(enum log_level, const char *, va_list) { return 0; }   // silent_err_func printf_err.hpp:47
+static int silent_err(enum log_level, const char *, va_list) { return 0; }
+static void free_combiners(mercury *m);   // silent_err_func printf_err.hpp:47
 
 static printf_err_ptr g_printf_err = stderr_err;
 
@@ -149,6 +154,7 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
 MFP_EXPORT int mercury_finalize(mercury_context mc) {
     if (!mc) return -1;
     for (auto &c : mc->ctx) if (c) mfp_finalize(c);
+    free_combiners(mc);
     if (mc->prev) mfp_prevalence_destroy(mc->prev);
     delete mc;
     return 0;
@@ -258,6 +264,161 @@ static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *p
     }
 }
 
+// ts->tv_sec == 0: the reference writes the time of tsc_clock, the TSC in
+// seconds (pkt_proc.cc:1086-1089, 1619-1622; tsc_clock.hpp:64-70) -- the
+// seconds since the counter started, not wall time; tv_nsec is left alone.
+// CLOCK_MONOTONIC counts from the same start (boot).
+static void fill_zero_ts(struct timespec *ts) {
+    if (!ts || ts->tv_sec != 0) return;
+    struct timespec m;
+    clock_gettime(CLOCK_MONOTONIC, &m);
+    ts->tv_sec = (time_t)((double)m.tv_sec + 1e-9 * (double)m.tv_nsec + 0.5);
+}
+
+// ---------------------------------------------------------------------------
+// Combining: libmerc's API is one packet per call, one processor per thread
+// (libmerc.h:227-231).  Each call on the device path is a batch of its own --
+// a copy in, a dozen kernel launches, a copy out -- so concurrent calls of
+// different processors are combined: a call queues its packet; the first
+// caller to find no batch in flight becomes the leader, takes every queued
+// packet (its own included), runs them as one batch on the shared context and
+// completes each caller's result; callers that arrive meanwhile wait and form
+// the next batch.  One thread calling alone pays one batch per packet, N
+// threads share batches of up to N packets.  Batches keep the arrival order,
+// which orders the fingerprint-prevalence LRU updates as the reference's shared
+// classifier sees concurrent calls.  (Processors with "reassembly" keep their
+// own flow table and run their packets one by one.)
+// ---------------------------------------------------------------------------
+struct Req {
+    const uint8_t *pkt;
+    size_t len;
+    uint16_t linktype;
+    uint64_t t_ns;
+    analysis_context *ac;       // the processor's context, filled by the leader
+    void *buf;                  // write_json: the caller's buffer (nullptr: analysis entry)
+    size_t buf_size;
+    size_t out_len = 0;         // write_json: bytes written (0: none)
+    bool valid = false;         // analysis entry: MFP_AN_VALID
+    bool err = false;
+    bool done = false;
+};
+
+struct Combiner {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<Req *> q;
+    bool busy = false;
+    // the leader's batch buffers (one leader at a time)
+    std::vector<uint8_t> arena;
+    std::vector<mfp_pkt_desc> desc;
+    std::vector<mfp_record> rec;
+    std::vector<char> fp;
+    std::vector<mfp_analysis> an;
+    std::vector<double> ap;
+    std::vector<uint64_t> ts, ends;
+    std::vector<char> out;
+};
+
+static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req *> &batch, bool json_entry) {
+    const size_t n = batch.size();
+    C.arena.clear();
+    C.desc.resize(n);
+    C.ts.resize(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; i++) {
+        const Req &r = *batch[i];
+        C.desc[i] = mfp_pkt_desc{(uint64_t)C.arena.size(), (uint32_t)r.len, r.linktype, 0};
+        C.arena.insert(C.arena.end(), r.pkt, r.pkt + r.len);
+        C.arena.resize((C.arena.size() + 15) & ~(size_t)15);   // 16-byte aligned packets
+        C.ts[i] = r.t_ns;
+        total += r.len;
+    }
+    C.arena.resize(C.arena.size() + 16);
+    const bool want_an = mfp_analysis_enabled(ctx);
+    const size_t cap = mfp_fp_arena_bound(n, total);
+    C.rec.resize(n);
+    C.fp.resize(cap);
+    if (want_an) { C.an.resize(n); C.ap.assign(n * MFP_ATTR_DB_TAGS, 0.0); }
+    const long long used = mfp_process_batch_host_ex(ctx, C.arena.data(), C.arena.size(), C.desc.data(), n, C.rec.data(),
+                                                     C.fp.data(), cap, want_an ? C.an.data() : nullptr,
+                                                     want_an ? C.ap.data() : nullptr);
+    if (used < 0) {
+        log_error("%s\n", mfp_last_error());
+        for (Req *r : batch) r->err = true;
+        return;
+    }
+    for (size_t i = 0; i < n; i++) {
+        Req &r = *batch[i];
+        fill_context(ctx, *r.ac, C.arena.data() + C.desc[i].offset, C.rec[i], C.fp.data(),
+                     want_an ? &C.an[i] : nullptr, want_an ? &C.ap[i * MFP_ATTR_DB_TAGS] : nullptr);
+        note_other(m, C.rec[i]);
+        r.valid = want_an && (C.an[i].flags & MFP_AN_VALID);
+    }
+    if (!json_entry) return;
+    C.ends.resize(n);
+    if (C.out.size() < ((size_t)1 << 16) + 64 * total) C.out.resize(((size_t)1 << 16) + 64 * total);
+    uint64_t skipped = 0;
+    long long w;
+    while (true) {
+        w = want_an ? mfp_write_json_batch_analysis(ctx, C.arena.data(), C.desc.data(), n, C.rec.data(), C.fp.data(),
+                                                    C.an.data(), C.ap.data(), C.ts.data(), C.out.data(), C.out.size(),
+                                                    C.ends.data(), &skipped, 1)
+                    : mfp_write_json_batch(C.arena.data(), C.desc.data(), n, C.rec.data(), C.fp.data(), C.ts.data(),
+                                           C.out.data(), C.out.size(), C.ends.data(), &skipped, 1);
+        if (w != -2) break;
+        C.out.resize(C.out.size() * 2);
+    }
+    if (w < 0) {
+        log_error("%s\n", mfp_last_error());
+        for (Req *r : batch) r->err = true;
+        return;
+    }
+    for (size_t i = 0; i < n; i++) {
+        Req &r = *batch[i];
+        const size_t b = i ? (size_t)C.ends[i - 1] : 0, e = (size_t)C.ends[i];
+        if (e == b && (C.rec[i].flags & MFP_FLAG_EMIT) && skipped) {
+            // the reference writes a record here; the writer could not rebuild it
+            // (an encapsulation chain the host walk cannot follow): say so
+            const uint8_t mg = C.rec[i].msg;
+            log_error("write_json: record not rebuilt by the MI355X JSON writer (%s)\n",
+                      mg == MFP_MSG_QUIC ? "QUIC Initial" : mg == MFP_MSG_STUN ? "STUN message"
+                      : mg == MFP_MSG_OPENVPN ? "OpenVPN record" : "encapsulation chain");
+        }
+        // buffer_stream keeps one byte for its NUL (pkt_proc.cc:1249-1253)
+        if (e > b && e - b < r.buf_size) { memcpy(r.buf, C.out.data() + b, e - b); r.out_len = e - b; }
+    }
+}
+
+static void free_combiners(mercury *m) {
+    for (Combiner *&cb : m->comb) { delete cb; cb = nullptr; }
+}
+
+static void submit(mercury *m, mfp_context ctx, int mode, Req &r) {
+    Combiner *C;
+    {
+        std::lock_guard<std::mutex> lk(m->mu);
+        if (!m->comb[mode]) m->comb[mode] = new Combiner;
+        C = m->comb[mode];
+    }
+    std::unique_lock<std::mutex> lk(C->m);
+    C->q.push_back(&r);
+    while (!r.done) {
+        if (!C->busy) {
+            C->busy = true;
+            std::vector<Req *> batch;
+            batch.swap(C->q);
+            lk.unlock();
+            run_batch(m, ctx, *C, batch, mode == MFP_MODE_WRITE_JSON);
+            lk.lock();
+            for (Req *x : batch) x->done = true;
+            C->busy = false;
+            C->cv.notify_all();
+        } else {
+            C->cv.wait(lk);
+        }
+    }
+}
+
 // write_json libmerc.cc:131-175 -> stateful_pkt_proc::write_json pkt_proc.cc:1256-1383: the record text
 // from a one-packet batch (device walk, --analysis classification, mfp_write_json_batch[_analysis]).
 // Returns 0 when nothing is written or the record does not fit buf_size (buffer_stream truncation,
@@ -268,7 +429,13 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
     if (!p || !buffer || !pkt || !ts) return 0;
     mfp_context ctx = get_ctx(p->mc, MFP_MODE_WRITE_JSON);
     if (!ctx) return 0;
-    if (ts->tv_sec == 0) clock_gettime(CLOCK_REALTIME, ts);   // pkt_proc.cc:1086-1089
+    fill_zero_ts(ts);
+    if (!mfp_reassembly_enabled(ctx)) {
+        Req r{pkt, len, linktype, (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec, &p->ac, buffer,
+              buffer_size};
+        submit(p->mc, ctx, MFP_MODE_WRITE_JSON, r);
+        return r.err ? 0 : r.out_len;
+    }
     p->arena.assign(pkt, pkt + len);
     p->arena.resize(len + 16);
     mfp_pkt_desc d{0, (uint32_t)len, linktype, 0};
@@ -336,6 +503,13 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
     if (!p || !pkt) return nullptr;
     mfp_context ctx = get_ctx(p->mc, MFP_MODE_ANALYSIS);
     if (!ctx) return nullptr;
+    fill_zero_ts(ts);
+    if (!mfp_reassembly_enabled(ctx)) {
+        Req r{pkt, len, linktype, ts ? (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec : 0, &p->ac,
+              nullptr, 0};
+        submit(p->mc, ctx, MFP_MODE_ANALYSIS, r);
+        return r.valid ? &p->ac : nullptr;
+    }
     p->arena.assign(pkt, pkt + len);
     p->arena.resize(len + 16);
     mfp_pkt_desc d{0, (uint32_t)len, linktype, 0};
@@ -350,7 +524,6 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
         // analyze_ip_packet with the processor's reassembler (pkt_proc.cc:1597-1662):
         // the flow table in stream order, flow_state_pkts_needed per packet
         if (!p->reasm) p->reasm = mfp_reassembler_create();
-        if (ts && ts->tv_sec == 0) clock_gettime(CLOCK_REALTIME, ts);   // pkt_proc.cc:1619-1622
         const uint64_t t = ts ? (uint64_t)ts->tv_sec * 1000000000ull + (uint64_t)ts->tv_nsec : 0;
         cap += mfp_fp_arena_bound(1, 8192 + 256);
         p->fp.resize(cap);

@@ -23,6 +23,7 @@
 //     rebuilt from the sightings before it (lru_at) and the decisions are the
 //     single pass's.
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <unordered_set>
 #include <cstring>
@@ -144,10 +145,16 @@ struct Lru {
 // The set after the accesses hash[0..end) applied to a set whose keys are
 // `init` (least to most recent): an LRU holds exactly the `cap` most recently
 // accessed distinct keys, in recency order, so it is rebuilt by walking back
-// from end-1 (then into init) until `cap` distinct keys are found.
-void lru_at(Lru &L, const uint64_t *hash, size_t end, const std::vector<uint64_t> &init) {
-    for (size_t i = end; i-- > 0 && L.size < L.cap;) L.append_lru(hash[i]);
-    for (size_t i = init.size(); i-- > 0 && L.size < L.cap;) L.append_lru(init[i]);
+// from end-1 (then into init) until `cap` distinct keys are found.  The walk
+// over the sequence stops after `budget` entries (a prefix of mostly repeated
+// hot keys): false then, and the caller takes the set another way.
+bool lru_at(Lru &L, const uint64_t *hash, size_t end, const std::vector<uint64_t> &init, size_t budget) {
+    const size_t stop = end > budget ? end - budget : 0;
+    size_t i = end;
+    for (; i-- > stop && L.size < L.cap;) L.append_lru(hash[i]);
+    if (L.size < L.cap && stop > 0) return false;
+    for (size_t j = init.size(); j-- > 0 && L.size < L.cap;) L.append_lru(init[j]);
+    return true;
 }
 
 }  // namespace
@@ -216,24 +223,39 @@ MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t 
         return 0;
     }
     // chunk t decides hash[s_t..e_t) with its own LRU set up as the shared one
-    // would be at s_t (lru_at): the same decisions as one pass, in parallel
+    // would be at s_t (lru_at): the same decisions as one pass, in parallel.
+    // A chunk whose walk back runs past its budget (4 chunk lengths) takes the
+    // previous chunk's finished set instead; the last chunk's set is the set
+    // after the whole sequence.
     std::vector<uint64_t> init;
     L.export_keys(init);
+    std::vector<Lru> sets(T, Lru(1));
+    std::vector<uint8_t> done(T, 0);
+    std::mutex dmu;
+    std::condition_variable dcv;
     std::vector<std::thread> th;
     for (size_t t = 0; t < T; t++)
         th.emplace_back([&, t]() {
             const size_t s = m * t / T, e = m * (t + 1) / T;
             Lru C(L.cap);
-            lru_at(C, hash, s, init);
+            if (t > 0 && !lru_at(C, hash, s, init, 4 * (e - s))) {
+                std::unique_lock<std::mutex> lk(dmu);
+                dcv.wait(lk, [&] { return done[t - 1] != 0; });
+                C = sets[t - 1];
+            } else if (t == 0) {
+                lru_at(C, hash, 0, init, 0);
+            }
             for (size_t j = s; j < e; j++) {
                 if (j + 8 < e) C.prefetch(hash[j + 8]);
                 seen[j] = C.access(hash[j]) ? 1 : 0;
             }
+            std::lock_guard<std::mutex> lk(dmu);
+            sets[t] = std::move(C);
+            done[t] = 1;
+            dcv.notify_all();
         });
-    Lru F(L.cap);                                  // the set after the whole sequence
-    lru_at(F, hash, m, init);
     for (auto &x : th) x.join();
-    std::swap(L, F);
+    std::swap(L, sets[T - 1]);
     return 0;
 }
 

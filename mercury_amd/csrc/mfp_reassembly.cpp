@@ -452,6 +452,12 @@ static void dtls_fragment(mfp_reassembler R, size_t i, const uint8_t *arena, con
     if (frag_off == 0 && !more_bytes) return;                        // a complete message
     if ((uint64_t)frag_len + more_bytes > kMaxData) return;         // beyond the buffer
     if (s.pay_off < 33 || (uint64_t)s.pay_off + frag_len > desc[i].caplen) return;
+    {   // rebuild() writes a UDP length 8 bytes before the fragment's record:
+        // only a handshake record right behind the UDP header takes part
+        const uint32_t ip = r.net & 0xffff, ipv = (r.net >> 16) & 15;
+        const uint32_t ip_end = ip + (ipv == 4 ? 4u * (pkt[ip] & 15u) : 40u);
+        if (pkt[s.pay_off - 25] != 22 || s.pay_off - 33 < ip_end) return;
+    }
     FlowKey k;
     if (!flow_key(pkt, desc[i].caplen, r, k, 17)) return;
     const uint8_t cid[2] = {pkt[s.pay_off - 8], pkt[s.pay_off - 7]};   // message_seq, big-endian (dtls.h:119)
