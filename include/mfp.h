@@ -390,6 +390,8 @@ typedef struct {
 MFP_EXPORT mfp_prevalence mfp_prevalence_create(uint32_t capacity);   /* the reference: 100000 */
 MFP_EXPORT void mfp_prevalence_destroy(mfp_prevalence p);
 MFP_EXPORT uint64_t mfp_prevalence_size(mfp_prevalence p);
+/* the capacity it was created with */
+MFP_EXPORT uint32_t mfp_prevalence_capacity(mfp_prevalence p);
 MFP_EXPORT int mfp_prevalence_contains(mfp_prevalence p, uint64_t hash);
 /* the set from least to most recently used (hashes); returns its size */
 MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t cap);
@@ -401,6 +403,21 @@ MFP_EXPORT int mfp_prevalence_distinct_exact(mfp_prevalence p, const mfp_sightin
 MFP_EXPORT int mfp_prevalence_resolve_distinct(mfp_prevalence p, mfp_sighting *d, size_t u);
 /* every sighting in stream order: seen[j] = 1 when hash[j] was in the LRU */
 MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen);
+/* Shards decided where they lie (each rank its own sightings; the set at a
+ * shard's start follows from the shards before it by their summaries):
+ *   summary: the distinct hashes of hash[0..m) by last sighting, most recent
+ *     first, at most the capacity (out holds capacity entries); returns the count;
+ *   resolve_shard: decide hash[0..m) from the set that `prior` (the earlier
+ *     shards' summaries, the nearest shard's first) leaves on top of p's set;
+ *     p is not changed;
+ *   advance: p becomes the set after a step of shards (`recent` = every
+ *     shard's summary, the last shard's first).
+ * Over shards in stream order these equal mfp_prevalence_resolve_sequence
+ * over the concatenation. */
+MFP_EXPORT long long mfp_prevalence_summary(mfp_prevalence p, const uint64_t *hash, size_t m, uint64_t *out);
+MFP_EXPORT int mfp_prevalence_resolve_shard(mfp_prevalence p, const uint64_t *hash, size_t m, const uint64_t *prior,
+                                            size_t nprior, uint8_t *seen);
+MFP_EXPORT int mfp_prevalence_advance(mfp_prevalence p, const uint64_t *recent, size_t n);
 
 /* the context's own LRU (created with the classifier) */
 MFP_EXPORT mfp_prevalence mfp_analysis_prevalence(mfp_context ctx);

@@ -180,6 +180,14 @@ def load_library():
     lib.mfp_prevalence_resolve_distinct.argtypes = [vp, vp, sz]
     lib.mfp_prevalence_resolve_sequence.restype = ctypes.c_int
     lib.mfp_prevalence_resolve_sequence.argtypes = [vp, vp, sz, vp]
+    lib.mfp_prevalence_capacity.restype = ctypes.c_uint32
+    lib.mfp_prevalence_capacity.argtypes = [vp]
+    lib.mfp_prevalence_summary.restype = ctypes.c_longlong
+    lib.mfp_prevalence_summary.argtypes = [vp, vp, sz, vp]
+    lib.mfp_prevalence_resolve_shard.restype = ctypes.c_int
+    lib.mfp_prevalence_resolve_shard.argtypes = [vp, vp, sz, vp, sz, vp]
+    lib.mfp_prevalence_advance.restype = ctypes.c_int
+    lib.mfp_prevalence_advance.argtypes = [vp, vp, sz]
     lib.mfp_analysis_prevalence.restype = vp
     lib.mfp_analysis_prevalence.argtypes = [vp]
     lib.mfp_analysis_set_prevalence.restype = ctypes.c_int
@@ -570,6 +578,39 @@ class Prevalence:
         if self.lib.mfp_prevalence_resolve_sequence(self.h, h.ctypes.data, len(h), seen.ctypes.data) != 0:
             raise MercuryAmdError(_err(self.lib))
         return seen[:len(h)]
+
+    @property
+    def capacity(self):
+        return int(self.lib.mfp_prevalence_capacity(self.h))
+
+    def summary(self, hashes):
+        """The distinct hashes of one shard's sightings by last sighting, most
+        recent first, at most the capacity (mfp_prevalence_summary)."""
+        h = np.ascontiguousarray(hashes, np.uint64)
+        out = np.zeros(max(self.capacity, 1), np.uint64)
+        k = self.lib.mfp_prevalence_summary(self.h, h.ctypes.data, len(h), out.ctypes.data)
+        if k < 0:
+            raise MercuryAmdError(_err(self.lib))
+        return out[:k]
+
+    def resolve_shard(self, hashes, prior):
+        """Decide one shard's sightings from the set the earlier shards'
+        summaries (`prior`, the nearest shard's first) leave on top of this
+        set; the set itself is not changed."""
+        h = np.ascontiguousarray(hashes, np.uint64)
+        pr = np.ascontiguousarray(prior, np.uint64)
+        seen = np.zeros(max(len(h), 1), np.uint8)
+        if self.lib.mfp_prevalence_resolve_shard(self.h, h.ctypes.data, len(h), pr.ctypes.data, len(pr),
+                                                 seen.ctypes.data) != 0:
+            raise MercuryAmdError(_err(self.lib))
+        return seen[:len(h)]
+
+    def advance(self, recent):
+        """This set becomes the set after a step of shards (`recent`: every
+        shard's summary, the last shard's first)."""
+        r = np.ascontiguousarray(recent, np.uint64)
+        if self.lib.mfp_prevalence_advance(self.h, r.ctypes.data, len(r)) != 0:
+            raise MercuryAmdError(_err(self.lib))
 
     def distinct_exact(self, sightings):
         d = np.ascontiguousarray(sightings, SIGHTING_DTYPE)

@@ -244,12 +244,16 @@ DEV uint32_t c_tolower(uint32_t c) { return c_isupper(c) ? c + 32 : c; }
 constexpr uint32_t FP_MAX = 8192;   // fingerprint::MAX_FP_STR_LEN fingerprint.h:15
 
 struct TlsPlan;
-template <bool EMIT>
+// FAST >= 0 (k_fp_tls1, TLS format FAST): pass 1 records the ClientHello plan
+// with the string's length by arithmetic (tls_ch_plan_fast), pass 2 emits it
+// with tls_ch_emit_fast
+template <bool EMIT, int FAST_FMT = -1>
 struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
     bool punt = false;       // the message needs a parser family this walker lacks
     DEV void punt_pkt() { punt = true; }
+    static constexpr int FAST = FAST_FMT;
     static constexpr bool PLAN = !EMIT;   // pass 1 records a ClientHello plan (TlsPlan) in *plan
     TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
@@ -1090,6 +1094,173 @@ DEV void tls_ch_emit(E &b, TlsPlan &pl) {
     b.putc(fmt == 0 ? ')' : ']');
 }
 
+// ---------------------------------------------------------------------------
+// The ClientHello plan with the length by arithmetic, and a uniform emitter
+// (k_fp_tls1).  The lanes of a wave hold different ClientHellos: the general
+// emitter's per-type branches (ext_fp0 / ext_fp1) run for the union of the
+// wave's extension types, byte pushes at a time.  Here every extension takes
+// the same instructions -- one 4-byte header load, a head word of up to 9
+// characters made branch-free, then the value as runs of 4 bytes -> 8 hex
+// characters -- so a wave's cost follows its longest string, not the union of
+// its paths.  The characters are tls_client_hello::fingerprint's (tls.h:1928-
+// 1964; extensions: tls_extensions::fingerprint tls.h:1549-1613 for format 0,
+// fingerprint_format1 tls.h:1413-1470 for formats 1/2).  QUIC transport
+// parameters (0x39, 0xffa5) leave the plan unset: the fallback lane writes them.
+// ---------------------------------------------------------------------------
+DEV bool static_ext_bit(uint32_t t) {                   // static_extension_types tls.h:1000
+    constexpr uint64_t M = (1ull << 1) | (1ull << 5) | (1ull << 7) | (1ull << 8) | (1ull << 9) | (1ull << 10) |
+                           (1ull << 11) | (1ull << 13) | (1ull << 15) | (1ull << 16) | (1ull << 17) | (1ull << 24) |
+                           (1ull << 27) | (1ull << 28) | (1ull << 43) | (1ull << 45) | (1ull << 50) | (1ull << 57);
+    return t < 64 ? ((M >> t) & 1) != 0 : (t == 21760 || t == 0xffa5);
+}
+// characters an extension adds (ext_fp0 / ext_fp1 agree on every length)
+DEV uint32_t ext_fp_len(uint32_t t, uint32_t vl) {
+    if (!static_ext_bit(t)) return 6;                   // "(" type ")"
+    if (t == 0x000a || t == 0x002b) {                   // ext_degreased_value tls.h:1513 (client role)
+        const uint32_t ung = t == 0x000a ? 2u : 1u;
+        const uint32_t skip = vl < ung ? vl : ung;
+        return 10 + 2 * skip + 2 * ((vl - skip) & ~1u);
+    }
+    return 10 + 2 * vl;                                  // "(" type length value ")"
+}
+template <int FMT, class E>
+DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const uint8_t *base,
+                          uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len) {
+    pl.ok = false;
+    // type prefix, "1/" or "2/", "(" version ")" "(" degreased ciphers ")", "(" or "[", ... ")" or "]"
+    uint32_t n = (type == 10 ? 5u : 4u) + (FMT ? 2u : 0u) + 2 + 2 * (uint32_t)clen(ch.version) + 2 +
+                 2 * ((uint32_t)clen(ch.ciphers) & ~1u) + 2;
+    uint64_t V[REG_EXT];                         // format 0: offsets; 1/2: key << 32 | offset
+#pragma unroll
+    for (int k = 0; k < REG_EXT; k++) V[k] = ~0ull;
+    int cnt = 0;
+    bool rare = false;
+    Cur p = ch.extensions;
+    while (clen(p) > 0) {
+        const uint8_t *start = p.d;
+        Ext x = ext_parse(p);
+        if (!x.ok) break;
+        if (x.type == 0) {                       // server_name: bytes after the 9-byte header (tls.h:1342)
+            Cur e = cmk(start, p.d);
+            cskip(e, 9);
+            sni_off = (uint32_t)(e.d - base); sni_len = (uint32_t)clen(e);
+        }
+        if (x.type == 16) tls_alpn(start, p.d, base, alpn_off, alpn_len);
+        if (rare) continue;
+        int bucket = 0;
+        if (FMT == 2) {
+            bucket = fmt2_bucket(x);
+            if (bucket < 0) continue;
+            int c3 = 0;                          // first three per bucket (tls.h:1695-1701)
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) c3 += (V[k] != ~0ull && (uint32_t)(V[k] >> 56) == (uint32_t)bucket);
+            if (c3 >= 3) continue;
+        }
+        if (cnt >= REG_EXT || x.type == 0x39 || x.type == 0xffa5) { rare = true; continue; }
+        const uint32_t off = (uint32_t)(start - ch.extensions.d);
+        if (FMT == 0) {
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) if (k == cnt) V[k] = off;
+        } else {
+            const uint32_t key = ext_key(x, FMT, bucket);
+            const uint64_t v = ((uint64_t)key << 32) | off;
+            uint32_t pos = 0;
+            bool tie = false;
+#pragma unroll
+            for (int k = 0; k < REG_EXT; k++) {
+                pos += V[k] < v ? 1u : 0u;
+                tie |= (uint32_t)(V[k] >> 32) == key;
+            }
+            if (tie && !key_is_grease(key, FMT)) rare = true;
+#pragma unroll
+            for (int k = REG_EXT - 1; k > 0; k--)
+                V[k] = (uint32_t)k > pos ? V[k - 1] : ((uint32_t)k == pos ? v : V[k]);
+            if (pos == 0) V[0] = v;
+        }
+        n += ext_fp_len(x.type, (uint32_t)clen(x.value));
+        cnt++;
+    }
+    b.n = n;
+    b.last_putc = true;                          // the string ends with ")" or "]"
+    if (rare) return;
+#pragma unroll
+    for (int k = 0; k < REG_EXT / 2; k++) pl.O[k] = ((uint32_t)V[2 * k] & 0xffff) | ((uint32_t)V[2 * k + 1] << 16);
+    pl.version = ch.version; pl.ciphers = ch.ciphers; pl.exts = ch.extensions;
+    pl.n = (uint32_t)cnt; pl.type = type; pl.fmt = (uint32_t)FMT;
+    pl.ok = true;
+}
+// degrease_uint16 (tls.h:776) of the two byte pairs of a little-endian word
+// (pair = bytes 0,1 and 2,3, the first byte the high one)
+DEV uint32_t degrease_pairs(uint32_t le) {
+    const uint32_t b0 = le & 0xff, b1 = (le >> 8) & 0xff, b2 = (le >> 16) & 0xff, b3 = le >> 24;
+    const uint32_t lo = (b0 == b1 && (b0 & 15) == 10) ? 0x0a0au : (le & 0xffff);
+    const uint32_t hi = (b2 == b3 && (b2 & 15) == 10) ? 0x0a0au : (le >> 16);
+    return lo | (hi << 16);
+}
+DEV uint64_t low_chars(uint64_t v, uint32_t k) { return k >= 8 ? v : (v & ((1ull << (8 * k)) - 1)); }
+// raw_as_hex (buffer_stream.h:1087) / raw_as_hex_degrease (tls.h:802, len
+// even) of p[0, len), 4 bytes -> 8 characters per push
+template <bool DEGREASE, class E>
+DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
+    if (len == 0) return;
+    LeStream s;
+    s.init(p, (long)len);
+    for (uint32_t i = 0; i < len; i += 4) {
+        uint32_t w = s.next();
+        if (DEGREASE) w = degrease_pairs(w);
+        const uint32_t k = len - i >= 4 ? 8u : 2 * (len - i);
+        b.push(low_chars(hex4(w), k), k);
+    }
+}
+template <int FMT, class E>
+DEV void tls_ch_emit_fast(E &b, TlsPlan &pl) {
+    if (pl.type == 10) b.push(0x2f736c7464ull, 5);                         // "dtls/"
+    else b.push(0x2f736c74ull, 4);                                          // "tls/"
+    if (FMT) b.push((uint64_t)('0' + FMT) | ((uint64_t)'/' << 8), 2);
+    {   // "(" version ")(": the version is 2 bytes (tls_ch_parse parsed it whole)
+        const uint32_t v = ld_be32n(pl.version.d, 2);
+        const uint64_t hx = hex4(__builtin_bswap32(v << 16));
+        b.push('(' | ((hx & 0xffffffffull) << 8) | ((uint64_t)')' << 40) | ((uint64_t)'(' << 48), 7);
+    }
+    hex_run<true>(b, pl.ciphers.d, (uint32_t)clen(pl.ciphers) & ~1u);
+    b.push(')' | ((FMT ? '[' : '(') << 8), 2);
+    for (uint32_t j = 0; j < pl.n; j++) {
+        const uint32_t off = pl.O[0] & 0xffff;
+#pragma unroll
+        for (int k = 0; k < REG_EXT / 2; k++)             // pop the front offset
+            pl.O[k] = (pl.O[k] >> 16) | (k + 1 < REG_EXT / 2 ? pl.O[k + 1] << 16 : 0u);
+        const uint8_t *h = pl.exts.d + off;
+        const uint32_t th = ld_be32n(h, 4);                // type << 16 | length (the plan kept whole extensions)
+        const uint32_t t = th >> 16, vl = th & 0xffff;
+        const bool st = static_ext_bit(t);
+        uint32_t w;                                        // head: type, length as a little-endian word
+        if (FMT == 0) {
+            w = degrease_pairs(__builtin_bswap32(th));     // hex_degrease of type and length (tls.h:1560-1600)
+        } else {
+            uint32_t enc = ext_is_grease(t) ? 0x0a0au : t;  // tls_extension::encoded_type (tls.h:1390)
+            if (FMT == 2) fmt2_bucket_t(t, enc);
+            w = ((enc >> 8) & 0xff) | ((enc & 0xff) << 8) | (degrease_pairs(__builtin_bswap32(th)) & 0xffff0000u);
+        }
+        const uint64_t hx = hex4(w);
+        // static: "(" + 8 head characters (+ value + ")"); other: "(" type ")"
+        b.push(st ? ('(' | (hx << 8)) : ('(' | ((hx & 0xffffffffull) << 8) | ((uint64_t)')' << 40)), st ? 8u : 6u);
+        if (st) {
+            b.push(hx >> 56, 1);
+            uint32_t skip = vl, gl = 0;
+            if (t == 0x000a || t == 0x002b) {              // ext_degreased_value tls.h:1513
+                const uint32_t ung = t == 0x000a ? 2u : 1u;
+                skip = vl < ung ? vl : ung;
+                gl = (vl - skip) & ~1u;
+            }
+            hex_run<false>(b, h + 4, skip);
+            hex_run<true>(b, h + 4 + skip, gl);
+            b.push(')', 1);
+        }
+    }
+    b.push(FMT ? ']' : ')', 1);
+    b.last_putc = true;
+}
+
 struct Sh { Cur version, cipher, extensions; };
 DEV Sh tls_sh_parse(Cur &rec) {                         // parse_tls_server_hello tls.h:2097
     Sh s; cset_null(s.version); cset_null(s.cipher); cset_null(s.extensions);
@@ -1653,7 +1824,10 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 1;
         if (clen(ch.ciphers) <= 0) o.flags |= MFP_FLAG_NO_CIPHERS;   // no "tls" object (tls.h:1882-1885)
         if constexpr (E::PLAN) {
-            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+            if constexpr (E::FAST >= 0)
+                tls_ch_plan_fast<E::FAST>(b, *b.plan, ch, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+            else
+                tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
         } else {
             fp_type_prefix(b, 1);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
@@ -1939,7 +2113,10 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 10;
         if (clen(ch.ciphers) <= 0) o.flags |= MFP_FLAG_NO_CIPHERS;   // no "dtls" object (tls.h:1882-1885)
         if constexpr (E::PLAN) {
-            tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+            if constexpr (E::FAST >= 0)
+                tls_ch_plan_fast<E::FAST>(b, *b.plan, ch, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+            else
+                tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
         } else {
             fp_type_prefix(b, 10);
             tls_ch_fp(b, ch, (int)cfg.tls_format);

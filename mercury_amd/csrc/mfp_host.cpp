@@ -328,6 +328,11 @@ struct Slot {
     uint8_t *d_seen_bits = nullptr; size_t cap_seen_bits = 0; // decisions per distinct / per sighting
     uint32_t *d_group_off = nullptr; size_t cap_group_off = 0;
     uint64_t *d_seq = nullptr; size_t cap_seq = 0;
+    // pinned host side of the decision round trip: the sightings in stream
+    // order (D2H), the per-group sighting bitmap (D2H), the decisions (H2D)
+    uint64_t *h_seq = nullptr; size_t cap_h_seq = 0;
+    uint64_t *h_gbits = nullptr; size_t cap_h_gbits = 0;
+    uint8_t *h_dec = nullptr; size_t cap_h_dec = 0;
     // the batch whose statuses wait for a decision (deferred, or pipelined until retire)
     struct Pending {
         bool live = false;
@@ -358,7 +363,7 @@ struct Slot {
                      d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
-        if (h_used) (void)hipHostFree(h_used);
+        for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec}) if (x) (void)hipHostFree(x);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -489,6 +494,17 @@ static int grow(T *&p, size_t &cap, size_t need) {
     return 0;
 }
 
+template <class T>
+static int grow_pinned(T *&p, size_t &cap, size_t need) {
+    if (need <= cap) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    size_t nc = std::max(need, cap + cap / 2);
+    if (hipHostMalloc((void **)&p, nc * sizeof(T), hipHostMallocDefault) != hipSuccess) { cap = 0; return -1; }
+    cap = nc;
+    return 0;
+}
+
 extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
@@ -584,12 +600,16 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
 
 // ---- deciding a batch's unknown-TLS sightings (mfp_prevalence) ----
 // the distinct list of the slot's pending batch; -3 when its table overflowed
-static long long slot_distinct(mfp_context c, Slot &S, std::vector<mfp_sighting> &d) {
+// `bound`: return -4 without exporting when the batch has more distinct
+// fingerprints than the bound (the LRU's capacity: the distinct form cannot
+// be exact then, mfp_prevalence_resolve_distinct)
+static long long slot_distinct(mfp_context c, Slot &S, std::vector<mfp_sighting> &d, uint64_t bound = ~0ull) {
     hipStream_t s = S.pend.stream;
     unsigned int cnt[4];
     HIPCHK(hipMemcpyAsync(cnt, S.seen.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (cnt[1] || cnt[0] > S.seen.list_cap) return -3;
+    if (cnt[0] > bound) return -4;
     d.resize(cnt[0]);
     if (cnt[0]) {
         if (mfp_launch_seen_export(&S.seen, cnt[0], S.d_sight, s) != 0) { mfp_set_error("export launch failed"); return -3; }
@@ -602,37 +622,43 @@ static long long slot_distinct(mfp_context c, Slot &S, std::vector<mfp_sighting>
 
 // the slot's pending sightings in stream order (hashes), and the per-group
 // offsets the resolve kernel indexes them with (left in S.d_group_off)
-static long long slot_sequence(mfp_context c, Slot &S, std::vector<uint64_t> &seq) {
+// (S.h_seq, pinned: valid until the slot's next sequence)
+static long long slot_sequence(mfp_context c, Slot &S) {
     hipStream_t s = S.pend.stream;
     const uint64_t groups = (S.pend.n + 63) / 64;
-    std::vector<uint64_t> bits(groups);
-    if (groups) HIPCHK(hipMemcpyAsync(bits.data(), S.d_pending, groups * 8, hipMemcpyDeviceToHost, s));
+    if (grow_pinned(S.h_gbits, S.cap_h_gbits, groups + 1)) { mfp_set_error("host allocation failed"); return -2; }
+    if (groups) HIPCHK(hipMemcpyAsync(S.h_gbits, S.d_pending, groups * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     std::vector<uint32_t> off(groups + 1, 0);
-    for (uint64_t g = 0; g < groups; g++) off[g + 1] = off[g] + (uint32_t)__builtin_popcountll(bits[g]);
+    for (uint64_t g = 0; g < groups; g++) off[g + 1] = off[g] + (uint32_t)__builtin_popcountll(S.h_gbits[g]);
     const uint64_t m = off[groups];
     if (grow(S.d_group_off, S.cap_group_off, groups + 1) || grow(S.d_seq, S.cap_seq, m + 1)) {
         mfp_set_error("device allocation failed");
         return -2;
     }
+    if (grow_pinned(S.h_seq, S.cap_h_seq, m + 1)) { mfp_set_error("host allocation failed"); return -2; }
     if (groups) HIPCHK(hipMemcpyAsync(S.d_group_off, off.data(), (groups + 1) * 4, hipMemcpyHostToDevice, s));
     if (mfp_launch_seen_sequence(mfp_classifier_device(c->clf), &S.seen, S.pend.n, S.pend.rec,
                                  (const uint8_t *)S.pend.fp, S.d_pending, S.d_group_off, S.d_seq, s) != 0) {
         mfp_set_error("sequence launch failed");
         return -3;
     }
-    seq.resize(m);
-    if (m) HIPCHK(hipMemcpyAsync(seq.data(), S.d_seq, m * 8, hipMemcpyDeviceToHost, s));
+    if (m) HIPCHK(hipMemcpyAsync(S.h_seq, S.d_seq, m * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return (long long)m;
 }
 
 // apply decisions to the slot's pending batch: per distinct entry (pos order)
 // or per sighting (seq), on the device records
+// (bits may be S.h_dec, pinned, or any host memory: staged through S.h_dec)
 static int slot_apply(mfp_context c, Slot &S, const uint8_t *bits, size_t nbits, bool per_sighting) {
     hipStream_t s = S.pend.stream;
     if (grow(S.d_seen_bits, S.cap_seen_bits, nbits + 1)) { mfp_set_error("device allocation failed"); return -2; }
-    if (nbits) HIPCHK(hipMemcpyAsync(S.d_seen_bits, bits, nbits, hipMemcpyHostToDevice, s));
+    if (bits != S.h_dec) {
+        if (grow_pinned(S.h_dec, S.cap_h_dec, nbits + 1)) { mfp_set_error("host allocation failed"); return -2; }
+        if (nbits) memcpy(S.h_dec, bits, nbits);
+    }
+    if (nbits) HIPCHK(hipMemcpyAsync(S.d_seen_bits, S.h_dec, nbits, hipMemcpyHostToDevice, s));
     if (mfp_launch_analysis_resolve(mfp_classifier_device(c->clf), &S.seen, S.pend.n, S.pend.rec,
                                     (const uint8_t *)S.pend.fp, S.pend.out, S.d_pending, c->mode,
                                     per_sighting ? nullptr : S.d_seen_bits, S.d_group_off,
@@ -649,7 +675,7 @@ static int slot_apply(mfp_context c, Slot &S, const uint8_t *bits, size_t nbits,
 static int slot_resolve(mfp_context c, Slot &S) {
     if (!S.pend.live) return 0;
     std::vector<mfp_sighting> d;
-    const long long u = slot_distinct(c, S, d);
+    const long long u = slot_distinct(c, S, d, mfp_prevalence_capacity(c->prev));
     if (u == -2) return -2;
     if (u >= 0) {
         // the device's distinct list is in insertion order: positions are
@@ -662,12 +688,11 @@ static int slot_resolve(mfp_context c, Slot &S) {
         }
         if (r != -2) return r;
     }
-    std::vector<uint64_t> seq;
-    const long long m = slot_sequence(c, S, seq);
+    const long long m = slot_sequence(c, S);
     if (m < 0) return (int)m;
-    std::vector<uint8_t> seen(seq.size());
-    if (mfp_prevalence_resolve_sequence(c->prev, seq.data(), seq.size(), seen.data()) != 0) return -1;
-    return slot_apply(c, S, seen.data(), seen.size(), true);
+    if (grow_pinned(S.h_dec, S.cap_h_dec, (size_t)m + 1)) { mfp_set_error("host allocation failed"); return -2; }
+    if (mfp_prevalence_resolve_sequence(c->prev, S.h_seq, (size_t)m, S.h_dec) != 0) return -1;
+    return slot_apply(c, S, S.h_dec, (size_t)m, true);
 }
 
 extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
@@ -697,7 +722,7 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
     S.pend.live = false;
     const size_t m = S.pend.n;
     std::vector<mfp_sighting> d;
-    const long long u = slot_distinct(c, S, d);
+    const long long u = slot_distinct(c, S, d, mfp_prevalence_capacity(c->prev));
     if (u == -2) return -2;
     if (u >= 0) {
         const int r = mfp_prevalence_resolve_distinct(c->prev, d.data(), d.size());
@@ -710,13 +735,13 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
         }
         if (r != -2) return r;
     }
-    std::vector<uint64_t> seq;
-    const long long ms = slot_sequence(c, S, seq);
+    const long long ms = slot_sequence(c, S);
     if (ms < 0) return (int)ms;
-    std::vector<uint8_t> seen(seq.size());
-    if (mfp_prevalence_resolve_sequence(c->prev, seq.data(), seq.size(), seen.data()) != 0) return -1;
+    if (grow_pinned(S.h_dec, S.cap_h_dec, (size_t)ms + 1)) { mfp_set_error("host allocation failed"); return -2; }
+    const uint8_t *seen = S.h_dec;
+    if (mfp_prevalence_resolve_sequence(c->prev, S.h_seq, (size_t)ms, S.h_dec) != 0) return -1;
     size_t k = 0;
-    for (size_t i = 0; i < m && k < seen.size(); i++)
+    for (size_t i = 0; i < m && k < (size_t)ms; i++)
         if (an[i].flags & MFP_AN_PENDING) host_patch(c, an[i], rec[i], seen[k++] != 0);
     return 0;
 }
@@ -979,10 +1004,9 @@ extern "C" MFP_EXPORT long long mfp_analysis_sequence(mfp_context c, uint64_t *h
     Slot *S = deferred_slot(c);
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
-    std::vector<uint64_t> seq;
-    const long long m = slot_sequence(c, *S, seq);
+    const long long m = slot_sequence(c, *S);
     if (m < 0) return m;
-    if (hash) memcpy(hash, seq.data(), std::min<size_t>(cap, seq.size()) * 8);
+    if (hash) memcpy(hash, S->h_seq, std::min<size_t>(cap, (size_t)m) * 8);
     return m;
 }
 
@@ -1007,9 +1031,9 @@ extern "C" MFP_EXPORT int mfp_analysis_resolve(mfp_context c, const mfp_sighting
             return -1;
         }
     }
-    std::vector<uint8_t> bits(u);
-    for (size_t i = 0; i < u; i++) bits[i] = (uint8_t)d[i].first_seen;
-    const int r = slot_apply(c, *S, bits.data(), u, false);
+    if (grow_pinned(S->h_dec, S->cap_h_dec, u + 1)) { mfp_set_error("host allocation failed"); return -2; }
+    for (size_t i = 0; i < u; i++) S->h_dec[i] = (uint8_t)d[i].first_seen;
+    const int r = slot_apply(c, *S, S->h_dec, u, false);
     if (r == 0) HIPCHK(hipStreamSynchronize(S->pend.stream));
     return r;
 }
@@ -1032,8 +1056,7 @@ extern "C" MFP_EXPORT int mfp_analysis_resolve_sequence(mfp_context c, const uin
     Slot *S = deferred_slot(c);
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
-    std::vector<uint64_t> seq;
-    const long long ms = slot_sequence(c, *S, seq);   // leaves the group offsets on the device
+    const long long ms = slot_sequence(c, *S);   // leaves the group offsets on the device
     if (ms < 0) return (int)ms;
     if ((size_t)ms != m) { mfp_set_error("sequence length %zu, batch has %lld sightings", m, ms); return -1; }
     const int r = slot_apply(c, *S, seen, m, true);

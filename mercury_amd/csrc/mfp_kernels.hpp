@@ -207,7 +207,7 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
 #ifndef MFP_TLS_ONEPASS
 #define MFP_TLS_ONEPASS 1
 #endif
-template <int = 0>
+template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
     __shared__ uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         TlsPlan plan;
         plan.ok = false;
         {
-            Em<false> e;
+            Em<false, FMT> e;
             e.plan = &plan;
             packet_walk<FAM_TLS>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
             punt = live && e.punt;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         if (len && fits) {
             Em<true> e;
             e.begin(P.fp_arena + base + excl, out_line[tid]);
-            tls_ch_emit(e, plan);
+            tls_ch_emit_fast<FMT>(e, plan);
             e.finish();
             *(uint64_t *)(P.fp_arena + base + excl + ((len + 7) & ~7u)) = e.hash();
         }
@@ -718,9 +718,13 @@ int launch_bin(const KParams &P, uint32_t *fallback, bool lds, const char *name,
     if (lds) {
         hipLaunchKernelGGL((k_fp_lds<false, MFP_LDS_STAGE, FAM>), dim3(lblocks), dim3(64), 0, stream, P, fallback);
     } else {
-        if constexpr (FAM == FAM_TLS && MFP_TLS_ONEPASS)   // (bin kernels always have a fallback list)
-            hipLaunchKernelGGL(k_fp_tls1<>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback);
-        else
+        if constexpr (FAM == FAM_TLS && MFP_TLS_ONEPASS) {   // (bin kernels always have a fallback list)
+            switch (P.cfg.tls_format) {
+            case 1: hipLaunchKernelGGL(k_fp_tls1<1>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback); break;
+            case 2: hipLaunchKernelGGL(k_fp_tls1<2>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback); break;
+            default: hipLaunchKernelGGL(k_fp_tls1<0>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback); break;
+            }
+        } else
             hipLaunchKernelGGL(k_fingerprint<FAM>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback);
     }
     if (prof) mfp_prof_end(prof, stream);

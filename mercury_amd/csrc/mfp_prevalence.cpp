@@ -26,6 +26,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <unordered_set>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -190,6 +191,8 @@ MFP_EXPORT uint64_t mfp_prevalence_size(mfp_prevalence p) {
     return p->lru.size;
 }
 
+MFP_EXPORT uint32_t mfp_prevalence_capacity(mfp_prevalence p) { return p ? p->lru.cap : 0; }
+
 MFP_EXPORT int mfp_prevalence_contains(mfp_prevalence p, uint64_t hash) {
     if (!p) return 0;
     std::lock_guard<std::mutex> lk(p->mu);
@@ -206,27 +209,29 @@ MFP_EXPORT long long mfp_prevalence_keys(mfp_prevalence p, uint64_t *out, size_t
     return (long long)k.size();
 }
 
-MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen) {
-    if (!p || (m && (!hash || !seen))) { mfp_set_error("mfp_prevalence_resolve_sequence: bad arguments"); return -1; }
-    std::lock_guard<std::mutex> lk(p->mu);
-    Lru &L = p->lru;
+}  // extern "C"
+
+// hash[0..m) decided against the set L, which becomes the set afterwards.
+// Long sequences go in parallel chunks: chunk t decides hash[s_t..e_t) with
+// its own LRU set up as the shared one would be at s_t (lru_at): the same
+// decisions as one pass.  A chunk whose walk back runs past its budget (4
+// chunk lengths) takes the previous chunk's finished set instead; the last
+// chunk's set is the set after the whole sequence.
+static void decide(Lru &L, const uint64_t *hash, size_t m, uint8_t *seen) {
     // chunks of at least 8 x capacity per thread (each chunk's starting set costs a walk back over about
     // `capacity` distinct keys); up to 16 threads, the per-GPU host share of the target machine
+    // (MFP_LRU_THREADS: a lower cap, e.g. for several ranks on one host's cores)
     const unsigned hw = std::thread::hardware_concurrency();
-    size_t T = m / (8 * (size_t)L.cap);
-    T = std::min<size_t>(T, std::min<size_t>(16, hw ? hw : 1));
+    size_t tmax = std::min<size_t>(16, hw ? hw : 1);
+    if (const char *e = getenv("MFP_LRU_THREADS")) tmax = std::max<size_t>(1, std::min<size_t>(tmax, strtoul(e, nullptr, 10)));
+    size_t T = std::min<size_t>(m / (8 * (size_t)L.cap), tmax);
     if (T <= 1) {
         for (size_t j = 0; j < m; j++) {
             if (j + 8 < m) L.prefetch(hash[j + 8]);
             seen[j] = L.access(hash[j]) ? 1 : 0;
         }
-        return 0;
+        return;
     }
-    // chunk t decides hash[s_t..e_t) with its own LRU set up as the shared one
-    // would be at s_t (lru_at): the same decisions as one pass, in parallel.
-    // A chunk whose walk back runs past its budget (4 chunk lengths) takes the
-    // previous chunk's finished set instead; the last chunk's set is the set
-    // after the whole sequence.
     std::vector<uint64_t> init;
     L.export_keys(init);
     std::vector<Lru> sets(T, Lru(1));
@@ -256,6 +261,62 @@ MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t 
         });
     for (auto &x : th) x.join();
     std::swap(L, sets[T - 1]);
+}
+
+// the set whose most recent keys are recent[0..n) (most recent first), then
+// the keys of `older` from its most recent down, up to the capacity
+static void set_from(Lru &out, const uint64_t *recent, size_t n, const Lru &older) {
+    for (size_t i = 0; i < n && out.size < out.cap; i++) out.append_lru(recent[i]);
+    for (uint32_t k = older.next[0]; k != 0 && out.size < out.cap; k = older.next[k]) out.append_lru(older.key[k]);
+}
+
+extern "C" {
+
+MFP_EXPORT int mfp_prevalence_resolve_sequence(mfp_prevalence p, const uint64_t *hash, size_t m, uint8_t *seen) {
+    if (!p || (m && (!hash || !seen))) { mfp_set_error("mfp_prevalence_resolve_sequence: bad arguments"); return -1; }
+    std::lock_guard<std::mutex> lk(p->mu);
+    decide(p->lru, hash, m, seen);
+    return 0;
+}
+
+// The distinct keys of hash[0..m) by their last sighting, most recent first,
+// at most the capacity of p: what a walk back over this shard contributes to
+// any later shard's starting set (lru_at)
+MFP_EXPORT long long mfp_prevalence_summary(mfp_prevalence p, const uint64_t *hash, size_t m, uint64_t *out) {
+    if (!p || (m && (!hash || !out))) { mfp_set_error("mfp_prevalence_summary: bad arguments"); return -1; }
+    Lru S(p->lru.cap);
+    for (size_t i = m; i-- > 0 && S.size < S.cap;) S.append_lru(hash[i]);
+    long long k = 0;
+    for (uint32_t n = S.next[0]; n != 0; n = S.next[n]) out[k++] = S.key[n];
+    return k;
+}
+
+// One shard of a stream whose earlier shards were decided elsewhere: the
+// shard starts from the set that the earlier shards' summaries (prior,
+// most recent shard first, each mfp_prevalence_summary) leave on top of p's
+// set; hash[0..m) is decided from there.  p is not changed (see
+// mfp_prevalence_advance).
+MFP_EXPORT int mfp_prevalence_resolve_shard(mfp_prevalence p, const uint64_t *hash, size_t m, const uint64_t *prior,
+                                            size_t nprior, uint8_t *seen) {
+    if (!p || (m && (!hash || !seen)) || (nprior && !prior)) {
+        mfp_set_error("mfp_prevalence_resolve_shard: bad arguments");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    Lru S(p->lru.cap);
+    set_from(S, prior, nprior, p->lru);
+    decide(S, hash, m, seen);
+    return 0;
+}
+
+// The set after a whole step of shards: `recent` = every shard's summary,
+// the last shard's first; p becomes that set (the same on every rank)
+MFP_EXPORT int mfp_prevalence_advance(mfp_prevalence p, const uint64_t *recent, size_t n) {
+    if (!p || (n && !recent)) { mfp_set_error("mfp_prevalence_advance: bad arguments"); return -1; }
+    std::lock_guard<std::mutex> lk(p->mu);
+    Lru S(p->lru.cap);
+    set_from(S, recent, n, p->lru);
+    std::swap(p->lru, S);
     return 0;
 }
 

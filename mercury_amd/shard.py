@@ -15,7 +15,11 @@ host-side ordered merge of SURVEY 8(e): every rank analyses its shard with the
 decision deferred, the ranks exchange their batch's distinct unknown-TLS
 fingerprints (a few hundred entries, fixed-size gloo all_gathers), and every rank applies
 the same decisions, in shard order, to an identical copy of the LRU -- so the
-sharded output equals one context over the concatenated stream.
+sharded output equals one context over the concatenated stream.  When the
+distinct form cannot be exact (more new fingerprints than the LRU holds), each
+rank decides its own sightings from the set the earlier shards leave, known
+from their summaries (at most the LRU's capacity each): every sighting is
+decided once, by its own rank.
 """
 import numpy as np
 
@@ -131,9 +135,15 @@ def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
             k = sum(len(x) for x in lists[:rank])
             ctx.analysis_resolve(allv[k:k + len(lists[rank])])
             return len(allv)
-    # the sequence form: every rank's sightings in shard order
-    seqs = _all_gather_rows(np.ascontiguousarray(ctx.analysis_sequence(), np.uint64), group)
-    seen = prev.resolve_sequence(np.concatenate(seqs) if seqs else np.zeros(0, np.uint64))
-    k = sum(len(x) for x in seqs[:rank])
-    ctx.analysis_resolve_sequence(seen[k:k + len(seqs[rank])])
-    return len(seen)
+    # the sequence form, decided once: each rank decides its own sightings,
+    # from the set that the earlier shards leave; a shard's effect on any later
+    # one is its summary -- its distinct fingerprints by last sighting, at most
+    # the LRU's capacity (what lru_at's walk back takes from it) -- so the ranks
+    # exchange summaries, not sightings, and the work per rank does not grow
+    # with the number of ranks
+    seq = np.ascontiguousarray(ctx.analysis_sequence(), np.uint64)
+    summaries = _all_gather_rows(prev.summary(seq), group)
+    prior = np.concatenate(summaries[:rank][::-1]) if rank else np.zeros(0, np.uint64)
+    ctx.analysis_resolve_sequence(prev.resolve_shard(seq, prior))
+    prev.advance(np.concatenate(summaries[::-1]))
+    return sum(len(x) for x in summaries)

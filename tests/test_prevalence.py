@@ -251,3 +251,39 @@ def test_lru_stream_two_shards_shared_prevalence():
     assert len(bad) == 0, f"{len(bad)} differ, first {bad[:5]}"
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("kind", ["few", "wide", "bursts", "cycle"])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_prevalence_shards_decided_where_they_lie(kind, world):
+    """mfp_prevalence_summary / resolve_shard / advance (shard.py's
+    decide-once merge): every shard decided from its predecessors' summaries,
+    then the set advanced, over three steps, equals one pass over the
+    concatenated stream -- decisions and the recency order at the end."""
+    rng = np.random.default_rng(["few", "wide", "bursts", "cycle"].index(kind) * 10 + world)
+    cap = 200
+    ranks = [mercury_amd.Prevalence(cap) for _ in range(world)]
+    whole = mercury_amd.Prevalence(cap)
+    for step in range(3):
+        shards = []
+        for r in range(world):
+            n = int(rng.integers(0, 5000)) if r != 1 else 40      # short shards too
+            if kind == "few":
+                keys = rng.integers(0, 150, n)
+            elif kind == "wide":
+                keys = rng.integers(0, 5000, n)
+            elif kind == "bursts":
+                keys = rng.integers(0, 120, n) + 50 * (np.arange(n) // 900) + 1000 * step
+            else:
+                keys = np.tile(np.arange(300), n // 300 + 1)[:n] + 7 * r
+            shards.append(key_hash(keys))
+        want = whole.resolve_sequence(np.concatenate(shards))
+        for p in ranks:                                   # every rank's copy, same inputs
+            summ = [p.summary(s) for s in shards]
+            assert all(len(x) <= cap for x in summ)
+            got = [p.resolve_shard(shards[r], np.concatenate(summ[:r][::-1]) if r else np.zeros(0, np.uint64))
+                   for r in range(world)]
+            assert np.array_equal(np.concatenate(got), want), (kind, world, step)
+        for p in ranks:
+            p.advance(np.concatenate([p.summary(s) for s in shards][::-1]))
+            assert np.array_equal(p.keys(), whole.keys()), (kind, world, step)

@@ -229,3 +229,71 @@ def test_ordered_prevalence_merge_world2_hip():
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, f"{len(bad)} statuses differ, first at {bad[:5]}"
     assert res[0][1] == res[1][1] and res[0][2] > 0
+
+
+def _scale_worker(rank, world, port, q, m, steps):
+    """One rank at the realistic-diversity leg's scale: m unknown-TLS sightings
+    per step (mostly distinct fingerprints, cycling the 100 000-entry LRU),
+    decided with shard.ordered_prevalence_merge; reports the merge's wall time
+    per step.  Two LRU threads per rank (MFP_LRU_THREADS), so world 4 fills
+    this host's 8 cores and no more."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo", MFP_LRU_THREADS="2")
+    import time
+    import torch.distributed as dist
+    import mercury_amd
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        prev = mercury_amd.Prevalence(100000)
+        ts, checks = [], []
+        for step in range(steps):
+            rng = np.random.default_rng(1000 * step + rank)
+            # 2 % of the sightings repeat a small hot set, the rest are ~350 k
+            # fingerprints per shard seen about 50 times each
+            keys = rng.integers(0, 350_000, m, dtype=np.int64) + (rank + world * step) * 1_000_000
+            hot = rng.random(m) < 0.02
+            keys[hot] = rng.integers(0, 64, int(hot.sum()))
+            c = _ShardCtx.__new__(_ShardCtx)
+            c.seq = (keys.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0x5EED)
+            c.dl, c.seen = None, None
+            c.analysis_distinct = lambda: None                       # the table overflowed: sequence form
+            dist.barrier()
+            t0 = time.perf_counter()
+            shard.ordered_prevalence_merge(c, prev, rank * m)
+            ts.append(time.perf_counter() - t0)
+            checks.append(int(c.seen.sum()))
+        q.put((rank, ts, checks, prev.keys()[-8:].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_scale(world, m, steps):
+    import multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ps = [ctxm.Process(target=_scale_worker, args=(r, world, port, q, m, steps)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {r: (t, c, k) for r, t, c, k in [q.get(timeout=600) for _ in ps]}
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+def test_ordered_prevalence_merge_scale_world2_world4():
+    """SURVEY 8(e) at the diversity leg's scale: 17.5 M sightings per rank per
+    step.  The sequence form decides every sighting once, on its own rank, so
+    the merge's time per step does not grow with the number of ranks (the
+    earlier form resolved all ranks' sightings on every rank: 4x the work at
+    world 4).  Every rank ends each step with the same LRU."""
+    m, steps = 17_500_000, 2
+    t = {}
+    for world in (2, 4):
+        res = _run_scale(world, m, steps)
+        assert len({tuple(v[2]) for v in res.values()}) == 1      # same LRU on every rank
+        t[world] = max(max(v[0][1:]) for v in res.values())      # steady state (the first step warms up)
+    print(f"merge per step: world 2 {t[2]:.2f} s, world 4 {t[4]:.2f} s")
+    assert t[4] < 1.6 * t[2], t
