@@ -267,6 +267,17 @@ MFP_EXPORT int mfp_analysis_enabled(mfp_context ctx);
 MFP_EXPORT int mfp_analyze_batch_device(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
                                         mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out,
                                         double *d_attr_prob, void *stream);
+/* Pipelined form of mfp_analyze_batch_device for a stream of device batches:
+ * launches this batch's kernels on `stream`, then decides the PREVIOUS
+ * batch's unknown-TLS sightings (stream order, the context's LRU) and applies
+ * them while the device runs this one.  A batch's analysis records are final
+ * after the next call or mfp_analysis_flush; keep its buffers until then.
+ * Decisions equal the synchronous call's. */
+MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context ctx, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
+                                                  size_t n, mfp_record *d_rec, const char *d_fp_arena,
+                                                  mfp_analysis *d_out, double *d_attr_prob, void *stream);
+/* decide the batch mfp_analyze_batch_device_pipelined left pending; waits */
+MFP_EXPORT int mfp_analysis_flush(mfp_context ctx);
 
 /* mfp_process_batch_host plus classification into analysis[n] (NULL: none)
  * and attr_prob[n * MFP_ATTR_DB_TAGS] (NULL: not wanted). */

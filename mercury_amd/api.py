@@ -89,6 +89,10 @@ def load_library():
     lib.mfp_analysis_enabled.argtypes = [vp]
     lib.mfp_analyze_batch_device.restype = ctypes.c_int
     lib.mfp_analyze_batch_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.mfp_analyze_batch_device_pipelined.restype = ctypes.c_int
+    lib.mfp_analyze_batch_device_pipelined.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.mfp_analysis_flush.restype = ctypes.c_int
+    lib.mfp_analysis_flush.argtypes = [vp]
     lib.mfp_process_batch_host_seg.restype = ctypes.c_longlong
     lib.mfp_process_batch_host_seg.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp]
     lib.mfp_reassembler_create.restype = vp
@@ -401,6 +405,19 @@ class Context:
         r = self.lib.mfp_analyze_batch_device(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out, d_attr_prob, stream)
         if r != 0:
             raise MercuryAmdError("mfp_analyze_batch_device failed: " + _err(self.lib))
+
+    def analyze_device_pipelined(self, d_arena, d_desc, n, d_rec, d_fp, d_out, stream=0, d_attr_prob=None):
+        """mfp_analyze_batch_device_pipelined: this batch's kernels run while
+        the previous batch's sightings are decided; a batch's records are final
+        after the next call or analysis_flush()."""
+        r = self.lib.mfp_analyze_batch_device_pipelined(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out, d_attr_prob,
+                                                         stream)
+        if r != 0:
+            raise MercuryAmdError("mfp_analyze_batch_device_pipelined failed: " + _err(self.lib))
+
+    def analysis_flush(self):
+        if self.lib.mfp_analysis_flush(self.h) != 0:
+            raise MercuryAmdError("mfp_analysis_flush failed: " + _err(self.lib))
 
     def process_name(self, pid):
         if pid == NO_PROCESS:

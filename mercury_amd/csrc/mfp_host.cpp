@@ -349,6 +349,11 @@ struct Slot {
     char *d_fp2 = nullptr; size_t cap_fp2 = 0;   // dense (compacted) fingerprints of a host batch
     unsigned long long *h_used = nullptr;   // pinned copy of d_used
     hipStream_t stream = nullptr;
+    // pipelined device batches (mfp_analyze_batch_device_pipelined): the
+    // batch's kernels done (on the caller's stream), the decision applied (on
+    // this slot's stream)
+    hipEvent_t ev_kernels = nullptr, ev_resolved = nullptr;
+    bool resolved_recorded = false;
 
     bool init() {
         return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
@@ -356,7 +361,9 @@ struct Slot {
                hipMalloc(&d_an_stats, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipMemset(d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
-               hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
+               hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_kernels, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_resolved, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
@@ -365,6 +372,7 @@ struct Slot {
         for (void *x : p) if (x) (void)hipFree(x);
         for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec}) if (x) (void)hipHostFree(x);
         if (stream) (void)hipStreamDestroy(stream);
+        for (hipEvent_t e : {ev_kernels, ev_resolved}) if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -387,7 +395,8 @@ struct mfp_context_s {
     bool defer = false;                  // mfp_analysis_defer
     bool report_os = false;              // libmerc_config.report_os (mfp_analysis_report_os)
     bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
-    Slot slot[3];
+    Slot slot[4];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2: host pipeline
+    int pipe_next = 0;                   // mfp_analyze_batch_device_pipelined: the slot of the next batch (0 or 3)
     int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
     std::mutex mu;
@@ -959,6 +968,61 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     // the batch's unknown-TLS sightings are decided now, in stream order: the
     // call waits for its kernels (a few microseconds of host time per batch)
     return slot_resolve(c, c->slot[0]);
+}
+
+// Pipelined device batches: batch k's kernels are launched, then batch k-1's
+// unknown-TLS sightings are decided (in stream order, on the host) and applied
+// while the device runs batch k.  Batches alternate between slots 0 and 3 (each
+// has its own sighting table and work lists); a slot's decision work runs on
+// the slot's own stream, after the batch's kernels (an event on the caller's
+// stream), and the caller's stream waits for it before the slot is reused.
+// The batch's analysis records are final after the next call, or
+// mfp_analysis_flush, for work the caller enqueues on its stream afterwards.
+extern "C" MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context c, const uint8_t *d_arena,
+                                                             const mfp_pkt_desc *d_desc, size_t n, mfp_record *d_rec,
+                                                             const char *d_fp_arena, mfp_analysis *d_out,
+                                                             double *d_attr_prob, void *stream) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t us = (hipStream_t)stream;
+    const int slot = c->pipe_next ? 3 : 0, other = c->pipe_next ? 0 : 3;
+    Slot &S = c->slot[slot];
+    if (S.pend.live) { int r = slot_resolve(c, S); if (r) return r; }   // (never: the previous call decided it)
+    if (S.resolved_recorded) HIPCHK(hipStreamWaitEvent(us, S.ev_resolved, 0));
+    int r = analyze_locked(c, slot, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, us);
+    if (r) return r;
+    HIPCHK(hipEventRecord(S.ev_kernels, us));
+    HIPCHK(hipStreamWaitEvent(S.stream, S.ev_kernels, 0));
+    S.pend.stream = S.stream;
+    c->pipe_next ^= 1;
+    Slot &O = c->slot[other];
+    if (O.pend.live) {
+        r = slot_resolve(c, O);
+        if (r) return r;
+        HIPCHK(hipEventRecord(O.ev_resolved, O.stream));
+        O.resolved_recorded = true;
+        HIPCHK(hipStreamWaitEvent(us, O.ev_resolved, 0));   // later work on the caller's stream sees its records
+    }
+    return 0;
+}
+
+// decide the pipelined batch still pending and wait for its records
+extern "C" MFP_EXPORT int mfp_analysis_flush(mfp_context c) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    for (int k = 0; k < 2; k++) {             // the older slot first
+        Slot &S = c->slot[(k == 0) == (c->pipe_next == 0) ? 0 : 3];
+        if (!S.pend.live) continue;
+        const int r = slot_resolve(c, S);
+        if (r) return r;
+        HIPCHK(hipEventRecord(S.ev_resolved, S.stream));
+        S.resolved_recorded = true;
+    }
+    for (int k : {0, 3}) HIPCHK(hipStreamSynchronize(c->slot[k].stream));
+    return 0;
 }
 
 // ---- the prevalence LRU: sharing across the shards of one stream ----

@@ -206,6 +206,49 @@ def test_lru_stream_pipelined_vs_reference(chunk):
 
 
 @pytest.mark.gpu
+def test_lru_stream_device_pipelined_vs_reference():
+    """mfp_analyze_batch_device_pipelined over device batches (two sets of
+    output buffers, alternating): batch k's kernels run while batch k-1 is
+    decided; after the flush every batch's statuses equal the reference's."""
+    import torch
+    a, d = synth.lru_batch(synth.lru_keys())
+    want = golden_status()
+    ctx = mercury_amd.Context(f"select=tls;resources={REF_ARCHIVE};analysis", device=0)
+    d_arena = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    chunk = 30000
+    cap = 64 * 1024 * 1024
+    bufs = [dict(rec=torch.empty(chunk * 32, dtype=torch.uint8, device="cuda"),
+                 fp=torch.empty(cap, dtype=torch.uint8, device="cuda"),
+                 used=torch.zeros(4, dtype=torch.int64, device="cuda"),
+                 an=torch.empty(chunk * mercury_amd.ANALYSIS_DTYPE.itemsize, dtype=torch.uint8, device="cuda"))
+            for _ in range(2)]
+    stream = torch.cuda.current_stream()
+    got, descs = [None] * ((len(d) + chunk - 1) // chunk), []
+    for k, lo in enumerate(range(0, len(d), chunk)):
+        dd = np.ascontiguousarray(d[lo:lo + chunk])
+        descs.append(torch.from_numpy(dd.view(np.uint8)).cuda())
+        b = bufs[k % 2]
+        if k >= 2:                                    # batch k-2 was decided by the previous call
+            got[k - 2] = _statuses(bufs[k % 2]["an"].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE))
+        b["used"].zero_()
+        ctx.process_device(d_arena.data_ptr(), descs[k].data_ptr(), len(dd), b["rec"].data_ptr(), b["fp"].data_ptr(),
+                           cap, b["used"].data_ptr(), stream.cuda_stream)
+        ctx.analyze_device_pipelined(d_arena.data_ptr(), descs[k].data_ptr(), len(dd), b["rec"].data_ptr(),
+                                     b["fp"].data_ptr(), b["an"].data_ptr(), stream.cuda_stream)
+    ctx.analysis_flush()
+    torch.cuda.synchronize()
+    nb = len(got)
+    for k in range(max(0, nb - 2), nb):
+        m = min(chunk, len(d) - k * chunk)
+        got[k] = _statuses(bufs[k % 2]["an"].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)[:m])
+    got = np.concatenate(got)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} statuses differ, first at {bad[:5]}"
+    assert ctx.analysis_stats()[3] == 100000
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_lru_stream_two_shards_shared_prevalence():
     """Two contexts on cuda:0 as two shards of one stream: each analyses its
     half (deferred), then the shards are decided in shard order against one
