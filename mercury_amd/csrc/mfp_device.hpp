@@ -247,7 +247,7 @@ struct TlsPlan;
 // FAST >= 0 (k_fp_tls1, TLS format FAST): pass 1 records the ClientHello plan
 // with the string's length by arithmetic (tls_ch_plan_fast), pass 2 emits it
 // with tls_ch_emit_fast
-template <bool EMIT, int FAST_FMT = -1>
+template <bool EMIT, int FAST_FMT = -1, int LINEW = 8>
 struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
@@ -258,10 +258,10 @@ struct Em {
     TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
     static constexpr bool emit_pass() { return EMIT; }
-    // Pass-2 output.  The string starts 64-byte aligned and owns its slot
-    // rounded up to 64 bytes.  Bytes gather in `acc`; whole 8-byte words go
-    // to a per-lane 64-byte line in LDS, and a full line leaves as four
-    // 16-byte stores.  Lanes reach a word or line boundary at different
+    // Pass-2 output.  The string starts 16-byte aligned and owns its slot
+    // rounded up to 16 bytes.  Bytes gather in `acc`; whole 8-byte words go
+    // to a per-lane line of LINEW words in LDS, and a full line leaves as
+    // LINEW / 2 16-byte stores.  Lanes reach a word or line boundary at different
     // pushes, so a store is issued for the lanes that have one; staging the
     // line in LDS makes those (divergent) global stores 8x rarer than
     // storing every word.
@@ -293,7 +293,7 @@ struct Em {
     DEV void put_word() {
         h ^= mfpc::word_term(acc, wi++);
         line[nw++] = acc;
-        if (nw == 8) { flush_line(8); out += 64; nw = 0; }
+        if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
     }
     DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
         if (EMIT) {
@@ -526,6 +526,58 @@ DEV uint64_t seg_expand(const uint32_t *sg, uint32_t nseg, const uint8_t *pkt, u
         h ^= mfpc::word_term(word, p0 >> 3);
     }
     return h;
+}
+
+// degrease_uint16 (tls.h:776) of the two byte pairs of a little-endian word
+// (pair = bytes 0,1 and 2,3, the first byte the high one)
+DEV uint32_t degrease_pairs(uint32_t le) {
+    const uint32_t b0 = le & 0xff, b1 = (le >> 8) & 0xff, b2 = (le >> 16) & 0xff, b3 = le >> 24;
+    const uint32_t lo = (b0 == b1 && (b0 & 15) == 10) ? 0x0a0au : (le & 0xffff);
+    const uint32_t hi = (b2 == b3 && (b2 & 15) == 10) ? 0x0a0au : (le >> 16);
+    return lo | (hi << 16);
+}
+DEV uint64_t low_chars(uint64_t v, uint32_t k) { return k >= 8 ? v : (v & ((1ull << (8 * k)) - 1)); }
+// raw_as_hex (buffer_stream.h:1087) / raw_as_hex_degrease (tls.h:802, len
+// even) of p[0, len), 4 bytes -> 8 characters per push
+template <bool DEGREASE, class E>
+DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
+    if (len == 0) return;
+    LeStream s;
+    s.init(p, (long)len);
+    for (uint32_t i = 0; i < len; i += 4) {
+        uint32_t w = s.next();
+        if (DEGREASE) w = degrease_pairs(w);
+        const uint32_t k = len - i >= 4 ? 8u : 2 * (len - i);
+        b.push(low_chars(hex4(w), k), k);
+    }
+}
+// Lane emission of one segment list (k_fp_seg): the lane writes its own
+// string, 4 packet bytes -> 8 hex characters per push, so the 64 lanes of a
+// wave write 64 strings at once (the wave-cooperative expansion above writes
+// one string at a time).  Every segment takes the same instructions whatever
+// its kind; `pool` is the literal pool in LDS.
+template <class E>
+DEV void seg_emit_lane(E &b, const uint32_t *sg, uint32_t nseg, const uint8_t *pkt, const uint8_t *pool) {
+    uint32_t start = 0;
+    for (uint32_t s = 0; s < nseg; s++) {
+        const uint32_t info = sg[s], end = seg_end(info), kind = seg_kind(info), src = seg_src(info);
+        const uint32_t k = end - start;
+        start = end;
+        if (kind == SK_POOL) {                            // at most 12 characters ("http_server/")
+            uint64_t w0 = 0, w1 = 0;
+            for (uint32_t i = 0; i < k; i++) {
+                const uint64_t c = pool[src + i];
+                if (i < 8) w0 |= c << (8 * i); else w1 |= c << (8 * (i - 8));
+            }
+            b.push(w0, k < 8 ? k : 8);
+            b.push(w1, k > 8 ? k - 8 : 0);
+        } else {
+            const bool paren = kind == SK_HEXP;
+            b.push(paren ? '(' : 0u, paren ? 1u : 0u);
+            hex_run<false>(b, pkt + src, (k - (paren ? 2u : 0u)) / 2);
+            b.push(paren ? ')' : 0u, paren ? 1u : 0u);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1188,29 +1240,6 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     pl.version = ch.version; pl.ciphers = ch.ciphers; pl.exts = ch.extensions;
     pl.n = (uint32_t)cnt; pl.type = type; pl.fmt = (uint32_t)FMT;
     pl.ok = true;
-}
-// degrease_uint16 (tls.h:776) of the two byte pairs of a little-endian word
-// (pair = bytes 0,1 and 2,3, the first byte the high one)
-DEV uint32_t degrease_pairs(uint32_t le) {
-    const uint32_t b0 = le & 0xff, b1 = (le >> 8) & 0xff, b2 = (le >> 16) & 0xff, b3 = le >> 24;
-    const uint32_t lo = (b0 == b1 && (b0 & 15) == 10) ? 0x0a0au : (le & 0xffff);
-    const uint32_t hi = (b2 == b3 && (b2 & 15) == 10) ? 0x0a0au : (le >> 16);
-    return lo | (hi << 16);
-}
-DEV uint64_t low_chars(uint64_t v, uint32_t k) { return k >= 8 ? v : (v & ((1ull << (8 * k)) - 1)); }
-// raw_as_hex (buffer_stream.h:1087) / raw_as_hex_degrease (tls.h:802, len
-// even) of p[0, len), 4 bytes -> 8 characters per push
-template <bool DEGREASE, class E>
-DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
-    if (len == 0) return;
-    LeStream s;
-    s.init(p, (long)len);
-    for (uint32_t i = 0; i < len; i += 4) {
-        uint32_t w = s.next();
-        if (DEGREASE) w = degrease_pairs(w);
-        const uint32_t k = len - i >= 4 ? 8u : 2 * (len - i);
-        b.push(low_chars(hex4(w), k), k);
-    }
 }
 template <int FMT, class E>
 DEV void tls_ch_emit_fast(E &b, TlsPlan &pl) {

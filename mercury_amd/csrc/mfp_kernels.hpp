@@ -341,15 +341,26 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
 #ifndef MFP_SEG_MINW
 #define MFP_SEG_MINW 4
 #endif
+// MFP_SEG_LANE (default): each lane writes its own string from its list
+// (seg_emit_lane: 64 strings per wave at once, 4-word LDS lines); 0: the
+// wave expands the strings one after another (seg_expand)
+#ifndef MFP_SEG_LANE
+#define MFP_SEG_LANE 1
+#endif
 constexpr int SEG_STRIDE = SEG_MAX + 1;   // odd word stride: lane-private lists are bank-conflict free
 constexpr uint32_t SEG_STAGE = 2048;      // packets up to this (minus alignment) are staged in LDS for expansion
+constexpr int SEG_LINEW = 4;              // lane emission: words per LDS line
 template <int = 0>
 __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32_t *fallback) {
     __shared__ uint32_t segs[TILE * SEG_STRIDE];
     __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
     __shared__ unsigned long long tile_base;
     __shared__ uint8_t pool[32];
+#if MFP_SEG_LANE
+    __shared__ uint64_t out_line[TILE][SEG_LINEW];
+#else
     __shared__ uint4 stage[TILE / 64][SEG_STAGE / 16];   // per wave: the packet being expanded
+#endif
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
     if (tid < 32) {
@@ -426,6 +437,15 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
         }
 
         KPH(1);
+#if MFP_SEG_LANE
+        if (len && fits) {
+            Em<true, -1, SEG_LINEW> em;
+            em.begin(P.fp_arena + base + excl, out_line[tid]);
+            seg_emit_lane(em, segs + tid * SEG_STRIDE, e.nseg, data, pool);
+            em.finish();
+            *(uint64_t *)(P.fp_arena + base + excl + ((len + 7) & ~7u)) = em.hash();
+        }
+#else
         // wave-cooperative expansion, one packet at a time
         uint64_t todo = fits ? __ballot(len != 0) : 0ull;
 #ifdef MFP_PROBE_SEG_NOEXPAND
@@ -479,6 +499,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             h = wave_xor64(h);
             if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
         }
+#endif
 
         KPH(2);
         if (live && !fb) {
