@@ -200,15 +200,19 @@ def per_packet_shim(seconds=2.0):
             for entry in ("json", "an"):
                 for th in ths:
                     r = subprocess.run([prog, lib, path, CONTRACT, res if entry == "an" else "-", str(th), str(seconds),
-                                        entry], capture_output=True, timeout=seconds * 6 + 120)
+                                        entry], capture_output=True, timeout=seconds * 6 + 120,
+                                       env=dict(os.environ, MFP_SHIM_STATS="1"))
                     if r.returncode != 0:
                         out["points"].append({"lib": name, "entry": entry, "threads": th,
                                               "error": r.stderr.decode(errors="replace")[-300:]})
                         continue
                     x = json.loads(r.stdout.decode().strip().splitlines()[-1])
-                    out["points"].append({"lib": name, "entry": x["entry"], "threads": th,
-                                          "kpkt_s": round(x["pps"] / 1e3, 2), "lat_us_p50": x["lat_us_p50"],
-                                          "lat_us_p99": x["lat_us_p99"]})
+                    pt = {"lib": name, "entry": x["entry"], "threads": th, "kpkt_s": round(x["pps"] / 1e3, 2),
+                          "lat_us_p50": x["lat_us_p50"], "lat_us_p99": x["lat_us_p99"]}
+                    for line in r.stderr.decode(errors="replace").splitlines():
+                        if '"shim_stats"' in line:        # the combiner's batches (MFP_SHIM_STATS)
+                            pt.update(json.loads(line)["shim_stats"])
+                    out["points"].append(pt)
     finally:
         os.unlink(path)
     return out

@@ -1039,6 +1039,10 @@ struct TlsPlan {
     Cur version, ciphers, exts;
     uint32_t n, type, fmt;
     bool ok;
+    // the fast plan (k_fp_tls1): the lane's rows in LDS -- offsets of the
+    // kept extensions by wire index, and the emission order as wire indices
+    uint16_t *off_row = nullptr;
+    uint8_t *ord_row = nullptr;
 };
 
 // pass 1 of a TLS/DTLS ClientHello: fingerprint length (through the counting
@@ -1175,6 +1179,24 @@ DEV uint32_t ext_fp_len(uint32_t t, uint32_t vl) {
     }
     return 10 + 2 * vl;                                  // "(" type length value ")"
 }
+// Formats 1/2 order the kept extensions by a 32-bit key (ext_key32): the
+// field the reference's comparator looks at first, then the length, then the
+// wire index (so equal keys keep wire order); the sorted list lives in 24
+// registers and an insertion is a max and a min per entry (inserting v into a
+// sorted list: new[k] = min(max(old[k-1], v), old[k]), no position search).  Equal keys that need the
+// reference's value comparison, lengths past the key's field and more than
+// REG_EXT kept extensions leave the plan unset (the fallback lane writes them).
+DEV uint32_t ext_key32(const Ext &x, int fmt, int bucket, uint32_t idx, bool &fits) {
+    const bool g = ext_is_grease(x.type);
+    if (fmt == 1) {                              // tls.h:1637: GREASE as 0x0a0a, then type, length
+        fits = g || x.length < 2048;
+        return g ? ((0x0a0au << 16) | idx) : ((x.type << 16) | ((x.length & 2047) << 5) | idx);
+    }
+    fits = true;                                 // tls.h:1709: bucket, GREASE first, length
+    return ((uint32_t)bucket << 24) | (g ? 0u : (1u << 23)) | (g ? 0u : (x.length << 5)) | idx;
+}
+DEV bool key32_grease(uint32_t k, int fmt) { return fmt == 1 ? (k >> 16) == 0x0a0a : !(k & (1u << 23)); }
+
 template <int FMT, class E>
 DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const uint8_t *base,
                           uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len) {
@@ -1182,10 +1204,10 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     // type prefix, "1/" or "2/", "(" version ")" "(" degreased ciphers ")", "(" or "[", ... ")" or "]"
     uint32_t n = (type == 10 ? 5u : 4u) + (FMT ? 2u : 0u) + 2 + 2 * (uint32_t)clen(ch.version) + 2 +
                  2 * ((uint32_t)clen(ch.ciphers) & ~1u) + 2;
-    uint64_t V[REG_EXT];                         // format 0: offsets; 1/2: key << 32 | offset
+    uint32_t V[REG_EXT];                         // formats 1/2: sorted ext_key32 values
 #pragma unroll
-    for (int k = 0; k < REG_EXT; k++) V[k] = ~0ull;
-    int cnt = 0;
+    for (int k = 0; k < REG_EXT; k++) V[k] = ~0u;
+    uint32_t cnt = 0;
     bool rare = false;
     Cur p = ch.extensions;
     while (clen(p) > 0) {
@@ -1203,42 +1225,43 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
         if (FMT == 2) {
             bucket = fmt2_bucket(x);
             if (bucket < 0) continue;
-            int c3 = 0;                          // first three per bucket (tls.h:1695-1701)
+            uint32_t c3 = 0;                     // first three per bucket (tls.h:1695-1701)
 #pragma unroll
-            for (int k = 0; k < REG_EXT; k++) c3 += (V[k] != ~0ull && (uint32_t)(V[k] >> 56) == (uint32_t)bucket);
+            for (int k = 0; k < REG_EXT; k++) c3 += (V[k] >> 24) == (uint32_t)bucket ? 1u : 0u;
             if (c3 >= 3) continue;
         }
-        if (cnt >= REG_EXT || x.type == 0x39 || x.type == 0xffa5) { rare = true; continue; }
-        const uint32_t off = (uint32_t)(start - ch.extensions.d);
-        if (FMT == 0) {
+        if (cnt >= (uint32_t)REG_EXT || x.type == 0x39 || x.type == 0xffa5) { rare = true; continue; }
+        pl.off_row[cnt] = (uint16_t)(start - ch.extensions.d);
+        if (FMT != 0) {
+            bool fits;
+            const uint32_t v = ext_key32(x, FMT, bucket, cnt, fits);
+            rare |= !fits;
+            uint32_t prev = 0;
 #pragma unroll
-            for (int k = 0; k < REG_EXT; k++) if (k == cnt) V[k] = off;
-        } else {
-            const uint32_t key = ext_key(x, FMT, bucket);
-            const uint64_t v = ((uint64_t)key << 32) | off;
-            uint32_t pos = 0;
-            bool tie = false;
-#pragma unroll
-            for (int k = 0; k < REG_EXT; k++) {
-                pos += V[k] < v ? 1u : 0u;
-                tie |= (uint32_t)(V[k] >> 32) == key;
+            for (int k = 0; k < REG_EXT; k++) {  // insert v into the sorted list
+                const uint32_t old = V[k];
+                const uint32_t hi = prev > v ? prev : v;
+                V[k] = hi < old ? hi : old;
+                prev = old;
             }
-            if (tie && !key_is_grease(key, FMT)) rare = true;
-#pragma unroll
-            for (int k = REG_EXT - 1; k > 0; k--)
-                V[k] = (uint32_t)k > pos ? V[k - 1] : ((uint32_t)k == pos ? v : V[k]);
-            if (pos == 0) V[0] = v;
         }
         n += ext_fp_len(x.type, (uint32_t)clen(x.value));
         cnt++;
     }
+    if (FMT != 0 && !rare) {                     // equal keys the reference orders by value
+#pragma unroll
+        for (int k = 0; k + 1 < REG_EXT; k++)
+            rare |= V[k + 1] != ~0u && (V[k] >> 5) == (V[k + 1] >> 5) && !key32_grease(V[k], FMT);
+    }
     b.n = n;
     b.last_putc = true;                          // the string ends with ")" or "]"
     if (rare) return;
+    if (FMT != 0) {
 #pragma unroll
-    for (int k = 0; k < REG_EXT / 2; k++) pl.O[k] = ((uint32_t)V[2 * k] & 0xffff) | ((uint32_t)V[2 * k + 1] << 16);
+        for (int k = 0; k < REG_EXT; k++) if ((uint32_t)k < cnt) pl.ord_row[k] = (uint8_t)(V[k] & 31);
+    }
     pl.version = ch.version; pl.ciphers = ch.ciphers; pl.exts = ch.extensions;
-    pl.n = (uint32_t)cnt; pl.type = type; pl.fmt = (uint32_t)FMT;
+    pl.n = cnt; pl.type = type; pl.fmt = (uint32_t)FMT;
     pl.ok = true;
 }
 template <int FMT, class E>
@@ -1254,10 +1277,7 @@ DEV void tls_ch_emit_fast(E &b, TlsPlan &pl) {
     hex_run<true>(b, pl.ciphers.d, (uint32_t)clen(pl.ciphers) & ~1u);
     b.push(')' | ((FMT ? '[' : '(') << 8), 2);
     for (uint32_t j = 0; j < pl.n; j++) {
-        const uint32_t off = pl.O[0] & 0xffff;
-#pragma unroll
-        for (int k = 0; k < REG_EXT / 2; k++)             // pop the front offset
-            pl.O[k] = (pl.O[k] >> 16) | (k + 1 < REG_EXT / 2 ? pl.O[k + 1] << 16 : 0u);
+        const uint32_t off = pl.off_row[FMT == 0 ? j : pl.ord_row[j]];
         const uint8_t *h = pl.exts.d + off;
         const uint32_t th = ld_be32n(h, 4);                // type << 16 | length (the plan kept whole extensions)
         const uint32_t t = th >> 16, vl = th & 0xffff;

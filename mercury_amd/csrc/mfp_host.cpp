@@ -383,6 +383,10 @@ struct mfp_context_s {
     uint32_t quic_format = 0;            // fingerprint_format::quic_fingerprint_format (global_config.h:41)
     uint32_t quic_grid = 512;            // k_quic workgroups (x 128 lanes, each with a scratch slot)
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|lane (A/B, debugging)
+    // batches of at most this many packets take the lane walker (one launch
+    // instead of the classify pass and a launch per bin: the per-packet API's
+    // latency); MFP_SMALL_BATCH
+    size_t small_batch = 256;
     // bin b -> kernel: k_fp_lds (LDS-staged walk) if bit b of bin_lds_mask
     // (MFP_BIN_LDS_MASK), else the HBM lane walker; the bins of bin_seg_mask
     // (MFP_BIN_SEG_MASK; default the two HTTP bins) use segment expansion
@@ -432,6 +436,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     c->reassembly = reassembly;
     const char *st = getenv("MFP_STRATEGY");
     if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
+    if (const char *sb = getenv("MFP_SMALL_BATCH")) c->small_batch = (size_t)strtoull(sb, nullptr, 0);
     const char *sm = getenv("MFP_BIN_SEG_MASK");
     if (sm) c->bin_seg_mask = (uint32_t)strtoul(sm, nullptr, 0);
     const char *dm = getenv("MFP_BIN_LDS_MASK");
@@ -541,7 +546,8 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
         d_seg = S.d_seg;
     }
     if (mfp_launch_fingerprint(c->select, c->block, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, d_seg, (uint8_t *)d_fp_arena,
-                               fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins, c->strategy,
+                               fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins,
+                               n <= c->small_batch ? (int)MFP_STRATEGY_LANE : c->strategy,
                                c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
                                c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));

@@ -211,6 +211,8 @@ template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
     __shared__ uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
+    __shared__ uint16_t ext_off[TILE][REG_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
+    __shared__ uint8_t ext_ord[FMT ? TILE : 1][REG_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -260,6 +262,8 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         bool punt = false;
         TlsPlan plan;
         plan.ok = false;
+        plan.off_row = ext_off[tid];
+        plan.ord_row = ext_ord[FMT ? tid : 0];
         {
             Em<false, FMT> e;
             e.plan = &plan;

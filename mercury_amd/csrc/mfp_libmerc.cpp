@@ -5,9 +5,11 @@
 // /root/reference/src/libmerc/.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <mutex>
@@ -308,6 +310,9 @@ struct Combiner {
     std::condition_variable cv;
     std::vector<Req *> q;
     bool busy = false;
+    // MFP_SHIM_STATS: batches, packets, nanoseconds in the device batch / the
+    // records and JSON text (printed by mercury_finalize)
+    uint64_t st_batches = 0, st_pkts = 0, st_dev_ns = 0, st_host_ns = 0;
     // the leader's batch buffers (one leader at a time)
     std::vector<uint8_t> arena;
     std::vector<mfp_pkt_desc> desc;
@@ -339,9 +344,21 @@ static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req 
     C.rec.resize(n);
     C.fp.resize(cap);
     if (want_an) { C.an.resize(n); C.ap.assign(n * MFP_ATTR_DB_TAGS, 0.0); }
+    const auto t0 = std::chrono::steady_clock::now();
     const long long used = mfp_process_batch_host_ex(ctx, C.arena.data(), C.arena.size(), C.desc.data(), n, C.rec.data(),
                                                      C.fp.data(), cap, want_an ? C.an.data() : nullptr,
                                                      want_an ? C.ap.data() : nullptr);
+    const auto t1 = std::chrono::steady_clock::now();
+    C.st_batches++;
+    C.st_pkts += n;
+    C.st_dev_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    struct HostClock {
+        Combiner &C; std::chrono::steady_clock::time_point t;
+        ~HostClock() {
+            C.st_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                std::chrono::steady_clock::now() - t).count();
+        }
+    } host_clock{C, t1};
     if (used < 0) {
         log_error("%s\n", mfp_last_error());
         for (Req *r : batch) r->err = true;
@@ -390,7 +407,17 @@ static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req 
 }
 
 static void free_combiners(mercury *m) {
-    for (Combiner *&cb : m->comb) { delete cb; cb = nullptr; }
+    const bool stats = getenv("MFP_SHIM_STATS") != nullptr;
+    for (Combiner *&cb : m->comb) {
+        if (cb && stats && cb->st_batches)
+            fprintf(stderr, "{\"shim_stats\": {\"batches\": %llu, \"packets\": %llu, \"pkts_per_batch\": %.2f, "
+                    "\"device_us_per_batch\": %.2f, \"host_us_per_batch\": %.2f}}\n",
+                    (unsigned long long)cb->st_batches, (unsigned long long)cb->st_pkts,
+                    (double)cb->st_pkts / (double)cb->st_batches, cb->st_dev_ns / 1e3 / (double)cb->st_batches,
+                    cb->st_host_ns / 1e3 / (double)cb->st_batches);
+        delete cb;
+        cb = nullptr;
+    }
 }
 
 static void submit(mercury *m, mfp_context ctx, int mode, Req &r) {
