@@ -40,6 +40,38 @@ namespace {
 
 const char HEX[] = "0123456789abcdef";
 
+// 8 bytes -> 16 lowercase hex characters, first byte first (SWAR on two
+// 64-bit words: nibbles spread to bytes, then '0'/'a' added by a carry test)
+inline void hex8(const uint8_t *x, char *o) {
+    uint64_t v;
+    memcpy(&v, x, 8);
+    auto spread = [](uint64_t b) {                 // 4 bytes (little-endian) -> 8 nibbles, high first
+        b = (b | (b << 16)) & 0x0000ffff0000ffffull;
+        b = (b | (b << 8)) & 0x00ff00ff00ff00ffull;
+        const uint64_t nib = ((b >> 4) & 0x000f000f000f000full) | ((b & 0x000f000f000f000full) << 8);
+        const uint64_t gt9 = ((nib + 0x7676767676767676ull) & 0x8080808080808080ull) >> 7;
+        return nib + 0x3030303030303030ull + gt9 * 0x27;
+    };
+    const uint64_t lo = spread(v & 0xffffffffull), hi = spread(v >> 32);
+    memcpy(o, &lo, 8);
+    memcpy(o + 8, &hi, 8);
+}
+// two characters per byte value
+struct Hex2 {
+    char t[256][2];
+    Hex2() { for (int i = 0; i < 256; i++) { t[i][0] = HEX[i >> 4]; t[i][1] = HEX[i & 15]; } }
+};
+const Hex2 HEX2;
+// base64 of 12 bits -> 2 characters
+struct B64T {
+    char t[4096][2];
+    B64T() {
+        static const char T[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+        for (int i = 0; i < 4096; i++) { t[i][0] = T[i >> 6]; t[i][1] = T[i & 63]; }
+    }
+};
+const B64T B64;
+
 // fingerprint::get_type_name fingerprint.h:159-192
 const char *fp_type_name(unsigned t) {
     static const char *name[] = {"unknown", "tls", "tls_server", "http", "http_server", "ssh", "ssh_kex",
@@ -85,7 +117,9 @@ struct W {
         p += tab.n[v & 255];
     }
     void hexb(const uint8_t *x, size_t n) {         // raw_as_hex
-        for (size_t k = 0; k < n; k++) { put(HEX[x[k] >> 4]); put(HEX[x[k] & 15]); }
+        size_t k = 0;
+        for (; k + 8 <= n; k += 8) { hex8(x + k, p); p += 16; }
+        for (; k < n; k++) { memcpy(p, HEX2.t[x[k]], 2); p += 2; }
     }
     void hexu(uint64_t v, int digits) {             // append_uint{8,16,32,64}_hex: fixed width
         for (int k = digits - 1; k >= 0; k--) put(HEX[(v >> (4 * k)) & 15]);
@@ -166,8 +200,10 @@ struct W {
         put('"');
         size_t i = 0, full = n - n % 3;
         for (; i < full; i += 3) {
-            uint32_t t = ((uint32_t)d[i] << 16) | ((uint32_t)d[i + 1] << 8) | d[i + 2];
-            put(T[t >> 18 & 63]); put(T[t >> 12 & 63]); put(T[t >> 6 & 63]); put(T[t & 63]);
+            const uint32_t t = ((uint32_t)d[i] << 16) | ((uint32_t)d[i + 1] << 8) | d[i + 2];
+            memcpy(p, B64.t[t >> 12], 2);
+            memcpy(p + 2, B64.t[t & 4095], 2);
+            p += 4;
         }
         if (n % 3) {
             uint32_t t = (uint32_t)d[i] << 16;
