@@ -134,6 +134,13 @@ def other_paths(torch, steps):
         prof = ctx.profile_read()
         ctx.profile(False)
         rec = d_rec.cpu().numpy().view(mercury_amd.RECORD_DTYPE)
+        phases = None
+        if os.environ.get("MFP_REPORT_PHASES"):      # probe builds (MFP_K_PHASES): k_quic's phase clock sums
+            import ctypes
+            fn = getattr(ctx.lib, "mfp_probe_read_quic", None)
+            words = (ctypes.c_uint64 * 8)()
+            if fn is not None and fn(words) == 0:
+                phases = [int(x) for x in words[:5]]
         ctx.close()
         byts = int(desc["caplen"].astype(np.int64).sum())
         kms = {k: round(v[1] / steps, 4) for k, v in prof.items()}
@@ -141,6 +148,8 @@ def other_paths(torch, steps):
                      "ms_per_step": round(el / steps * 1e3, 4), "gb_per_s": round(byts * steps / el / 1e9, 3),
                      "fingerprints_per_step": int((rec["fp_type"] > 0).sum()), "kernel_ms": kms,
                      "what": f"{npz} (reference pcaps + synthetic) replicated on the device, {sel}"}
+        if phases:
+            out[name]["quic_phase_clocks"] = phases
         del d_arena, d_desc, d_rec, d_fp
         torch.cuda.empty_cache()
     # the reassembly path: one host batch of the three reassembly streams,

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "mfp_device.hpp"
+#include "mfp_kphase.hpp"
 #define QHD __device__ __forceinline__
 #include "mfp_quic_crypto.hpp"
 
@@ -653,6 +654,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
     uint8_t *pt = scratch + ((uint64_t)blockIdx.x * QT + tid) * Q_SLOT;
     uint8_t *cb = pt + Q_PT;
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    KPH_DECL
     for (uint64_t tile = blockIdx.x; tile * QT < count; tile += gridDim.x) {
         const uint64_t t = tile * QT + tid;
         const bool live = t < count;
@@ -672,6 +674,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             c.classify = 1;
             packet_walk(e, c, o, data, dsc.caplen, dsc.linktype);
         }
+        KPH(0);
         QRes q;
         q.flags = 0; q.hello = false; q.pre = false; q.ver = nullptr; q.more = 0; q.min_off = ~0u;
         const bool ovpn = live && o.msg == MFP_MSG_OPENVPN;
@@ -696,6 +699,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             v = ovpn_process(cmk(data + o.pay_off, data + o.pay_off + o.pay_len), pt);
             q.flags = v.present ? MFP_FLAG_EMIT : 0;
         }
+        KPH(1);
         const uint32_t fmt = q.pre ? 0u : quic_format;
         uint32_t len = 0, fp_type = 0;
         QMeta m; cset_null(m.sni); cset_null(m.ua); cset_null(m.alpn);
@@ -764,6 +768,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         const unsigned long long base = tile_base;
         const bool fits = base != ~0ull;
 
+        KPH(2);
         uint32_t sni_off = 0, sni_len = 0xffff, ua_off = 0, ua_len = 0xffff;
         uint8_t *out = P.fp_arena + (fits ? base + excl : 0);
         uint8_t *sc = out + ((len + 7) & ~7u) + 8;
@@ -774,6 +779,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             e.finish();
             *(uint64_t *)(sc - 8) = e.hash();
         }
+        KPH(3);
         if (side && fits) {
             // header: {u16 alpn_off, u16 alpn_len, u16 side_len, u16 json_off}, then
             // the server name, user agent and ALPN list (classifier inputs)
@@ -784,7 +790,7 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
                 offs[k] = at;
                 lens[k] = len && !cnull(parts[k]) ? (uint32_t)clen(parts[k]) : 0xffffu;
                 const uint32_t sl = len ? span_len(parts[k]) : 0u;
-                for (uint32_t j = 0; j < sl; j++) sc[at + j] = (uint8_t)ld(parts[k].d + j);
+                copy_bytes(sc + at, parts[k].d, sl);
                 at += sl;
             }
             if (len) { sni_off = offs[0]; sni_len = lens[0]; ua_off = offs[1]; ua_len = lens[1]; }
@@ -803,9 +809,9 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
                 hdr[12] = hdr[13] = hdr[14] = hdr[15] = 0;
                 for (int k = 0; k < 16; k++) sc[at + k] = hdr[k];
                 at += 16;
-                for (uint32_t j = 0; j < pt_n; j++) sc[at + j] = (uint8_t)ld(q.plain.d + j);
+                copy_bytes(sc + at, q.plain.d, pt_n);
                 at += pt_n;
-                for (uint32_t j = 0; j < hs_n; j++) sc[at + j] = (uint8_t)ld(q.hs.d + j);
+                copy_bytes(sc + at, q.hs.d, hs_n);
                 at += hs_n;
             }
             const uint32_t hv2[4] = {offs[2], lens[2], side, json_off};
@@ -834,7 +840,9 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             write_seg(P, i, o);
         }
         __syncthreads();   // tile_base / wave_tot reuse
+        KPH(4);
     }
+    KPH_FLUSH();
 }
 
 }  // namespace mfp
@@ -849,5 +857,7 @@ extern "C" int mfp_launch_quic(const void *kparams, uint8_t *scratch, uint32_t q
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+KPH_READER(quic)
 
 extern "C" size_t mfp_quic_scratch_bytes(uint32_t grid) { return (size_t)grid * mfp::QT * mfp::Q_SLOT + 64; }
