@@ -266,6 +266,7 @@ struct Em {
     // line in LDS makes those (divergent) global stores 8x rarer than
     // storing every word.
     uint8_t *out = nullptr;  // next 64-byte line of the string
+    uint8_t *out_end = nullptr; // (optional) end of the string's slot: lines past it are not stored
     uint64_t *line = nullptr;   // this lane's LDS line (8 words)
     uint64_t acc = 0;        // staged bytes of the current word
     uint32_t nacc = 0;       // bytes in acc
@@ -288,6 +289,7 @@ struct Em {
 #endif
         const uint4 *l4 = (const uint4 *)line;
         uint4 *o4 = (uint4 *)out;
+        if (out_end && out + 8 * ((words + 1) & ~1u) > out_end) return;   // (an over-long string: dropped anyway)
         for (uint32_t k = 0; 2 * k < words; k++) o4[k] = l4[k];
     }
     DEV void put_word() {
@@ -376,8 +378,24 @@ struct Em {
 // ---------------------------------------------------------------------------
 constexpr int SEG_MAX = 24;
 enum : uint32_t { SK_POOL = 0, SK_HEX = 1, SK_HEXP = 3 };   // SK_HEXP: '(' hex ')'
-#define MFP_SEG_POOL "http_server/http/()"
-constexpr uint32_t POOL_HTTP_SERVER = 0, POOL_HTTP = 12, POOL_OPEN = 17, POOL_CLOSE = 18;
+#define MFP_SEG_POOL "http_server/http/()20ssh_kex_server/ssh_kex/ssh_init_server/ssh_init/ssh_server/ssh/"
+constexpr uint32_t POOL_HTTP_SERVER = 0, POOL_HTTP = 12, POOL_OPEN = 17, POOL_CLOSE = 18, POOL_2 = 19, POOL_0 = 20;
+constexpr uint32_t SEG_POOL_BYTES = 96;
+// a type prefix's place in the pool (fp_type_prefix's literals for HTTP and
+// SSH, told apart by first character and length); ~0u: not in the pool
+DEV uint32_t seg_pool_lit(uint32_t c0, uint32_t k) {
+    if (c0 == 'h') return k == 12 ? 0u : k == 5 ? 12u : ~0u;
+    if (c0 != 's') return ~0u;
+    switch (k) {
+    case 15: return 21;   // ssh_kex_server/
+    case 8: return 36;    // ssh_kex/
+    case 16: return 44;   // ssh_init_server/
+    case 9: return 60;    // ssh_init/
+    case 11: return 69;   // ssh_server/
+    case 4: return 80;    // ssh/
+    }
+    return ~0u;
+}
 DEV uint32_t seg_end(uint32_t s) { return s & 0x1fff; }
 DEV uint32_t seg_kind(uint32_t s) { return (s >> 13) & 3; }
 DEV uint32_t seg_src(uint32_t s) { return s >> 15; }
@@ -421,6 +439,8 @@ struct SegEm {
             flush_open();
             if (c == '(') open = true;
             else if (c == ')') store(SK_POOL, POOL_CLOSE, n + 1);
+            else if (c == '2') store(SK_POOL, POOL_2, n + 1);     // the SSH protocol/comment delimiter "20"
+            else if (c == '0') store(SK_POOL, POOL_0, n + 1);
             else ovf = true;
         }
         n += 1;
@@ -439,8 +459,8 @@ struct SegEm {
         last_putc = false;
         uint32_t k = 0;
         while (s[k]) k++;
-        if (s[0] == 'h' && k == 5) store(SK_POOL, POOL_HTTP, n + 5);
-        else if (s[0] == 'h' && k == 12) store(SK_POOL, POOL_HTTP_SERVER, n + 12);
+        const uint32_t at = seg_pool_lit((uint8_t)s[0], k);
+        if (at != ~0u) store(SK_POOL, at, n + k);
         else ovf = true;
         n += k;
     }
@@ -1855,11 +1875,11 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
     o.msg = msg;
     if (cfg.classify) return;
     const bool tls_msg = msg == MFP_MSG_TLS_CH || msg == MFP_MSG_TLS_SH || msg == MFP_MSG_TLS_CERT;
-    if (E::SEG || (tls_msg && !(FAM & FAM_TLS)) || (!tls_msg && !(FAM & FAM_SSH))) {
+    if ((E::SEG && (FAM & FAM_TLS)) || (tls_msg && !(FAM & FAM_TLS)) || (!tls_msg && !(FAM & FAM_SSH))) {
         b.punt_pkt();          // a parser this walker lacks: the fallback lane fingerprints it
         return;
     }
-    if constexpr (!E::SEG) {
+    if constexpr (!E::SEG || !(FAM & FAM_TLS)) {
     switch (msg) {
     case MFP_MSG_TLS_CH: {
         if constexpr (!(FAM & FAM_TLS)) return; else {

@@ -198,7 +198,8 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
                                                                   : lane_name[b];
         const uint32_t lb = (uint32_t)lblocks, fb = (uint32_t)fblocks;
         int rc;
-        if (seg) rc = mfp_launch_bin_seg(&P, fallback, lds, nm, lb, fb, stream, prof);
+        if (seg && b == 6) rc = mfp_launch_bin_ssh_seg(&P, fallback, lds, nm, lb, fb, stream, prof);
+        else if (seg) rc = mfp_launch_bin_seg(&P, fallback, lds, nm, lb, fb, stream, prof);
         else switch (b) {
         case 0: case 5: rc = mfp_launch_bin_tls(&P, fallback, lds, nm, lb, fb, stream, prof); break;    // TLS ClientHello, ServerHello/Certificate
         case 1: case 3: rc = mfp_launch_bin_http(&P, fallback, lds, nm, lb, fb, stream, prof); break;   // HTTP request, response

@@ -339,12 +339,12 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
 constexpr int SEG_STRIDE = SEG_MAX + 1;   // odd word stride: lane-private lists are bank-conflict free
 constexpr uint32_t SEG_STAGE = 2048;      // packets up to this (minus alignment) are staged in LDS for expansion
 constexpr int SEG_LINEW = 4;              // lane emission: words per LDS line
-template <int = 0>
+template <uint32_t FAM = FAM_HTTP>
 __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32_t *fallback) {
     __shared__ uint32_t segs[TILE * SEG_STRIDE];
     __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
     __shared__ unsigned long long tile_base;
-    __shared__ uint8_t pool[32];
+    __shared__ uint8_t pool[SEG_POOL_BYTES];
 #if MFP_SEG_LANE
     __shared__ uint64_t out_line[TILE][SEG_LINEW];
 #else
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 #endif
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
-    if (tid < 32) {
+    if (tid < (int)SEG_POOL_BYTES) {
         const char *lp = MFP_SEG_POOL;
         pool[tid] = (uint8_t)(tid < (int)sizeof(MFP_SEG_POOL) ? lp[tid] : 0);
     }
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 
         Out o;
         SegEm e(data, segs + tid * SEG_STRIDE);
-        packet_walk<FAM_HTTP>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+        packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
         e.finish();
         const bool fb = live && e.ovf;
         uint32_t len = 0;
@@ -536,12 +536,12 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
     __shared__ uint4 stage[STG / 16];
     __shared__ uint64_t out_line[SEGMODE ? 1 : 64][8];
     __shared__ uint32_t segs[SEGMODE ? 64 * SEG_STRIDE : 1];
-    __shared__ uint8_t pool[32];
+    __shared__ uint8_t pool[SEG_POOL_BYTES];
     const uint32_t lane = threadIdx.x;
     uint8_t *stg = (uint8_t *)&stage[0];
-    if (SEGMODE && lane < 32) {
+    if (SEGMODE) {
         const char *lp = MFP_SEG_POOL;
-        pool[lane] = (uint8_t)(lane < sizeof(MFP_SEG_POOL) ? lp[lane] : 0);
+        for (uint32_t k = lane; k < SEG_POOL_BYTES; k += 64) pool[k] = (uint8_t)(k < sizeof(MFP_SEG_POOL) ? lp[k] : 0);
     }
     __builtin_amdgcn_wave_barrier();
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -606,7 +606,7 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
             if constexpr (SEGMODE) {
                 SegEm e(data, segs + lane * SEG_STRIDE);
                 if (in) {
-                    packet_walk<FAM_HTTP>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+                    packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
                     e.finish();
                     fb = e.ovf;
                     if (!fb && o.fp_type) {
@@ -753,6 +753,7 @@ MFP_BIN_LAUNCHER(tcp);
 MFP_BIN_LAUNCHER(ssh);
 MFP_BIN_LAUNCHER(dtls);
 MFP_BIN_LAUNCHER(all);
-// the HTTP segment-expansion kernels (k_fp_lds<true> when lds, else k_fp_seg)
+// the HTTP segment-expansion kernels (k_fp_lds<true> when lds, else k_fp_seg), and SSH's
 MFP_BIN_LAUNCHER(seg);
+MFP_BIN_LAUNCHER(ssh_seg);
 

@@ -642,11 +642,14 @@ DEV void ovpn_fp(E &b, const OvRes &v) {
     tls_ch_fp(b, v.ch, 0);
 }
 
-__global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32_t quic_format) {
+#ifndef MFP_QUIC_MINW
+#define MFP_QUIC_MINW 1
+#endif
+__global__ __launch_bounds__(QT, MFP_QUIC_MINW) void k_quic(KParams P, uint8_t *scratch, uint32_t quic_format) {
     __shared__ uint32_t s_te[256];
     __shared__ uint64_t s_gh[32 * QT];
     __shared__ uint64_t out_line[QT][8];
-    __shared__ uint32_t wave_tot[QT / 64], wave_len[QT / 64];
+    __shared__ uint32_t wave_tot[QT / 64];
     __shared__ unsigned long long tile_base;
     const int tid = threadIdx.x;
     for (int k = tid; k < 256; k += QT) s_te[k] = mfpq::kAes.te0[k];
@@ -701,19 +704,24 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         }
         KPH(1);
         const uint32_t fmt = q.pre ? 0u : quic_format;
-        uint32_t len = 0, fp_type = 0;
+        // the string's slot: QUIC, from an upper bound (every byte of the
+        // handshake yields at most 2.5 characters: a 4-byte extension header
+        // 10, a transport parameter's 1-byte id and length 4), so the string is
+        // written in one pass and its length known after; OpenVPN, exact (a
+        // counting pass)
+        uint32_t len = 0, fp_type = 0, bound = 0;
         QMeta m; cset_null(m.sni); cset_null(m.ua); cset_null(m.alpn);
         if (q.hello) {
-            Em<false> e;
-            quic_fp(e, q, fmt);
-            if (e.valid()) { len = e.n; fp_type = 12; }       // fingerprint::final drops truncated strings
+            const uint32_t hb = 5 * span_len(q.hs) / 2 + 64;
+            bound = hb < FP_MAX ? hb : FP_MAX;
+            fp_type = 12;
             m = quic_meta(q.ch.extensions);
         } else if (v.hello) {
             Em<false> e;
             TlsPlan plan;
             e.plan = &plan;
             ovpn_fp(e, v);
-            if (e.valid()) { len = e.n; fp_type = 14; }
+            if (e.valid()) { len = e.n; bound = len; fp_type = 14; }
         }
         // the sidecar (include/mfp.h MFP_FLAG_SIDECAR): an 8-byte header, the
         // classifier inputs, and on the write_json path the bytes the JSON
@@ -727,13 +735,13 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         const bool json = quic && (P.cfg.mode == MFP_MODE_WRITE_JSON || reasm);
         const uint32_t pt_n = json ? span_len(q.plain) : 0u;
         const uint32_t hs_n = json && q.hello && P.cfg.mode == MFP_MODE_WRITE_JSON ? span_len(q.hs) : 0u;
-        const uint32_t meta = len && !ovpn ? span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
+        const uint32_t meta = bound && !ovpn ? span_len(m.sni) + span_len(m.ua) + span_len(m.alpn) : 0u;
         const uint32_t jlen = json ? 16 + pt_n + hs_n : 0u;
-        const uint32_t side = (len && !ovpn) || json ? 8 + meta + jlen : 0u;
+        const uint32_t side = (bound && !ovpn) || json ? 8 + meta + jlen : 0u;
 
-        // tile reservation of 64-byte slots: string, hash, sidecar
+        // tile reservation of 64-byte slots: string (its bound), hash, sidecar
         const int lane = tid & 63, wid = tid >> 6;
-        const uint32_t slot = len || side ? (((len + 7) & ~7u) + 8 + side + 63) & ~63u : 0u;
+        const uint32_t slot = bound || side ? (((bound + 7) & ~7u) + 8 + side + 63) & ~63u : 0u;
         uint32_t incl = slot;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -741,10 +749,6 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
             if (lane >= d) incl += y;
         }
         if (lane == 63) wave_tot[wid] = incl;
-        uint32_t lsum = len;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) lsum += __shfl_xor(lsum, d, 64);
-        if (lane == 0) wave_len[wid] = lsum;
         __syncthreads();
         uint32_t wbase = 0, total = 0;
 #pragma unroll
@@ -757,11 +761,6 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         if (tid == 0) {
             unsigned long long b = total ? atomicAdd(&P.fp_used[0], (unsigned long long)total) : 0ull;
             if (b + total > P.fp_cap) { atomicExch(&P.fp_used[1], 1ull); b = ~0ull; }
-            else if (total) {
-                uint32_t lt = 0;
-                for (int w = 0; w < QT / 64; w++) lt += wave_len[w];
-                atomicAdd(&P.fp_used[2], (unsigned long long)lt);
-            }
             tile_base = b;
         }
         __syncthreads();
@@ -771,13 +770,26 @@ __global__ __launch_bounds__(QT) void k_quic(KParams P, uint8_t *scratch, uint32
         KPH(2);
         uint32_t sni_off = 0, sni_len = 0xffff, ua_off = 0, ua_len = 0xffff;
         uint8_t *out = P.fp_arena + (fits ? base + excl : 0);
-        uint8_t *sc = out + ((len + 7) & ~7u) + 8;
-        if (len && fits) {
+        uint8_t *sc = out;
+        if (bound && fits) {
             Em<true> e;
             e.begin(out, out_line[tid]);
+            e.out_end = out + ((bound + 7) & ~7u) + 8;   // (a final 16-byte store may cover the hash's place)
             if (ovpn) ovpn_fp(e, v); else quic_fp(e, q, fmt);
             e.finish();
-            *(uint64_t *)(sc - 8) = e.hash();
+            if (e.valid() && e.n <= bound) {
+                len = e.n;
+                *(uint64_t *)(out + ((len + 7) & ~7u)) = e.hash();
+            } else {
+                fp_type = 0;                               // fingerprint::final drops truncated strings
+            }
+        }
+        sc = out + ((len + 7) & ~7u) + 8;
+        {   // bytes written (fp_used[2]): the exact lengths
+            uint32_t lsum = fits ? len : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) lsum += __shfl_xor(lsum, d, 64);
+            if (lane == 0 && lsum) atomicAdd(&P.fp_used[2], (unsigned long long)lsum);
         }
         KPH(3);
         if (side && fits) {

@@ -1,8 +1,10 @@
 #!/bin/bash
 # follow-up of tools/gpu_suite.sh: the per-packet shim leg, then an A/B of
-# library variants (VARIANTS, see tools/gpu_ab_lib.sh) on config 4
+# library variants (VARIANTS, see tools/gpu_ab_lib.sh) on config 4, then
+# k_quic's phase clocks when QUIC_PHASES is set
 #   tools/after_suite.sh <outdir>
 out=$1
 tools/shim_bench.sh "$out" || exit $?
-[ -n "$VARIANTS" ] && TAG=${out#gpurun_out/}_ab tools/gpu_ab_lib.sh
+if [ -n "$VARIANTS" ]; then TAG=${out#gpurun_out/}_ab tools/gpu_ab_lib.sh || exit $?; fi
+if [ -n "$QUIC_PHASES" ]; then tools/quic_phases.sh "$out" || exit $?; fi
 exit 0
