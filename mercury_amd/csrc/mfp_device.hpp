@@ -704,6 +704,52 @@ DEV bool qtp_less(Cur a, Cur b) {                       // fmt-1 id comparator t
     return ccmp(a, b) < 0;
 }
 
+// The sorted transport parameter ids of a 0x39 / 0xffa5 extension
+// (fingerprint_format1 tls.h:1440-1470) from one parse: each id's sort key in
+// a register list (insertion by max/min), then written in order.  The key:
+// GREASE ids as 0x1b, the others by value -- the comparator's byte order
+// (datum::cmp) for minimally encoded ids -- then the wire offset.  Returns
+// false, having written nothing, for more than QTP_MAX ids, a non-minimal
+// encoding or a value past 2^46 (the caller's selection handles those).
+constexpr int QTP_MAX = 20;
+template <class E>
+DEV bool qtp_sorted_fp(E &b, const Ext &x) {
+    uint64_t K[QTP_MAX];
+#pragma unroll
+    for (int k = 0; k < QTP_MAX; k++) K[k] = ~0ull;
+    uint32_t cnt = 0;
+    Cur v = x.value;
+    while (!cnull(v)) {
+        Cur id;
+        if (!qtp_parse(v, id)) continue;
+        if (cnt >= (uint32_t)QTP_MAX) return false;
+        const uint32_t L = (uint32_t)clen(id);
+        const uint64_t val = vli_value(id);
+        const bool minimal = L == 1 || (L == 2 && val >= 64) || (L == 4 && val >= 16384) || (L == 8 && val >= (1ull << 30));
+        if (!minimal || val >= (1ull << 46)) return false;
+        const uint64_t key = ((val % 31 == 27 ? 0x1bull : val) << 17) | (uint64_t)(id.d - x.value.d);
+        uint64_t prev = 0;
+#pragma unroll
+        for (int k = 0; k < QTP_MAX; k++) {
+            const uint64_t old = K[k];
+            const uint64_t hi = prev > key ? prev : key;
+            K[k] = hi < old ? hi : old;
+            prev = old;
+        }
+        cnt++;
+    }
+    for (uint32_t j = 0; j < cnt; j++) {
+        const uint64_t e = K[0];
+#pragma unroll
+        for (int k = 0; k + 1 < QTP_MAX; k++) K[k] = K[k + 1];
+        Cur id;
+        id.d = x.value.d + (e & 0x1ffff);
+        id.e = id.d + vli_len(ld(id.d));
+        b.putc('('); qtp_write_id(b, id); b.putc(')');
+    }
+    return true;
+}
+
 // fmt-1 output of one extension: tls_extension::fingerprint_format1 tls.h:1413
 template <class E>
 DEV void ext_fp1(E &b, Ext &x, int role) {
@@ -720,7 +766,8 @@ DEV void ext_fp1(E &b, Ext &x, int role) {
             Cur prev; cset_null(prev);
             bool have_prev = false;
             long prev_pos = -1;
-            while (true) {
+            const bool sorted = qtp_sorted_fp(b, x);
+            while (!sorted) {
                 Cur best; cset_null(best); long best_pos = -1;
                 Cur v = x.value; long pos = 0;
                 while (!cnull(v)) {
@@ -1199,13 +1246,18 @@ DEV uint32_t ext_fp_len(uint32_t t, uint32_t vl) {
     }
     return 10 + 2 * vl;                                  // "(" type length value ")"
 }
+// At most FAST_EXT kept extensions (MFP_FAST_EXT; more leave the plan unset).
+#ifndef MFP_FAST_EXT
+#define MFP_FAST_EXT 24
+#endif
+constexpr int FAST_EXT = MFP_FAST_EXT;
 // Formats 1/2 order the kept extensions by a 32-bit key (ext_key32): the
 // field the reference's comparator looks at first, then the length, then the
 // wire index (so equal keys keep wire order); the sorted list lives in 24
 // registers and an insertion is a max and a min per entry (inserting v into a
 // sorted list: new[k] = min(max(old[k-1], v), old[k]), no position search).  Equal keys that need the
 // reference's value comparison, lengths past the key's field and more than
-// REG_EXT kept extensions leave the plan unset (the fallback lane writes them).
+// FAST_EXT kept extensions leave the plan unset (the fallback lane writes them).
 DEV uint32_t ext_key32(const Ext &x, int fmt, int bucket, uint32_t idx, bool &fits) {
     const bool g = ext_is_grease(x.type);
     if (fmt == 1) {                              // tls.h:1637: GREASE as 0x0a0a, then type, length
@@ -1224,9 +1276,9 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     // type prefix, "1/" or "2/", "(" version ")" "(" degreased ciphers ")", "(" or "[", ... ")" or "]"
     uint32_t n = (type == 10 ? 5u : 4u) + (FMT ? 2u : 0u) + 2 + 2 * (uint32_t)clen(ch.version) + 2 +
                  2 * ((uint32_t)clen(ch.ciphers) & ~1u) + 2;
-    uint32_t V[REG_EXT];                         // formats 1/2: sorted ext_key32 values
+    uint32_t V[FAST_EXT];                         // formats 1/2: sorted ext_key32 values
 #pragma unroll
-    for (int k = 0; k < REG_EXT; k++) V[k] = ~0u;
+    for (int k = 0; k < FAST_EXT; k++) V[k] = ~0u;
     uint32_t cnt = 0;
     bool rare = false;
     Cur p = ch.extensions;
@@ -1247,10 +1299,10 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
             if (bucket < 0) continue;
             uint32_t c3 = 0;                     // first three per bucket (tls.h:1695-1701)
 #pragma unroll
-            for (int k = 0; k < REG_EXT; k++) c3 += (V[k] >> 24) == (uint32_t)bucket ? 1u : 0u;
+            for (int k = 0; k < FAST_EXT; k++) c3 += (V[k] >> 24) == (uint32_t)bucket ? 1u : 0u;
             if (c3 >= 3) continue;
         }
-        if (cnt >= (uint32_t)REG_EXT || x.type == 0x39 || x.type == 0xffa5) { rare = true; continue; }
+        if (cnt >= (uint32_t)FAST_EXT || x.type == 0x39 || x.type == 0xffa5) { rare = true; continue; }
         pl.off_row[cnt] = (uint16_t)(start - ch.extensions.d);
         if (FMT != 0) {
             bool fits;
@@ -1258,7 +1310,7 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
             rare |= !fits;
             uint32_t prev = 0;
 #pragma unroll
-            for (int k = 0; k < REG_EXT; k++) {  // insert v into the sorted list
+            for (int k = 0; k < FAST_EXT; k++) {  // insert v into the sorted list
                 const uint32_t old = V[k];
                 const uint32_t hi = prev > v ? prev : v;
                 V[k] = hi < old ? hi : old;
@@ -1270,7 +1322,7 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     }
     if (FMT != 0 && !rare) {                     // equal keys the reference orders by value
 #pragma unroll
-        for (int k = 0; k + 1 < REG_EXT; k++)
+        for (int k = 0; k + 1 < FAST_EXT; k++)
             rare |= V[k + 1] != ~0u && (V[k] >> 5) == (V[k + 1] >> 5) && !key32_grease(V[k], FMT);
     }
     b.n = n;
@@ -1278,7 +1330,7 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     if (rare) return;
     if (FMT != 0) {
 #pragma unroll
-        for (int k = 0; k < REG_EXT; k++) if ((uint32_t)k < cnt) pl.ord_row[k] = (uint8_t)(V[k] & 31);
+        for (int k = 0; k < FAST_EXT; k++) if ((uint32_t)k < cnt) pl.ord_row[k] = (uint8_t)(V[k] & 31);
     }
     pl.version = ch.version; pl.ciphers = ch.ciphers; pl.exts = ch.extensions;
     pl.n = cnt; pl.type = type; pl.fmt = (uint32_t)FMT;

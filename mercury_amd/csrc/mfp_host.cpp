@@ -846,10 +846,14 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
         HIPCHK(hipMemcpyAsync(attr_prob, S.d_ap, n * MFP_ATTR_DB_TAGS * sizeof(double), hipMemcpyDeviceToHost, S.stream));
     if (n) HIPCHK(hipMemcpyAsync(rec, S.d_rec, n * sizeof(mfp_record), hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
+    // small batches (the per-packet API): the packed strings' likely extent
+    // comes back with the records, one round trip instead of two
+    const size_t spec = n <= c->small_batch ? std::min<size_t>(fp_cap, (size_t)256 << 10) : 0;
+    if (spec) HIPCHK(hipMemcpyAsync(fp_arena, S.d_fp2, spec, hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
     const unsigned long long used = S.h_used[2];   // dense bytes
     if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
-    if (used) HIPCHK(hipMemcpy(fp_arena, S.d_fp2, used, hipMemcpyDeviceToHost));
+    if (used > spec) HIPCHK(hipMemcpy(fp_arena + spec, S.d_fp2 + spec, used - spec, hipMemcpyDeviceToHost));
     return (long long)used;
 }
 

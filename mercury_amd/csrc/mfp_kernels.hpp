@@ -196,8 +196,8 @@ template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
     __shared__ uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
-    __shared__ uint16_t ext_off[TILE][REG_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
-    __shared__ uint8_t ext_ord[FMT ? TILE : 1][REG_EXT + 4];   // emission order (formats 1/2)
+    __shared__ uint16_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
+    __shared__ uint8_t ext_ord[FMT ? TILE : 1][FAST_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;

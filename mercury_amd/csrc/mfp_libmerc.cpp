@@ -4,6 +4,9 @@
 // interface is the batch API.  File:line cites are relative to
 // /root/reference/src/libmerc/.
 #include <algorithm>
+#include <new>
+
+#include <hip/hip_runtime.h>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -305,6 +308,42 @@ struct Req {
     bool done = false;
 };
 
+// a growable host buffer in page-locked memory: the batch's copies to and
+// from the device are then DMA transfers the stream queues, not staged
+// through a driver bounce buffer with a wait per copy (pageable memory)
+extern "C++" {
+template <class T>
+struct PinnedVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    bool pinned = false;
+    PinnedVec() = default;
+    PinnedVec(const PinnedVec &) = delete;
+    PinnedVec &operator=(const PinnedVec &) = delete;
+    ~PinnedVec() { release(); }
+    void release() {
+        if (p) { if (pinned) (void)hipHostFree(p); else free(p); }
+        p = nullptr; cap = 0;
+    }
+    void reserve(size_t c) {
+        if (c <= cap) return;
+        const size_t nc = std::max(c, cap * 2 + 64);
+        T *q = nullptr;
+        bool pq = hipHostMalloc((void **)&q, nc * sizeof(T), hipHostMallocDefault) == hipSuccess;
+        if (!pq) { q = static_cast<T *>(malloc(nc * sizeof(T))); if (!q) throw std::bad_alloc(); }
+        if (n) memcpy(q, p, n * sizeof(T));
+        release();
+        p = q; cap = nc; pinned = pq;
+    }
+    void resize(size_t k) { reserve(k); n = k; }
+    void clear() { n = 0; }
+    void append(const T *x, size_t k) { reserve(n + k); memcpy(p + n, x, k * sizeof(T)); n += k; }
+    size_t size() const { return n; }
+    T *data() { return p; }
+    T &operator[](size_t i) { return p[i]; }
+};
+}  // extern "C++"
+
 struct Combiner {
     std::mutex m;
     std::condition_variable cv;
@@ -313,13 +352,13 @@ struct Combiner {
     // MFP_SHIM_STATS: batches, packets, nanoseconds in the device batch / the
     // records and JSON text (printed by mercury_finalize)
     uint64_t st_batches = 0, st_pkts = 0, st_dev_ns = 0, st_host_ns = 0;
-    // the leader's batch buffers (one leader at a time)
-    std::vector<uint8_t> arena;
-    std::vector<mfp_pkt_desc> desc;
-    std::vector<mfp_record> rec;
-    std::vector<char> fp;
-    std::vector<mfp_analysis> an;
-    std::vector<double> ap;
+    // the leader's batch buffers (one leader at a time), page-locked
+    PinnedVec<uint8_t> arena;
+    PinnedVec<mfp_pkt_desc> desc;
+    PinnedVec<mfp_record> rec;
+    PinnedVec<char> fp;
+    PinnedVec<mfp_analysis> an;
+    PinnedVec<double> ap;
     std::vector<uint64_t> ts, ends;
     std::vector<char> out;
 };
@@ -333,17 +372,27 @@ static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req 
     for (size_t i = 0; i < n; i++) {
         const Req &r = *batch[i];
         C.desc[i] = mfp_pkt_desc{(uint64_t)C.arena.size(), (uint32_t)r.len, r.linktype, 0};
-        C.arena.insert(C.arena.end(), r.pkt, r.pkt + r.len);
-        C.arena.resize((C.arena.size() + 15) & ~(size_t)15);   // 16-byte aligned packets
+        C.arena.append(r.pkt, r.len);
+        const size_t at = C.arena.size();
+        C.arena.resize((at + 15) & ~(size_t)15);               // 16-byte aligned packets
+        memset(C.arena.data() + at, 0, C.arena.size() - at);
         C.ts[i] = r.t_ns;
         total += r.len;
     }
-    C.arena.resize(C.arena.size() + 16);
+    {
+        const size_t at = C.arena.size();
+        C.arena.resize(at + 16);
+        memset(C.arena.data() + at, 0, 16);
+    }
     const bool want_an = mfp_analysis_enabled(ctx);
     const size_t cap = mfp_fp_arena_bound(n, total);
     C.rec.resize(n);
     C.fp.resize(cap);
-    if (want_an) { C.an.resize(n); C.ap.assign(n * MFP_ATTR_DB_TAGS, 0.0); }
+    if (want_an) {
+        C.an.resize(n);
+        C.ap.resize(n * MFP_ATTR_DB_TAGS);
+        memset(C.ap.data(), 0, n * MFP_ATTR_DB_TAGS * sizeof(double));
+    }
     const auto t0 = std::chrono::steady_clock::now();
     const long long used = mfp_process_batch_host_ex(ctx, C.arena.data(), C.arena.size(), C.desc.data(), n, C.rec.data(),
                                                      C.fp.data(), cap, want_an ? C.an.data() : nullptr,
