@@ -251,6 +251,8 @@ def per_packet_shim(seconds=2.0):
                     for line in r.stderr.decode(errors="replace").splitlines():
                         if '"shim_stats"' in line:        # the combiner's batches (MFP_SHIM_STATS)
                             pt.update(json.loads(line)["shim_stats"])
+                        if '"shim_kernels"' in line:      # [launches, total ms] per kernel
+                            pt.setdefault("kernels", {}).update(json.loads(line)["shim_kernels"])
                     out["points"].append(pt)
     finally:
         os.unlink(path)

@@ -390,8 +390,8 @@ struct mfp_context_s {
     // bin b -> kernel: k_fp_lds (LDS-staged walk) if bit b of bin_lds_mask
     // (MFP_BIN_LDS_MASK), else the HBM lane walker; the bins of bin_seg_mask
     // (MFP_BIN_SEG_MASK; default the two HTTP bins) use segment expansion
-    uint32_t bin_seg_mask = 0xa;
-    uint32_t bin_lds_mask = 0xe0;        // TLS server, SSH, DTLS: measured faster from LDS (r02c/d)
+    uint32_t bin_seg_mask = 0x4a;        // HTTP request/response and SSH: segment lists + lane emission (r04g)
+    uint32_t bin_lds_mask = 0xa0;        // TLS server, DTLS: measured faster from LDS (r02c/d)
     uint32_t an_lane_max_p = ~0u;        // classifier: lane-per-packet scoring up to this P (MFP_AN_LANE_MAX_P, tests)
     mfp_classifier *clf = nullptr;       // --analysis classifier (resources=...;analysis)
     mfp_prevalence own_prev = nullptr;   // the context's fingerprint_prevalence LRU

@@ -85,6 +85,7 @@ static int stderr_err(enum log_level level, const char *format, va_list args) {
 }
 static int silent_err(enum log_level, const char *, va_list) { return 0; }
 static void free_combiners(mercury *m);   // silent_err_func printf_err.hpp:47
+static void print_kernel_stats(mfp_context c);
 
 static printf_err_ptr g_printf_err = stderr_err;
 
@@ -158,6 +159,8 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
 
 MFP_EXPORT int mercury_finalize(mercury_context mc) {
     if (!mc) return -1;
+    if (getenv("MFP_SHIM_STATS"))
+        for (auto &c : mc->ctx) if (c) print_kernel_stats(c);
     for (auto &c : mc->ctx) if (c) mfp_finalize(c);
     free_combiners(mc);
     if (mc->prev) mfp_prevalence_destroy(mc->prev);
@@ -175,9 +178,21 @@ static mfp_context get_ctx(mercury *m, int mode) {
             mfp_analysis_set_prevalence(c, m->prev);
             mfp_analysis_report_os(c, m->report_os ? 1 : 0);
         }
+        if (getenv("MFP_SHIM_STATS")) mfp_profile_enable(c, 1);   // kernel times, printed by mercury_finalize
         m->ctx[mode] = c;
     }
     return m->ctx[mode];
+}
+
+// MFP_SHIM_STATS: the device time of each kernel the per-packet calls launched
+static void print_kernel_stats(mfp_context c) {
+    char name[64];
+    uint64_t launches = 0;
+    double ms = 0;
+    fprintf(stderr, "{\"shim_kernels\": {");
+    for (uint32_t i = 0; mfp_profile_read(c, i, name, sizeof name, &launches, &ms) == 0; i++)
+        fprintf(stderr, "%s\"%s\": [%llu, %.3f]", i ? ", " : "", name, (unsigned long long)launches, ms);
+    fprintf(stderr, "}}\n");
 }
 
 MFP_EXPORT mercury_packet_processor mercury_packet_processor_construct(mercury_context mc) {
