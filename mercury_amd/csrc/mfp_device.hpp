@@ -711,7 +711,7 @@ DEV bool qtp_less(Cur a, Cur b) {                       // fmt-1 id comparator t
 // (datum::cmp) for minimally encoded ids -- then the wire offset.  Returns
 // false, having written nothing, for more than QTP_MAX ids, a non-minimal
 // encoding or a value past 2^46 (the caller's selection handles those).
-constexpr int QTP_MAX = 20;
+constexpr int QTP_MAX = 16;
 template <class E>
 DEV bool qtp_sorted_fp(E &b, const Ext &x) {
     uint64_t K[QTP_MAX];

@@ -18,6 +18,7 @@
 
 #include "../../include/mfp.h"
 #include "mfp_analysis.h"
+#include "mfp_common.hpp"
 #include "mfp_internal.h"
 
 extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_tab *T, const uint8_t *arena,
@@ -383,9 +384,9 @@ struct mfp_context_s {
     uint32_t quic_format = 0;            // fingerprint_format::quic_fingerprint_format (global_config.h:41)
     uint32_t quic_grid = 512;            // k_quic workgroups (x 128 lanes, each with a scratch slot)
     int strategy = MFP_STRATEGY_BINNED;  // MFP_STRATEGY=binned|lane (A/B, debugging)
-    // batches of at most this many packets take the lane walker (one launch
-    // instead of the classify pass and a launch per bin: the per-packet API's
-    // latency); MFP_SMALL_BATCH
+    // batches of at most this many packets take MFP_STRATEGY_SMALL (the
+    // LDS-staged walker, no classify pass: the per-packet API's latency);
+    // MFP_SMALL_BATCH
     size_t small_batch = 256;
     // bin b -> kernel: k_fp_lds (LDS-staged walk) if bit b of bin_lds_mask
     // (MFP_BIN_LDS_MASK), else the HBM lane walker; the bins of bin_seg_mask
@@ -547,7 +548,8 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
     }
     if (mfp_launch_fingerprint(c->select, c->block, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, d_seg, (uint8_t *)d_fp_arena,
                                fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins,
-                               n <= c->small_batch ? (int)MFP_STRATEGY_LANE : c->strategy,
+                               c->strategy == MFP_STRATEGY_BINNED && n <= c->small_batch ? (int)MFP_STRATEGY_SMALL
+                                                                                         : c->strategy,
                                c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
                                c->prof) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -766,7 +768,7 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
 // pointer handed to the kernels is the staging buffer minus the (256-byte
 // aligned) start of the copied span
 static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
-                            size_t n, size_t fp_cap, bool analysis, bool attr_prob) {
+                            size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false) {
     Slot &S = c->slot[slot];
     uint64_t lo = UINT64_MAX, hi = 0, total = 0;
     for (size_t i = 0; i < n; i++) {
@@ -814,7 +816,7 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
         if (r) return r;
         // the synchronous host batch decides its unknown-TLS sightings now;
         // pipeline slots when they retire (chunk order), on the host copies
-        if (slot == 0 && !c->defer) { r = slot_resolve(c, S); if (r) return r; }
+        if (slot == 0 && !c->defer && !host_resolve) { r = slot_resolve(c, S); if (r) return r; }
     }
     // strings to a dense arena in packet order (d_fp2, d_used[2] bytes), records re-pointed;
     // the bin lists in d_work are dead by now and hold the scan scratch
@@ -829,6 +831,26 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     return 0;
 }
 
+// A small synchronous batch (the per-packet API) decides its unknown-TLS
+// sightings on the host from the copies it returns -- the string hashes of the
+// pending records, in packet order, against the LRU -- instead of the device
+// round trips of slot_resolve (the same decisions: both are the sequence form)
+static int resolve_on_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp_record *rec, const char *fp, size_t n) {
+    S.pend.live = false;
+    std::vector<uint64_t> keys;
+    std::vector<size_t> idx;
+    for (size_t i = 0; i < n; i++)
+        if (an[i].flags & MFP_AN_PENDING) {
+            keys.push_back(mfpc::str_hash((const uint8_t *)fp + rec[i].fp_offset, rec[i].fp_len));
+            idx.push_back(i);
+        }
+    if (keys.empty()) return 0;
+    std::vector<uint8_t> seen(keys.size());
+    if (mfp_prevalence_resolve_sequence(c->prev, keys.data(), keys.size(), seen.data()) != 0) return -1;
+    for (size_t k = 0; k < keys.size(); k++) host_patch(c, an[idx[k]], rec[idx[k]], seen[k] != 0);
+    return 0;
+}
+
 extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const uint8_t *arena, size_t arena_len,
                                                           const mfp_pkt_desc *desc, size_t n, mfp_record *rec,
                                                           char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
@@ -839,7 +861,9 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     HIPCHK(hipSetDevice(c->device));
     if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
     Slot &S = c->slot[0];
-    int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, analysis != nullptr, attr_prob != nullptr);
+    const bool host_resolve = analysis && n <= c->small_batch && !c->defer;
+    int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, analysis != nullptr, attr_prob != nullptr,
+                             host_resolve);
     if (r) return r;
     if (analysis && n) HIPCHK(hipMemcpyAsync(analysis, S.d_an, n * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
     if (analysis && attr_prob && n)
@@ -854,6 +878,10 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     const unsigned long long used = S.h_used[2];   // dense bytes
     if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
     if (used > spec) HIPCHK(hipMemcpy(fp_arena + spec, S.d_fp2 + spec, used - spec, hipMemcpyDeviceToHost));
+    if (host_resolve) {
+        const int rr = resolve_on_host(c, S, analysis, rec, fp_arena, n);
+        if (rr) return rr;
+    }
     return (long long)used;
 }
 

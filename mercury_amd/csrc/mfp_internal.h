@@ -16,7 +16,11 @@ int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t
 uint32_t mfp_context_mode(mfp_context c);   // MFP_MODE_*
 
 // kernel strategies of the fingerprint pass (mfp_kernels.hip)
-enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_LANE = 2 };
+// BINNED: classify, then a kernel per protocol bin; LANE: one HBM lane walker
+// over the whole batch; SMALL (small batches, the per-packet API): one
+// LDS-staged walker over the whole batch (no classify pass, the packets'
+// dependent reads are LDS round trips), then the fallback lane
+enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_LANE = 2, MFP_STRATEGY_SMALL = 3 };
 
 // per-kernel HIP-event timing (mfp_profile_enable): the launchers bracket
 // every launch with begin/end when `p` is non-null

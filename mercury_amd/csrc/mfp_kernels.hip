@@ -164,6 +164,18 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
         if (mfp_launch_bin_all(&P, nullptr, 0, "k_fingerprint", 0, (uint32_t)tiles, stream, prof) != 0) return -1;
         return launch_quic();
     }
+    if (strategy == MFP_STRATEGY_SMALL) {
+        // the whole batch through the all-family LDS walker, then the
+        // fallback lane over what it handed back (packets past its stage,
+        // QUIC / OpenVPN on their way to k_quic)
+        uint32_t *fallback = work + (uint64_t)mfp::NBINS * n;
+        const uint64_t lb = (n + 63) / 64 < 2048 ? (n + 63) / 64 : 2048;
+        if (mfp_launch_bin_all(&P, fallback, 1, "k_fp_lds/small", (uint32_t)lb, 0, stream, prof) != 0) return -1;
+        P.idx = fallback;
+        P.count = fp_used + 3;
+        if (mfp_launch_bin_all(&P, nullptr, 0, "k_fingerprint/fallback", 0, (uint32_t)tiles, stream, prof) != 0) return -1;
+        return launch_quic();
+    }
     // classify, then one launch per protocol bin over its index list: the
     // LDS-staged walker (bin_lds_mask), the HBM lane walker, or for the HTTP
     // bins (bin_seg_mask) the segment-expansion variant of either

@@ -544,11 +544,12 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
         for (uint32_t k = lane; k < SEG_POOL_BYTES; k += 64) pool[k] = (uint8_t)(k < sizeof(MFP_SEG_POOL) ? lp[k] : 0);
     }
     __builtin_amdgcn_wave_barrier();
-    const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (idx == nullptr: the whole batch, MFP_STRATEGY_SMALL)
+    const uint64_t count = P.idx ? (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P.n;
     for (uint64_t g = blockIdx.x; g * 64 < count; g += gridDim.x) {
         const uint64_t t = g * 64 + lane;
         const bool live = t < count;
-        const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
+        const uint64_t i = live ? (P.idx ? (uint64_t)P.idx[t] : t) : 0;
         mfp_pkt_desc dsc;
         if (live) dsc = P.desc[i];
         else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }

@@ -178,6 +178,17 @@ def test_lane_strategy_vs_reference(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_small_batch_strategy_vs_reference(monkeypatch):
+    """MFP_STRATEGY_SMALL (batches up to MFP_SMALL_BATCH packets, the
+    per-packet API): the all-family LDS-staged walker over the whole batch,
+    then the fallback lane -- here forced for every batch size."""
+    monkeypatch.setenv("MFP_SMALL_BATCH", str(1 << 40))
+    for fmt in (0, 1):
+        bad, _ = _vs_reference("binmix", fmt)
+        assert not bad, f"fmt {fmt}: {len(bad)} mismatches, first {bad[:5]}"
+
+
+@pytest.mark.gpu
 def test_analysis_mode_vs_reference():
     """get_analysis_context semantics: no TCP SYN fingerprints (pkt_proc.cc:1624-1651)."""
     bad, rec = _vs_reference("analysis_mode", 1, "an")

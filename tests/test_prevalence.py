@@ -196,6 +196,25 @@ def test_lru_stream_batches_vs_reference():
 
 
 @pytest.mark.gpu
+def test_lru_stream_small_batches_vs_reference():
+    """Batches of at most MFP_SMALL_BATCH packets (the per-packet API's size)
+    decide their sightings on the host from the returned copies
+    (mfp_host.cpp resolve_on_host): the first 24 000 packets of the LRU stream
+    in 200-packet batches give the reference's statuses."""
+    a, d = synth.lru_batch(synth.lru_keys())
+    want = golden_status()[:24000]
+    ctx = mercury_amd.Context(f"select=tls;resources={REF_ARCHIVE};analysis", device=0)
+    got = []
+    for lo in range(0, 24000, 200):
+        _, _, an = ctx.process_host_analysis(a, d[lo:lo + 200])
+        got.append(_statuses(an))
+    ctx.close()
+    got = np.concatenate(got)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} statuses differ, first at {bad[:5]}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("chunk", [25000, 170000])
 def test_lru_stream_pipelined_vs_reference(chunk):
     a, d = synth.lru_batch(synth.lru_keys())

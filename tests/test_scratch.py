@@ -74,9 +74,10 @@ def kernel_scratch():
 # (one instance per TLS format, round 4: plan length by arithmetic, uniform
 # emitter) spills nothing for formats 0 and 1 and 8 bytes for format 2.
 BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8, "k_an_features": 8, "k_fingerprintILj2E": 176, "k_fingerprintILj4E": 28,
-                  "k_fingerprintILj16E": 444, "k_fingerprintILj63E": 896, "k_fp_ldsILb0ELj36864ELj63E": 176,
+                  "k_fingerprintILj16E": 496, "k_fingerprintILj63E": 944, "k_fp_ldsILb0ELj36864ELj63E": 176,
                   "k_fp_ldsILb0ELj36864ELj2E": 176,
-                  # the LDS TLS walker carries the one-parse transport parameter sort (round 4)
+                  # the one-parse transport parameter sort (round 4): the LDS TLS walker +12, the DTLS
+                  # HBM lane walker (not a default bin kernel: DTLS runs from LDS) 444 -> 496, the fallback lane 896 -> 944
                   "k_fp_ldsILb0ELj36864ELj1E": 12}
 
 
