@@ -299,6 +299,15 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis, reso
                                      capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
                 pr = json.loads(out.decode().strip().splitlines()[-1])
                 points[str(th)] = {"threads": th, "write_json_mpkt_s": round(pr["pps"] / 1e6, 4)}
+            # the scaling check: the same leg without --analysis (no prevalence
+            # LRU) at 1 thread and on all cores
+            plain = {}
+            if analysis:
+                for th in sorted({1, len(os.sched_getaffinity(0))}):
+                    out = subprocess.run([ref, "time", path, CONTRACT, "-", str(th), str(seconds / 4), "json"],
+                                         capture_output=True, check=True, timeout=seconds * 4 + 120).stdout
+                    pr = json.loads(out.decode().strip().splitlines()[-1])
+                    plain[str(th)] = {"threads": th, "write_json_mpkt_s": round(pr["pps"] / 1e6, 4)}
             # the baseline: the better of the two per-GPU shares of the host
             # (nproc / 8 and OMP_NUM_THREADS); the reference's rate falls past
             # about 16 threads (its shared LRU lock, analysis.h:372,390)
@@ -310,6 +319,7 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis, reso
                     "get_analysis_context_mpkt_s": round(rates["an"]["pps"] / 1e6, 4),
                     "get_analysis_context_threads": threads,
                     "thread_points": points,
+                    "thread_points_without_analysis": plain,
                     "host": host,
                     "sample": f"{sample_n} {workload} packets looped >= {seconds:.0f} s per entry point "
                               f"({seconds / 2:.0f} s for the extra thread counts), libmerc {what}, one processor "
