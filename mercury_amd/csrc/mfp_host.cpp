@@ -6,9 +6,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -402,6 +404,7 @@ struct mfp_context_s {
     bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
     Slot slot[4];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2: host pipeline
     int pipe_next = 0;                   // mfp_analyze_batch_device_pipelined: the slot of the next batch (0 or 3)
+    std::atomic<size_t> attr_names_len{SIZE_MAX};   // mfp_attribute_names_len
     int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
     std::mutex mu;
@@ -1180,6 +1183,21 @@ extern "C" MFP_EXPORT const char *mfp_resource_version(mfp_context c) {
 
 extern "C" MFP_EXPORT int mfp_attribute_count(mfp_context c) {
     return c && c->clf ? mfp_classifier_attr_count(c->clf) : 0;
+}
+
+// the attribute names' total length (the JSON writer's per-record bound), once per context
+size_t mfp_attribute_names_len(mfp_context c) {
+    if (!c || !c->clf) return 0;
+    size_t v = c->attr_names_len.load(std::memory_order_relaxed);
+    if (v != SIZE_MAX) return v;
+    v = 0;
+    const int na = mfp_classifier_attr_count(c->clf);
+    for (int k = 0; k < na; k++) {
+        const char *nm = mfp_classifier_attr_name(c->clf, (uint32_t)k);
+        v += nm ? strlen(nm) : 0;
+    }
+    c->attr_names_len.store(v, std::memory_order_relaxed);
+    return v;
 }
 
 extern "C" MFP_EXPORT int mfp_analysis_report_os(mfp_context c, int on) {

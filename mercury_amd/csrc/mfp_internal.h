@@ -27,3 +27,6 @@ enum { MFP_STRATEGY_BINNED = 0, MFP_STRATEGY_LANE = 2, MFP_STRATEGY_SMALL = 3 };
 struct mfp_prof;
 void mfp_prof_begin(mfp_prof *p, const char *kernel, hipStream_t s);
 void mfp_prof_end(mfp_prof *p, hipStream_t s);
+
+// the total length of the context's attribute names (computed once; mfp_json.cpp's bounds)
+size_t mfp_attribute_names_len(mfp_context c);

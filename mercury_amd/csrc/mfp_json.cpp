@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <time.h>
+#include <cmath>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -295,8 +296,44 @@ bool is_tcp_msg(unsigned m) {
     return m != MFP_MSG_DTLS_CH && m != MFP_MSG_DTLS_SH && m != MFP_MSG_DTLS_HVR && m != MFP_MSG_QUIC && m != MFP_MSG_STUN;
 }
 
-// "%f" (json_object::print_key_float json_object.h:174-177)
+// "%f" (json_object::print_key_float json_object.h:174-177).  printf's %f
+// is the exact decimal value rounded to 6 places, ties to even; for |d| <
+// 1e12 that is computed here from the double's binary form (m * 2^e times
+// 10^6, exactly, in 128 bits, then rounded), without snprintf's cost; other
+// values (and NaN, infinities) go through snprintf.
 void put_float(W &w, double d) {
+    uint64_t bits;
+    memcpy(&bits, &d, 8);
+    const bool neg = (bits >> 63) != 0;
+    const uint32_t be = (uint32_t)((bits >> 52) & 0x7ff);
+    if (be < 0x7ff && std::fabs(d) < 1e12) {
+        uint64_t m = bits & ((1ull << 52) - 1);
+        int e;
+        if (be == 0) e = -1074; else { m |= 1ull << 52; e = (int)be - 1075; }
+        uint64_t q;
+        if (e >= 0) {
+            q = (m << e) * 1000000ull;                   // (|d| < 1e12: no overflow)
+        } else {
+            const unsigned __int128 x = (unsigned __int128)m * 1000000u;
+            const int sh = -e;
+            if (sh >= 128) {
+                q = 0;
+            } else {
+                q = (uint64_t)(x >> sh);
+                const unsigned __int128 rem = x & ((((unsigned __int128)1) << sh) - 1);
+                const unsigned __int128 half = ((unsigned __int128)1) << (sh - 1);
+                if (rem > half || (rem == half && (q & 1))) q++;
+            }
+        }
+        if (neg) w.put('-');
+        w.udec(q / 1000000u);
+        w.put('.');
+        uint32_t f = (uint32_t)(q % 1000000u);
+        char t[6];
+        for (int k = 5; k >= 0; k--) { t[k] = (char)('0' + f % 10); f /= 10; }
+        w.mem(t, 6);
+        return;
+    }
     char t[352];   // %f of the largest double is 316 digits + sign, dot, 6 decimals
     const int n = snprintf(t, sizeof t, "%f", d);
     w.mem(t, n > 0 ? (size_t)n : 0);
@@ -304,9 +341,7 @@ void put_float(W &w, double d) {
 
 // worst-case text of a record's "analysis" object
 size_t analysis_bound(mfp_context ctx, const mfp_analysis &a) {
-    size_t b = 400 + 16 * 64;                       // keys, numbers, 16 attribute entries
-    const int na = mfp_attribute_count(ctx);
-    for (int k = 0; k < na; k++) { const char *nm = mfp_attribute_name(ctx, (uint32_t)k); b += nm ? strlen(nm) : 0; }
+    size_t b = 400 + 16 * 64 + mfp_attribute_names_len(ctx);   // keys, numbers, 16 attribute entries, names
     if (a.process != MFP_NO_PROCESS) b += 256;      // max_proc holds at most 255 bytes (result.h:198)
     if (a.proc_slot != MFP_NO_PROCESS) {
         const int cnt = mfp_process_os_info(ctx, a.proc_slot, 0, nullptr, nullptr);

@@ -351,24 +351,25 @@ DEV void cb_extend(CState &s, uint64_t off, uint64_t len, Cur data, uint8_t *cb,
     s.total += (uint32_t)len;
     if (s.count < 20) s.count++;
 }
-// PADDING runs skipped word-wide in quic_frames (pending a GPU run: off)
+// PADDING runs skipped word-wide in quic_frames (MI355X: k_quic 65.2 -> 51.9 ms per 2 M Initials, profiles/r04i_quic_*)
 #ifndef MFP_QUIC_PADSKIP
-#define MFP_QUIC_PADSKIP 0
+#define MFP_QUIC_PADSKIP 1
 #endif
 // the end of a run of zero bytes from d (at most e): four aligned 8-byte
 // loads per step, so an Initial's PADDING (hundreds of one-byte frames) costs a
-// few dependent loads, not one per byte; may read up to 31 bytes past e
+// few dependent loads, not one per byte; reads only [d, e)
 DEV const uint8_t *skip_zeros(const uint8_t *d, const uint8_t *e) {
     while (d < e && ((uintptr_t)d & 7)) { if (ld(d)) return d; d++; }
-    while (d < e) {
+    while (d + 32 <= e) {
         const uint64_t *q = (const uint64_t *)d;
         const uint64_t w[4] = {q[0], q[1], q[2], q[3]};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            if (w[k]) { const uint8_t *r = d + 8 * k + (__builtin_ctzll(w[k]) >> 3); return r < e ? r : e; }
+            if (w[k]) return d + 8 * k + (__builtin_ctzll(w[k]) >> 3);
         }
         d += 32;
     }
+    while (d < e) { if (ld(d)) return d; d++; }
     return e;
 }
 

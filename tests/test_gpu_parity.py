@@ -183,7 +183,7 @@ def test_small_batch_strategy_vs_reference(monkeypatch):
     per-packet API): the all-family LDS-staged walker over the whole batch,
     then the fallback lane -- here forced for every batch size."""
     monkeypatch.setenv("MFP_SMALL_BATCH", str(1 << 40))
-    for fmt in (0, 1):
+    for fmt in (0, 2):
         bad, _ = _vs_reference("binmix", fmt)
         assert not bad, f"fmt {fmt}: {len(bad)} mismatches, first {bad[:5]}"
 
