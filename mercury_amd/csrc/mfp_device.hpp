@@ -1348,10 +1348,18 @@ DEV void tls_ch_emit_fast(E &b, TlsPlan &pl) {
     }
     hex_run<true>(b, pl.ciphers.d, (uint32_t)clen(pl.ciphers) & ~1u);
     b.push(')' | ((FMT ? '[' : '(') << 8), 2);
+    // the next extension's header is loaded while this one is written (its
+    // load's latency hidden behind an extension's emission)
+    uint32_t off_next = pl.n ? pl.off_row[FMT == 0 ? 0 : pl.ord_row[0]] : 0u;
+    uint32_t th_next = pl.n ? ld_be32n(pl.exts.d + off_next, 4) : 0u;
     for (uint32_t j = 0; j < pl.n; j++) {
-        const uint32_t off = pl.off_row[FMT == 0 ? j : pl.ord_row[j]];
+        const uint32_t off = off_next;
         const uint8_t *h = pl.exts.d + off;
-        const uint32_t th = ld_be32n(h, 4);                // type << 16 | length (the plan kept whole extensions)
+        const uint32_t th = th_next;                       // type << 16 | length (the plan kept whole extensions)
+        if (j + 1 < pl.n) {
+            off_next = pl.off_row[FMT == 0 ? j + 1 : pl.ord_row[j + 1]];
+            th_next = ld_be32n(pl.exts.d + off_next, 4);
+        }
         const uint32_t t = th >> 16, vl = th & 0xffff;
         const bool st = static_ext_bit(t);
         uint32_t w;                                        // head: type, length as a little-endian word
