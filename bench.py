@@ -338,7 +338,42 @@ def cpu_baseline(workload, draw_seed, sample_n, threads, seconds, analysis, reso
             "sample": f"{sample_n} {workload} packets x {reps} passes, C oracle, {threads} threads"}
 
 
+def gpu_local_cpus(torch, dev):
+    """(NUMA node, CPUs of this process on it) of the GPU's PCIe attachment, or None."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        if node < 0:
+            return None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        cpus &= os.sched_getaffinity(0)
+        return (node, cpus) if cpus else None
+    except Exception:
+        return None
+
+
 def end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world, with_json):
+    """Runs _end_to_end with the host threads (and so the page-locked buffers
+    they allocate) on the GPU's NUMA node when MFP_E2E_NUMA=1."""
+    loc = gpu_local_cpus(torch, torch.cuda.current_device()) if os.environ.get("MFP_E2E_NUMA") == "1" else None
+    old = os.sched_getaffinity(0)
+    if loc:
+        os.sched_setaffinity(0, loc[1])
+    try:
+        out = _end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world, with_json)
+    finally:
+        if loc:
+            os.sched_setaffinity(0, old)
+    if out is not None:
+        out["numa"] = {"node": loc[0], "cpus": len(loc[1])} if loc else None
+    return out
+
+
+def _end_to_end(torch, ctx, ua, ud, n_buf, per_rank, analysis, chunk, dist, world, with_json):
     """Config 5's host-resident rate: `per_rank` packets per rank from
     page-locked host memory (a buffer of n_buf packets, looped), records,
     fingerprints (and classifier results) back into page-locked host memory,
