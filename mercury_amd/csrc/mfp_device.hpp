@@ -298,6 +298,24 @@ struct Em {
         if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
     }
     DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
+#ifdef MFP_PUSH_BRANCHFREE   // (A/B: no divergent branch on a completed word)
+        if (EMIT) {
+            const uint32_t sh = 8 * nacc;
+            const uint64_t lo = acc | (v << sh);
+            const uint64_t hi = sh ? (v >> (64 - sh)) : 0ull;
+            const uint32_t t = nacc + k;
+            const bool full = t >= 8;
+            line[nw] = lo;                          // (a partial word is rewritten by a later push)
+            h ^= full ? mfpc::word_term(lo, wi) : 0ull;
+            wi += full ? 1u : 0u;
+            nw += full ? 1u : 0u;
+            acc = full ? hi : lo;
+            nacc = full ? t - 8 : t;
+            if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
+        }
+        n += k;
+        return;
+#endif
         if (EMIT) {
             const uint32_t room = 8 - nacc;
             if (k < room) {
@@ -561,14 +579,32 @@ DEV uint64_t low_chars(uint64_t v, uint32_t k) { return k >= 8 ? v : (v & ((1ull
 // even) of p[0, len), 4 bytes -> 8 characters per push
 template <bool DEGREASE, class E>
 DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
-    if (len == 0) return;
+#ifdef MFP_HEXRUN_STREAM   // (A/B: one dword load per 4 bytes)
     LeStream s;
     s.init(p, (long)len);
     for (uint32_t i = 0; i < len; i += 4) {
         uint32_t w = s.next();
         if (DEGREASE) w = degrease_pairs(w);
-        const uint32_t k = len - i >= 4 ? 8u : 2 * (len - i);
-        b.push(low_chars(hex4(w), k), k);
+        const uint32_t c = len - i >= 4 ? 8u : 2 * (len - i);
+        b.push(low_chars(hex4(w), c), c);
+    }
+    return;
+#endif
+    // 32 bytes per round trip: the block's dword loads are all issued before
+    // the first is used (LeBlock), then 8 characters per push
+    for (uint32_t i0 = 0; i0 < len; i0 += 32) {
+        LeBlock blk;
+        blk.load(p + i0, (long)(len - i0));
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t i = i0 + 4 * (uint32_t)k;
+            if (i < len) {
+                uint32_t w = blk.v[k];
+                if (DEGREASE) w = degrease_pairs(w);
+                const uint32_t c = len - i >= 4 ? 8u : 2 * (len - i);
+                b.push(low_chars(hex4(w), c), c);
+            }
+        }
     }
 }
 // Lane emission of one segment list (k_fp_seg): the lane writes its own
