@@ -298,24 +298,6 @@ struct Em {
         if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
     }
     DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
-#ifdef MFP_PUSH_BRANCHFREE   // (A/B: no divergent branch on a completed word)
-        if (EMIT) {
-            const uint32_t sh = 8 * nacc;
-            const uint64_t lo = acc | (v << sh);
-            const uint64_t hi = sh ? (v >> (64 - sh)) : 0ull;
-            const uint32_t t = nacc + k;
-            const bool full = t >= 8;
-            line[nw] = lo;                          // (a partial word is rewritten by a later push)
-            h ^= full ? mfpc::word_term(lo, wi) : 0ull;
-            wi += full ? 1u : 0u;
-            nw += full ? 1u : 0u;
-            acc = full ? hi : lo;
-            nacc = full ? t - 8 : t;
-            if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
-        }
-        n += k;
-        return;
-#endif
         if (EMIT) {
             const uint32_t room = 8 - nacc;
             if (k < room) {
