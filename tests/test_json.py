@@ -183,6 +183,14 @@ def test_libmerc_write_json_linktype_device():
         # a buffer one byte short of the record: nothing written (pkt_proc.cc:1249-1253)
         if want:
             assert f(p, buf, len(want), pkt, ln, ctypes.byref(ts), 1) == 0
+    # a zero timestamp is filled in with tsc_clock's seconds since the counter
+    # started (pkt_proc.cc:1086-1089; here CLOCK_MONOTONIC), tv_nsec untouched
+    import time
+    off, ln = int(desc[0]["offset"]), int(desc[0]["caplen"])
+    pkt = ctypes.create_string_buffer(arena[off:off + ln].tobytes() + bytes(16))
+    ts = Timespec(0, 123)
+    f(p, buf, len(buf), pkt, ln, ctypes.byref(ts), 1)
+    assert abs(ts.tv_sec - time.monotonic()) < 3 and ts.tv_nsec == 123
     lib.mercury_packet_processor_destruct(p)
     lib.mercury_finalize(mc)
 
