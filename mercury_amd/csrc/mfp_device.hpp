@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mfp.h"
 #include "mfp_common.hpp"
 
@@ -97,6 +99,38 @@ struct LeBlock {
         for (int k = 0; k < 8; k++) v[k] = sh ? (w[k] >> sh) | (w[k + 1] << (32 - sh)) : w[k];
     }
 };
+// LeBlock from the aligned 16-byte blocks that hold the bytes (at most 3 load
+// instructions per 32 bytes instead of 9), realigned in registers.  Global
+// memory only (k_fp_tls1 / k_fp_seg emission: Em's WIDE parameter,
+// MFP_LEBLOCK16); the LDS-staged walker keeps LeBlock.
+#ifndef MFP_LEBLOCK16
+#define MFP_LEBLOCK16 0
+#endif
+struct LeBlock16 {
+    uint32_t v[8];
+    DEV void load(const uint8_t *p, long len) {
+        const uintptr_t a = (uintptr_t)p;
+        const uint4 *q4 = (const uint4 *)(a & ~(uintptr_t)15);
+        const uint32_t off = (uint32_t)(a & 15);
+        const long nb = len < 32 ? len : 32;
+        const uint32_t nq = (uint32_t)((off + nb + 15) >> 4);   // 1..3
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 x0 = q4[0], x1 = nq > 1 ? q4[1] : z, x2 = nq > 2 ? q4[2] : z;
+        // scalars, not an array: a select between two array elements would
+        // become a load from a selected address (private memory)
+#define MFP_LB16_W(i)                                                                                   \
+    ((i) == 0 ? x0.x : (i) == 1 ? x0.y : (i) == 2 ? x0.z : (i) == 3 ? x0.w : (i) == 4 ? x1.x : (i) == 5 ? x1.y \
+     : (i) == 6 ? x1.z : (i) == 7 ? x1.w : (i) == 8 ? x2.x : (i) == 9 ? x2.y : (i) == 10 ? x2.z : x2.w)
+        const uint32_t s4 = off >> 2, sb = off & 3;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t lo = s4 == 0 ? MFP_LB16_W(k) : s4 == 1 ? MFP_LB16_W(k + 1) : s4 == 2 ? MFP_LB16_W(k + 2) : MFP_LB16_W(k + 3);
+            const uint32_t hi = s4 == 0 ? MFP_LB16_W(k + 1) : s4 == 1 ? MFP_LB16_W(k + 2) : s4 == 2 ? MFP_LB16_W(k + 3) : MFP_LB16_W(k + 4);
+            v[k] = __builtin_amdgcn_alignbyte(hi, lo, sb);
+        }
+#undef MFP_LB16_W
+    }
+};
 // 4 bytes (b0 lowest) -> 8 lowercase hex characters, little-endian (b0's high nibble first)
 DEV uint64_t hex4(uint32_t le) {
     uint64_t x = le;
@@ -178,10 +212,38 @@ DEV uint64_t swar_alpha(uint64_t w) {                  // isalpha (ASCII)
 #ifndef MFP_SWB
 #define MFP_SWB 4
 #endif
+// MFP_SWAR16: the 32 bytes of a round trip from two aligned 16-byte loads
+#ifndef MFP_SWAR16
+#define MFP_SWAR16 0
+#endif
 template <class F>
 DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag) {
     if (!p || p >= e) return e;
     const uintptr_t ee = (uintptr_t)e;
+#if MFP_SWAR16
+    {
+        const uintptr_t pp = (uintptr_t)p;
+        uintptr_t a = pp & ~(uintptr_t)15;
+        while (true) {
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            const uint4 x0 = *(const uint4 *)a, x1 = a + 16 < ee ? *(const uint4 *)(a + 16) : z;
+            const uint64_t w[4] = {(uint64_t)x0.x | (uint64_t)x0.y << 32, (uint64_t)x0.z | (uint64_t)x0.w << 32,
+                                   (uint64_t)x1.x | (uint64_t)x1.y << 32, (uint64_t)x1.z | (uint64_t)x1.w << 32};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uintptr_t ak = a + 8 * k;
+                if (ak >= ee) return e;
+                if (ak + 8 <= pp) continue;                      // (first round) wholly before p
+                uint64_t m = flag(w[k]);
+                if (ak < pp) m &= ~0ull << (8 * (pp - ak));
+                const uintptr_t in = ee - ak;
+                if (in < 8) m &= (1ull << (8 * in)) - 1;
+                if (m) return (const uint8_t *)(ak + (__builtin_ctzll(m) >> 3));
+            }
+            a += 32;
+        }
+    }
+#endif
     uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
     uint64_t m0 = ~0ull << (8 * ((uintptr_t)p & 7));   // bytes before p in the first word
     while (true) {
@@ -247,13 +309,14 @@ struct TlsPlan;
 // FAST >= 0 (k_fp_tls1, TLS format FAST): pass 1 records the ClientHello plan
 // with the string's length by arithmetic (tls_ch_plan_fast), pass 2 emits it
 // with tls_ch_emit_fast
-template <bool EMIT, int FAST_FMT = -1, int LINEW = 8>
+template <bool EMIT, int FAST_FMT = -1, int LINEW = 8, bool WIDE = false>
 struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
     bool punt = false;       // the message needs a parser family this walker lacks
     DEV void punt_pkt() { punt = true; }
     static constexpr int FAST = FAST_FMT;
+    static constexpr bool WIDE_LOADS = WIDE;   // hex_run reads global memory with LeBlock16
     static constexpr bool PLAN = !EMIT;   // pass 1 records a ClientHello plan (TlsPlan) in *plan
     TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
@@ -402,6 +465,7 @@ DEV uint32_t seg_src(uint32_t s) { return s >> 15; }
 
 struct SegEm {
     static constexpr bool SEG = true;
+    static constexpr bool WIDE_LOADS = false;
     static constexpr bool PLAN = false;
     static constexpr bool emit_pass() { return false; }
     uint32_t n = 0;                     // characters produced
@@ -575,7 +639,7 @@ DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
     // 32 bytes per round trip: the block's dword loads are all issued before
     // the first is used (LeBlock), then 8 characters per push
     for (uint32_t i0 = 0; i0 < len; i0 += 32) {
-        LeBlock blk;
+        typename std::conditional<E::WIDE_LOADS, LeBlock16, LeBlock>::type blk;
         blk.load(p + i0, (long)(len - i0));
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -1610,13 +1674,151 @@ DEV bool http_delim(Cur &p, Cur del) {                  // delimiter(datum&, con
     (void)crlf;
     return cnotempty(dl);
 }
+// MFP_HTTP_FAST: the header loop's delimiter checks and the ':' / whitespace
+// step read the bytes they test with one block load each (the delimiter
+// packed once per message, up to 4 bytes) instead of one dependent byte load
+// per comparison
+// (A/B on MI355X, profiles/r04w_ab_*, r04x_ab_*: http_req 13.8 -> 11.4 ms and
+// http_resp 4.2 -> 3.1 ms with 1; 2 takes http_resp to 2.95 ms)
+#ifndef MFP_HTTP_FAST
+#define MFP_HTTP_FAST 2
+#endif
+// p[0, n) (n = 1..4) little-endian, bytes above n zero: from the aligned
+// 16-byte block holding p (and the next one when the bytes cross into it)
+DEV uint32_t ld_le4n(const uint8_t *p, long n) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint4 *q = (const uint4 *)(a & ~(uintptr_t)15);
+    const uint32_t off = (uint32_t)(a & 15);
+    const uint4 x0 = q[0];
+    const uint32_t x1 = off + (uint32_t)n > 16 ? q[1].x : 0u;
+    const uint32_t i = off >> 2;
+    const uint32_t lo = i == 0 ? x0.x : i == 1 ? x0.y : i == 2 ? x0.z : x0.w;
+    const uint32_t hi = i == 0 ? x0.y : i == 1 ? x0.z : i == 2 ? x0.w : x1;
+    const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, off & 3);
+    return n >= 4 ? v : v & ((1u << (8 * n)) - 1);
+}
+// http_delim with the delimiter packed (dl <= 4 bytes, value dv)
+DEV bool http_delim4(Cur &p, uint32_t dv, long dl) {
+    if (!p.d) return false;
+    const long L = p.e - p.d;
+    if (L <= 0) return false;                         // (dl = 0 matches but consumes nothing: false too)
+    const uint32_t w = ld_le4n(p.d, L < 4 ? L : 4);
+    if (dl <= L && (dl == 0 || (w & (dl >= 4 ? ~0u : (1u << (8 * dl)) - 1)) == dv)) {
+        p.d += dl;
+        return dl != 0;
+    }
+    if (L >= 2 && (w & 0xffff) == 0x0a0d) { p.d += 2; return true; }
+    if ((w & 0xff) == 0x0a) { p.d += 1; return true; }
+    return false;
+}
+// p[0, n) (n = 1..8) little-endian, bytes above n zero (as ld_le4n)
+DEV uint64_t ld_le8n(const uint8_t *p, long n) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint4 *q = (const uint4 *)(a & ~(uintptr_t)15);
+    const uint32_t off = (uint32_t)(a & 15);
+    const uint4 x0 = q[0];
+    const uint2 x1 = off + (uint32_t)n > 16 ? *(const uint2 *)(q + 1) : make_uint2(0, 0);
+    const uint32_t i = off >> 2, sb = off & 3;
+    const uint32_t d0 = i == 0 ? x0.x : i == 1 ? x0.y : i == 2 ? x0.z : x0.w;
+    const uint32_t d1 = i == 0 ? x0.y : i == 1 ? x0.z : i == 2 ? x0.w : x1.x;
+    const uint32_t d2 = i == 0 ? x0.z : i == 1 ? x0.w : i == 2 ? x1.x : x1.y;
+    const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sb) |
+                       (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sb) << 32;
+    return n >= 8 ? v : v & ((1ull << (8 * n)) - 1);
+}
+// http_delim4 on bytes already loaded: w holds p[0, min(4, len)) (bytes past
+// the cursor's end are never tested)
+DEV bool http_delim4w(Cur &p, uint32_t dv, long dl, uint32_t w) {
+    if (!p.d) return false;
+    const long L = p.e - p.d;
+    if (L <= 0) return false;
+    if (dl <= L && (dl == 0 || (w & (dl >= 4 ? ~0u : (1u << (8 * dl)) - 1)) == dv)) {
+        p.d += dl;
+        return dl != 0;
+    }
+    if (L >= 2 && (w & 0xffff) == 0x0a0d) { p.d += 2; return true; }
+    if ((w & 0xff) == 0x0a) { p.d += 1; return true; }
+    return false;
+}
 // new_http_headers::fingerprint http.h:335 + httpheader http.h:146
 template <class E>
 DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {
     Cur tmp = body;
+#if MFP_HTTP_FAST
+    const long dl = clen(delim);
+    const uint32_t dv = dl > 0 && dl <= 4 ? ld_le4n(delim.d, dl) : 0u;
+    const bool d4 = dl <= 4;
+    // (the segment walker leaves longer delimiters to the fallback lane)
+    if (E::SEG && !d4) { b.punt_pkt(); return; }
+#define MFP_HDELIM(c) ((E::SEG || d4) ? http_delim4(c, dv, dl) : http_delim(c, delim))
+    // MFP_HTTP_FAST >= 2 (segment walker): the delimiter after a value is
+    // tested from an 8-byte window that also holds the next header's first
+    // bytes (the loop-top test reads no memory), and the value's end is
+    // searched from the ':' while the whitespace after it is loaded: one
+    // memory round trip for both
+    constexpr bool F2 = E::SEG && MFP_HTTP_FAST >= 2;
+    uint32_t wnext = 0;
+    bool have_next = false;
+#define MFP_HTOP(c) (F2 && have_next ? http_delim4w(c, dv, dl, wnext) : MFP_HDELIM(c))
+#else
+#define MFP_HDELIM(c) http_delim(c, delim)
+#define MFP_HTOP(c) http_delim(c, delim)
+#endif
     while (true) {
-        if (http_delim(tmp, delim)) break;
+        if (MFP_HTOP(tmp)) break;
         Cur hdr_body = tmp, name; cset_null(name);
+#if MFP_HTTP_FAST
+        // the ':' found is the byte the reference tests next; none found leaves
+        // the name's first byte, which is not ':'
+        if (!cnotempty(tmp)) { cset_null(tmp); }
+        else {
+            name.d = tmp.d; name.e = tmp.e;
+            const uint8_t *q = swar_find(tmp.d, tmp.e, [](uint64_t w) { return swar_eq(w, ':'); });
+            if (q < tmp.e) { name.e = q; tmp.d = q + 1; } else cset_null(tmp);
+        }
+        Cur value;
+        if constexpr (F2) {
+            // whitespace (up to 4 bytes from one load) and the value's end: the
+            // first CR or LF after the ':' is the first after the whitespace,
+            // which holds neither
+            long L = 0;
+            uint32_t w = 0;
+            if (tmp.d && tmp.d < tmp.e) { L = tmp.e - tmp.d; w = ld_le4n(tmp.d, L < 4 ? L : 4); }
+            const uint8_t *q2 = tmp.d ? swar_find(tmp.d, tmp.e, [](uint64_t x) { return swar_eq(x, '\r') | swar_eq(x, '\n'); })
+                                      : nullptr;
+            if (L > 0) {
+                int k = 0;
+                while (k < 4 && k < L && (((w >> (8 * k)) & 0xff) == '\t' || ((w >> (8 * k)) & 0xff) == ' ')) k++;
+                tmp.d += k;
+                if (k == 4)
+                    while (tmp.d < tmp.e && (ld(tmp.d) == '\t' || ld(tmp.d) == ' ')) tmp.d++;
+            }
+            // cparse_to_delims(value, tmp, '\r', '\n')
+            value.d = tmp.d;
+            if (tmp.d) { tmp.d = q2; value.e = q2; } else value.e = tmp.e;
+            // the delimiter, and the next header's first bytes, from one window
+            uint64_t w8 = 0;
+            if (tmp.d && tmp.d < tmp.e) { const long L8 = tmp.e - tmp.d; w8 = ld_le8n(tmp.d, L8 < 8 ? L8 : 8); }
+            const uint8_t *at = tmp.d;
+            http_delim4w(tmp, dv, dl, (uint32_t)w8);
+            wnext = (uint32_t)(w8 >> (8 * (uint32_t)(tmp.d - at)));
+            have_next = true;
+        } else {
+        bool more_ws = false;
+        if (tmp.d && tmp.d < tmp.e) {                    // up to 4 bytes of whitespace from one load
+            const long L = tmp.e - tmp.d;
+            const uint32_t w = ld_le4n(tmp.d, L < 4 ? L : 4);
+            int k = 0;
+            while (k < 4 && k < L && (((w >> (8 * k)) & 0xff) == '\t' || ((w >> (8 * k)) & 0xff) == ' ')) k++;
+            tmp.d += k;
+            more_ws = k == 4;
+        }
+        if (more_ws)
+            while (tmp.d && tmp.d < tmp.e && (ld(tmp.d) == '\t' || ld(tmp.d) == ' ')) tmp.d++;
+        cparse_to_delims(value, tmp, '\r', '\n');
+        MFP_HDELIM(tmp);
+        }
+#else
         if (!cnotempty(tmp)) { cset_null(tmp); }
         else {
             name.d = tmp.d; name.e = tmp.e;
@@ -1627,7 +1829,8 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         while (tmp.d && tmp.d < tmp.e && (ld(tmp.d) == '\t' || ld(tmp.d) == ' ')) tmp.d++;
         Cur value;
         cparse_to_delims(value, tmp, '\r', '\n');
-        http_delim(tmp, delim);
+        MFP_HDELIM(tmp);
+#endif
         hdr_body.e = value.e;
         if (cnull(tmp)) break;
         uint32_t info = 0;
@@ -1644,6 +1847,8 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
             }
         }
     }
+#undef MFP_HDELIM
+#undef MFP_HTOP
 }
 
 // ---------------------------------------------------------------------------

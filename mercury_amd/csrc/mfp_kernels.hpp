@@ -282,7 +282,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         KPH(2);
         // emit from the plan, the ClientHello still in the cache
         if (len && fits) {
-            Em<true> e;
+            Em<true, -1, 8, MFP_LEBLOCK16 != 0> e;   // the packet is in HBM
             e.begin(P.fp_arena + base + excl, out_line[tid]);
             tls_ch_emit_fast<FMT>(e, plan);
             e.finish();
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
         KPH(1);
 #if MFP_SEG_LANE
         if (len && fits) {
-            Em<true, -1, SEG_LINEW> em;
+            Em<true, -1, SEG_LINEW, MFP_LEBLOCK16 != 0> em;   // the packet is in HBM
             em.begin(P.fp_arena + base + excl, out_line[tid]);
             seg_emit_lane(em, segs + tid * SEG_STRIDE, e.nseg, data, pool);
             em.finish();

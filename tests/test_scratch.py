@@ -78,7 +78,10 @@ BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8
                   "k_fp_ldsILb0ELj36864ELj2E": 176,
                   # the one-parse transport parameter sort (round 4): the LDS TLS walker +12, the DTLS
                   # HBM lane walker (not a default bin kernel: DTLS runs from LDS) 444 -> 496, the fallback lane 896 -> 944
-                  "k_fp_ldsILb0ELj36864ELj1E": 12}
+                  "k_fp_ldsILb0ELj36864ELj1E": 12,
+                  # the HTTP segment walker with the header loop's windowed delimiter tests
+                  # (MFP_HTTP_FAST 2, round 4): 8 bytes at its 128-VGPR cap
+                  "k_fp_segILj4E": 8}
 
 
 def test_classifier_and_crypto_kernels_use_no_scratch():
