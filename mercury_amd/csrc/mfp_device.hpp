@@ -1967,6 +1967,25 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         cparse_to_delim(f1, p, ' ');
         long ml = clen(f1);
         if (ml < 3 || ml > 16) return false;
+#if MFP_HTTP_FAST >= 3
+        // the method's bytes (<= 16) loaded with the URI search, "HTTP/" with
+        // the search for the line's end: one memory round trip each
+        const uint64_t m0 = ld_le8n(f1.d, ml < 8 ? ml : 8);
+        const uint64_t m1 = ml > 8 ? ld_le8n(f1.d + 8, ml - 8) : 0ull;
+        cskip(p, 1);
+        cparse_to_delim(uri, p, ' ');
+        {   // every byte of the method 'A'..'Z'
+            const uint64_t k0 = ml >= 8 ? 0x8080808080808080ull : 0x8080808080808080ull & ((1ull << (8 * ml)) - 1);
+            const long r1 = ml - 8;
+            const uint64_t k1 = r1 <= 0 ? 0ull : r1 >= 8 ? 0x8080808080808080ull : 0x8080808080808080ull & ((1ull << (8 * r1)) - 1);
+            if ((swar_upper(m0) & k0) != k0 || (swar_upper(m1) & k1) != k1) return false;
+        }
+        cskip(p, 1);
+        const long pl = clen(p);
+        const uint64_t h5 = p.d && pl > 0 ? ld_le8n(p.d, pl < 5 ? pl : 5) : 0ull;
+        cparse_to_delims(f2, p, '\r', '\n');
+        if (!(f2.d && clen(f2) >= 5 && h5 == 0x2f50545448ull)) return false;   // "HTTP/"
+#else
         if (swar_find(f1.d, f1.e, [](uint64_t w) { return ~swar_upper(w) & 0x8080808080808080ull; }) < f1.e) return false;
         cskip(p, 1);
         cparse_to_delim(uri, p, ' ');
@@ -1975,6 +1994,7 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         if (!(f2.d && clen(f2) >= 5 && ld(f2.d) == 'H' && ld(f2.d + 1) == 'T' && ld(f2.d + 2) == 'T' &&
               ld(f2.d + 3) == 'P' && ld(f2.d + 4) == '/'))
             return false;
+#endif
     } else {
         cparse_to_delim(f1, p, ' ');
         cskip(p, 1);
