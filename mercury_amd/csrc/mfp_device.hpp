@@ -216,8 +216,9 @@ DEV uint64_t swar_alpha(uint64_t w) {                  // isalpha (ASCII)
 #ifndef MFP_SWAR16
 #define MFP_SWAR16 0
 #endif
+// (w0: when given, receives the first round's words, from p & ~7)
 template <class F>
-DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag) {
+DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag, uint64_t *w0 = nullptr) {
     if (!p || p >= e) return e;
     const uintptr_t ee = (uintptr_t)e;
 #if MFP_SWAR16
@@ -250,6 +251,11 @@ DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag) {
         uint64_t w[MFP_SWB];
 #pragma unroll
         for (int k = 0; k < MFP_SWB; k++) w[k] = a + 8 * k < ee ? *(const uint64_t *)(a + 8 * k) : 0ull;
+        if (w0) {
+#pragma unroll
+            for (int k = 0; k < MFP_SWB; k++) w0[k] = w[k];
+            w0 = nullptr;
+        }
 #pragma unroll
         for (int k = 0; k < MFP_SWB; k++) {
             const uintptr_t ak = a + 8 * k;
@@ -463,9 +469,13 @@ DEV uint32_t seg_end(uint32_t s) { return s & 0x1fff; }
 DEV uint32_t seg_kind(uint32_t s) { return (s >> 13) & 3; }
 DEV uint32_t seg_src(uint32_t s) { return s >> 15; }
 
+struct HdrKey;
 struct SegEm {
     static constexpr bool SEG = true;
     static constexpr bool WIDE_LOADS = false;
+    // (MFP_HTTP_NAMEWIN) LDS copies of the header-name tables, set by k_fp_seg
+    const uint8_t *slots_req = nullptr, *slots_resp = nullptr;
+    const HdrKey *keys_req = nullptr, *keys_resp = nullptr;
     static constexpr bool PLAN = false;
     static constexpr bool emit_pass() { return false; }
     uint32_t n = 0;                     // characters produced
@@ -1636,6 +1646,32 @@ DEV uint64_t swar_tolower(uint64_t w) {
 // match -- the lowercased name as four packed words (aligned 8-byte loads of
 // the name's bytes), one hashed slot, one word-wise comparison; returns the
 // table index and the entry's incl_value | capture << 8
+// the table lookup of a name whose aligned words aw[0..4] (from n.d & ~7) are
+// loaded; the tables may be the __constant__ ones or LDS copies
+DEV int name_match(bool req, Cur n, const uint64_t (&aw)[5], const uint8_t *slots_req, const uint8_t *slots_resp,
+                   const HdrKey *keys_req, const HdrKey *keys_resp, uint32_t &info) {
+    const long l = clen(n);
+    const uint32_t sh = (uint32_t)((uintptr_t)n.d & 7) * 8;
+    uint64_t nw[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint64_t w = sh ? (aw[k] >> sh) | (aw[k + 1] << (64 - sh)) : aw[k];
+        const long rem = l - 8 * k;
+        if (rem <= 0) w = 0;
+        else if (rem < 8) w &= (1ull << (8 * rem)) - 1;
+        nw[k] = swar_tolower(w);
+    }
+    const uint64_t key = name_key(nw[0], nw[1], nw[2], nw[3], (uint64_t)l);
+    const int c = req ? (int)slots_req[(key * REQ_MUL) >> (64 - REQ_BITS)] - 1
+                      : (int)slots_resp[(key * RESP_MUL) >> (64 - RESP_BITS)] - 1;
+    if (c < 0) return -1;
+    const HdrKey &k = req ? keys_req[c] : keys_resp[c];
+    if (k.len == (uint32_t)l && k.w[0] == nw[0] && k.w[1] == nw[1] && k.w[2] == nw[2] && k.w[3] == nw[3]) {
+        info = k.info;
+        return c;
+    }
+    return -1;
+}
 DEV int name_lookup(bool req, Cur n, uint32_t &info) {
     const long l = clen(n);
     if (l <= 0 || l > 32) return -1;
@@ -1741,9 +1777,15 @@ DEV bool http_delim4w(Cur &p, uint32_t dv, long dl, uint32_t w) {
     return false;
 }
 // new_http_headers::fingerprint http.h:335 + httpheader http.h:146
+// MFP_HTTP_NAMEWIN (segment walker): the header name's lookup right after the
+// ':' search, from that search's words and LDS copies of the tables
+#ifndef MFP_HTTP_NAMEWIN
+#define MFP_HTTP_NAMEWIN 0
+#endif
 template <class E>
 DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {
     Cur tmp = body;
+    constexpr bool NW = E::SEG && MFP_HTTP_NAMEWIN && MFP_HTTP_FAST >= 1;
 #if MFP_HTTP_FAST
     const long dl = clen(delim);
     const uint32_t dv = dl > 0 && dl <= 4 ? ld_le4n(delim.d, dl) : 0u;
@@ -1757,6 +1799,7 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
     // searched from the ':' while the whitespace after it is loaded: one
     // memory round trip for both
     constexpr bool F2 = E::SEG && MFP_HTTP_FAST >= 2;
+    static_assert(MFP_SWB == 4, "the name window is the ':' search's first four words");
     uint32_t wnext = 0;
     bool have_next = false;
 #define MFP_HTOP(c) (F2 && have_next ? http_delim4w(c, dv, dl, wnext) : MFP_HDELIM(c))
@@ -1770,11 +1813,28 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
 #if MFP_HTTP_FAST
         // the ':' found is the byte the reference tests next; none found leaves
         // the name's first byte, which is not ':'
+        int early_idx = -1;
+        uint32_t early_info = 0;
         if (!cnotempty(tmp)) { cset_null(tmp); }
         else {
             name.d = tmp.d; name.e = tmp.e;
-            const uint8_t *q = swar_find(tmp.d, tmp.e, [](uint64_t w) { return swar_eq(w, ':'); });
-            if (q < tmp.e) { name.e = q; tmp.d = q + 1; } else cset_null(tmp);
+            uint64_t w0[MFP_SWB];
+            const uint8_t *q = swar_find(tmp.d, tmp.e, [](uint64_t w) { return swar_eq(w, ':'); }, NW ? w0 : nullptr);
+            if (q < tmp.e) {
+                name.e = q; tmp.d = q + 1;
+                if constexpr (NW) {
+                    // the name's table lookup now, from the search's first 32
+                    // bytes when they hold the name, and from the LDS tables
+                    const long l = q - name.d;
+                    const uintptr_t a = (uintptr_t)name.d & ~(uintptr_t)7;
+                    if (l > 0 && l <= 32 && (uintptr_t)q <= a + 8 * MFP_SWB) {
+                        const uint64_t aw[5] = {w0[0], w0[1], w0[2], w0[3], 0ull};
+                        early_idx = name_match(req, name, aw, b.slots_req, b.slots_resp, b.keys_req, b.keys_resp, early_info);
+                    } else {
+                        early_idx = name_lookup(req, name, early_info);
+                    }
+                }
+            } else cset_null(tmp);
         }
         Cur value;
         if constexpr (F2) {
@@ -1819,6 +1879,8 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         MFP_HDELIM(tmp);
         }
 #else
+        const int early_idx = -1;
+        const uint32_t early_info = 0;
         if (!cnotempty(tmp)) { cset_null(tmp); }
         else {
             name.d = tmp.d; name.e = tmp.e;
@@ -1833,8 +1895,8 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
 #endif
         hdr_body.e = value.e;
         if (cnull(tmp)) break;
-        uint32_t info = 0;
-        const int idx = name_lookup(req, name, info);
+        uint32_t info = early_info;
+        const int idx = NW ? early_idx : name_lookup(req, name, info);
         if (idx >= 0) {
 #ifndef MFP_PROBE_LNOEMIT
             b.putc('(');

@@ -345,6 +345,10 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
     __shared__ uint32_t wave_tot[TILE / 64], wave_len[TILE / 64];
     __shared__ unsigned long long tile_base;
     __shared__ uint8_t pool[SEG_POOL_BYTES];
+#if MFP_HTTP_NAMEWIN
+    __shared__ HdrKey s_keys[N_REQ_NAMES + N_RESP_NAMES];
+    __shared__ uint8_t s_slots[(1 << REQ_BITS) + (1 << RESP_BITS)];
+#endif
 #if MFP_SEG_LANE
     __shared__ uint64_t out_line[TILE][SEG_LINEW];
 #else
@@ -356,6 +360,12 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
         const char *lp = MFP_SEG_POOL;
         pool[tid] = (uint8_t)(tid < (int)sizeof(MFP_SEG_POOL) ? lp[tid] : 0);
     }
+#if MFP_HTTP_NAMEWIN
+    if (tid < N_REQ_NAMES) s_keys[tid] = k_req_keys[tid];
+    else if (tid < N_REQ_NAMES + N_RESP_NAMES) s_keys[tid] = k_resp_keys[tid - N_REQ_NAMES];
+    if (tid < (1 << REQ_BITS)) s_slots[tid] = k_req_slots.s[tid];
+    else if (tid < (1 << REQ_BITS) + (1 << RESP_BITS)) s_slots[tid] = k_resp_slots.s[tid - (1 << REQ_BITS)];
+#endif
     __syncthreads();
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     KPH_DECL
@@ -370,6 +380,10 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 
         Out o;
         SegEm e(data, segs + tid * SEG_STRIDE);
+#if MFP_HTTP_NAMEWIN
+        e.slots_req = s_slots; e.slots_resp = s_slots + (1 << REQ_BITS);
+        e.keys_req = s_keys; e.keys_resp = s_keys + N_REQ_NAMES;
+#endif
         packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
         e.finish();
         const bool fb = live && e.ovf;
