@@ -1779,8 +1779,9 @@ DEV bool http_delim4w(Cur &p, uint32_t dv, long dl, uint32_t w) {
 // new_http_headers::fingerprint http.h:335 + httpheader http.h:146
 // MFP_HTTP_NAMEWIN (segment walker): the header name's lookup right after the
 // ':' search, from that search's words and LDS copies of the tables
+// (http_req 11.1 -> 10.0 ms, http_resp 2.9 -> 2.7 at config 4, profiles/r04y_ab_*)
 #ifndef MFP_HTTP_NAMEWIN
-#define MFP_HTTP_NAMEWIN 0
+#define MFP_HTTP_NAMEWIN 1
 #endif
 template <class E>
 DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {

@@ -361,10 +361,12 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
         pool[tid] = (uint8_t)(tid < (int)sizeof(MFP_SEG_POOL) ? lp[tid] : 0);
     }
 #if MFP_HTTP_NAMEWIN
-    if (tid < N_REQ_NAMES) s_keys[tid] = k_req_keys[tid];
-    else if (tid < N_REQ_NAMES + N_RESP_NAMES) s_keys[tid] = k_resp_keys[tid - N_REQ_NAMES];
-    if (tid < (1 << REQ_BITS)) s_slots[tid] = k_req_slots.s[tid];
-    else if (tid < (1 << REQ_BITS) + (1 << RESP_BITS)) s_slots[tid] = k_resp_slots.s[tid - (1 << REQ_BITS)];
+    if constexpr ((FAM & FAM_HTTP) != 0) {   // the header-name tables, for walkers that parse HTTP
+        if (tid < N_REQ_NAMES) s_keys[tid] = k_req_keys[tid];
+        else if (tid < N_REQ_NAMES + N_RESP_NAMES) s_keys[tid] = k_resp_keys[tid - N_REQ_NAMES];
+        if (tid < (1 << REQ_BITS)) s_slots[tid] = k_req_slots.s[tid];
+        else if (tid < (1 << REQ_BITS) + (1 << RESP_BITS)) s_slots[tid] = k_resp_slots.s[tid - (1 << REQ_BITS)];
+    }
 #endif
     __syncthreads();
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
