@@ -1903,12 +1903,39 @@ extern "C" size_t mfp_analysis_huge_bytes(uint32_t max_nproc) {
     return (size_t)mfpa::HUGE_WAVES * stride * 9;
 }
 
+// blocks of the per-segment kernels (k_analyze, k_an_features: AW segments per
+// block, equal work each) at most: a whole number of resident rounds of both, so
+// neither's last round leaves CUs idle (5 and 4 blocks per CU on 256 CUs: 5120;
+// the flat 2048 was 1.6 rounds of k_analyze).  MFP_GRID_ROUND=0: 2048.
+static uint64_t seg_block_cap() {
+    static const uint64_t cap = [] {
+        const char *e = getenv("MFP_GRID_ROUND");
+        if (e && e[0] == '0') return (uint64_t)2048;
+        int dev = 0, cus = 0, a = 0, f = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, mfpa::k_analyze, 64 * mfpa::AW, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&f, mfpa::k_an_features, 64 * mfpa::AW, 0) != hipSuccess ||
+            cus <= 0 || a <= 0 || f <= 0) {
+            (void)hipGetLastError();
+            return (uint64_t)2048;
+        }
+        const uint64_t ra = (uint64_t)cus * (uint64_t)a, rf = (uint64_t)cus * (uint64_t)f;
+        uint64_t x = ra, y = rf;
+        while (y) { const uint64_t t = x % y; x = y; y = t; }
+        const uint64_t l = ra / x * rf;
+        return l <= 8192 ? l : (uint64_t)2048;
+    }();
+    return cap;
+}
+
 // the per-wave segments of one batch: k_analyze's waves (segments) and the
 // items a segment holds at most (64 per group a wave can take)
 extern "C" void mfp_analysis_segments(uint64_t n, uint32_t *nseg, uint32_t *seg_cap) {
     const uint64_t groups = (n + 63) / 64;
     uint64_t blocks = (groups + mfpa::AW - 1) / mfpa::AW;
-    if (blocks > 2048) blocks = 2048;
+    const uint64_t cap = seg_block_cap();
+    if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
     const uint64_t ns = blocks * mfpa::AW;
     *nseg = (uint32_t)ns;

@@ -735,6 +735,27 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
 #define MFP_LDS_STAGE_SEG (32 * 1024)
 #endif
 
+// A persistent bin kernel's grid as a whole number of resident rounds: its
+// blocks take equal shares of the bin's tiles (static stride), so a grid of 2048
+// at 3 blocks per CU (k_fp_tls1, 768 resident on 256 CUs) ran its last third of a
+// round on two thirds of the CUs.  MFP_GRID_ROUND=0: the grid as given.
+template <auto KERN>
+inline uint32_t round_grid(uint32_t want) {
+    static const uint32_t res = [] {
+        const char *e = getenv("MFP_GRID_ROUND");
+        if (e && e[0] == '0') return 0u;
+        int dev = 0, cus = 0, nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KERN, TILE, 0) != hipSuccess || cus <= 0 || nb <= 0) {
+            (void)hipGetLastError();
+            return 0u;
+        }
+        return (uint32_t)(cus * nb);
+    }();
+    return res && want > res ? want / res * res : want;
+}
+
 // one protocol bin's kernel: the LDS-staged walker (lds) or the HBM lane
 // walker of family FAM; the HTTP segment variants are launched by
 // mfp_launch_bin_seg (mfp_k_http.hip) whatever the bin
@@ -747,12 +768,13 @@ int launch_bin(const KParams &P, uint32_t *fallback, bool lds, const char *name,
     } else {
         if constexpr (FAM == FAM_TLS && MFP_TLS_ONEPASS) {   // (bin kernels always have a fallback list)
             switch (P.cfg.tls_format) {
-            case 1: hipLaunchKernelGGL(k_fp_tls1<1>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback); break;
-            case 2: hipLaunchKernelGGL(k_fp_tls1<2>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback); break;
-            default: hipLaunchKernelGGL(k_fp_tls1<0>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback); break;
+            case 1: hipLaunchKernelGGL(k_fp_tls1<1>, dim3(round_grid<k_fp_tls1<1>>(fblocks)), dim3(TILE), 0, stream, P, fallback); break;
+            case 2: hipLaunchKernelGGL(k_fp_tls1<2>, dim3(round_grid<k_fp_tls1<2>>(fblocks)), dim3(TILE), 0, stream, P, fallback); break;
+            default: hipLaunchKernelGGL(k_fp_tls1<0>, dim3(round_grid<k_fp_tls1<0>>(fblocks)), dim3(TILE), 0, stream, P, fallback); break;
             }
         } else
-            hipLaunchKernelGGL(k_fingerprint<FAM>, dim3(fblocks), dim3(TILE), 0, stream, P, fallback);
+            hipLaunchKernelGGL(k_fingerprint<FAM>, dim3(round_grid<k_fingerprint<FAM>>(fblocks)), dim3(TILE), 0, stream, P,
+                               fallback);
     }
     if (prof) mfp_prof_end(prof, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
