@@ -1929,6 +1929,26 @@ static uint64_t seg_block_cap() {
     return cap;
 }
 
+// k_an_score's grid: every block it can hold resident (10 per CU, LDS-bound:
+// 5 waves per SIMD), over the segments with a stride; the flat 1024 ran it at 2
+// waves per SIMD.  MFP_GRID_ROUND=0: 1024.
+static uint32_t score_grid(uint32_t blocks) {
+    static const uint32_t res = [] {
+        const char *e = getenv("MFP_GRID_ROUND");
+        if (e && e[0] == '0') return 1024u;
+        int dev = 0, cus = 0, nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, mfpa::k_an_score, 64 * mfpa::SW, 0) != hipSuccess ||
+            cus <= 0 || nb <= 0) {
+            (void)hipGetLastError();
+            return 1024u;
+        }
+        return (uint32_t)(cus * nb);
+    }();
+    return blocks < res ? blocks : res;
+}
+
 // the per-wave segments of one batch: k_analyze's waves (segments) and the
 // items a segment holds at most (64 per group a wave can take)
 extern "C" void mfp_analysis_segments(uint64_t n, uint32_t *nseg, uint32_t *seg_cap) {
@@ -1975,7 +1995,7 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
     if (prof) mfp_prof_begin(prof, "k_an_score", stream);
-    hipLaunchKernelGGL(mfpa::k_an_score, dim3(blocks < 1024 ? blocks : 1024), dim3(64 * mfpa::SW), 0, stream, P);
+    hipLaunchKernelGGL(mfpa::k_an_score, dim3(score_grid(blocks)), dim3(64 * mfpa::SW), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
     if (prof) mfp_prof_begin(prof, "k_analyze_wave", stream);
