@@ -1923,8 +1923,9 @@ static uint64_t seg_block_cap() {
         const uint64_t ra = (uint64_t)cus * (uint64_t)a, rf = (uint64_t)cus * (uint64_t)f;
         uint64_t x = ra, y = rf;
         while (y) { const uint64_t t = x % y; x = y; y = t; }
-        const uint64_t l = ra / x * rf;
-        return l <= 8192 ? l : (uint64_t)2048;
+        uint64_t l = ra / x * rf;
+        if (const char *r = getenv("MFP_SEG_ROUNDS")) l *= strtoul(r, nullptr, 10) ? strtoul(r, nullptr, 10) : 1;
+        return l <= 32768 ? l : (uint64_t)2048;
     }();
     return cap;
 }
@@ -1947,6 +1948,33 @@ static uint32_t score_grid(uint32_t blocks) {
         return (uint32_t)(cus * nb);
     }();
     return blocks < res ? blocks : res;
+}
+
+// k_seen_scan's grid: contiguous group ranges, one per block; every block the
+// CUs hold (4 per CU, LDS-bound) once there are 256 groups per block, instead of
+// one block per 1024 groups (763 blocks at 50 M packets: three quarters of the
+// CUs).  MFP_GRID_ROUND=0: one block per 1024 groups, at most 1024.
+static uint64_t seen_grid(uint64_t groups) {
+    static const uint64_t res = [] {
+        const char *e = getenv("MFP_GRID_ROUND");
+        if (e && e[0] == '0') return (uint64_t)0;
+        int dev = 0, cus = 0, nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, mfpa::k_seen_scan, 64 * mfpa::SEEN_WPB, 0) != hipSuccess ||
+            cus <= 0 || nb <= 0) {
+            (void)hipGetLastError();
+            return (uint64_t)0;
+        }
+        return (uint64_t)cus * (uint64_t)nb;
+    }();
+    uint64_t sb = (groups + 1023) / 1024;
+    if (sb > 1024) sb = 1024;
+    if (res) {
+        const uint64_t b = (groups + 255) / 256;
+        sb = b < res ? b : res;
+    }
+    return sb ? sb : 1;
 }
 
 // the per-wave segments of one batch: k_analyze's waves (segments) and the
@@ -1983,8 +2011,7 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
     {
-        uint64_t sb = (groups + 1023) / 1024;        // about 1024 groups per block, at most 1024 blocks
-        if (sb > 1024) sb = 1024;
+        const uint64_t sb = seen_grid(groups);
         if (prof) mfp_prof_begin(prof, "k_seen_scan", stream);
         hipLaunchKernelGGL(mfpa::k_seen_scan, dim3((uint32_t)sb), dim3(64 * mfpa::SEEN_WPB), 0, stream, P);
         if (prof) mfp_prof_end(prof, stream);
