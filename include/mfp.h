@@ -54,7 +54,7 @@ typedef struct {
     uint8_t  fp_type;    /* enum fingerprint_type (libmerc.h:351-373)     */
     uint8_t  msg;        /* protocol tag, MFP_MSG_*                       */
     uint8_t  flags;      /* MFP_FLAG_*                                    */
-    uint8_t  status;     /* reserved, 0 (the classifier status is mfp_analysis.status) */
+    uint8_t  xflags;     /* MFP_XF_* (the classifier status is mfp_analysis.status) */
     /* classifier inputs (destination_context, result.h:346): offsets are
      * relative to the packet start, len 0xffff = absent */
     uint16_t sni_off, sni_len;
@@ -130,11 +130,20 @@ enum {
                                   data may need reassembly has the block too (its plaintext).
                                   Packed host arenas keep it. */
 };
+enum {
+    MFP_XF_TLS_UA = 1,   /* (D)TLS ClientHello: ua_off/ua_len hold the user agent of a
+                            quic_transport_parameters_draft extension (transport parameter
+                            0x3129, tls_extensions::set_meta_data tls.h:1346-1355), not the
+                            ALPN list; host outputs re-read the ALPN list from the packet */
+};
 /* For MFP_MSG_TLS_SH / MFP_MSG_TLS_CERT records sni_off/sni_len hold the
  * certificate_list datum (tls.h:275-296), the bytes the JSON writer's
  * "certs" array is built from; len 0xffff = no list.  For MFP_MSG_TLS_CH and
  * MFP_MSG_DTLS_CH records ua_off/ua_len hold the ALPN protocol_name_list
- * (destination_context::alpn_array, analysis_context_get_alpns). */
+ * (destination_context::alpn_array, analysis_context_get_alpns), unless
+ * MFP_XF_TLS_UA; sni_off/sni_len hold the LAST server_name extension (the
+ * destination context's, tls.h:1316-1345; the JSON text prints the first,
+ * tls.h:1052-1080, which the writer re-reads from the packet). */
 
 enum {
     MFP_MSG_NONE = 0, MFP_MSG_TLS_CH, MFP_MSG_TLS_SH, MFP_MSG_TLS_CERT,
@@ -193,9 +202,15 @@ typedef struct mfp_context_s *mfp_context;
  * tcp.syn_ack, dtls, quic (QUIC Initial packets: decrypted and fingerprinted
  * on the device), stun, openvpn_tcp, gre, vxlan, geneve (decapsulation,
  * pkt_proc.cc:959-1049); "format=" takes tls/N and quic/N; "reassembly"
- * enables mfp_process_batch_reassembly.  ""/"all" (the reference's ~45
- * protocols) are refused.  Returns NULL on error (unknown protocol, no HIP
- * device, extension not loadable). */
+ * enables mfp_process_batch_reassembly; "report_os" as the reference's.
+ * ""/"all" and names of protocols outside the path are accepted: their
+ * messages get MFP_MSG_OTHER and no record.  Options that change the
+ * reference's records (metadata, certs-json, raw-features of tls/stun/all,
+ * crypto-assess, network-behavioral-detections, exposed-creds, http-headers,
+ * http-body-max > 0, nonselected-tcp-data / -udp-data, quic-trial-decryption,
+ * minimize-ram, fp_proc_threshold / proc_dst_threshold > 0, stats) are
+ * refused.  Returns NULL on error (refused option, no HIP device, extension
+ * not loadable). */
 MFP_EXPORT mfp_context mfp_init(const char *packet_filter_cfg, int device, int mode);
 /* mfp_init with the resource archive's decryption key (libmerc_config.enc_key,
  * libmerc.h:124-125): 16 bytes, AES-128-CBC with the IV as the file's first

@@ -8,7 +8,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("caplen", "<u4"), ("linktype", "<u2"), ("flags", "<u2")])
 RECORD_DTYPE = np.dtype([("fp_offset", "<u8"), ("fp_len", "<u4"), ("fp_type", "u1"), ("msg", "u1"),
-                         ("flags", "u1"), ("status", "u1"), ("sni_off", "<u2"), ("sni_len", "<u2"),
+                         ("flags", "u1"), ("xflags", "u1"), ("sni_off", "<u2"), ("sni_len", "<u2"),
                          ("ua_off", "<u2"), ("ua_len", "<u2"), ("src_port", "<u2"), ("dst_port", "<u2"),
                          ("net", "<u4")])
 ANALYSIS_DTYPE = np.dtype([("score", "<f8"), ("malware_prob", "<f8"), ("process", "<u4"), ("attr", "<u2"),

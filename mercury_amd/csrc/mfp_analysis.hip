@@ -766,7 +766,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
         mfp_record r;
         if (live) r = P.rec[i];
         else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; r.fp_offset = 0; r.net = 0; r.msg = 0;
-               r.sni_off = 0; r.sni_len = 0xffff; r.ua_off = 0; r.ua_len = 0xffff; r.dst_port = 0; }
+               r.sni_off = 0; r.sni_len = 0xffff; r.ua_off = 0; r.ua_len = 0xffff; r.dst_port = 0; r.xflags = 0; }
         const uint8_t *fp = P.fp_arena + r.fp_offset;
         mfp_entry E;
         E.proc_off = 0; E.nproc = 0; E.malware_db = 0; E.generic_dmz = 0;
@@ -833,7 +833,10 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             // wave scorer escapes it into LDS (slow_lookups)
             ssh_ua = r.msg == MFP_MSG_SSH_INIT && r.ua_len != 0xffff;
             stun_ua = r.msg == MFP_MSG_STUN;
-            uint32_t ul = r.ua_len == 0xffff || r.msg == MFP_MSG_TLS_CH || ssh_ua || stun_ua ? 0u : r.ua_len;
+            // (a TLS ClientHello's ua span is its ALPN list unless MFP_XF_TLS_UA: the
+            // user agent of a draft transport-parameter extension, tls.h:1346-1355)
+            const bool tls_alpn_span = r.msg == MFP_MSG_TLS_CH && !(r.xflags & MFP_XF_TLS_UA);
+            uint32_t ul = r.ua_len == 0xffff || tls_alpn_span || ssh_ua || stun_ua ? 0u : r.ua_len;
             if (ul > 511) ul = 511;
             const uint8_t *up = sbase + r.ua_off;
             uint64_t uh = 0;

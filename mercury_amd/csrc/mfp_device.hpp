@@ -784,6 +784,14 @@ DEV bool qtp_parse(Cur &d, Cur &id) {                   // quic_transport_parame
     return !cnull(val);
 }
 DEV bool qtp_is_grease(Cur id) { return vli_value(id) % 31 == 27; }
+// variable_length_integer (quic_vli.hpp): a failed read yields 0 and a null cursor
+DEV uint64_t vli_rd(Cur &c) {
+    const uint32_t b = rd_u8(c);
+    const int len = vli_len(b);
+    uint64_t v = b & 0x3f;
+    for (int i = 1; i < len; i++) v = v * 256 + rd_u8(c);
+    return v;
+}
 template <class E>
 DEV void qtp_write_id(E &b, Cur id) {
     if (!qtp_is_grease(id)) b.hex(id.d, clen(id));
@@ -1168,9 +1176,31 @@ DEV void tls_alpn(const uint8_t *start, const uint8_t *end, const uint8_t *base,
     if (rd_uint(e, 2, l) && (uint64_t)clen(e) >= l) { off = (uint32_t)(e.d - base); len = (uint32_t)l; }
     else { off = 0; len = 0xffff; }
 }
+// the user agent of a quic_transport_parameters_draft extension [start, end)
+// (tls_extensions::set_meta_data tls.h:1346-1355: transport parameter 0x3129,
+// quic_transport_parameter tls.h:1244; the last one wins and a value that does
+// not parse is a null -- empty -- user agent).  It takes the record's ua span,
+// which otherwise holds the ALPN list, and sets MFP_XF_TLS_UA; the ALPN list is
+// then re-read from the packet by the host outputs.
+DEV void tls_draft_ua(const uint8_t *start, const uint8_t *end, const uint8_t *base, uint32_t &off, uint32_t &len,
+                      uint32_t &xf) {
+    Cur e = cmk(start, end);
+    cskip(e, 4);
+    while (clen(e) > 0) {
+        Cur id; cparse(id, e, vli_len(look_u8(e)));
+        const uint64_t vl = vli_rd(e);
+        Cur val; cparse(val, e, (long)vl);
+        if (vli_value(id) == 0x3129) {
+            off = cnull(val) ? 0u : (uint32_t)(val.d - base);
+            len = cnull(val) ? 0u : (uint32_t)clen(val);
+            xf |= MFP_XF_TLS_UA;
+        }
+    }
+}
 // server name (tls_extensions::set_meta_data tls.h:1316-1366; the last one
 // wins) and ALPN list of a ClientHello's extensions
-DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len, uint32_t &aoff, uint32_t &alen) {
+DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len, uint32_t &aoff, uint32_t &alen,
+                 uint32_t &xf) {
     Cur p = exts;
     while (clen(p) > 0) {
         const uint8_t *start = p.d;
@@ -1183,7 +1213,8 @@ DEV void tls_sni(Cur exts, const uint8_t *base, uint32_t &off, uint32_t &len, ui
             cskip(e, 9);
             off = (uint32_t)(e.d - base); len = (uint32_t)clen(e);
         }
-        if (t == 16) tls_alpn(start, p.d, base, aoff, alen);
+        if (t == 16 && !(xf & MFP_XF_TLS_UA)) tls_alpn(start, p.d, base, aoff, alen);
+        if (t == 0xffa5) tls_draft_ua(start, p.d, base, aoff, alen, xf);
     }
 }
 // ClientHello plan: pass 1 of the lane kernels records what pass 2 needs to
@@ -1209,7 +1240,7 @@ struct TlsPlan {
 // one wins) and the plan -- one walk over the extension list
 template <class E>
 DEV void tls_ch_plan(E &b, TlsPlan &pl, const Ch &ch, int fmt, uint32_t type, const uint8_t *base,
-                     uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len) {
+                     uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len, uint32_t &xf) {
     pl.ok = false;
     fp_type_prefix(b, type);
     if (fmt >= 1 && fmt <= 2) { b.putc('0' + fmt); b.putc('/'); }
@@ -1232,7 +1263,8 @@ DEV void tls_ch_plan(E &b, TlsPlan &pl, const Ch &ch, int fmt, uint32_t type, co
             cskip(e, 9);
             sni_off = (uint32_t)(e.d - base); sni_len = (uint32_t)clen(e);
         }
-        if (x.type == 16) tls_alpn(start, p.d, base, alpn_off, alpn_len);
+        if (x.type == 16 && !(xf & MFP_XF_TLS_UA)) tls_alpn(start, p.d, base, alpn_off, alpn_len);
+        if (x.type == 0xffa5) tls_draft_ua(start, p.d, base, alpn_off, alpn_len, xf);
         if (rare) continue;
         int bucket = 0;
         if (fmt == 2) {
@@ -1384,6 +1416,9 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
             sni_off = (uint32_t)(e.d - base); sni_len = (uint32_t)clen(e);
         }
         if (x.type == 16) tls_alpn(start, p.d, base, alpn_off, alpn_len);
+        // a draft transport-parameter extension may carry the user agent
+        // (tls_draft_ua): the fallback lane writes such a hello's record
+        if (x.type == 0xffa5) rare = true;
         if (rare) continue;
         int bucket = 0;
         if (FMT == 2) {
@@ -1919,6 +1954,7 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
 // ---------------------------------------------------------------------------
 struct Out {
     uint32_t fp_type, msg, flags;
+    uint32_t xflags;     // MFP_XF_* (mfp_record.xflags)
     uint32_t sni_off, sni_len, ua_off, ua_len;
     uint32_t src_port, dst_port;
     uint32_t net;        // innermost IP header offset | version << 16 (flow key, flow_key.h:71)
@@ -2262,11 +2298,11 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
             if constexpr (E::FAST >= 0)
                 tls_ch_plan_fast<E::FAST>(b, *b.plan, ch, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
             else
-                tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+                tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
         } else {
             fp_type_prefix(b, 1);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
-            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
         }
         return;
         }
@@ -2551,11 +2587,11 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
             if constexpr (E::FAST >= 0)
                 tls_ch_plan_fast<E::FAST>(b, *b.plan, ch, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
             else
-                tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+                tls_ch_plan(b, *b.plan, ch, (int)cfg.tls_format, 10, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
         } else {
             fp_type_prefix(b, 10);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
-            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
+            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
         }
     } else if (msg == MFP_MSG_DTLS_SH) {
         Cur b2 = body;
@@ -2826,7 +2862,7 @@ DEV void ip_path(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
 // and analyze_packet pkt_proc.cc:1814
 template <uint32_t FAM = FAM_ALL, class E>
 DEV void packet_walk(E &b, const Cfg &cfg, Out &o, const uint8_t *data, uint32_t len, uint32_t linktype) {
-    o.fp_type = 0; o.msg = 0; o.flags = 0;
+    o.fp_type = 0; o.msg = 0; o.flags = 0; o.xflags = 0;
     o.sni_off = o.ua_off = 0; o.sni_len = o.ua_len = 0xffff;
     o.src_port = o.dst_port = 0;
     o.net = 0;

@@ -198,19 +198,44 @@ static void parse_format(const std::string &s, uint32_t &tls_format, SelState &s
 // (config_generator.cc:115-162): ';'-separated tokens, trimmed, key=value or a
 // bare key; a key no option recognises is taken as a protocol list.  Warnings
 // (what the reference logs and goes on from) land in *warn.
+//
+// The reference's other options (config_generator.cc:28-44,
+// global_config.h:350-365) fall in three groups here:
+//  * no effect on the records this path writes -- accepted: stats-blocking,
+//    max_stats_entries (the stats aggregator, off), dns-json (DNS/mDNS
+//    records only, pkt_proc_util.h:284-313: this path writes none),
+//    raw-features naming only bittorrent/smb/ssdp (or none), http-body-max=0,
+//    and any boolean option set to a value other than "" or "1" (off);
+//  * report_os: honoured (*report_os = 1 / 0; -1 when absent);
+//  * options that change the records (metadata, certs-json, raw-features of
+//    tls/stun/all, crypto-assess, network-behavioral-detections,
+//    exposed-creds, http-headers, http-body-max > 0, nonselected-tcp-data,
+//    nonselected-udp-data, quic-trial-decryption, minimize-ram,
+//    fp_proc_threshold / proc_dst_threshold > 0, stats): REFUSED -- false with
+//    the reason in mfp_last_error(), so no caller gets records that differ
+//    from the reference's without being told.
 bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
-                      bool *reassembly, uint32_t *block_out, std::string *warn) {
+                      bool *reassembly, uint32_t *block_out, std::string *warn, int *report_os) {
     tls_format = 0;
+    if (report_os) *report_os = -1;
     SelState st;
     std::string s = cfg ? cfg : "";
     if (s.find(';') == std::string::npos) {
         parse_select(s, st);
     } else {
-        static const char *const ignored[] = {   // recognised options that do not affect this path's output
-            "quic-trial-decryption", "stats-blocking", "raw-features", "crypto-assess", "minimize-ram",
-            "network-behavioral-detections", "exposed-creds", "http-headers", "http-body-max", "dns-json",
-            "certs-json", "metadata", "stats", "report_os", "nonselected-tcp-data", "nonselected-udp-data",
-            "fp_proc_threshold", "proc_dst_threshold", "max_stats_entries"};
+        static const char *const no_effect[] = {"stats-blocking", "max_stats_entries", "dns-json"};
+        // boolean setters of config_mapper: on for "" or "1" (config_generator.cc:31-43)
+        static const char *const refused_on[] = {"metadata", "certs-json", "network-behavioral-detections",
+                                                 "nonselected-tcp-data", "nonselected-udp-data", "stats"};
+        // extended setters that turn their feature on whatever the value (global_config.h:356-364)
+        static const char *const refused_any[] = {"crypto-assess", "exposed-creds", "http-headers",
+                                                  "quic-trial-decryption", "minimize-ram"};
+        auto refuse = [&](const std::string &key, const std::string &why) {
+            mfp_set_error("packet_filter_cfg option \"%s\" %s; libmercury_amd writes the reference's records with it "
+                          "off only, and refuses it rather than ignore it", key.c_str(), why.c_str());
+            return false;
+        };
+        auto in = [](const char *const *b, const char *const *e, const std::string &k) { return std::find(b, e, k) != e; };
         size_t pos = 0;
         while (pos <= s.size()) {
             size_t c = s.find(';', pos);
@@ -218,14 +243,41 @@ bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std:
             if (!tok.empty()) {
                 size_t eq = tok.find('=');
                 std::string key = trim(tok.substr(0, eq)), val = eq == std::string::npos ? "" : trim(tok.substr(eq + 1));
+                const bool on = val.empty() || val == "1";
                 if (key == "select" || key == "-s" || key == "--select") parse_select(val, st);
                 else if (key == "format") parse_format(val, tls_format, st);
                 else if (key == "resources") { if (resources) *resources = val; }
                 else if (key == "analysis" || key == "-a" || key == "--analysis") {
-                    if (analysis) *analysis = val.empty() || val == "1";
+                    if (analysis) *analysis = on;
                 } else if (key == "reassembly" || key == "tcp-reassembly") {   // global_config.h:354-355
                     if (reassembly) *reassembly = true;
-                } else if (std::find(std::begin(ignored), std::end(ignored), key) == std::end(ignored)) {
+                } else if (key == "report_os") {                              // config_generator.cc:35
+                    if (report_os) *report_os = on ? 1 : 0;
+                } else if (in(std::begin(no_effect), std::end(no_effect), key)) {
+                } else if (in(std::begin(refused_on), std::end(refused_on), key)) {
+                    if (on) return refuse(key, "changes the JSON records (write_metadata pkt_proc_util.h:264-333, "
+                                               "pkt_proc.cc:1157-1253)");
+                } else if (in(std::begin(refused_any), std::end(refused_any), key)) {
+                    return refuse(key, "changes the records or the classifier (global_config.h:356-364)");
+                } else if (key == "raw-features") {                           // global_config.h:277-294
+                    for (const char *p : {"all", "tls", "stun"}) {
+                        size_t at = 0;
+                        std::string v = val;
+                        v.erase(std::remove_if(v.begin(), v.end(), ::isspace), v.end());
+                        while ((at = v.find(p, at)) != std::string::npos) {
+                            const size_t end = at + strlen(p);
+                            if ((at == 0 || v[at - 1] == ',') && (end == v.size() || v[end] == ','))
+                                return refuse(key + "=" + val, "adds the \"features\" string to TLS/STUN records "
+                                                               "(tls.h:1909-1913)");
+                            at = end;
+                        }
+                    }
+                } else if (key == "http-body-max") {                          // global_config.h:327-345
+                    if (val != "0") return refuse(key + "=" + val, "adds HTTP bodies to the records");
+                } else if (key == "fp_proc_threshold" || key == "proc_dst_threshold") {
+                    if (strtof(val.c_str(), nullptr) > 0.0f)                  // analysis.h:836: fingerprint_db_lite.json
+                        return refuse(key + "=" + val, "switches the classifier's database");
+                } else {
                     parse_select(key, st);   // config_generator.cc:156-160
                 }
             }
@@ -404,6 +456,7 @@ struct mfp_context_s {
     bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
     Slot slot[4];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2: host pipeline
     int pipe_next = 0;                   // mfp_analyze_batch_device_pipelined: the slot of the next batch (0 or 3)
+    bool pipe_active = false;            // a pipelined batch may be pending in slot 0 or 3
     std::atomic<size_t> attr_names_len{SIZE_MAX};   // mfp_attribute_names_len
     int an_slot = 0;                     // slot of the last classified batch (mfp_analysis_stats)
     mfp_prof *prof = nullptr;            // mfp_profile_enable
@@ -428,7 +481,9 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     uint32_t sel, fmt, blk = 0;
     std::string resources;
     bool analysis = false, reassembly = false;
-    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly, &blk)) return nullptr;
+    int report_os = -1;
+    if (!mfp_parse_config(packet_filter_cfg, sel, fmt, &resources, &analysis, &reassembly, &blk, nullptr, &report_os))
+        return nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         mfp_set_error("no HIP device available: the mercury_amd fingerprint path runs only on the GPU");
@@ -438,6 +493,7 @@ extern "C" MFP_EXPORT mfp_context mfp_init_ex(const char *packet_filter_cfg, int
     auto *c = new mfp_context_s;
     c->device = device; c->select = sel; c->block = blk; c->tls_format = fmt & 0xff; c->quic_format = (fmt >> 8) & 0xff; c->mode = mode;
     c->reassembly = reassembly;
+    c->report_os = report_os == 1;
     const char *st = getenv("MFP_STRATEGY");
     if (st && !strcmp(st, "lane")) c->strategy = MFP_STRATEGY_LANE;
     if (const char *sb = getenv("MFP_SMALL_BATCH")) c->small_batch = (size_t)strtoull(sb, nullptr, 0);
@@ -715,6 +771,25 @@ static int slot_resolve(mfp_context c, Slot &S) {
     return slot_apply(c, S, S.h_dec, (size_t)m, true);
 }
 
+// Decide the pipelined device batches still pending (slots 0 and 3, the
+// older first) before any other analysis call takes slot 0 or the LRU: a
+// synchronous batch between pipelined ones must neither overwrite slot 0's
+// undecided batch nor decide its own sightings ahead of earlier ones (the LRU
+// follows stream order, analysis.h:362-421).
+static int flush_pipelined_locked(mfp_context c) {
+    if (!c->pipe_active) return 0;
+    for (int k = 0; k < 2; k++) {
+        Slot &S = c->slot[(k == 0) == (c->pipe_next == 0) ? 0 : 3];
+        if (!S.pend.live) continue;
+        const int r = slot_resolve(c, S);
+        if (r) return r;
+        HIPCHK(hipEventRecord(S.ev_resolved, S.stream));
+        S.resolved_recorded = true;
+    }
+    c->pipe_active = false;
+    return 0;
+}
+
 extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t *d_arena, const mfp_pkt_desc *d_desc,
                                                    size_t n, mfp_record *d_rec, char *d_fp_arena, size_t fp_cap,
                                                    uint64_t *d_fp_used, void *stream) {
@@ -830,7 +905,9 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
         mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
-    S.pend.fp = S.d_fp2;   // the records now point into the dense arena
+    // the records now point into the dense arena (a fingerprint-only batch in
+    // slot 0 leaves a pipelined batch pending there untouched)
+    if (analysis) S.pend.fp = S.d_fp2;
     return 0;
 }
 
@@ -864,6 +941,7 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     HIPCHK(hipSetDevice(c->device));
     if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
     Slot &S = c->slot[0];
+    if (analysis) { const int fr = flush_pipelined_locked(c); if (fr) return fr; }
     const bool host_resolve = analysis && n <= c->small_batch && !c->defer;
     int r = stage_and_launch(c, 0, arena, arena_len, desc, n, fp_cap, analysis != nullptr, attr_prob != nullptr,
                              host_resolve);
@@ -932,6 +1010,7 @@ extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8
     if (analysis && !c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     if (hipSetDevice(c->device) != hipSuccess) { mfp_set_error("hipSetDevice failed"); return -2; }
+    if (analysis) { const int fr = flush_pipelined_locked(c); if (fr) return fr; }
     const long long r = pipelined_locked(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, attr_prob, chunk);
     if (r < 0) {
         // an error path may leave copies into the caller's buffers queued on
@@ -1004,6 +1083,7 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     if (!c) { mfp_set_error("null context"); return -1; }
     if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
+    if (const int fr = flush_pipelined_locked(c)) return fr;
     const int r = analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, (hipStream_t)stream);
     if (r || c->defer) return r;
     // the batch's unknown-TLS sightings are decided now, in stream order: the
@@ -1025,12 +1105,18 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context c, cons
                                                              double *d_attr_prob, void *stream) {
     if (!c) { mfp_set_error("null context"); return -1; }
     if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
+    if (c->defer) {   // the deferred (shard-merge) mode decides its batches through mfp_analysis_resolve*
+        mfp_set_error("mfp_analyze_batch_device_pipelined: the context defers its prevalence decisions "
+                      "(mfp_analysis_defer); use mfp_analyze_batch_device");
+        return -1;
+    }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t us = (hipStream_t)stream;
     const int slot = c->pipe_next ? 3 : 0, other = c->pipe_next ? 0 : 3;
     Slot &S = c->slot[slot];
-    if (S.pend.live) { int r = slot_resolve(c, S); if (r) return r; }   // (never: the previous call decided it)
+    // a deferred or failed synchronous batch left in slot 0 is decided first
+    if (S.pend.live) { int r = slot_resolve(c, S); if (r) return r; }
     if (S.resolved_recorded) HIPCHK(hipStreamWaitEvent(us, S.ev_resolved, 0));
     int r = analyze_locked(c, slot, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, us);
     if (r) return r;
@@ -1038,10 +1124,19 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context c, cons
     HIPCHK(hipStreamWaitEvent(S.stream, S.ev_kernels, 0));
     S.pend.stream = S.stream;
     c->pipe_next ^= 1;
+    c->pipe_active = true;
     Slot &O = c->slot[other];
     if (O.pend.live) {
         r = slot_resolve(c, O);
-        if (r) return r;
+        if (r) {
+            // the older batch's statuses stay undecided; the new batch stays
+            // pending (the next call or mfp_analysis_flush decides it), so the
+            // context remains usable -- the error says which records are unfinished
+            O.pend.live = false;
+            mfp_set_error("mfp_analyze_batch_device_pipelined: deciding the previous batch's prevalence failed "
+                          "(its unknown-TLS statuses are undecided): %s", mfp_last_error());
+            return r;
+        }
         HIPCHK(hipEventRecord(O.ev_resolved, O.stream));
         O.resolved_recorded = true;
         HIPCHK(hipStreamWaitEvent(us, O.ev_resolved, 0));   // later work on the caller's stream sees its records
@@ -1054,14 +1149,8 @@ extern "C" MFP_EXPORT int mfp_analysis_flush(mfp_context c) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
-    for (int k = 0; k < 2; k++) {             // the older slot first
-        Slot &S = c->slot[(k == 0) == (c->pipe_next == 0) ? 0 : 3];
-        if (!S.pend.live) continue;
-        const int r = slot_resolve(c, S);
-        if (r) return r;
-        HIPCHK(hipEventRecord(S.ev_resolved, S.stream));
-        S.resolved_recorded = true;
-    }
+    c->pipe_active = true;                    // whatever is pending in 0 / 3, the older first
+    if (const int r = flush_pipelined_locked(c)) return r;
     for (int k : {0, 3}) HIPCHK(hipStreamSynchronize(c->slot[k].stream));
     return 0;
 }

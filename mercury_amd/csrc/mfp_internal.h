@@ -11,7 +11,8 @@
 
 void mfp_set_error(const char *fmt, ...);
 bool mfp_parse_config(const char *cfg, uint32_t &sel, uint32_t &tls_format, std::string *resources, bool *analysis,
-                      bool *reassembly, uint32_t *block = nullptr, std::string *warn = nullptr);
+                      bool *reassembly, uint32_t *block = nullptr, std::string *warn = nullptr,
+                      int *report_os = nullptr);
 int mfp_set_config(mfp_context c, uint32_t select, uint32_t tls_format, uint32_t mode);
 uint32_t mfp_context_mode(mfp_context c);   // MFP_MODE_*
 
@@ -30,3 +31,7 @@ void mfp_prof_end(mfp_prof *p, hipStream_t s);
 
 // the total length of the context's attribute names (computed once; mfp_json.cpp's bounds)
 size_t mfp_attribute_names_len(mfp_context c);
+
+// (D)TLS ClientHello records with MFP_XF_TLS_UA: the ALPN list re-read from
+// the packet (mfp_json.cpp)
+bool mfp_hello_alpn(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const uint8_t **alpn, uint32_t *len);

@@ -619,9 +619,10 @@ void write_stun(W &w, const uint8_t *m, size_t len) {
     w.put('}');
 }
 
+void client_hello_json(W &w, Obj &rec, mfpe::Cur p);
+
 // openvpn_tcp::write_json (openvpn.h:411-442) + tls_client_hello::write_json
-// (tls.h:1882-1917, metadata off); false when the hello carries QUIC
-// transport parameters (printed by the reference, not rebuilt here)
+// (tls.h:1882-1917, metadata off)
 bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
     struct R { unsigned op, replay, nid, msg; bool ctrl; };
     std::vector<R> ctrl, ack;
@@ -682,8 +683,8 @@ bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
     }
     if ((uint8_t)nrec == 0) return true;
     // the ClientHello: tls_record -> tls_handshake -> tls_client_hello
-    HC ext{nullptr, nullptr};
-    bool hello = false, ciphers = false;
+    HC chb{nullptr, nullptr};
+    bool hello = false;
     if (!ctrl.empty() && !buf_null && used) {
         // tls_record::parse tls.h:153 / tls_handshake::parse tls.h:244 (outer-bounded),
         // tls_client_hello::parse tls.h:1811
@@ -696,6 +697,7 @@ bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
         HC p{buf, buf + used}, frag{nullptr, nullptr}, body{nullptr, nullptr};
         if (hlen(p) >= 5) { hrd(p, 1); hrd(p, 2); frag = outer(p, hrd(p, 2)); }
         if (hlen(frag) >= 4) { hrd(frag, 1); const uint64_t hl = hrd(frag, 3); if (hl <= 32768) body = outer(frag, hl); }
+        chb = body;
         HC b = body;
         HC ver = hparse(b, 2);
         if (ver.d && ver.e > ver.d) {
@@ -711,12 +713,10 @@ bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
             if (ok && hlen(b) < 2) ok = false;
             long cl = 0;
             if (ok) { cl = (long)hrd(b, 2); if (cl & 1) ok = false; }
-            HC cs{nullptr, nullptr}, cm{nullptr, nullptr};
-            if (ok) { cs = hparse(b, cl); if (hlen(b) < 1) ok = false; }
+            HC cm{nullptr, nullptr};
+            if (ok) { hparse(b, cl); if (hlen(b) < 1) ok = false; }
             if (ok) { const long ml = (long)hrd(b, 1); cm = hparse(b, ml); }
-            ciphers = cs.d && cs.e > cs.d;
             hello = cm.d && cm.e > cm.d;
-            if (ok && hlen(b) >= 2) { const long el = (long)hrd(b, 2); ext.d = b.d; ext.e = b.d + std::min(el, hlen(b)); }
         }
     }
     rec.key("openvpn");
@@ -742,24 +742,7 @@ bool write_openvpn(W &w, Obj &rec, const uint8_t *m, size_t len) {
     if (total) { o.key("data_len"); w.udec(total); }
     if (hello) { o.key("has_tls"); w.puts("true"); }
     w.put('}');
-    if (hello && ciphers) {
-        // extensions: the first server_name, and no QUIC transport parameters
-        HC sn{nullptr, nullptr};
-        HC e = ext;
-        while (hlen(e) > 0) {
-            const uint8_t *st = e.d;
-            const unsigned t = (unsigned)hrd(e, 2);
-            const long l = (long)hrd(e, 2);
-            if (!e.d || l > hlen(e)) break;
-            e.d += l;
-            if (t == 0 && !sn.d) { sn.d = st + 9 < e.d ? st + 9 : e.d; sn.e = e.d; }
-            if (t == 0x39 || t == 0xffa5) return false;
-        }
-        rec.key("tls");
-        w.puts("{\"client\":{");
-        if (sn.d && sn.e > sn.d) { w.puts("\"server_name\":\""); w.utf8(sn.d, (size_t)(sn.e - sn.d)); w.put('"'); }
-        w.puts("}}");
-    }
+    if (hello) client_hello_json(w, rec, mfpe::Cur{chb.d, chb.e});   // openvpn.h:438-440
     return true;
 }
 
@@ -856,32 +839,47 @@ void quic_cc(W &w, Obj &qo, const uint8_t *f, const uint8_t *end) {   // quic_fr
     w.puts(",\"ack\":"); ack(); w.put('}');
 }
 
-// the "tls" object of a QUIC hello (tls_client_hello::write_json tls.h:1882-1917,
-// metadata off): the first server_name, every quic_transport_parameters
-// extension with the user agents inside it (tls.h:1264-1311)
-void quic_tls(W &w, Obj &rec, const uint8_t *hs, uint32_t hs_len) {
-    mfpe::Cur d{hs, hs + hs_len};
-    if (d.len() < 4) return;                               // tls_handshake::parse tls.h:244-262
-    uint64_t mt, hl;
-    d.rd(1, mt); d.rd(3, hl);
-    if (hl > 32768) return;
-    mfpe::Cur p{d.d, hl < (uint64_t)d.len() ? d.d + hl : d.e};
-    // tls_client_hello::parse tls.h:1811-1869 (QUIC: no DTLS cookie)
+// the "tls" (or "dtls") object of a ClientHello (tls_client_hello::write_json
+// tls.h:1882-1917, metadata off) from its handshake body: the first
+// server_name, every quic_transport_parameters extension with the user agents
+// inside it (tls.h:1264-1311).  Used for TLS ClientHellos over TCP, DTLS
+// ClientHellos, QUIC hellos and OpenVPN's, so that the JSON text follows the
+// reference's own parse of the hello rather than the classifier's view in the
+// record (whose server name is the LAST server_name extension,
+// tls_extensions::set_meta_data tls.h:1316-1345).
+// tls_client_hello::parse tls.h:1811-1869 over a handshake body: false unless
+// the hello is not empty (compression methods present, tls.h:443); the
+// extensions (soft-failed to the bytes present), whether the cipher-suite
+// vector is readable, and the DTLS bit (a 0xfe.. version: cookie, "dtls")
+bool hello_extensions(mfpe::Cur p, mfpe::Cur &ext, bool &ciphers_ok, bool &dtls) {
+    ext = mfpe::Cur{nullptr, nullptr};
+    ciphers_ok = false;
     const mfpe::Cur ver = take(p, 2);
-    if (ver.null() || ver.len() <= 0) return;
+    if (ver.null() || ver.len() <= 0) return false;
+    dtls = ver.d[0] == 0xfe;                               // tls.h:1823-1825
     take(p, 32);
     uint64_t l = 0;
-    if (!p.rd(1, l)) return;
+    if (!p.rd(1, l)) return false;
     take(p, (long)l);
-    if (!p.rd(2, l) || (l & 1)) return;
+    if (dtls) {                                            // tls.h:1836-1844
+        if (p.null() || p.len() < 1) return false;
+        if (!p.skip((long)p.d[0] + 1)) return false;
+    }
+    if (!p.rd(2, l) || (l & 1)) return false;
     const mfpe::Cur ciphers = take(p, (long)l);
-    if (!p.rd(1, l)) return;
+    if (!p.rd(1, l)) return false;
     const mfpe::Cur comp = take(p, (long)l);
-    if (comp.null() || comp.len() <= 0) return;            // hello.is_not_empty()
-    if (ciphers.null() || ciphers.len() == 0) return;     // ciphersuite_vector.is_not_readable()
-    mfpe::Cur ext{nullptr, nullptr};
+    if (comp.null() || comp.len() <= 0) return false;      // hello.is_not_empty()
+    ciphers_ok = !ciphers.null() && ciphers.len() > 0;     // !ciphersuite_vector.is_not_readable()
     if (p.rd(2, l)) { ext.d = p.d; ext.e = p.d + ((long)l < p.len() ? (long)l : p.len()); }   // parse_soft_fail
-    rec.key("tls");
+    return true;
+}
+
+void client_hello_json(W &w, Obj &rec, mfpe::Cur p) {
+    mfpe::Cur ext;
+    bool ciphers_ok = false, dtls = false;
+    if (!hello_extensions(p, ext, ciphers_ok, dtls) || !ciphers_ok) return;   // tls.h:1883-1885
+    if (dtls) rec.key("dtls"); else rec.key("tls");
     w.puts("{\"client\":{");
     Obj cl{w};
     // get_server_name (tls.h:1052-1080): the first SNI extension, past its 5-byte header
@@ -914,6 +912,54 @@ void quic_tls(W &w, Obj &rec, const uint8_t *hs, uint32_t hs_len) {
         }
     }
     w.puts("}}");
+}
+
+// a QUIC hello's handshake message (tls_handshake::parse tls.h:244-262)
+void quic_tls(W &w, Obj &rec, const uint8_t *hs, uint32_t hs_len) {
+    mfpe::Cur d{hs, hs + hs_len};
+    if (d.len() < 4) return;
+    uint64_t mt, hl;
+    d.rd(1, mt); d.rd(3, hl);
+    if (hl > 32768) return;
+    client_hello_json(w, rec, mfpe::Cur{d.d, hl < (uint64_t)d.len() ? d.d + hl : d.e});
+}
+
+// The handshake body of a TLS_CH / DTLS_CH record, found again from the
+// record's innermost IP header (ip::parse ip.h:619-632): the TCP payload
+// (tcp_packet::parse tcpip.h:154-163) through tls_record / tls_handshake
+// (tls.h:145-262, as set_tcp_protocol builds the hello, pkt_proc.cc:525-534),
+// or the UDP payload (udp.h:89-110) through dtls_record / dtls_handshake
+// (dtls.h:19-96, dtls_client_hello dtls.h:121-127).
+bool client_hello_body(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, mfpe::Cur &body) {
+    const uint32_t ip = r.net & 0xffff;
+    if (ip >= caplen) return false;
+    mfpe::Cur p{pkt + ip, pkt + caplen};
+    uint32_t off = 0;
+    int ipv = 0;
+    mfpe::ip_parse(p, pkt, off, ipv);
+    if (p.null()) return false;
+    uint64_t x, l;
+    if (r.msg == MFP_MSG_TLS_CH) {
+        if (p.len() < 20) return false;
+        const long opt = (long)(p.d[12] >> 4) * 4 - 20;
+        p.d += 20;
+        if (!p.skip(opt)) return false;
+        if (p.len() < 5) return false;
+        p.rd(1, x); p.rd(2, x); p.rd(2, l);
+        mfpe::Cur frag{p.d, p.d + std::min<long>((long)l, p.len())};
+        if (frag.len() < 4) return false;
+        frag.rd(1, x); frag.rd(3, l);
+        if (l > 32768) return false;
+        body = mfpe::Cur{frag.d, frag.d + std::min<long>((long)l, frag.len())};
+        return true;
+    }
+    if (!p.skip(8) || p.len() < 13) return false;
+    p.rd(1, x); p.rd(2, x); p.rd(2, x); p.rd(6, x); p.rd(2, l);
+    mfpe::Cur frag = take(p, (long)l);
+    if (frag.null() || frag.len() < 12) return false;
+    frag.rd(1, x); frag.rd(3, x); frag.rd(2, x); frag.rd(3, x); frag.rd(3, l);
+    body = take(frag, (long)l);
+    return !body.null();
 }
 
 bool write_quic(W &w, Obj &rec, const QuicJson &q) {
@@ -973,6 +1019,7 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint
     o.need(1000 + (size_t)r.fp_len + sni_x * (r.sni_len == 0xffff ? 0 : r.sni_len) +
            6 * (r.ua_len == 0xffff ? 0 : r.ua_len) +
            (r.msg == MFP_MSG_QUIC ? 2 * (size_t)(qj.pay_len + qj.pt_len) + 6 * (size_t)qj.hs_len + 600 : 0) +
+           (r.msg == MFP_MSG_TLS_CH || r.msg == MFP_MSG_DTLS_CH ? 8 * (size_t)caplen : 0) +
            (with_an ? analysis_bound(ctx, *an) : 0));
     W w{o.buf.get() + o.len};
     // a readable, non-empty datum (print_key_json_string skips empty ones, json_object.h:104-108)
@@ -987,13 +1034,13 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint
     }
     switch (r.msg) {
     case MFP_MSG_TLS_CH:
-    case MFP_MSG_DTLS_CH:
-        if (r.flags & MFP_FLAG_NO_CIPHERS) break;      // tls_client_hello::write_json tls.h:1882-1885
-        if (r.msg == MFP_MSG_TLS_CH) rec.key("tls"); else rec.key("dtls");
-        w.puts("{\"client\":{");
-        if (span_ok(r.sni_off, r.sni_len)) { w.puts("\"server_name\":\""); w.utf8(pkt + r.sni_off, r.sni_len); w.put('"'); }
-        w.puts("}}");
+    case MFP_MSG_DTLS_CH: {
+        // the hello's own parse (the record's sni span is the classifier's,
+        // the last server_name extension)
+        mfpe::Cur body{nullptr, nullptr};
+        if (!(r.flags & MFP_FLAG_NO_CIPHERS) && client_hello_body(pkt, caplen, r, body)) client_hello_json(w, rec, body);
         break;
+    }
     case MFP_MSG_TLS_SH:
     case MFP_MSG_TLS_CERT:
         if (span_ok(r.sni_off, r.sni_len)) {
@@ -1085,6 +1132,30 @@ bool write_record(Out &o, TsCache &tc, const uint8_t *pkt, uint32_t caplen, uint
 }
 
 }  // namespace
+
+// The ALPN protocol_name_list of a (D)TLS ClientHello record, re-read from the
+// packet (tls_extensions::set_meta_data tls.h:1357-1362: the last ALPN
+// extension; a list shorter than its length field is none) -- for records
+// whose ua span holds a draft user agent instead (MFP_XF_TLS_UA).
+bool mfp_hello_alpn(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const uint8_t **alpn, uint32_t *len) {
+    *alpn = nullptr; *len = 0;
+    mfpe::Cur body{nullptr, nullptr}, ext;
+    bool ciphers_ok = false, dtls = false;
+    if (!client_hello_body(pkt, caplen, r, body) || !hello_extensions(body, ext, ciphers_ok, dtls)) return false;
+    bool found = false;
+    for (mfpe::Cur e = ext; e.len() > 0;) {
+        const uint8_t *st = e.d;
+        uint64_t t, el;
+        if (!e.rd(2, t) || !e.rd(2, el) || !e.skip((long)el)) break;
+        if (t != 16) continue;
+        mfpe::Cur a{st + 4, e.d};
+        uint64_t al = 0;
+        found = a.rd(2, al) && (uint64_t)a.len() >= al;
+        if (found) { *alpn = a.d; *len = (uint32_t)al; }
+        else { *alpn = nullptr; *len = 0; }
+    }
+    return found;
+}
 
 static long long write_json_batch(mfp_context ctx, const uint16_t *props, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    size_t n,

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
         r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
         r.msg = (uint8_t)o.msg;
         r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
-        r.status = 0;
+        r.xflags = (uint8_t)o.xflags;
         r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
         r.sni_len = (uint16_t)o.sni_len;
         r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
             r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
             r.msg = (uint8_t)o.msg;
             r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
-            r.status = 0;
+            r.xflags = (uint8_t)o.xflags;
             r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
             r.sni_len = (uint16_t)o.sni_len;
             r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
             r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
             r.msg = (uint8_t)o.msg;
             r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
-            r.status = 0;
+            r.xflags = (uint8_t)o.xflags;
             r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
             r.sni_len = (uint16_t)o.sni_len;
             r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
                 r.fp_type = (uint8_t)(fits ? o.fp_type : 0);
                 r.msg = (uint8_t)o.msg;
                 r.flags = (uint8_t)(o.flags | (fits && len ? MFP_FLAG_HASHED : 0));
-                r.status = 0;
+                r.xflags = (uint8_t)o.xflags;
                 r.sni_off = (uint16_t)(o.sni_len == 0xffff ? 0 : o.sni_off);
                 r.sni_len = (uint16_t)o.sni_len;
                 r.ua_off = (uint16_t)(o.ua_len == 0xffff ? 0 : o.ua_off);

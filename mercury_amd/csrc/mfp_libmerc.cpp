@@ -124,12 +124,25 @@ MFP_EXPORT void register_printf_err_callback(printf_err_ptr callback) {
 MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int verbosity) {
     (void)verbosity;
     if (!vars) return nullptr;
-    if (vars->do_stats) {
-        // the stats aggregator (stats.h, --stats) is outside this path: refuse at
-        // init, as the reference refuses a configuration it cannot honour
-        log_error("do_stats: fingerprint/destination statistics are not provided by libmercury_amd\n");
-        return nullptr;
-    }
+    // libmerc_config fields that change the records (pkt_proc.cc:1157-1253,
+    // write_metadata pkt_proc_util.h:264-333, analysis.h:836): refused at init
+    // with the reason, as unsupported configurations are refused, rather than
+    // silently giving records that differ from the reference's.  dns_json_output
+    // changes DNS records only, which this path does not write: accepted.
+    const struct { bool on; const char *what; } refused[] = {
+        {vars->do_stats, "do_stats: fingerprint/destination statistics (stats.h)"},
+        {vars->metadata_output, "metadata_output: the metadata JSON fields (write_metadata pkt_proc_util.h:264)"},
+        {vars->certs_json_output, "certs_json_output: certificates as parsed JSON (tls.h, x509.h)"},
+        {vars->output_tcp_initial_data, "output_tcp_initial_data: tcp.data records for unselected TCP payloads"},
+        {vars->output_udp_initial_data, "output_udp_initial_data: udp.data records for unselected UDP payloads"},
+        {vars->fp_proc_threshold > 0.0f || vars->proc_dst_threshold > 0.0f,
+         "fp_proc_threshold / proc_dst_threshold: the thresholded database (analysis.h:836)"},
+    };
+    for (const auto &r : refused)
+        if (r.on) {
+            log_error("%s is not provided by libmercury_amd\n", r.what);
+            return nullptr;
+        }
     auto *m = new mercury;
     // the archive key: 16 bytes whatever key_type says (analysis.h:1211,
     // "TODO: key type"; cryptovar<16>)
@@ -143,17 +156,19 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
         cfg += std::string(";resources=") + vars->resources + ";analysis";
         m->analysis = true;
     }
-    m->report_os = vars->report_os;
     m->cfg = cfg;
     // validate now, so a bad configuration fails at init as in the reference
     uint32_t sel, fmt;
-    const int prc = mfp_parse_filter(cfg.c_str(), &sel, &fmt);
-    if (prc < 0) {
+    int ros = -1;
+    std::string warn;
+    if (!mfp_parse_config(cfg.c_str(), sel, fmt, nullptr, nullptr, nullptr, nullptr, &warn, &ros)) {
         log_error("%s\n", mfp_last_error());
         delete m;
         return nullptr;
     }
-    if (prc > 0) log_error("%s\n", mfp_last_error());   // printf_err(log_err, ...) as set_protocols does, and go on
+    if (!warn.empty()) log_error("%s\n", warn.c_str());   // printf_err(log_err, ...) as set_protocols does, and go on
+    // the config string's report_os setter overrides the field (config_generator.cc:35)
+    m->report_os = ros < 0 ? vars->report_os : ros == 1;
     return m;
 }
 
@@ -213,8 +228,8 @@ static void copy_cstr(char *dst, size_t cap, const uint8_t *src, size_t len) {  
 
 // the processor's analysis_context from one classified packet (the state the
 // reference's accessors read after write_json or get_analysis_context)
-static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *pkt, const mfp_record &rec,
-                         const char *fp, const mfp_analysis *an, const double *ap) {
+static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *pkt, uint32_t caplen,
+                         const mfp_record &rec, const char *fp, const mfp_analysis *an, const double *ap) {
     ac.fp_type = rec.fp_type;
     copy_cstr(ac.fp, sizeof ac.fp, (const uint8_t *)fp + rec.fp_offset, rec.fp_type ? rec.fp_len : 0);
     // the sni slot holds the certificate_list (TLS server), the STUN message or
@@ -242,13 +257,25 @@ static void fill_context(mfp_context ctx, analysis_context &ac, const uint8_t *p
         const uint32_t n = rec.ua_len == 0xffff ? 0 : mfpc::utf8_safe_512(pkt + rec.ua_off, rec.ua_len, ac.ua);
         ac.ua[n] = 0;
     } else {
-        copy_cstr(ac.ua, sizeof ac.ua, sb + rec.ua_off, rec.ua_len == 0xffff || hello ? 0 : rec.ua_len);
+        // a (D)TLS hello's ua span is its ALPN list, unless it holds the user
+        // agent of a draft transport-parameter extension (MFP_XF_TLS_UA)
+        const bool alpn_span = hello && !(rec.xflags & MFP_XF_TLS_UA);
+        copy_cstr(ac.ua, sizeof ac.ua, sb + rec.ua_off, rec.ua_len == 0xffff || alpn_span ? 0 : rec.ua_len);
     }
     ac.alpn_len = 0;
     ac.alpn[0] = 0;
-    if (hello && rec.ua_len != 0xffff) {   // alpn.write_to_buffer(alpn_array, 128) (result.h:352-353)
-        ac.alpn_len = rec.ua_len;
-        memcpy(ac.alpn, pkt + rec.ua_off, std::min<size_t>(rec.ua_len, sizeof ac.alpn));
+    if (hello) {   // alpn.write_to_buffer(alpn_array, 128) (result.h:352-353)
+        const uint8_t *a = nullptr;
+        uint32_t al = 0;
+        if (!(rec.xflags & MFP_XF_TLS_UA)) {
+            if (rec.ua_len != 0xffff) { a = pkt + rec.ua_off; al = rec.ua_len; }
+        } else {
+            mfp_hello_alpn(pkt, caplen, rec, &a, &al);
+        }
+        if (a) {
+            ac.alpn_len = al;
+            memcpy(ac.alpn, a, std::min<size_t>(al, sizeof ac.alpn));
+        }
     }
     ac.status = 0; ac.has_process = false; ac.process.clear(); ac.score = 0; ac.malware = false;
     ac.classify_malware = false; ac.malware_prob = -1; ac.os.clear(); ac.attr = 0; ac.n_tags = 0;
@@ -430,7 +457,7 @@ static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req 
     }
     for (size_t i = 0; i < n; i++) {
         Req &r = *batch[i];
-        fill_context(ctx, *r.ac, C.arena.data() + C.desc[i].offset, C.rec[i], C.fp.data(),
+        fill_context(ctx, *r.ac, C.arena.data() + C.desc[i].offset, C.desc[i].caplen, C.rec[i], C.fp.data(),
                      want_an ? &C.an[i] : nullptr, want_an ? &C.ap[i * MFP_ATTR_DB_TAGS] : nullptr);
         note_other(m, C.rec[i]);
         r.valid = want_an && (C.an[i].flags & MFP_AN_VALID);
@@ -499,11 +526,29 @@ static void submit(mercury *m, mfp_context ctx, int mode, Req &r) {
             std::vector<Req *> batch;
             batch.swap(C->q);
             lk.unlock();
-            run_batch(m, ctx, *C, batch, mode == MFP_MODE_WRITE_JSON);
-            lk.lock();
-            for (Req *x : batch) x->done = true;
-            C->busy = false;
-            C->cv.notify_all();
+            // the leader hands the batch back on every exit path: an exception
+            // out of run_batch (an allocation of the staging vectors) fails the
+            // batch's calls instead of leaving busy set and the waiters asleep,
+            // and never crosses the extern "C" boundary (libmerc.cc:145-149
+            // turns exceptions into 0 / NULL the same way)
+            struct Release {
+                Combiner *C; std::unique_lock<std::mutex> &lk; std::vector<Req *> &batch;
+                ~Release() {
+                    lk.lock();
+                    for (Req *x : batch) x->done = true;
+                    C->busy = false;
+                    C->cv.notify_all();
+                }
+            } release{C, lk, batch};
+            try {
+                run_batch(m, ctx, *C, batch, mode == MFP_MODE_WRITE_JSON);
+            } catch (const std::exception &e) {
+                log_error("per-packet batch failed: %s\n", e.what());
+                for (Req *x : batch) x->err = true;
+            } catch (...) {
+                log_error("per-packet batch failed\n");
+                for (Req *x : batch) x->err = true;
+            }
         } else {
             C->cv.wait(lk);
         }
@@ -555,7 +600,7 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
         size_t flen = 0;
         const uint8_t *fr = mfp_reassembler_frames(p->reasm, &flen);
         if (d2.offset >= len + 16 && fr) p->arena.insert(p->arena.end(), fr, fr + flen);
-        fill_context(ctx, p->ac, p->arena.data() + d2.offset, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+        fill_context(ctx, p->ac, p->arena.data() + d2.offset, d2.caplen, rec, p->fp.data(), want_an ? &an : nullptr, ap);
         note_other(p->mc, rec);
         n = want_an ? mfp_write_json_batch_reassembly_analysis(ctx, p->arena.data(), &d2, 1, &rec, p->fp.data(), &props,
                                                                &an, ap, &t, (char *)buffer, buffer_size, &end, &skipped, 1)
@@ -565,7 +610,7 @@ MFP_EXPORT size_t mercury_packet_processor_write_json_linktype(mercury_packet_pr
         long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec, p->fp.data(),
                                                    cap, want_an ? &an : nullptr, want_an ? ap : nullptr);
         if (used < 0) { log_error("%s\n", mfp_last_error()); return 0; }
-        fill_context(ctx, p->ac, pkt, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+        fill_context(ctx, p->ac, pkt, (uint32_t)len, rec, p->fp.data(), want_an ? &an : nullptr, ap);
         note_other(p->mc, rec);
         n = want_an ? mfp_write_json_batch_analysis(ctx, p->arena.data(), &d, 1, &rec, p->fp.data(), &an, ap, &t,
                                                     (char *)buffer, buffer_size, &end, &skipped, 1)
@@ -611,6 +656,7 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
     p->fp.resize(cap);
     bool want_an = mfp_analysis_enabled(ctx);
     const uint8_t *base = pkt;
+    uint32_t base_len = (uint32_t)len;
     if (mfp_reassembly_enabled(ctx)) {
         // analyze_ip_packet with the processor's reassembler (pkt_proc.cc:1597-1662):
         // the flow table in stream order, flow_state_pkts_needed per packet
@@ -630,6 +676,7 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
         const uint8_t *fr = mfp_reassembler_frames(p->reasm, &flen);
         if (d2.offset >= len + 16 && fr) p->arena.insert(p->arena.end(), fr, fr + flen);
         base = p->arena.data() + d2.offset;
+        base_len = d2.caplen;
     } else {
         const long long used = mfp_process_batch_host_ex(ctx, p->arena.data(), p->arena.size(), &d, 1, &rec,
                                                          p->fp.data(), cap, want_an ? &an : nullptr,
@@ -637,7 +684,7 @@ static const analysis_context *analyze(mercury_packet_processor p, uint8_t *pkt,
         if (used < 0) { log_error("%s\n", mfp_last_error()); return nullptr; }
     }
     analysis_context &ac = p->ac;
-    fill_context(ctx, ac, base, rec, p->fp.data(), want_an ? &an : nullptr, ap);
+    fill_context(ctx, ac, base, base_len, rec, p->fp.data(), want_an ? &an : nullptr, ap);
     note_other(p->mc, rec);
     if (!want_an) return nullptr;   // no classifier: analysis result never valid
     return (an.flags & MFP_AN_VALID) ? &ac : nullptr;
@@ -665,11 +712,13 @@ MFP_EXPORT enum fingerprint_type analysis_context_get_fingerprint_type(const str
 MFP_EXPORT const char *analysis_context_get_fingerprint_string(const struct analysis_context *ac) {
     return ac ? ac->fp : nullptr;
 }
+// analysis_context::get_server_name / get_user_agent result.h:391-403: NULL
+// when the string is empty
 MFP_EXPORT const char *analysis_context_get_server_name(const struct analysis_context *ac) {
-    return ac ? ac->sn : nullptr;
+    return ac && ac->sn[0] ? ac->sn : nullptr;
 }
 MFP_EXPORT const char *analysis_context_get_user_agent(const struct analysis_context *ac) {
-    return ac ? ac->ua : nullptr;
+    return ac && ac->ua[0] ? ac->ua : nullptr;
 }
 // analysis_result::get_process_info result.h:268-276
 MFP_EXPORT bool analysis_context_get_process_info(const struct analysis_context *ac, const char **probable_process,

@@ -40,15 +40,6 @@ constexpr uint32_t Q_PT = 2048;                  // decrypted payload (pt_buf_le
 constexpr uint32_t Q_CB = 8192;                  // CRYPTO buffer (cryptographic_buffer::crypto_buf_len quic.h:1206)
 constexpr uint32_t Q_SLOT = Q_PT + Q_CB + 64;    // per-lane scratch (the emitter may read an aligned word past the end)
 
-// variable_length_integer (quic_vli.hpp): a failed read yields 0 and a null cursor
-DEV uint64_t vli_rd(Cur &c) {
-    const uint32_t b = rd_u8(c);
-    const int len = vli_len(b);
-    uint64_t v = b & 0x3f;
-    for (int i = 1; i < len; i++) v = v * 256 + rd_u8(c);
-    return v;
-}
-
 // ---- the long header (quic_initial_packet::parse quic.h:421-522)
 struct QHdr {
     uint32_t ci;                                 // connection_info (protected first byte)
@@ -840,7 +831,7 @@ __global__ __launch_bounds__(QT, MFP_QUIC_MINW) void k_quic(KParams P, uint8_t *
             r.msg = (uint8_t)o.msg;
             r.flags = (uint8_t)(q.flags | (o.flags & MFP_FLAG_ENCAP) | (fits && len ? MFP_FLAG_HASHED : 0) |
                                 (fits && side ? MFP_FLAG_SIDECAR : 0));
-            r.status = 0;
+            r.xflags = 0;
             r.sni_off = (uint16_t)(sni_len == 0xffff ? 0 : sni_off);
             r.sni_len = (uint16_t)sni_len;
             r.ua_off = (uint16_t)(ua_len == 0xffff ? 0 : ua_off);

@@ -15,6 +15,8 @@
 //   idx  valid  fp_type  status  process  score  malware  p_malware  more  fp_string
 // Mode "json": the write_json record text, one line per packet (empty line
 // when the reference writes nothing).
+// Mode "meta": analysis_context path, one TSV line per packet:
+//   idx  valid  server_name(hex)  user_agent(hex)   ("-" = NULL)
 // Mode "attr": analysis_context path, the accessors the embedders read, one
 // TSV line per packet:
 //   idx  valid  status  attributes  os_info  alpn
@@ -261,6 +263,27 @@ int main(int argc, char **argv) {
                    (int)analysis_context_get_fingerprint_status(ac),
                    proc ? proc : "", score, (int)mal, pm, mp,
                    analysis_context_get_fingerprint_string(ac));
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "meta") {
+        // analysis_context path: the destination context's strings the
+        // embedders read (libmerc.cc:276-288), hex; "-" when NULL
+        //   idx  valid  server_name  user_agent
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        auto hex = [](const char *s) {
+            if (!s) return std::string("-");
+            std::string h;
+            char t[3];
+            for (const char *c = s; *c; c++) { snprintf(t, sizeof t, "%02x", (unsigned)(uint8_t)*c); h += t; }
+            return h;
+        };
+        for (size_t i = 0; i < pkts.size(); i++) {
+            struct timespec ts{(time_t)tsv[i], 0};
+            const analysis_context *ac = mercury_packet_processor_get_analysis_context_linktype(
+                p, (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
+            if (!ac) { printf("%zu\t0\t-\t-\n", i); continue; }
+            printf("%zu\t1\t%s\t%s\n", i, hex(analysis_context_get_server_name(ac)).c_str(),
+                   hex(analysis_context_get_user_agent(ac)).c_str());
         }
         mercury_packet_processor_destruct(p);
     } else if (mode == "attr") {

@@ -4,6 +4,7 @@ the GPU parity tests (which compare the HIP path with those reference
 outputs).  Every case is regenerated from seeds and the committed
 ref_packets.npz; only the reference's outputs are committed."""
 import os
+import struct
 
 import numpy as np
 
@@ -77,6 +78,76 @@ def corpus_case():
     return out
 
 
+def _qtp(t, params):
+    """a quic_transport_parameters(_draft) extension: (id, value) pairs as
+    variable-length integers (tls.h:1237-1262)"""
+    def vli(v):
+        if v < 64:
+            return bytes([v])
+        if v < 16384:
+            return struct.pack(">H", 0x4000 | v)
+        return struct.pack(">I", 0x80000000 | v)
+    return synth.ext(t, b"".join(vli(i) + vli(len(v)) + v for i, v in params))
+
+
+def _hello_body(exts, version=0x0303, cookie=None, ciphers=b"\x13\x01\x13\x02\xc0\x2b", ext_claim=None):
+    body = struct.pack(">H", version) + bytes(range(32)) + b"\x00"
+    if cookie is not None:
+        body += bytes([len(cookie)]) + cookie
+    e = b"".join(exts)
+    body += struct.pack(">H", len(ciphers)) + ciphers + b"\x01\x00"
+    return body + struct.pack(">H", len(e) if ext_claim is None else ext_claim) + e
+
+
+def hello_meta_case():
+    """Crafted ClientHellos whose JSON text and destination context depend on
+    WHICH extension the reference reads: duplicate, empty and malformed
+    server_name extensions (write_json prints the first, tls.h:1052-1080; the
+    analysis context keeps the last, tls.h:1316-1345), ALPN twice, QUIC
+    transport parameters (and the draft type) over TCP with Google user
+    agents (tls.h:1264-1311), a DTLS version over TCP (tls.h:1823-1844: cookie
+    and "dtls" label), a soft-failed extension list; each over TCP/IPv4,
+    TCP/IPv6 and DTLS (UDP/443)."""
+    sni = synth.sni_ext
+    ext = synth.ext
+    sets = [
+        [sni("first.example"), sni("second.example")],
+        [ext(0, b""), sni("after.example")],
+        [sni("only.example"), ext(0, b"\x00\x01\x00")],
+        [sni("a"), ext(0, struct.pack(">HBH", 3, 0, 0))],
+        [sni("x1.example"), sni("x2.example"), sni("x3.example")],
+        [sni("q.example"), _qtp(0x39, [(1, b"\x00\x10"), (0x3129, b"Chrome/99.0"), (4, b"")])],
+        [_qtp(0xffa5, [(0x3129, b"UA-draft")]), _qtp(0x39, [(0x3129, b"UA-v1"), (0x3129, b"UA-v1b")]),
+         sni("both.example")],
+        [],
+        [synth.alpn_ext(["h2"]), sni("alpn.example"), synth.alpn_ext(["http/1.1"])],
+        [sni("ok.example"), ext(0, bytes(20)), ext(23, b"")],
+        [sni("café.example"), ext(0, struct.pack(">HBH", 7, 0, 4) + b"\xff\xfeAB")],
+        [sni("v.example"), ext(0x39, b"\x71\x29\x05UA"), ext(0x39, b"")],
+        [sni("p.example"), ext(0x0a0a, b""), sni("g.example")],
+    ]
+    out = []
+    for k, exts in enumerate(sets):
+        bodies = [_hello_body(exts)]
+        # the extension list claims more bytes than the packet holds (parse_soft_fail tls.h:1865)
+        bodies.append(_hello_body(exts, ext_claim=len(b"".join(exts)) + 40))
+        for b in bodies:
+            hs = b"\x01" + struct.pack(">I", len(b))[1:] + b
+            rec = struct.pack(">BHH", 0x16, 0x0301, len(hs)) + hs
+            out.append((1, synth.frame(synth.tcp(rec, sport=40000 + k, dport=443), 6)))
+            out.append((1, synth.frame(synth.tcp(rec, sport=41000 + k, dport=443), 6, v6=True)))
+        db = _hello_body(exts, version=0xfefd, cookie=b"\xaa\xbb\xcc\xdd")
+        dhs = b"\x01" + struct.pack(">I", len(db))[1:] + struct.pack(">H", 0) + b"\x00\x00\x00" + \
+            struct.pack(">I", len(db))[1:] + db
+        drec = struct.pack(">BHH", 0x16, 0xfefd, 0) + bytes(6) + struct.pack(">H", len(dhs)) + dhs
+        out.append((1, synth.frame(synth.udp(drec, sport=42000 + k, dport=443), 17)))
+        # a DTLS version in a ClientHello over TCP: the cookie is skipped, the object is "dtls"
+        hs = b"\x01" + struct.pack(">I", len(db))[1:] + db
+        out.append((1, synth.frame(synth.tcp(struct.pack(">BHH", 0x16, 0x0301, len(hs)) + hs, sport=43000 + k,
+                                             dport=443), 6)))
+    return out
+
+
 def batch(pkts):
     return pcaplib.make_batch(pkts)
 
@@ -90,10 +161,10 @@ def tls_ch_unique_head(n=20000):
 
 # name -> (packets builder, [(fmt, mode)])
 CASES = {
-    "fuzz0": (lambda: fuzz_case(0), [(0, "fp")]),
-    "fuzz1": (lambda: fuzz_case(1), [(1, "fp")]),
-    "fuzz2": (lambda: fuzz_case(2), [(2, "fp")]),
-    "edge": (edge_case, [(0, "fp"), (1, "fp"), (2, "fp")]),
+    "fuzz0": (lambda: fuzz_case(0), [(0, "fp"), (0, "json")]),
+    "fuzz1": (lambda: fuzz_case(1), [(1, "fp"), (1, "json")]),
+    "fuzz2": (lambda: fuzz_case(2), [(2, "fp"), (2, "json")]),
+    "edge": (edge_case, [(0, "fp"), (1, "fp"), (2, "fp"), (0, "json"), (1, "json"), (2, "json")]),
     "binmix": (binmix_case, [(0, "fp"), (2, "fp")]),
     "synth_mixed0": (lambda: synth_case("mixed", 0), [(0, "fp")]),
     "synth_mixed1": (lambda: synth_case("mixed", 1), [(1, "fp")]),
@@ -102,13 +173,40 @@ CASES = {
     "synth_tls_ch1": (lambda: synth_case("tls_ch", 1), [(1, "fp")]),
     "synth_tls_ch2": (lambda: synth_case("tls_ch", 2), [(2, "fp")]),
     "analysis_mode": (analysis_mode_case, [(1, "an")]),
-    "corpus": (corpus_case, [(0, "fp"), (1, "fp"), (2, "fp")]),
+    "corpus": (corpus_case, [(0, "fp"), (1, "fp"), (2, "fp"), (0, "json"), (1, "json"), (2, "json")]),
+    "hello_meta": (hello_meta_case, [(0, "fp"), (1, "fp"), (2, "fp"), (0, "json"), (1, "json"), (2, "json"),
+                                     (1, "meta")]),
     "tls_ch_head": (tls_ch_unique_head, [(0, "fp")]),
 }
 
 
+# the "meta" runs read the analysis context, which needs a classifier
+META_RESOURCES = os.path.join(GOLD, "resources-test.tgz")
+
+
 def golden_path(name, fmt, mode):
-    return os.path.join(GOLD, "cases", f"{name}.{mode}{fmt}.tsv.gz")
+    ext = "txt" if mode == "json" else "tsv"
+    return os.path.join(GOLD, "cases", f"{name}.{mode}{fmt}.{ext}.gz")
+
+
+def load_json_golden(name, fmt):
+    """The reference's write_json text per packet (b"" when it writes none)."""
+    import gzip
+    with gzip.open(golden_path(name, fmt, "json"), "rb") as f:
+        return f.read().split(b"\n")[:-1]
+
+
+def load_meta_golden(name, fmt=1):
+    """(valid, server_name, user_agent) per packet from the analysis context
+    accessors; None for a NULL string."""
+    import gzip
+    rows = []
+    with gzip.open(golden_path(name, fmt, "meta"), "rt") as f:
+        for line in f:
+            p = line.rstrip("\n").split("\t")
+            rows.append((int(p[1]), None if p[2] == "-" else bytes.fromhex(p[2]),
+                         None if p[3] == "-" else bytes.fromhex(p[3])))
+    return rows
 
 
 def load_golden(name, fmt, mode):

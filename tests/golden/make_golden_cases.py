@@ -33,8 +33,9 @@ def main():
         tmp = f"/tmp/golden_case_{name}.mfpb"
         pcaplib.write_mfpb(tmp, a, d)
         for fmt, mode in runs:
-            out = subprocess.run([REF, mode, tmp, ref_config(fmt), "-"], capture_output=True, check=True).stdout
-            with gzip.open(cases.golden_path(name, fmt, mode), "wb") as g:
+            res = cases.META_RESOURCES if mode == "meta" else "-"
+            out = subprocess.run([REF, mode, tmp, ref_config(fmt), res], capture_output=True, check=True).stdout
+            with gzip.GzipFile(cases.golden_path(name, fmt, mode), "wb", mtime=0) as g:
                 g.write(out)
         os.unlink(tmp)
         man["cases"][name] = {"packets": len(pk), "runs": [f"{m}{f}" for f, m in runs],

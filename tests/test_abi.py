@@ -94,7 +94,7 @@ SEL_EVERY = (1 << 16) - 1
     ("all;format=tls/1;reassembly", SEL_EVERY, BLK_ALL), ("select=;format=tls/1", SEL_EVERY, BLK_ALL),
     ("tls,dns", oracle.SEL["tls"], (1 << 1) | (1 << 2)), ("quic,mdns", 1 << 10, 1 << 2),
     ("tls,arp,icmp,tofsee", oracle.SEL["tls"], 0), ("http,rdp,telnet", oracle.SEL["http"], (1 << 13) | (1 << 19)),
-    ("all,none", 0, 0), ("tls;metadata;none", 0, 0), ("format=tls/1", 0, 0),
+    ("all,none", 0, 0), ("tls;metadata=0;none", 0, 0), ("format=tls/1", 0, 0),
 ])
 def test_parse_filter_other_protocols(cfg, sel, other):
     assert mercury_amd.api.parse_filter_ex(cfg)[:2] == (sel, other)

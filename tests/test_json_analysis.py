@@ -57,10 +57,14 @@ def _check(lines, gold, skipped):
     assert skipped == 0
 
 
-def _json_device(arena, desc, resources, threads=1):
-    ctx = mercury_amd.Context(f"select={CONTRACT};resources={resources};analysis", device=0)
+def _json_device(arena, desc, resources, threads=1, report_os_in_cfg=False):
+    """report_os through mfp_analysis_report_os, or through the config
+    string's report_os option (config_generator.cc:35)"""
+    extra = ";report_os" if report_os_in_cfg else ""
+    ctx = mercury_amd.Context(f"select={CONTRACT};resources={resources};analysis{extra}", device=0)
     assert ctx.analysis_enabled
-    ctx.report_os(True)
+    if not report_os_in_cfg:
+        ctx.report_os(True)
     rec, fp, an, ap = ctx.process_host_analysis(arena, desc, attr_prob=True)
     lines, skipped = mercury_amd.write_json(arena, desc, rec, fp, ts_ns=np.full(len(desc), TS, np.uint64),
                                             threads=threads, ctx=ctx, analysis=an, attr_prob=ap)
@@ -70,7 +74,7 @@ def _json_device(arena, desc, resources, threads=1):
 @pytest.mark.gpu
 def test_json_analysis_crafted_device():
     arena, desc, gold, _ = _crafted()
-    ctx, lines, skipped, an = _json_device(arena, desc, SYNTH_RES)
+    ctx, lines, skipped, an = _json_device(arena, desc, SYNTH_RES, report_os_in_cfg=True)
     _check(lines, gold, skipped)
     # every attribute branch is exercised by the crafted set
     names = {ctx.attribute_name(b) for a in an for b in range(16) if (int(a["attr"]) >> b) & 1}

@@ -268,6 +268,71 @@ def test_lru_stream_device_pipelined_vs_reference():
 
 
 @pytest.mark.gpu
+def test_lru_stream_pipelined_mixed_with_sync_calls():
+    """Synchronous analysis calls (host batches, a synchronous device batch)
+    interleaved with pipelined device batches: each synchronous call first
+    decides the pipelined batches still pending, so the LRU sees the stream in
+    order and the statuses of all of them equal the reference's."""
+    import torch
+    a, d = synth.lru_batch(synth.lru_keys())
+    want = golden_status()
+    ctx = mercury_amd.Context(f"select=tls;resources={REF_ARCHIVE};analysis", device=0)
+    d_arena = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    chunk = 20000
+    cap = 48 * 1024 * 1024
+    stream = torch.cuda.current_stream()
+    got = np.full(len(d), 255, np.uint8)
+    pending = []                                         # (lo, m, buffers) of pipelined batches
+    for k, lo in enumerate(range(0, len(d), chunk)):
+        dd = np.ascontiguousarray(d[lo:lo + chunk])
+        m = len(dd)
+        if k % 3 == 2:                                   # a synchronous host batch
+            _, _, an = ctx.process_host_analysis(a, dd)
+            got[lo:lo + m] = _statuses(an)
+        elif k % 6 == 4:                                 # a synchronous device batch
+            b = dict(desc=torch.from_numpy(dd.view(np.uint8)).cuda(),
+                     rec=torch.empty(m * 32, dtype=torch.uint8, device="cuda"),
+                     fp=torch.empty(cap, dtype=torch.uint8, device="cuda"),
+                     used=torch.zeros(4, dtype=torch.int64, device="cuda"),
+                     an=torch.empty(m * mercury_amd.ANALYSIS_DTYPE.itemsize, dtype=torch.uint8, device="cuda"))
+            ctx.process_device(d_arena.data_ptr(), b["desc"].data_ptr(), m, b["rec"].data_ptr(), b["fp"].data_ptr(),
+                               cap, b["used"].data_ptr(), stream.cuda_stream)
+            ctx.analyze_device(d_arena.data_ptr(), b["desc"].data_ptr(), m, b["rec"].data_ptr(), b["fp"].data_ptr(),
+                               b["an"].data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            got[lo:lo + m] = _statuses(b["an"].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE))
+        else:                                            # pipelined (own buffers per batch: read at the end)
+            b = dict(desc=torch.from_numpy(dd.view(np.uint8)).cuda(),
+                     rec=torch.empty(m * 32, dtype=torch.uint8, device="cuda"),
+                     fp=torch.empty(cap, dtype=torch.uint8, device="cuda"),
+                     used=torch.zeros(4, dtype=torch.int64, device="cuda"),
+                     an=torch.empty(m * mercury_amd.ANALYSIS_DTYPE.itemsize, dtype=torch.uint8, device="cuda"))
+            ctx.process_device(d_arena.data_ptr(), b["desc"].data_ptr(), m, b["rec"].data_ptr(), b["fp"].data_ptr(),
+                               cap, b["used"].data_ptr(), stream.cuda_stream)
+            ctx.analyze_device_pipelined(d_arena.data_ptr(), b["desc"].data_ptr(), m, b["rec"].data_ptr(),
+                                         b["fp"].data_ptr(), b["an"].data_ptr(), stream.cuda_stream)
+            pending.append((lo, m, b))
+    ctx.analysis_flush()
+    torch.cuda.synchronize()
+    for lo, m, b in pending:
+        got[lo:lo + m] = _statuses(b["an"].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE))
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} statuses differ, first at {bad[:5]}"
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_device_pipelined_refuses_deferred_context():
+    import torch
+    ctx = mercury_amd.Context(f"select=tls;resources={REF_ARCHIVE};analysis", device=0)
+    ctx.defer(True)
+    z = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(mercury_amd.api.MercuryAmdError, match="defers"):
+        ctx.analyze_device_pipelined(z.data_ptr(), z.data_ptr(), 0, z.data_ptr(), z.data_ptr(), z.data_ptr(), 0)
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_lru_stream_two_shards_shared_prevalence():
     """Two contexts on cuda:0 as two shards of one stream: each analyses its
     half (deferred), then the shards are decided in shard order against one
