@@ -409,6 +409,11 @@ struct Slot {
     // this slot's stream)
     hipEvent_t ev_kernels = nullptr, ev_resolved = nullptr;
     bool resolved_recorded = false;
+    // the last device-pointer call that used this slot's scratch on the
+    // caller's stream (mfp_process_batch_device, mfp_analyze_batch_device*):
+    // a host batch staged on the slot's own stream waits for it
+    hipEvent_t ev_dev = nullptr;
+    bool dev_recorded = false;
 
     bool init() {
         return hipMalloc(&d_used, 4 * sizeof(unsigned long long)) == hipSuccess &&
@@ -418,7 +423,8 @@ struct Slot {
                hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
                hipEventCreateWithFlags(&ev_kernels, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_resolved, hipEventDisableTiming) == hipSuccess;
+               hipEventCreateWithFlags(&ev_resolved, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_dev, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
@@ -427,7 +433,7 @@ struct Slot {
         for (void *x : p) if (x) (void)hipFree(x);
         for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec}) if (x) (void)hipHostFree(x);
         if (stream) (void)hipStreamDestroy(stream);
-        for (hipEvent_t e : {ev_kernels, ev_resolved}) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {ev_kernels, ev_resolved, ev_dev}) if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -785,6 +791,9 @@ static int flush_pipelined_locked(mfp_context c) {
         if (r) return r;
         HIPCHK(hipEventRecord(S.ev_resolved, S.stream));
         S.resolved_recorded = true;
+        // the decision's kernels finish before the caller's next work reuses
+        // the slot's tables (on whichever stream) or reads the records
+        HIPCHK(hipStreamSynchronize(S.stream));
     }
     c->pipe_active = false;
     return 0;
@@ -795,8 +804,13 @@ extern "C" MFP_EXPORT int mfp_process_batch_device(mfp_context c, const uint8_t 
                                                    uint64_t *d_fp_used, void *stream) {
     if (!c) { mfp_set_error("null context"); return -1; }
     std::lock_guard<std::mutex> lk(c->mu);
-    return process_device_locked(c, c->slot[0], d_arena, d_desc, n, d_rec, d_fp_arena, fp_cap, d_fp_used,
-                                 (hipStream_t)stream);
+    Slot &S = c->slot[0];
+    const int r = process_device_locked(c, S, d_arena, d_desc, n, d_rec, d_fp_arena, fp_cap, d_fp_used,
+                                        (hipStream_t)stream);
+    if (r) return r;
+    HIPCHK(hipEventRecord(S.ev_dev, (hipStream_t)stream));
+    S.dev_recorded = true;
+    return 0;
 }
 
 // decide the slot's pending batch against c->prev and patch the host copies
@@ -848,6 +862,8 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
 static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                             size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false) {
     Slot &S = c->slot[slot];
+    // device-pointer calls may still be using this slot's scratch on the caller's stream
+    if (S.dev_recorded) { HIPCHK(hipStreamWaitEvent(S.stream, S.ev_dev, 0)); S.dev_recorded = false; }
     uint64_t lo = UINT64_MAX, hi = 0, total = 0;
     for (size_t i = 0; i < n; i++) {
         uint64_t end = desc[i].offset + desc[i].caplen;
@@ -1085,7 +1101,10 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device(mfp_context c, const uint8_t 
     std::lock_guard<std::mutex> lk(c->mu);
     if (const int fr = flush_pipelined_locked(c)) return fr;
     const int r = analyze_locked(c, 0, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, (hipStream_t)stream);
-    if (r || c->defer) return r;
+    if (r) return r;
+    HIPCHK(hipEventRecord(c->slot[0].ev_dev, (hipStream_t)stream));
+    c->slot[0].dev_recorded = true;
+    if (c->defer) return 0;
     // the batch's unknown-TLS sightings are decided now, in stream order: the
     // call waits for its kernels (a few microseconds of host time per batch)
     return slot_resolve(c, c->slot[0]);
@@ -1121,6 +1140,8 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context c, cons
     int r = analyze_locked(c, slot, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, us);
     if (r) return r;
     HIPCHK(hipEventRecord(S.ev_kernels, us));
+    HIPCHK(hipEventRecord(S.ev_dev, us));
+    S.dev_recorded = true;
     HIPCHK(hipStreamWaitEvent(S.stream, S.ev_kernels, 0));
     S.pend.stream = S.stream;
     c->pipe_next ^= 1;
