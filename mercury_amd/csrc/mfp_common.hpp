@@ -30,7 +30,11 @@ MFP_HD uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
     return x;
 }
+#ifdef MFP_PROBE_CHEAPHASH   // (profiling probe only: what the per-word mixing costs; breaks the classifier's keys)
+MFP_HD uint64_t word_term(uint64_t w, uint32_t j) { return w + j; }
+#else
 MFP_HD uint64_t word_term(uint64_t w, uint32_t j) { return mix64(w + (uint64_t)(j + 1) * 0x9e3779b97f4a7c15ULL); }
+#endif
 MFP_HD uint64_t hash_final(uint64_t acc, uint32_t len) { return mix64(acc ^ ((uint64_t)len * 0x2545f4914f6cdd1dULL)); }
 MFP_HD uint64_t load_word(const uint8_t *s, uint32_t len, uint32_t j) {
     uint64_t w = 0;

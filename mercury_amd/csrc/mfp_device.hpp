@@ -650,7 +650,12 @@ DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
     // the first is used (LeBlock), then 8 characters per push
     for (uint32_t i0 = 0; i0 < len; i0 += 32) {
         typename std::conditional<E::WIDE_LOADS, LeBlock16, LeBlock>::type blk;
+#ifdef MFP_PROBE_HEXRUN_NOLOAD   // (profiling probe only: the value loads' cost)
+#pragma unroll
+        for (int k = 0; k < 8; k++) blk.v[k] = (uint32_t)(uintptr_t)p + i0 + k;
+#else
         blk.load(p + i0, (long)(len - i0));
+#endif
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const uint32_t i = i0 + 4 * (uint32_t)k;
@@ -1233,6 +1238,8 @@ struct TlsPlan {
     // kept extensions by wire index, and the emission order as wire indices
     uint16_t *off_row = nullptr;
     uint8_t *ord_row = nullptr;
+    uint8_t *win = nullptr;    // (k_fp_tls1) the extension-header window in LDS (ExtWin::wv)
+    uint32_t win_lane = 0;
 };
 
 // pass 1 of a TLS/DTLS ClientHello: fingerprint length (through the counting
@@ -1393,6 +1400,75 @@ DEV uint32_t ext_key32(const Ext &x, int fmt, int bucket, uint32_t idx, bool &fi
 }
 DEV bool key32_grease(uint32_t k, int fmt) { return fmt == 1 ? (k >> 16) == 0x0a0a : !(k & (1u << 23)); }
 
+// The extension headers of a ClientHello through a per-lane 64-byte LDS
+// window filled by four independent 16-byte loads (k_fp_tls1): a run of short
+// extensions costs one memory round trip instead of one per header (each
+// header's address depends on the previous length, tls.h:1383).  Only the
+// blocks that hold bytes before `end` are loaded (the 16-byte block holding a
+// packet's last byte is readable, include/mfp.h); bytes past `end` in the
+// window are never used.
+#ifndef MFP_EXT_WIN
+#define MFP_EXT_WIN 2
+#endif
+// MFP_EXT_WIN 2: the blocks go straight to LDS (global_load_lds_dwordx4, no
+// VGPRs); the wave's window area is 4 x 1 KiB, block k of lane l at
+// wv + 1024 k + 16 l (the instruction writes lane l's 16 bytes at the
+// wave-uniform base + 16 l).  MFP_EXT_WIN 1: through VGPRs into a per-lane
+// 64-byte row.
+struct ExtWin {
+    uint8_t *wv;                 // the wave's window area in LDS (4 KiB; MFP_EXT_WIN 1: the lane's 64-byte row)
+    uint32_t lane;
+    const uint8_t *base;         // the window's first byte (16-byte aligned); nullptr: empty
+    DEV const uint32_t *dw(uint32_t k) const {
+        return MFP_EXT_WIN == 2 ? (const uint32_t *)(wv + 1024 * (k >> 2) + 16 * lane + 4 * (k & 3))
+                                : (const uint32_t *)wv + k;
+    }
+};
+// the 4 bytes at a, big-endian (a < end; bytes at or past end are garbage)
+DEV uint32_t win_be32(ExtWin &wn, const uint8_t *a, const uint8_t *end) {
+    uint64_t o = (uint64_t)(a - wn.base);
+    if (wn.base == nullptr || a < wn.base || o > 56) {
+        const uint8_t *b = (const uint8_t *)((uintptr_t)a & ~(uintptr_t)15);
+        const uint4 *s = (const uint4 *)b;
+        if (MFP_EXT_WIN == 2) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (k == 0 || b + 16 * k < end)
+                    __builtin_amdgcn_global_load_lds((const void *)(s + k),
+                                                     (void __attribute__((address_space(3))) *)(wn.wv + 1024 * k),
+                                                     16, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            const uint4 v0 = s[0];
+            const uint4 v1 = b + 16 < end ? s[1] : z;
+            const uint4 v2 = b + 32 < end ? s[2] : z;
+            const uint4 v3 = b + 48 < end ? s[3] : z;
+            uint4 *w4 = (uint4 *)wn.wv;
+            w4[0] = v0; w4[1] = v1; w4[2] = v2; w4[3] = v3;
+        }
+        wn.base = b;
+        o = (uint64_t)(a - b);
+    }
+    const uint32_t k = (uint32_t)o >> 2, sh = (uint32_t)o & 3;
+    const uint32_t lo = *wn.dw(k), hi = *wn.dw(k + 1);
+    return __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, sh));
+}
+// ext_parse (tls_extension ctor tls.h:1383) with the header from the window
+DEV Ext ext_parse_win(Cur &p, ExtWin &wn) {
+    if (!MFP_EXT_WIN || !wn.wv || !p.d || p.e - p.d < 4) return ext_parse(p);
+    Ext x;
+    const uint32_t th = win_be32(wn, p.d, p.e);
+    x.type = th >> 16; x.length = th & 0xffff;
+    x.type_ptr = p.d; x.length_ptr = p.d + 2;
+    x.encoded_type = ((x.type & 0x0f0f) == 0x0a0a) ? 0x0a0a : x.type;
+    p.d += 4;
+    x.ok = (long)x.length <= p.e - p.d;
+    if (x.ok) { x.value.d = p.d; x.value.e = p.d + x.length; p.d += x.length; }
+    else cset_null(x.value);
+    return x;
+}
+
 template <int FMT, class E>
 DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const uint8_t *base,
                           uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len) {
@@ -1406,16 +1482,25 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     uint32_t cnt = 0;
     bool rare = false;
     Cur p = ch.extensions;
+    ExtWin wn{pl.win, pl.win_lane, nullptr};
     while (clen(p) > 0) {
         const uint8_t *start = p.d;
-        Ext x = ext_parse(p);
+        Ext x = ext_parse_win(p, wn);
         if (!x.ok) break;
         if (x.type == 0) {                       // server_name: bytes after the 9-byte header (tls.h:1342)
             Cur e = cmk(start, p.d);
             cskip(e, 9);
             sni_off = (uint32_t)(e.d - base); sni_len = (uint32_t)clen(e);
         }
-        if (x.type == 16) tls_alpn(start, p.d, base, alpn_off, alpn_len);
+        if (x.type == 16) {                      // tls_alpn: protocol_name_list tls.h:1172-1176
+            if (MFP_EXT_WIN && wn.wv) {
+                const uint32_t l = x.length >= 2 ? win_be32(wn, start + 4, p.e) >> 16 : 0u;
+                if (x.length >= 2 && x.length - 2 >= l) { alpn_off = (uint32_t)(start + 6 - base); alpn_len = l; }
+                else { alpn_off = 0; alpn_len = 0xffff; }
+            } else {
+                tls_alpn(start, p.d, base, alpn_off, alpn_len);
+            }
+        }
         // a draft transport-parameter extension may carry the user agent
         // (tls_draft_ua): the fallback lane writes such a hello's record
         if (x.type == 0xffa5) rare = true;
@@ -1435,6 +1520,10 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
             bool fits;
             const uint32_t v = ext_key32(x, FMT, bucket, cnt, fits);
             rare |= !fits;
+#ifdef MFP_PROBE_NOSORT   // (profiling probe only: the insertion's cost; wrong order for formats 1/2)
+#pragma unroll
+            for (int k = 0; k < FAST_EXT; k++) if ((uint32_t)k == cnt) V[k] = v;
+#else
             uint32_t prev = 0;
 #pragma unroll
             for (int k = 0; k < FAST_EXT; k++) {  // insert v into the sorted list
@@ -1443,6 +1532,7 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
                 V[k] = hi < old ? hi : old;
                 prev = old;
             }
+#endif
         }
         n += ext_fp_len(x.type, (uint32_t)clen(x.value));
         cnt++;
@@ -2295,6 +2385,9 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         o.flags |= MFP_FLAG_EMIT; o.fp_type = 1;
         if (clen(ch.ciphers) <= 0) o.flags |= MFP_FLAG_NO_CIPHERS;   // no "tls" object (tls.h:1882-1885)
         if constexpr (E::PLAN) {
+#ifdef MFP_PROBE_NOPLAN   // (profiling probe only: the walk up to the ClientHello; everything punted)
+            if constexpr (E::FAST >= 0) { o.fp_type = 0; return; }
+#endif
             if constexpr (E::FAST >= 0)
                 tls_ch_plan_fast<E::FAST>(b, *b.plan, ch, 1, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len);
             else

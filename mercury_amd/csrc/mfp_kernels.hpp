@@ -195,7 +195,7 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
 template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
-    __shared__ uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
+    __shared__ __attribute__((aligned(16))) uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
     __shared__ uint16_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
     __shared__ uint8_t ext_ord[FMT ? TILE : 1][FAST_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
@@ -249,6 +249,9 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         plan.ok = false;
         plan.off_row = ext_off[tid];
         plan.ord_row = ext_ord[FMT ? tid : 0];
+        // free until the emission: the extension-header window (ExtWin)
+        plan.win = MFP_EXT_WIN == 2 ? (uint8_t *)&out_line[0][0] + 4096 * wid : (uint8_t *)out_line[tid];
+        plan.win_lane = (uint32_t)lane;
         {
             Em<false, FMT> e;
             e.plan = &plan;
@@ -281,7 +284,11 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         }
         KPH(2);
         // emit from the plan, the ClientHello still in the cache
+#ifdef MFP_PROBE_NOEMIT   // (profiling probe only: the walk and plan alone)
+        if (len && fits && dsc.caplen == 0xffffffffu) {
+#else
         if (len && fits) {
+#endif
             Em<true, -1, 8, MFP_LEBLOCK16 != 0> e;   // the packet is in HBM
             e.begin(P.fp_arena + base + excl, out_line[tid]);
             tls_ch_emit_fast<FMT>(e, plan);
