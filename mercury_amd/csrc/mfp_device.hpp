@@ -286,114 +286,6 @@ DEV uint32_t cparse_to_delims(Cur &dst, Cur &r, uint8_t d1, uint8_t d2) {   // d
     dst.e = r.e;
     return 0;
 }
-// ---------------------------------------------------------------------------
-// Per-lane packet window (k_fp_seg's HTTP walk): the header loop's searches and
-// small reads go through a window of MFP_PW_BLK 16-byte blocks in LDS, filled
-// by direct-to-LDS loads (global_load_lds_dwordx4, no VGPRs) when a read falls
-// outside it, so a run of short header lines costs one memory round trip per
-// window instead of several dependent ones per line.  Only blocks that start
-// before the packet's end are loaded (the 16-byte block holding a packet's
-// last byte is readable, include/mfp.h); callers read only bytes before the
-// end.  NoWin: plain global loads (every other walker).
-// ---------------------------------------------------------------------------
-// (A/B on MI355X, config 3 scale, profiles/r05_ab/r05j_*: http_req 10.20 ms
-// without, 11.79 with 2 blocks, 13.62 with 4 -- the header loop's SWAR
-// searches already fetch 32 bytes per round trip, and a refill's wait for
-// every outstanding load costs more than the reads it saves: off by default)
-#ifndef MFP_PW_BLK
-#define MFP_PW_BLK 0
-#endif
-struct NoWin {
-    DEV bool on() const { return false; }
-    DEV uint64_t ld8(uintptr_t a) { return *(const uint64_t *)a; }
-};
-struct PktWin {
-    uint8_t *wv = nullptr;       // the wave's window area: block k of lane l at wv + 1024 k + 16 l
-    uint32_t lane = 0;
-    uintptr_t base = 0;          // the window's first byte (16-byte aligned); 0: empty
-    uintptr_t end = 0;           // the packet's end
-    DEV bool on() const { return wv != nullptr; }
-    DEV uint64_t ld8(uintptr_t a) {                  // the 8 bytes at a (8-byte aligned, a < end)
-        if (!wv) return *(const uint64_t *)a;
-        uintptr_t o = a - base;
-        if (base == 0 || a < base || o > (uintptr_t)(16 * MFP_PW_BLK - 8)) {
-            const uintptr_t b = a & ~(uintptr_t)15;
-#pragma unroll
-            for (int k = 0; k < MFP_PW_BLK; k++)
-                if (k == 0 || b + 16 * k < end)
-                    __builtin_amdgcn_global_load_lds((const void *)(b + 16 * k),
-                                                     (void __attribute__((address_space(3))) *)(wv + 1024 * k),
-                                                     16, 0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            base = b;
-            o = a - b;
-        }
-        return *(const uint64_t *)(wv + 1024 * (o >> 4) + 16 * lane + (o & 8));
-    }
-};
-// swar_find through a window (the plain path of swar_find, loads from W)
-template <class W, class F>
-DEV const uint8_t *swar_find_w(W &win, const uint8_t *p, const uint8_t *e, F flag, uint64_t *w0 = nullptr) {
-    if (!win.on()) return swar_find(p, e, flag, w0);
-    if (!p || p >= e) return e;
-    const uintptr_t ee = (uintptr_t)e;
-    uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
-    uint64_t m0 = ~0ull << (8 * ((uintptr_t)p & 7));
-    while (true) {
-        uint64_t w[MFP_SWB];
-#pragma unroll
-        for (int k = 0; k < MFP_SWB; k++) w[k] = a + 8 * k < ee ? win.ld8(a + 8 * k) : 0ull;
-        if (w0) {
-#pragma unroll
-            for (int k = 0; k < MFP_SWB; k++) w0[k] = w[k];
-            w0 = nullptr;
-        }
-#pragma unroll
-        for (int k = 0; k < MFP_SWB; k++) {
-            const uintptr_t ak = a + 8 * k;
-            if (ak >= ee) return e;
-            uint64_t m = flag(w[k]) & (k == 0 ? m0 : ~0ull);
-            const uintptr_t in = ee - ak;
-            if (in < 8) m &= (1ull << (8 * in)) - 1;
-            if (m) return (const uint8_t *)(ak + (__builtin_ctzll(m) >> 3));
-        }
-        a += 8 * MFP_SWB;
-        m0 = ~0ull;
-    }
-}
-// p[0, n) (n = 1..8) little-endian, bytes above n zero, through a window
-template <class W>
-DEV uint64_t win_le8n(W &win, const uint8_t *p, long n) {
-    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 7);
-    const uint64_t w0 = win.ld8(a);
-    const uint64_t w1 = (long)sh + n > 8 ? win.ld8(a + 8) : 0ull;
-    const uint64_t v = sh ? (w0 >> (8 * sh)) | (w1 << (64 - 8 * sh)) : w0;
-    return n >= 8 ? v : v & ((1ull << (8 * n)) - 1);
-}
-template <class W>
-DEV uint32_t win_ld1(W &win, const uint8_t *p) {
-    return (uint32_t)(win.ld8((uintptr_t)p & ~(uintptr_t)7) >> (8 * ((uintptr_t)p & 7))) & 0xffu;
-}
-template <class W>
-DEV void cparse_to_delim_w(W &win, Cur &dst, Cur &r, uint8_t delim) {   // datum::parse_up_to_delim datum.h:313
-    if (!cnotempty(r)) { cset_null(r); cset_null(dst); return; }
-    dst.d = r.d;
-    const uint8_t *q = swar_find_w(win, r.d, r.e, [=](uint64_t w) { return swar_eq(w, delim); });
-    if (q < r.e) { dst.e = r.d = q; return; }
-    dst.e = r.e;
-}
-template <class W>
-DEV uint32_t cparse_to_delims_w(W &win, Cur &dst, Cur &r, uint8_t d1, uint8_t d2) {   // datum.h:328
-    dst.d = r.d;
-    if (r.d) {
-        const uint8_t *q = swar_find_w(win, r.d, r.e, [=](uint64_t w) { return swar_eq(w, d1) | swar_eq(w, d2); });
-        r.d = q;
-        if (q < r.e) { dst.e = q; return win.on() ? win_ld1(win, q) : ld(q); }
-    }
-    dst.e = r.e;
-    return 0;
-}
 DEV bool ccompare_n(Cur c, const uint8_t *x, long n) {        // datum::compare_nbytes datum.h:873
     if (!(c.d && clen(c) >= n)) return false;
     for (long i = 0; i < n; i++) if (ld(c.d + i) != ld(x + i)) return false;
@@ -435,7 +327,6 @@ struct Em {
     TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
     static constexpr bool emit_pass() { return EMIT; }
-    NoWin pw;                             // (no packet window: plain loads)
     // Pass-2 output.  The string starts 16-byte aligned and owns its slot
     // rounded up to 16 bytes.  Bytes gather in `acc`; whole 8-byte words go
     // to a per-lane line of LINEW words in LDS, and a full line leaves as
@@ -585,7 +476,6 @@ struct SegEm {
     // (MFP_HTTP_NAMEWIN) LDS copies of the header-name tables, set by k_fp_seg
     const uint8_t *slots_req = nullptr, *slots_resp = nullptr;
     const HdrKey *keys_req = nullptr, *keys_resp = nullptr;
-    PktWin pw;                          // (k_fp_seg) the HTTP walk's packet window; off when wv is null
     static constexpr bool PLAN = false;
     static constexpr bool emit_pass() { return false; }
     uint32_t n = 0;                     // characters produced
@@ -2021,25 +1911,14 @@ DEV bool http_delim4w(Cur &p, uint32_t dv, long dl, uint32_t w) {
 template <class E>
 DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua) {
     Cur tmp = body;
-    auto &W = b.pw;                      // the packet window (SegEm in k_fp_seg), else plain loads
-    auto hw_le4n = [&](const uint8_t *q, long n) -> uint32_t { return W.on() ? (uint32_t)win_le8n(W, q, n) : ld_le4n(q, n); };
-    auto hw_le8n = [&](const uint8_t *q, long n) -> uint64_t { return W.on() ? win_le8n(W, q, n) : ld_le8n(q, n); };
-    auto hw_ld1 = [&](const uint8_t *q) -> uint32_t { return W.on() ? win_ld1(W, q) : ld(q); };
-    // http_delim4 with the loads through the window
-    auto hdelim4 = [&](Cur &c, uint32_t dv_, long dl_) -> bool {
-        if (!c.d) return false;
-        const long L = c.e - c.d;
-        if (L <= 0) return false;
-        return http_delim4w(c, dv_, dl_, hw_le4n(c.d, L < 4 ? L : 4));
-    };
     constexpr bool NW = E::SEG && MFP_HTTP_NAMEWIN && MFP_HTTP_FAST >= 1;
 #if MFP_HTTP_FAST
     const long dl = clen(delim);
-    const uint32_t dv = dl > 0 && dl <= 4 ? hw_le4n(delim.d, dl) : 0u;
+    const uint32_t dv = dl > 0 && dl <= 4 ? ld_le4n(delim.d, dl) : 0u;
     const bool d4 = dl <= 4;
     // (the segment walker leaves longer delimiters to the fallback lane)
     if (E::SEG && !d4) { b.punt_pkt(); return; }
-#define MFP_HDELIM(c) ((E::SEG || d4) ? hdelim4(c, dv, dl) : http_delim(c, delim))
+#define MFP_HDELIM(c) ((E::SEG || d4) ? http_delim4(c, dv, dl) : http_delim(c, delim))
     // MFP_HTTP_FAST >= 2 (segment walker): the delimiter after a value is
     // tested from an 8-byte window that also holds the next header's first
     // bytes (the loop-top test reads no memory), and the value's end is
@@ -2066,7 +1945,7 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
         else {
             name.d = tmp.d; name.e = tmp.e;
             uint64_t w0[MFP_SWB];
-            const uint8_t *q = swar_find_w(W, tmp.d, tmp.e, [](uint64_t w) { return swar_eq(w, ':'); }, NW ? w0 : nullptr);
+            const uint8_t *q = swar_find(tmp.d, tmp.e, [](uint64_t w) { return swar_eq(w, ':'); }, NW ? w0 : nullptr);
             if (q < tmp.e) {
                 name.e = q; tmp.d = q + 1;
                 if constexpr (NW) {
@@ -2090,22 +1969,22 @@ DEV void http_headers_fp(E &b, Cur body, Cur delim, bool req, Cur &host, Cur &ua
             // which holds neither
             long L = 0;
             uint32_t w = 0;
-            if (tmp.d && tmp.d < tmp.e) { L = tmp.e - tmp.d; w = hw_le4n(tmp.d, L < 4 ? L : 4); }
-            const uint8_t *q2 = tmp.d ? swar_find_w(W, tmp.d, tmp.e, [](uint64_t x) { return swar_eq(x, '\r') | swar_eq(x, '\n'); })
+            if (tmp.d && tmp.d < tmp.e) { L = tmp.e - tmp.d; w = ld_le4n(tmp.d, L < 4 ? L : 4); }
+            const uint8_t *q2 = tmp.d ? swar_find(tmp.d, tmp.e, [](uint64_t x) { return swar_eq(x, '\r') | swar_eq(x, '\n'); })
                                       : nullptr;
             if (L > 0) {
                 int k = 0;
                 while (k < 4 && k < L && (((w >> (8 * k)) & 0xff) == '\t' || ((w >> (8 * k)) & 0xff) == ' ')) k++;
                 tmp.d += k;
                 if (k == 4)
-                    while (tmp.d < tmp.e && (hw_ld1(tmp.d) == '\t' || hw_ld1(tmp.d) == ' ')) tmp.d++;
+                    while (tmp.d < tmp.e && (ld(tmp.d) == '\t' || ld(tmp.d) == ' ')) tmp.d++;
             }
             // cparse_to_delims(value, tmp, '\r', '\n')
             value.d = tmp.d;
             if (tmp.d) { tmp.d = q2; value.e = q2; } else value.e = tmp.e;
             // the delimiter, and the next header's first bytes, from one window
             uint64_t w8 = 0;
-            if (tmp.d && tmp.d < tmp.e) { const long L8 = tmp.e - tmp.d; w8 = hw_le8n(tmp.d, L8 < 8 ? L8 : 8); }
+            if (tmp.d && tmp.d < tmp.e) { const long L8 = tmp.e - tmp.d; w8 = ld_le8n(tmp.d, L8 < 8 ? L8 : 8); }
             const uint8_t *at = tmp.d;
             http_delim4w(tmp, dv, dl, (uint32_t)w8);
             wnext = (uint32_t)(w8 >> (8 * (uint32_t)(tmp.d - at)));
@@ -2270,13 +2149,11 @@ DEV void fp_type_prefix(E &b, uint32_t t) {             // fingerprint::set_type
 // 426-553); returns false when the message is empty (no record)
 template <class E>
 DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
-    auto &W = b.pw;                      // the packet window (SegEm in k_fp_seg), else plain loads
-    auto hw_ld1 = [&](const uint8_t *q) -> uint32_t { return W.on() ? win_ld1(W, q) : ld(q); };
     Cur f1, f2, f3;   // req: method, protocol ; resp: version, status, reason
     cset_null(f1); cset_null(f2); cset_null(f3);
     if (req) {
         Cur uri;
-        cparse_to_delim_w(W, f1, p, ' ');
+        cparse_to_delim(f1, p, ' ');
         long ml = clen(f1);
         if (ml < 3 || ml > 16) return false;
 #if MFP_HTTP_FAST >= 3
@@ -2285,7 +2162,7 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         const uint64_t m0 = ld_le8n(f1.d, ml < 8 ? ml : 8);
         const uint64_t m1 = ml > 8 ? ld_le8n(f1.d + 8, ml - 8) : 0ull;
         cskip(p, 1);
-        cparse_to_delim_w(W, uri, p, ' ');
+        cparse_to_delim(uri, p, ' ');
         {   // every byte of the method 'A'..'Z'
             const uint64_t k0 = ml >= 8 ? 0x8080808080808080ull : 0x8080808080808080ull & ((1ull << (8 * ml)) - 1);
             const long r1 = ml - 8;
@@ -2295,28 +2172,28 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         cskip(p, 1);
         const long pl = clen(p);
         const uint64_t h5 = p.d && pl > 0 ? ld_le8n(p.d, pl < 5 ? pl : 5) : 0ull;
-        cparse_to_delims_w(W, f2, p, '\r', '\n');
+        cparse_to_delims(f2, p, '\r', '\n');
         if (!(f2.d && clen(f2) >= 5 && h5 == 0x2f50545448ull)) return false;   // "HTTP/"
 #else
-        if (swar_find_w(W, f1.d, f1.e, [](uint64_t w) { return ~swar_upper(w) & 0x8080808080808080ull; }) < f1.e) return false;
+        if (swar_find(f1.d, f1.e, [](uint64_t w) { return ~swar_upper(w) & 0x8080808080808080ull; }) < f1.e) return false;
         cskip(p, 1);
-        cparse_to_delim_w(W, uri, p, ' ');
+        cparse_to_delim(uri, p, ' ');
         cskip(p, 1);
-        cparse_to_delims_w(W, f2, p, '\r', '\n');
-        if (!(f2.d && clen(f2) >= 5 && hw_ld1(f2.d) == 'H' && hw_ld1(f2.d + 1) == 'T' && hw_ld1(f2.d + 2) == 'T' &&
-              hw_ld1(f2.d + 3) == 'P' && hw_ld1(f2.d + 4) == '/'))
+        cparse_to_delims(f2, p, '\r', '\n');
+        if (!(f2.d && clen(f2) >= 5 && ld(f2.d) == 'H' && ld(f2.d + 1) == 'T' && ld(f2.d + 2) == 'T' &&
+              ld(f2.d + 3) == 'P' && ld(f2.d + 4) == '/'))
             return false;
 #endif
     } else {
-        cparse_to_delim_w(W, f1, p, ' ');
+        cparse_to_delim(f1, p, ' ');
         cskip(p, 1);
-        cparse_to_delim_w(W, f2, p, ' ');
+        cparse_to_delim(f2, p, ' ');
         cskip(p, 1);
-        cparse_to_delims_w(W, f3, p, '\r', '\n');
+        cparse_to_delims(f3, p, '\r', '\n');
         if (!cnotempty(f2)) return false;
     }
     Cur delim; delim.d = p.d;
-    if (p.d) p.d = swar_find_w(W, p.d, p.e, [](uint64_t w) { return swar_alpha(w); });
+    if (p.d) p.d = swar_find(p.d, p.e, [](uint64_t w) { return swar_alpha(w); });
     delim.e = p.d;
     fp_type_prefix(b, req ? 3 : 4);
     b.putc('('); b.hex(f1.d, clen(f1)); b.putc(')');

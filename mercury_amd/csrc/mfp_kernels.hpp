@@ -357,10 +357,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
     __shared__ uint8_t s_slots[(1 << REQ_BITS) + (1 << RESP_BITS)];
 #endif
 #if MFP_SEG_LANE
-    __shared__ __attribute__((aligned(16))) uint64_t out_line[TILE][SEG_LINEW];
-#if MFP_PW_BLK > 2
-    __shared__ __attribute__((aligned(16))) uint8_t pw_area[TILE / 64][1024 * MFP_PW_BLK];
-#endif
+    __shared__ uint64_t out_line[TILE][SEG_LINEW];
 #else
     __shared__ uint4 stage[TILE / 64][SEG_STAGE / 16];   // per wave: the packet being expanded
 #endif
@@ -395,18 +392,6 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 #if MFP_HTTP_NAMEWIN
         e.slots_req = s_slots; e.slots_resp = s_slots + (1 << REQ_BITS);
         e.keys_req = s_keys; e.keys_resp = s_keys + N_REQ_NAMES;
-#endif
-#if MFP_SEG_LANE && MFP_PW_BLK
-        // the HTTP walk's packet window (PktWin): the emission line's LDS while
-        // the walk runs (2 blocks), or its own area
-        static_assert(MFP_PW_BLK > 2 || SEG_LINEW * 8 * 64 == 1024 * MFP_PW_BLK, "window = the wave's emission lines");
-#if MFP_PW_BLK > 2
-        e.pw.wv = &pw_area[wid][0];
-#else
-        e.pw.wv = (uint8_t *)&out_line[64 * wid][0];
-#endif
-        e.pw.lane = lane;
-        e.pw.end = (uintptr_t)data + dsc.caplen;
 #endif
         packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
         e.finish();
