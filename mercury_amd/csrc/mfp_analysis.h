@@ -23,7 +23,11 @@ struct mfp_entry {
     uint32_t malware_db;    // fingerprint_data::malware_db
     uint32_t generic_dmz;   // index of "generic dmz process" or 0xffffffff
     uint32_t mal_bits;      // bit p: process p is malware (p < 32)
-    uint32_t pad[3];
+    // the entry's own region of the feature table: slots [feat_base, feat_base +
+    // feat_mask] (a power of two), probed by feat_slot_hash & feat_mask -- the
+    // probes of packets with the same fingerprint touch the same few lines
+    uint32_t feat_base, feat_mask;
+    uint32_t pad;
 };
 
 // feature-table slot, keyed by (entry, kind, key) -- key is the value itself
@@ -71,7 +75,7 @@ struct mfp_classifier_dev {
     uint32_t *proc_id = nullptr;
     uint8_t *proc_mal = nullptr;
     uint32_t *proc_attr = nullptr;
-    mfp_feat_slot *feat_slots = nullptr; uint64_t feat_mask = 0;
+    mfp_feat_slot *feat_slots = nullptr;   // per-entry regions (mfp_entry::feat_base / feat_mask)
     mfp_update *upd = nullptr;
     char *pool = nullptr;
     // pyasn.db as the reference's LC-tries (mfp_lctrie.hpp); n_* = node count, 0: no table

@@ -79,10 +79,13 @@ ADEV uint32_t probe_string(const mfp_fp_slot *slots, uint64_t mask, const char *
 }
 
 struct Hit { uint32_t off, cnt; };
-ADEV Hit probe_feature(const mfp_classifier_dev &D, uint32_t entry, uint32_t kind, uint64_t key, const uint8_t *s,
-                       uint32_t len, bool verify, uint32_t lane) {
-    for (uint64_t k = feat_slot_hash(entry, kind, key) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
-        const mfp_feat_slot sl = D.feat_slots[k];
+// an entry's region of the feature table (mfp_entry::feat_base / feat_mask)
+struct FeatRegion { uint32_t base, mask; };
+ADEV FeatRegion feat_region(const mfp_entry &E) { return FeatRegion{E.feat_base, E.feat_mask}; }
+ADEV Hit probe_feature(const mfp_classifier_dev &D, FeatRegion R, uint32_t entry, uint32_t kind, uint64_t key,
+                       const uint8_t *s, uint32_t len, bool verify, uint32_t lane) {
+    for (uint32_t k = (uint32_t)feat_slot_hash(entry, kind, key) & R.mask;; k = (k + 1) & R.mask) {
+        const mfp_feat_slot sl = D.feat_slots[R.base + k];
         const uint32_t e = rfl(sl.entry);
         if (e == 0xffffffffu) return Hit{0, 0};
         if (e == entry && rfl(sl.kind) == kind && rfl64(sl.key) == key) {
@@ -234,10 +237,10 @@ ADEV uint32_t cand_string_lane(const mfp_fp_slot *slots, uint64_t mask, uint64_t
         if (sl.hash == h && sl.str_len == len) { str_off = sl.str_off; return sl.id; }
     }
 }
-ADEV bool cand_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_t kind, uint64_t key, uint32_t len,
-                            Hit &hit, uint32_t &str_off) {
-    for (uint64_t k = feat_slot_hash(entry, kind, key) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
-        const mfp_feat_slot sl = D.feat_slots[k];
+ADEV bool cand_feature_lane(const mfp_classifier_dev &D, FeatRegion R, uint32_t entry, uint32_t kind, uint64_t key,
+                            uint32_t len, Hit &hit, uint32_t &str_off) {
+    for (uint32_t k = (uint32_t)feat_slot_hash(entry, kind, key) & R.mask;; k = (k + 1) & R.mask) {
+        const mfp_feat_slot sl = D.feat_slots[R.base + k];
         if (sl.entry == 0xffffffffu) return false;
         if (sl.entry == entry && sl.kind == kind && sl.key == key && sl.str_len == len) {
             hit = Hit{sl.upd_off, sl.upd_cnt};
@@ -291,10 +294,10 @@ ADEV bool wave_verify(bool has, const uint8_t *a, const uint8_t *b, uint32_t len
 
 // feature slot of (entry, kind, key); s/len: the string to verify (len ==
 // ~0u: integer key, nothing to verify)
-ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, uint32_t entry, uint32_t kind, uint64_t key,
+ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, FeatRegion R, uint32_t entry, uint32_t kind, uint64_t key,
                             const uint8_t *s, uint32_t len) {
-    for (uint64_t k = feat_slot_hash(entry, kind, key) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
-        const mfp_feat_slot sl = D.feat_slots[k];
+    for (uint32_t k = (uint32_t)feat_slot_hash(entry, kind, key) & R.mask;; k = (k + 1) & R.mask) {
+        const mfp_feat_slot sl = D.feat_slots[R.base + k];
         if (sl.entry == 0xffffffffu) return Hit{0, 0};
         if (sl.entry == entry && sl.kind == kind && sl.key == key &&
 #ifdef MFP_PROBE_AN_NOVERIFY
@@ -771,6 +774,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
         mfp_entry E;
         E.proc_off = 0; E.nproc = 0; E.malware_db = 0; E.generic_dmz = 0;
         if (scored) E = D.entry[entry];
+        const FeatRegion FR = scored ? feat_region(E) : FeatRegion{0, 0};
         uint32_t np = E.nproc;
         if (scored && np > 64 * MAXP_CHUNKS_BIG) atomicAdd(&P.stats[2], 1ull);   // scored by k_analyze_huge
         uint32_t hoff[NFEAT], hcnt[NFEAT];
@@ -846,17 +850,17 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             // ---- the six feature lookups
             n_look += 2u + (ipv != 0) + (!ssh_ua && !stun_ua) + (plain ? 2u : 0u);
             Hit h;
-            h = probe_feature_lane(D, entry, F_ASN, asn, nullptr, 0xffffffffu);
+            h = probe_feature_lane(D, FR, entry, F_ASN, asn, nullptr, 0xffffffffu);
             hoff[0] = h.off; hcnt[0] = h.cnt;
-            h = probe_feature_lane(D, entry, F_PORT, dport, nullptr, 0xffffffffu);
+            h = probe_feature_lane(D, FR, entry, F_PORT, dport, nullptr, 0xffffffffu);
             hoff[1] = h.off; hcnt[1] = h.cnt;
             if (ipv == 4) {
-                h = probe_feature_lane(D, entry, F_IPV4, ipkey, nullptr, 0xffffffffu);
+                h = probe_feature_lane(D, FR, entry, F_IPV4, ipkey, nullptr, 0xffffffffu);
                 hoff[2] = h.off; hcnt[2] = h.cnt;
             } else if (ipv == 6) {
                 // the 16 normalized bytes, verified against the pool
-                for (uint64_t k = feat_slot_hash(entry, F_IPV6, ipkey) & D.feat_mask;; k = (k + 1) & D.feat_mask) {
-                    const mfp_feat_slot s6 = D.feat_slots[k];
+                for (uint32_t k = (uint32_t)feat_slot_hash(entry, F_IPV6, ipkey) & FR.mask;; k = (k + 1) & FR.mask) {
+                    const mfp_feat_slot s6 = D.feat_slots[FR.base + k];
                     if (s6.entry == 0xffffffffu) break;
                     if (s6.entry == entry && s6.kind == F_IPV6 && s6.key == ipkey && s6.str_len == 16) {
                         const uint8_t *ps = (const uint8_t *)D.pool + s6.str_off;
@@ -869,12 +873,12 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             }
             // string features: candidate slots here, byte-exact check by the wave below
             vs[0] = up; vl[0] = ul; vk[0] = uh;
-            has[0] = !ssh_ua && !stun_ua && cand_feature_lane(D, entry, F_UA, uh, ul, vh[0], voff[0]);
+            has[0] = !ssh_ua && !stun_ua && cand_feature_lane(D, FR, entry, F_UA, uh, ul, vh[0], voff[0]);
             if (plain) {   // else k_analyze_wave normalises the name (wave, LDS)
                 vs[1] = sp + tld; vl[1] = sl - tld; vk[1] = lane_hash(sp + tld, sl - tld);
-                has[1] = cand_feature_lane(D, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
+                has[1] = cand_feature_lane(D, FR, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
                 vs[2] = sp; vl[2] = sl; vk[2] = nh;
-                has[2] = cand_feature_lane(D, entry, F_SNI, nh, sl, vh[2], voff[2]);
+                has[2] = cand_feature_lane(D, FR, entry, F_SNI, nh, sl, vh[2], voff[2]);
             }
         }
         // byte-exact check of the candidates.  Lane by lane: each lane compares
@@ -890,7 +894,7 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
 #endif
             if (has[v]) {
                 // a hash collision (ok == false) takes the full probe, which keeps looking
-                const Hit h = ok ? vh[v] : probe_feature_lane(D, entry, v == 0 ? F_UA : v == 1 ? F_DOMAIN : F_SNI, vk[v],
+                const Hit h = ok ? vh[v] : probe_feature_lane(D, FR, entry, v == 0 ? F_UA : v == 1 ? F_DOMAIN : F_SNI, vk[v],
                                                               vs[v], vl[v]);
                 hoff[3 + v] = h.off; hcnt[3 + v] = h.cnt;
             }
@@ -1054,6 +1058,7 @@ ADEV uint32_t slow_lookups(const AParams &P, uint32_t i, uint32_t entry, uint32_
                            uint32_t (&off)[NFEAT], uint32_t (&cnt)[NFEAT], uint32_t lane) {
     const mfp_classifier_dev &D = P.D;
     uint32_t changed = 0;
+    const FeatRegion FR{rfl(D.entry[entry].feat_base), rfl(D.entry[entry].feat_mask)};
     if (flags & 1u) {
         const mfp_record r = P.rec[i];
         const uint32_t sni = rfl((uint32_t)r.sni_off | ((uint32_t)r.sni_len << 16));
@@ -1066,10 +1071,10 @@ ADEV uint32_t slow_lookups(const AParams &P, uint32_t i, uint32_t entry, uint32_
         __builtin_amdgcn_wave_barrier();
         const int tld = (int)rfl((uint32_t)(lane == 0 ? tld_domain_offset(nbuf, nlen) : 0));
         const uint8_t *dom = (const uint8_t *)nbuf + tld;
-        Hit h = probe_feature(D, entry, F_DOMAIN, wave_hash(dom, (uint32_t)(nlen - tld), lane), dom,
+        Hit h = probe_feature(D, FR, entry, F_DOMAIN, wave_hash(dom, (uint32_t)(nlen - tld), lane), dom,
                               (uint32_t)(nlen - tld), true, lane);
         off[4] = h.off; cnt[4] = h.cnt;
-        h = probe_feature(D, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
+        h = probe_feature(D, FR, entry, F_SNI, wave_hash((const uint8_t *)nbuf, (uint32_t)nlen, lane),
                           (const uint8_t *)nbuf, (uint32_t)nlen, true, lane);
         off[5] = h.off; cnt[5] = h.cnt;
         __builtin_amdgcn_wave_barrier();
@@ -1098,7 +1103,7 @@ ADEV uint32_t slow_lookups(const AParams &P, uint32_t i, uint32_t entry, uint32_
         }
         ulen = (int)rfl((uint32_t)ulen);
         __builtin_amdgcn_wave_barrier();
-        const Hit h = probe_feature(D, entry, F_UA, wave_hash((const uint8_t *)ub, (uint32_t)ulen, lane),
+        const Hit h = probe_feature(D, FR, entry, F_UA, wave_hash((const uint8_t *)ub, (uint32_t)ulen, lane),
                                     (const uint8_t *)ub, (uint32_t)ulen, true, lane);
         off[3] = h.off; cnt[3] = h.cnt;
         __builtin_amdgcn_wave_barrier();

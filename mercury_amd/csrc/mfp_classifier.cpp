@@ -1154,10 +1154,20 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
                            (uint32_t)fs.size());
     }
     // entries, processes, features
-    uint64_t nfeat = 0;
-    for (auto &e : c->entries)
-        for (auto &f : e->f) nfeat += f.by_str.size() + f.by_int.size() + f.by_v6.size();
-    t.feat_slots.assign(pow2_at_least(2 * nfeat + 2), mfp_feat_slot{0, 0xffffffffu, 0, 0, 0, 0, 0});
+    // the feature table: one open-addressing region per entry (a power of two,
+    // at most half full), so a packet's six probes -- and those of every other
+    // packet with the same fingerprint -- stay within the entry's few lines
+    std::vector<uint64_t> reg_base(c->entries.size()), reg_mask(c->entries.size());
+    uint64_t nslots = 0;
+    for (uint32_t eid = 0; eid < c->entries.size(); eid++) {
+        uint64_t nf = 0;
+        for (auto &f : c->entries[eid]->f) nf += f.by_str.size() + f.by_int.size() + f.by_v6.size();
+        const uint64_t r = pow2_at_least(2 * nf + 2);
+        reg_base[eid] = nslots; reg_mask[eid] = r - 1;
+        nslots += r;
+    }
+    if (nslots >> 32) { mfp_set_error("feature table too large"); return -1; }
+    t.feat_slots.assign(nslots ? nslots : 1, mfp_feat_slot{0, 0xffffffffu, 0, 0, 0, 0, 0});
     auto put_feat = [&](uint32_t eid, uint32_t kind, uint64_t key, const std::vector<Upd> &lst, const std::string *str) {
         mfp_feat_slot s;
         s.key = key; s.entry = eid; s.kind = kind;
@@ -1173,9 +1183,9 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
         }
         s.str_off = str ? pool_add(t, *str) : 0; s.str_len = str ? (uint32_t)str->size() : 0;
         for (auto &u : lst) t.upd.push_back(mfp_update{u.idx, 0, u.val});
-        uint64_t mask = t.feat_slots.size() - 1;
+        const uint64_t base = reg_base[eid], mask = reg_mask[eid];
         for (uint64_t k = mfpc::feat_slot_hash(eid, kind, key) & mask;; k = (k + 1) & mask)
-            if (t.feat_slots[k].entry == 0xffffffffu) { t.feat_slots[k] = s; break; }
+            if (t.feat_slots[base + k].entry == 0xffffffffu) { t.feat_slots[base + k] = s; break; }
     };
     for (uint32_t eid = 0; eid < c->entries.size(); eid++) {
         Entry &e = *c->entries[eid];
@@ -1184,7 +1194,8 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
         me.nproc = (uint32_t)e.prior.size();
         me.malware_db = e.malware_db;
         me.generic_dmz = 0xffffffffu;
-        me.mal_bits = 0; me.pad[0] = me.pad[1] = me.pad[2] = 0;
+        me.mal_bits = 0; me.pad = 0;
+        me.feat_base = (uint32_t)reg_base[eid]; me.feat_mask = (uint32_t)reg_mask[eid];
         for (uint32_t i = 0; i < me.nproc; i++) {
             if (i < 32 && e.malware[i]) me.mal_bits |= 1u << i;
             t.prior.push_back(e.prior[i]);
@@ -1228,7 +1239,7 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     if (t.pool.empty()) t.pool.push_back(0);
     if (t.upd.empty()) t.upd.push_back(mfp_update{0, 0, 0});
     if (t.prior.empty()) { t.prior.push_back(0); t.proc_id.push_back(0); t.proc_mal.push_back(0); t.proc_attr.push_back(0); }
-    if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0, 0, {0, 0, 0}});
+    if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0, 0, 0, 0, 0});
     if (t.doh_v4.empty()) t.doh_v4.push_back(0);
     if (t.doh_v6.empty()) { t.doh_v6.push_back(0); t.doh_v6.push_back(0); }
     if (t.dom_info.empty()) { t.dom_info.push_back(0); t.dom_info.push_back(0); }
@@ -1270,7 +1281,6 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
     }
     d.fp_mask = t.fp_slots.size() - 1;
     d.prev_mask = t.prev_slots.size() - 1;
-    d.feat_mask = t.feat_slots.size() - 1;
     d.n_asn4 = (uint32_t)t.asn4.node.size();
     d.n_asn6 = (uint32_t)t.asn6.node.size();
     const char *rnd[3] = {"tls/randomized", "tls/1/randomized", "tls/2/randomized"};
