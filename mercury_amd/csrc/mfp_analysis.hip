@@ -309,6 +309,41 @@ ADEV Hit probe_feature_lane(const mfp_classifier_dev &D, FeatRegion R, uint32_t 
     }
 }
 
+// The same probes started from their home slot, loaded beforehand: the
+// kernel issues the home-slot loads of all its lookups together (one memory
+// round trip instead of one per lookup); a probe that does not end at its
+// home slot walks on from there
+ADEV uint32_t home_slot(FeatRegion R, uint32_t entry, uint32_t kind, uint64_t key) {
+    return (uint32_t)feat_slot_hash(entry, kind, key) & R.mask;
+}
+ADEV mfp_feat_slot empty_slot() {
+    mfp_feat_slot s;
+    s.key = 0; s.entry = 0xffffffffu; s.kind = 0; s.upd_off = 0; s.upd_cnt = 0; s.str_off = 0; s.str_len = 0;
+    return s;
+}
+ADEV Hit probe_int_from(const mfp_classifier_dev &D, FeatRegion R, uint32_t entry, uint32_t kind, uint64_t key,
+                        uint32_t k, mfp_feat_slot sl) {
+    for (;;) {
+        if (sl.entry == 0xffffffffu) return Hit{0, 0};
+        if (sl.entry == entry && sl.kind == kind && sl.key == key) return Hit{sl.upd_off, sl.upd_cnt};
+        k = (k + 1) & R.mask;
+        sl = D.feat_slots[R.base + k];
+    }
+}
+ADEV bool cand_from(const mfp_classifier_dev &D, FeatRegion R, uint32_t entry, uint32_t kind, uint64_t key,
+                    uint32_t len, uint32_t k, mfp_feat_slot sl, Hit &hit, uint32_t &str_off) {
+    for (;;) {
+        if (sl.entry == 0xffffffffu) return false;
+        if (sl.entry == entry && sl.kind == kind && sl.key == key && sl.str_len == len) {
+            hit = Hit{sl.upd_off, sl.upd_cnt};
+            str_off = sl.str_off;
+            return true;
+        }
+        k = (k + 1) & R.mask;
+        sl = D.feat_slots[R.base + k];
+    }
+}
+
 // subnet_data::get_asn_info (addr.cc:172-208): lct_find on the reference's
 // tries (mfp_lctrie.hpp), the subnet's ASN or 0
 ADEV uint32_t asn_v4_lane(const mfp_classifier_dev &D, uint32_t addr_host) {
@@ -810,7 +845,9 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             uint32_t asn = 0;
             uint64_t ipkey = 0, v6w0 = 0, v6w1 = 0;
             if (ipv == 4) {
+#ifndef MFP_PROBE_AN_NOASN
                 asn = asn_v4_lane(D, __builtin_bswap32(dd.v4));
+#endif
                 ipkey = normalize_ipv4(dd.v4);
             } else if (ipv == 6) {
                 v6w0 = __builtin_bswap64(dd.hi);
@@ -828,7 +865,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             const uint8_t *sp = sbase + r.sni_off;
             uint32_t tld = 0;
             uint64_t nh = 0;
+#ifdef MFP_PROBE_AN_NOSTR
+            plain = sl != 0; nh = sl; tld = 0;
+#else
             plain = plain_server_name(sp, sl, tld, nh);   // no NUL in a plain name
+#endif
             // user agent (strncpy 511, NUL stops); TLS has none (its slot holds
             // the ALPN list); QUIC's is transport parameter 0x3129 (tls.h:1346-1355)
             // SSH (protocol + comment, the delimiting space dropped) is built and
@@ -844,23 +885,39 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             if (ul > 511) ul = 511;
             const uint8_t *up = sbase + r.ua_off;
             uint64_t uh = 0;
+#ifdef MFP_PROBE_AN_NOSTR
+            uh = ul;
+#else
             ul = cstr_hash(up, ul, uh);
+#endif
             const uint32_t dport = r.dst_port;
 
-            // ---- the six feature lookups
+            // ---- the six feature lookups: every home slot loaded at once
             n_look += 2u + (ipv != 0) + (!ssh_ua && !stun_ua) + (plain ? 2u : 0u);
+            const bool has_ua = !ssh_ua && !stun_ua;
+            uint64_t dk = 0;
+            if (plain) dk = lane_hash(sp + tld, sl - tld);
+            const uint32_t kA = home_slot(FR, entry, F_ASN, asn), kP = home_slot(FR, entry, F_PORT, dport);
+            const uint32_t kI = home_slot(FR, entry, ipv == 6 ? F_IPV6 : F_IPV4, ipkey);
+            const uint32_t kU = home_slot(FR, entry, F_UA, uh), kD = home_slot(FR, entry, F_DOMAIN, dk);
+            const uint32_t kS = home_slot(FR, entry, F_SNI, nh);
+            const mfp_feat_slot sA = D.feat_slots[FR.base + kA], sP = D.feat_slots[FR.base + kP];
+            const mfp_feat_slot sI = ipv ? D.feat_slots[FR.base + kI] : empty_slot();
+            const mfp_feat_slot sU = has_ua ? D.feat_slots[FR.base + kU] : empty_slot();
+            const mfp_feat_slot sD = plain ? D.feat_slots[FR.base + kD] : empty_slot();
+            const mfp_feat_slot sS = plain ? D.feat_slots[FR.base + kS] : empty_slot();
             Hit h;
-            h = probe_feature_lane(D, FR, entry, F_ASN, asn, nullptr, 0xffffffffu);
+            h = probe_int_from(D, FR, entry, F_ASN, asn, kA, sA);
             hoff[0] = h.off; hcnt[0] = h.cnt;
-            h = probe_feature_lane(D, FR, entry, F_PORT, dport, nullptr, 0xffffffffu);
+            h = probe_int_from(D, FR, entry, F_PORT, dport, kP, sP);
             hoff[1] = h.off; hcnt[1] = h.cnt;
             if (ipv == 4) {
-                h = probe_feature_lane(D, FR, entry, F_IPV4, ipkey, nullptr, 0xffffffffu);
+                h = probe_int_from(D, FR, entry, F_IPV4, ipkey, kI, sI);
                 hoff[2] = h.off; hcnt[2] = h.cnt;
             } else if (ipv == 6) {
                 // the 16 normalized bytes, verified against the pool
-                for (uint32_t k = (uint32_t)feat_slot_hash(entry, F_IPV6, ipkey) & FR.mask;; k = (k + 1) & FR.mask) {
-                    const mfp_feat_slot s6 = D.feat_slots[FR.base + k];
+                mfp_feat_slot s6 = sI;
+                for (uint32_t k = kI;; k = (k + 1) & FR.mask, s6 = D.feat_slots[FR.base + k]) {
                     if (s6.entry == 0xffffffffu) break;
                     if (s6.entry == entry && s6.kind == F_IPV6 && s6.key == ipkey && s6.str_len == 16) {
                         const uint8_t *ps = (const uint8_t *)D.pool + s6.str_off;
@@ -873,12 +930,12 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
             }
             // string features: candidate slots here, byte-exact check by the wave below
             vs[0] = up; vl[0] = ul; vk[0] = uh;
-            has[0] = !ssh_ua && !stun_ua && cand_feature_lane(D, FR, entry, F_UA, uh, ul, vh[0], voff[0]);
+            has[0] = has_ua && cand_from(D, FR, entry, F_UA, uh, ul, kU, sU, vh[0], voff[0]);
             if (plain) {   // else k_analyze_wave normalises the name (wave, LDS)
-                vs[1] = sp + tld; vl[1] = sl - tld; vk[1] = lane_hash(sp + tld, sl - tld);
-                has[1] = cand_feature_lane(D, FR, entry, F_DOMAIN, vk[1], vl[1], vh[1], voff[1]);
+                vs[1] = sp + tld; vl[1] = sl - tld; vk[1] = dk;
+                has[1] = cand_from(D, FR, entry, F_DOMAIN, dk, vl[1], kD, sD, vh[1], voff[1]);
                 vs[2] = sp; vl[2] = sl; vk[2] = nh;
-                has[2] = cand_feature_lane(D, FR, entry, F_SNI, nh, sl, vh[2], voff[2]);
+                has[2] = cand_from(D, FR, entry, F_SNI, nh, sl, kS, sS, vh[2], voff[2]);
             }
         }
         // byte-exact check of the candidates.  Lane by lane: each lane compares
