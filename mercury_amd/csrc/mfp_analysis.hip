@@ -2063,7 +2063,11 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
                                    void *deferred, uint32_t *seg_n, unsigned long long *stats, uint32_t mode,
                                    uint32_t lane_max_p, void *huge_rows, hipStream_t stream, mfp_prof *prof) {
     if (n == 0) return 0;
-    mfpa::AParams P = make_params(D, *T, arena, desc, n, rec, fp_arena, out, pending, deferred, stats, mode, lane_max_p);
+    // T == nullptr: no sighting table (a small batch decided on the host from
+    // its records, mfp_process_small_pinned): k_seen_scan is not launched
+    const mfp_seen_tab none{};
+    mfpa::AParams P = make_params(D, T ? *T : none, arena, desc, n, rec, fp_arena, out, pending, deferred, stats, mode,
+                                  lane_max_p);
     P.attr_prob = attr_prob;
     P.work = (mfpa::WorkItem *)work;
     P.lanel = (mfpa::Deferred *)lanel;
@@ -2075,7 +2079,7 @@ extern "C" int mfp_launch_analysis(const mfp_classifier_dev *D, const mfp_seen_t
     hipLaunchKernelGGL(mfpa::k_analyze, dim3(blocks), dim3(64 * mfpa::AW), 0, stream, P);
     if (prof) mfp_prof_end(prof, stream);
     if (hipGetLastError() != hipSuccess) return -1;
-    {
+    if (T) {
         const uint64_t sb = seen_grid(groups);
         if (prof) mfp_prof_begin(prof, "k_seen_scan", stream);
         hipLaunchKernelGGL(mfpa::k_seen_scan, dim3((uint32_t)sb), dim3(64 * mfpa::SEEN_WPB), 0, stream, P);

@@ -119,7 +119,80 @@ __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t 
     }
 }
 
+// A small batch (the per-packet API, n <= 1024) in one launch: the scan in
+// LDS, then the packed strings, the re-pointed records, the classifier's
+// results and the counters written straight into the caller's page-locked
+// host buffers (no device-to-host copies after it).  Strings are copied only
+// when the packed total fits `cap` (the host reports the overflow).
+__global__ __launch_bounds__(1024) void k_compact_small(const mfp_record *rec, uint32_t n, const uint8_t *src,
+                                                        uint8_t *dst, uint64_t cap, mfp_record *rec_out,
+                                                        const unsigned long long *used, unsigned long long *used_out,
+                                                        const uint64_t *an, uint64_t *an_out, uint32_t an_words,
+                                                        const uint64_t *ap, uint64_t *ap_out, uint32_t ap_words) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t s_off[1024], s_len[1024];
+    __shared__ uint64_t s_src[1024];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    mfp_record r;
+    uint32_t len = 0;
+    if (tid < n) { r = rec[tid]; len = packed_len(r, src); }
+    uint32_t incl = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        if ((uint32_t)w < wid) base += wsum[w];
+        total += wsum[w];
+    }
+    const uint32_t off = base + incl - len;
+    if (tid < n) {
+        s_off[tid] = off; s_len[tid] = len; s_src[tid] = r.fp_offset;
+        if (len) { r.fp_offset = off; r.flags &= (uint8_t)~MFP_FLAG_HASHED; }
+        rec_out[tid] = r;
+    }
+    __syncthreads();
+    if ((uint64_t)total <= cap)
+        for (uint32_t j = wid; j < n; j += 16) {
+            const uint32_t L = s_len[j];
+            const uint8_t *sj = src + s_src[j];
+            uint8_t *dj = dst + s_off[j];
+            for (uint32_t k = lane; k < L; k += 64) dj[k] = sj[k];
+        }
+    for (uint32_t k = tid; k < an_words; k += 1024) an_out[k] = an[k];
+    for (uint32_t k = tid; k < ap_words; k += 1024) ap_out[k] = ap[k];
+    if (tid == 0) { used_out[0] = used[0]; used_out[1] = used[1]; used_out[2] = total; used_out[3] = used[3]; }
+    // used_out[4]: done -- every thread's host writes made visible first
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&used_out[4], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace mfpk
+
+// k_compact_small's launch: every *_out pointer is page-locked host memory
+// (hipHostMalloc) the device writes directly; an / ap may be null; used_host
+// holds 5 words, [4] set last (the host polls it)
+extern "C" int mfp_launch_compact_small(const mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst_host,
+                                        uint64_t cap, mfp_record *rec_host, const unsigned long long *used,
+                                        unsigned long long *used_host, const mfp_analysis *an, mfp_analysis *an_host,
+                                        const double *ap, double *ap_host, hipStream_t stream, mfp_prof *prof) {
+    static_assert(sizeof(mfp_analysis) % 8 == 0, "mfp_analysis copied as 8-byte words");
+    if (n == 0 || n > 1024) return -1;
+    const uint32_t an_words = an ? (uint32_t)(n * sizeof(mfp_analysis) / 8) : 0u;
+    const uint32_t ap_words = ap ? (uint32_t)(n * MFP_ATTR_DB_TAGS) : 0u;
+    if (prof) mfp_prof_begin(prof, "k_compact_small", stream);
+    hipLaunchKernelGGL(mfpk::k_compact_small, dim3(1), dim3(1024), 0, stream, rec, (uint32_t)n, src, dst_host, cap,
+                       rec_host, used, used_host, (const uint64_t *)an, (uint64_t *)an_host, an_words,
+                       (const uint64_t *)ap, (uint64_t *)ap_host, ap_words);
+    if (prof) mfp_prof_end(prof, stream);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // scratch: local = u32[n], block_sum = u64[(n + 255) / 256]; *total (device) =
 // the packed bytes

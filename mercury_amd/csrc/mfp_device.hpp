@@ -2064,6 +2064,8 @@ struct Cfg {
     uint32_t classify;   // stop after protocol identification (o.msg), emit nothing
     uint32_t seg;        // the caller wants the reassembly inputs (KParams::seg)
     uint32_t block;      // BLK_*: selected protocols outside this path that are identified first
+    uint32_t spread;     // k_fp_lds over a small batch: one packet per wave (lane 0), the packets'
+                         // walks side by side on separate SIMDs instead of divergent lanes of one wave
 };
 // Protocols the selection may name ("all" names every one) that this path does
 // not parse, but whose matchers or ports the reference consults before one of

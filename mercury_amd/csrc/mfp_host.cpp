@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -54,6 +55,11 @@ extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *sr
                                   unsigned long long *block_sum, unsigned long long *total, hipStream_t stream,
                                   mfp_prof *prof);
 
+
+extern "C" int mfp_launch_compact_small(const mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst_host,
+                                        uint64_t cap, mfp_record *rec_host, const unsigned long long *used,
+                                        unsigned long long *used_host, const mfp_analysis *an, mfp_analysis *an_host,
+                                        const double *ap, double *ap_host, hipStream_t stream, mfp_prof *prof);
 
 static thread_local std::string g_err;
 
@@ -402,7 +408,11 @@ struct Slot {
     bool seg_on = false;
     char *d_fp = nullptr; size_t cap_fp = 0;
     char *d_fp2 = nullptr; size_t cap_fp2 = 0;   // dense (compacted) fingerprints of a host batch
-    unsigned long long *h_used = nullptr;   // pinned copy of d_used
+    unsigned long long *h_used = nullptr;   // pinned copy of d_used ([4]: k_compact_small's done flag)
+    // the small-batch staging copy (mfp_process_small_pinned): counters
+    // (zeroed), descriptors and packets in one host-to-device transfer
+    uint8_t *d_small = nullptr; size_t cap_small = 0;
+    uint8_t *h_small = nullptr; size_t cap_h_small = 0;
     hipStream_t stream = nullptr;
     // pipelined device batches (mfp_analyze_batch_device_pipelined): the
     // batch's kernels done (on the caller's stream), the decision applied (on
@@ -420,7 +430,7 @@ struct Slot {
                hipMalloc(&d_bins, 16 * sizeof(unsigned long long)) == hipSuccess &&
                hipMalloc(&d_an_stats, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipMemset(d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
-               hipHostMalloc((void **)&h_used, 4 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
+               hipHostMalloc((void **)&h_used, 8 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
                hipEventCreateWithFlags(&ev_kernels, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&ev_resolved, hipEventDisableTiming) == hipSuccess &&
@@ -428,10 +438,11 @@ struct Slot {
     }
     void release() {
         void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
-                     d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2,
+                     d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2, d_small,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
-        for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec}) if (x) (void)hipHostFree(x);
+        for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec, (void *)h_small})
+            if (x) (void)hipHostFree(x);
         if (stream) (void)hipStreamDestroy(stream);
         for (hipEvent_t e : {ev_kernels, ev_resolved, ev_dev}) if (e) (void)hipEventDestroy(e);
     }
@@ -461,6 +472,12 @@ struct mfp_context_s {
     bool report_os = false;              // libmerc_config.report_os (mfp_analysis_report_os)
     bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
     Slot slot[4];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2: host pipeline
+    // the per-packet shim's concurrent small batches (mfp_process_small_pinned):
+    // each on a slot of its own, so batches of different callers overlap on the
+    // device; taken and returned under mu, waited for outside it
+    static constexpr int NSMALL = 8;
+    Slot small[NSMALL];
+    bool small_init[NSMALL] = {}, small_busy[NSMALL] = {};
     int pipe_next = 0;                   // mfp_analyze_batch_device_pipelined: the slot of the next batch (0 or 3)
     bool pipe_active = false;            // a pipelined batch may be pending in slot 0 or 3
     std::atomic<size_t> attr_names_len{SIZE_MAX};   // mfp_attribute_names_len
@@ -547,6 +564,7 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (c->clf) mfp_classifier_free(c->clf);
     if (c->own_prev) mfp_prevalence_destroy(c->own_prev);
     for (Slot &S : c->slot) S.release();
+    for (int j = 0; j < mfp_context_s::NSMALL; j++) if (c->small_init[j]) c->small[j].release();
     delete c->prof;
     delete c;
 }
@@ -593,9 +611,11 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
     return 0;
 }
 
+// d_bins: the classify pass's bin counts, already zeroed together with
+// d_fp_used (the small-batch staging copy); nullptr: the slot's, cleared here
 static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
-                                 hipStream_t s) {
+                                 hipStream_t s, unsigned long long *d_bins = nullptr) {
     HIPCHK(hipSetDevice(c->device));
     if (grow(S.d_work, S.cap_work, 11 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     if ((c->select & (SEL_QUIC | SEL_OPENVPN)) && !S.d_quic &&
@@ -604,15 +624,18 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
         mfp_set_error("device allocation failed (QUIC scratch)");
         return -2;
     }
-    HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(S.d_bins, 0, 16 * sizeof(unsigned long long), s));
+    if (!d_bins) {
+        HIPCHK(hipMemsetAsync(d_fp_used, 0, 4 * sizeof(unsigned long long), s));
+        HIPCHK(hipMemsetAsync(S.d_bins, 0, 16 * sizeof(unsigned long long), s));
+        d_bins = S.d_bins;
+    }
     mfp_tcp_seg *d_seg = nullptr;
     if (S.seg_on) {
         if (grow(S.d_seg, S.cap_seg, n + 1)) { mfp_set_error("device allocation failed"); return -2; }
         d_seg = S.d_seg;
     }
     if (mfp_launch_fingerprint(c->select, c->block, c->tls_format, c->mode, d_arena, d_desc, n, d_rec, d_seg, (uint8_t *)d_fp_arena,
-                               fp_cap, (unsigned long long *)d_fp_used, S.d_work, S.d_bins,
+                               fp_cap, (unsigned long long *)d_fp_used, S.d_work, d_bins,
                                c->strategy == MFP_STRATEGY_BINNED && n <= c->small_batch ? (int)MFP_STRATEGY_SMALL
                                                                                          : c->strategy,
                                c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
@@ -647,17 +670,19 @@ static int seen_reserve(Slot &S, size_t n, hipStream_t s) {
     return 0;
 }
 
-static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
-                          mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, double *d_attr_prob,
-                          hipStream_t s) {
-    Slot &S = c->slot[slot];
+// d_stats: the batch's counters, already zeroed (the small-batch staging
+// copy), and no sighting table -- the batch is decided on the host from its
+// records (resolve_on_host); nullptr: the slot's counters and table
+static int analyze_slot(mfp_context c, Slot &S, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
+                        mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, double *d_attr_prob,
+                        hipStream_t s, unsigned long long *d_stats) {
     HIPCHK(hipSetDevice(c->device));
     uint32_t nseg = 0, seg_cap = 0;
     mfp_analysis_segments(n, &nseg, &seg_cap);
     const size_t items = (size_t)nseg * seg_cap + 1;
     if (grow(S.d_pending, S.cap_pending, n + 1) || grow(S.d_work_items, S.cap_work_items, items) ||
         grow(S.d_lanel, S.cap_lanel, 4 * items) || grow(S.d_deferred, S.cap_deferred, 5 * items) ||
-        grow(S.d_segn, S.cap_segn, 3 * (size_t)nseg + 1) || seen_reserve(S, n, s)) {
+        grow(S.d_segn, S.cap_segn, 3 * (size_t)nseg + 1) || (!d_stats && seen_reserve(S, n, s))) {
         mfp_set_error("device allocation failed");
         return -2;
     }
@@ -667,13 +692,22 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
         mfp_set_error("device allocation failed");
         return -2;
     }
-    HIPCHK(hipMemsetAsync(S.d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long), s));
-    if (mfp_launch_analysis(D, &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out, d_attr_prob,
-                            S.d_pending, S.d_work_items, S.d_lanel, S.d_deferred, S.d_segn, S.d_an_stats, c->mode,
+    if (!d_stats) HIPCHK(hipMemsetAsync(S.d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long), s));
+    if (mfp_launch_analysis(D, d_stats ? nullptr : &S.seen, d_arena, d_desc, n, d_rec, (const uint8_t *)d_fp_arena, d_out,
+                            d_attr_prob, S.d_pending, S.d_work_items, S.d_lanel, S.d_deferred, S.d_segn,
+                            d_stats ? d_stats : S.d_an_stats, c->mode,
                             c->an_lane_max_p, S.d_huge, s, c->prof) != 0) {
         mfp_set_error("analysis kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
+    return 0;
+}
+static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
+                          mfp_record *d_rec, const char *d_fp_arena, mfp_analysis *d_out, double *d_attr_prob,
+                          hipStream_t s) {
+    Slot &S = c->slot[slot];
+    const int r = analyze_slot(c, S, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, s, nullptr);
+    if (r) return r;
     c->an_slot = slot;
     S.pend.live = true;
     S.pend.n = n; S.pend.rec = d_rec; S.pend.fp = d_fp_arena; S.pend.out = d_out; S.pend.stream = s;
@@ -855,16 +889,11 @@ static int slot_resolve_host(mfp_context c, Slot &S, mfp_analysis *an, const mfp
     return 0;
 }
 
-// copy a host batch into slot `slot` (grown as needed) and launch its kernels
-// on the slot's stream; descriptors keep their offsets: the device arena
-// pointer handed to the kernels is the staging buffer minus the (256-byte
-// aligned) start of the copied span
-static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
-                            size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false) {
-    Slot &S = c->slot[slot];
-    // device-pointer calls may still be using this slot's scratch on the caller's stream
-    if (S.dev_recorded) { HIPCHK(hipStreamWaitEvent(S.stream, S.ev_dev, 0)); S.dev_recorded = false; }
-    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+// the bytes a host batch's descriptors span: [lo, hi) (lo 256-byte aligned)
+// and the packet bytes in it (a QUIC packet's reassembled CRYPTO data included)
+static int batch_span(const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc, size_t n, uint64_t &lo,
+                      uint64_t &hi, uint64_t &total) {
+    lo = UINT64_MAX; hi = 0; total = 0;
     for (size_t i = 0; i < n; i++) {
         uint64_t end = desc[i].offset + desc[i].caplen;
         if (desc[i].flags & MFP_DESC_QUIC_CRYPTO) {
@@ -881,14 +910,28 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
         hi = std::max<uint64_t>(hi, end);
         total += desc[i].caplen;
     }
+    if (n == 0) lo = hi = 0;   // (a capture ring hands packets in arena order; this scan is a few ms per 1M)
+    lo &= ~(uint64_t)255;
+    if (hi > arena_len) { mfp_set_error("descriptor past the end of the arena"); return -1; }
+    return 0;
+}
+
+// copy a host batch into slot `slot` (grown as needed) and launch its kernels
+// on the slot's stream; descriptors keep their offsets: the device arena
+// pointer handed to the kernels is the staging buffer minus the (256-byte
+// aligned) start of the copied span
+static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                            size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false) {
+    Slot &S = c->slot[slot];
+    // device-pointer calls may still be using this slot's scratch on the caller's stream
+    if (S.dev_recorded) { HIPCHK(hipStreamWaitEvent(S.stream, S.ev_dev, 0)); S.dev_recorded = false; }
+    uint64_t lo, hi, total;
+    if (batch_span(arena, arena_len, desc, n, lo, hi, total)) return -1;
     // the device arena holds the strings at their reserved slots (the TLS
     // ClientHello bin reserves by an upper bound, k_fp_tls1): sized by the
     // bound, whatever the caller's dense capacity; the callers check that the
     // packed strings fit theirs
     const size_t dcap = std::max(fp_cap, mfp_fp_arena_bound(n, total));
-    if (n == 0) lo = hi = 0;   // (a capture ring hands packets in arena order; this scan is a few ms per 1M)
-    lo &= ~(uint64_t)255;
-    if (hi > arena_len) { mfp_set_error("descriptor past the end of the arena"); return -1; }
     const uint64_t span = hi - lo;
     // 64 bytes of padding after the span: the kernels read the aligned block
     // that holds a packet's last byte
@@ -976,6 +1019,116 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
     if (used > spec) HIPCHK(hipMemcpy(fp_arena + spec, S.d_fp2 + spec, used - spec, hipMemcpyDeviceToHost));
     if (host_resolve) {
+        const int rr = resolve_on_host(c, S, analysis, rec, fp_arena, n);
+        if (rr) return rr;
+    }
+    return (long long)used;
+}
+
+// The per-packet shim's batch (mfp_libmerc.cpp run_batch): every buffer is
+// page-locked host memory (hipHostMalloc), so the batch is one transfer in --
+// counters (zeroed by the copy itself), descriptors and packets staged
+// together -- the walker, the classifier when asked, and one kernel that writes
+// the packed strings, the records and the results straight into the caller's
+// buffers: one host-to-device copy, no memsets, no copies back, one wait.
+// Same results as mfp_process_batch_host_ex, which it defers to for anything
+// else (larger batches, deferred decisions, reassembly contexts).
+long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                                   size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                   double *attr_prob) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    if (n == 0 || n > c->small_batch || n > 1024 || c->defer || (analysis && !c->clf) || getenv("MFP_SMALL_COPIES"))
+        return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, attr_prob);
+    if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
+    uint64_t lo, hi, total;
+    if (batch_span(arena, arena_len, desc, n, lo, hi, total)) return -1;
+    int k = -1;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        if (analysis) { const int fr = flush_pipelined_locked(c); if (fr) return fr; }
+        for (int j = 0; j < mfp_context_s::NSMALL && k < 0; j++) {
+            if (c->small_busy[j]) continue;
+            if (!c->small_init[j]) {
+                if (!c->small[j].init()) { mfp_set_error("small-batch slot: HIP allocation failed"); return -2; }
+                c->small_init[j] = true;
+            }
+            c->small_busy[j] = true;
+            k = j;
+        }
+    }
+    // every slot taken (more concurrent callers than NSMALL): the copying path
+    if (k < 0) return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, attr_prob);
+    struct Give {   // the slot goes back on every exit (its next batch is ordered behind this one on its stream)
+        mfp_context c; int k;
+        ~Give() {
+            std::lock_guard<std::mutex> lk(c->mu);
+            c->small_busy[k] = false;
+        }
+    } give{c, k};
+    Slot &S = c->small[k];
+    const size_t dcap = std::max(fp_cap, mfp_fp_arena_bound(n, total));
+    // staging layout: [fp counters 4 | bin counts 16 | classifier counters] [descriptors] [packets + 64]
+    constexpr size_t W = 8;
+    const size_t n_cnt = 4 + 16 + MFP_AN_STATS_WORDS;
+    const size_t at_desc = (n_cnt * W + 255) & ~(size_t)255;
+    const size_t at_pkt = (at_desc + n * sizeof(mfp_pkt_desc) + 255) & ~(size_t)255;
+    const uint64_t copy = std::min<uint64_t>(hi - lo + 16, arena_len - lo);
+    const size_t bytes = at_pkt + copy;
+    {
+        // launches under mu: the classifier tables and the context's
+        // configuration are shared with the other slots' calls
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        if (grow(S.d_small, S.cap_small, bytes + 64) || grow(S.d_rec, S.cap_rec, n + 1) ||
+            grow(S.d_fp, S.cap_fp, dcap + 64) || (analysis && grow(S.d_an, S.cap_an, n + 1)) ||
+            (analysis && attr_prob && grow(S.d_ap, S.cap_ap, MFP_ATTR_DB_TAGS * (n + 1)))) {
+            mfp_set_error("device allocation failed");
+            return -2;
+        }
+        if (grow_pinned(S.h_small, S.cap_h_small, bytes + 64)) { mfp_set_error("host allocation failed"); return -2; }
+        memset(S.h_small, 0, at_desc);
+        __atomic_store_n(&S.h_used[4], 0ull, __ATOMIC_RELAXED);   // set by k_compact_small when all is written
+        memcpy(S.h_small + at_desc, desc, n * sizeof(mfp_pkt_desc));
+        memcpy(S.h_small + at_pkt, arena + lo, copy);
+        HIPCHK(hipMemcpyAsync(S.d_small, S.h_small, bytes, hipMemcpyHostToDevice, S.stream));
+        auto *d_used = (unsigned long long *)S.d_small;
+        const mfp_pkt_desc *d_desc = (const mfp_pkt_desc *)(S.d_small + at_desc);
+        const uint8_t *d_base = S.d_small + at_pkt - lo;
+        int r = process_device_locked(c, S, d_base, d_desc, n, S.d_rec, S.d_fp, dcap, (uint64_t *)d_used, S.stream,
+                                      d_used + 4);
+        if (r) return r;
+        if (analysis) {
+            r = analyze_slot(c, S, d_base, d_desc, n, S.d_rec, S.d_fp, S.d_an, attr_prob ? S.d_ap : nullptr, S.stream,
+                             d_used + 20);
+            if (r) return r;
+        }
+        if (mfp_launch_compact_small(S.d_rec, n, (const uint8_t *)S.d_fp, (uint8_t *)fp_arena, fp_cap, rec, d_used,
+                                     S.h_used, analysis ? S.d_an : nullptr, analysis,
+                                     analysis && attr_prob ? S.d_ap : nullptr, attr_prob, S.stream, c->prof) != 0) {
+            mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return -3;
+        }
+    }
+    // the batch is done when k_compact_small's flag lands in host memory (its
+    // writes before it): no wake-up through the runtime; a batch not done
+    // within 2 ms waits on the stream, which also reports a failed launch
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        bool done = false;
+        for (uint32_t spin = 0; !done; spin++) {
+            done = __atomic_load_n(&S.h_used[4], __ATOMIC_ACQUIRE) != 0;
+            if (!done && (spin & 255) == 255 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+                break;
+        }
+        if (!done) HIPCHK(hipStreamSynchronize(S.stream));
+    }
+    const unsigned long long used = S.h_used[2];
+    if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    // decided on the host from the records (the prevalence LRU has its own
+    // lock; concurrent callers' batches are decided in the order they finish)
+    if (analysis) {
         const int rr = resolve_on_host(c, S, analysis, rec, fp_arena, n);
         if (rr) return rr;
     }

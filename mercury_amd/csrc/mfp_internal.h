@@ -35,3 +35,8 @@ size_t mfp_attribute_names_len(mfp_context c);
 // (D)TLS ClientHello records with MFP_XF_TLS_UA: the ALPN list re-read from
 // the packet (mfp_json.cpp)
 bool mfp_hello_alpn(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, const uint8_t **alpn, uint32_t *len);
+// mfp_process_batch_host_ex for the per-packet shim's small batches, whose
+// buffers are all page-locked (mfp_host.cpp)
+long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                                   size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
+                                   double *attr_prob);

@@ -140,7 +140,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
     } while (0)
     if (n == 0) return 0;
     mfp::KParams P;
-    P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0;
+    P.cfg.select = select; P.cfg.tls_format = tls_format; P.cfg.mode = mode; P.cfg.classify = 0; P.cfg.spread = 0;
     P.cfg.seg = seg ? 1u : 0u;
     P.cfg.block = block;
     P.arena = arena; P.desc = desc; P.n = n; P.rec = rec; P.fp_arena = fp_arena; P.fp_cap = fp_cap;
@@ -165,15 +165,17 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
         return launch_quic();
     }
     if (strategy == MFP_STRATEGY_SMALL) {
-        // the whole batch through the all-family LDS walker, then the
-        // fallback lane over what it handed back (packets past its stage,
-        // QUIC / OpenVPN on their way to k_quic)
+        // the whole batch through the all-family LDS walker (then k_quic
+        // over the QUIC / OpenVPN packets it queued)
         uint32_t *fallback = work + (uint64_t)mfp::NBINS * n;
-        const uint64_t lb = (n + 63) / 64 < 2048 ? (n + 63) / 64 : 2048;
+        // (one packet per wave: a batch's walk takes as long as its slowest
+        // packet, not the sum of the protocols its lanes diverge over)
+        P.cfg.spread = 1;
+        const uint64_t lb = n < 2048 ? n : 2048;
         if (mfp_launch_bin_all(&P, fallback, 1, "k_fp_lds/small", (uint32_t)lb, 0, stream, prof) != 0) return -1;
-        P.idx = fallback;
-        P.count = fp_used + 3;
-        if (mfp_launch_bin_all(&P, nullptr, 0, "k_fingerprint/fallback", 0, (uint32_t)tiles, stream, prof) != 0) return -1;
+        P.cfg.spread = 0;
+        // (spread: the walker handled its large packets and queued its QUIC
+        // and OpenVPN packets itself -- no fallback lane)
         return launch_quic();
     }
     // classify, then one launch per protocol bin over its index list: the

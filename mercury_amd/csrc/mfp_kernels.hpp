@@ -569,16 +569,23 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
     __builtin_amdgcn_wave_barrier();
     // (idx == nullptr: the whole batch, MFP_STRATEGY_SMALL)
     const uint64_t count = P.idx ? (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P.n;
-    for (uint64_t g = blockIdx.x; g * 64 < count; g += gridDim.x) {
-        const uint64_t t = g * 64 + lane;
-        const bool live = t < count;
+#ifdef MFP_PROBE_REPEAT   // (latency probe: the whole walk R times in the same wave)
+    for (int rep_ = 0; rep_ < MFP_PROBE_REPEAT; rep_++)
+#endif
+    const bool spread = P.cfg.spread != 0;   // (P.idx == nullptr then)
+    for (uint64_t g = blockIdx.x; (spread ? g : g * 64) < count; g += gridDim.x) {
+        const uint64_t t = spread ? g : g * 64 + lane;
+        const bool live = spread ? lane == 0 : t < count;
         const uint64_t i = live ? (P.idx ? (uint64_t)P.idx[t] : t) : 0;
         mfp_pkt_desc dsc;
         if (live) dsc = P.desc[i];
         else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
         const uint32_t a16 = (uint32_t)(dsc.offset & 15);
         const uint32_t pk_bytes = (a16 + dsc.caplen + 15) & ~15u;      // whole 16-byte blocks
-        const uint32_t need = pk_bytes;
+        // spread (one packet per wave): a packet larger than the stage is
+        // walked straight from global memory by its own wave, not handed on
+        const bool glob = spread && live && pk_bytes > STG;
+        const uint32_t need = glob ? 0u : pk_bytes;
         const bool big = live && need > STG;
         {   // too large for any sub-round: the fallback lane walks it from HBM
             const uint64_t bm = __ballot(big);
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
             const bool in = todo && incl <= STG;
             const uint32_t sbase = incl - x;
             // stage: one packet after the other, 1 KiB per wave-instruction
-            for (uint64_t m = __ballot(in); m; m &= m - 1) {
+            for (uint64_t m = __ballot(in && !glob); m; m &= m - 1) {
                 const int j = __builtin_ctzll(m);
                 const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)sbase, j);
                 const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)pk_bytes, j) >> 4;
@@ -619,7 +626,7 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
-            const uint8_t *data = stg + sbase + a16;
+            const uint8_t *data = glob ? P.arena + dsc.offset : stg + sbase + a16;
 
             Out o;
             uint32_t len = 0;
@@ -673,7 +680,12 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
                                             ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(b >> 32), 0, 64) << 32);
             const bool fits = base != ~0ull;
             const uint32_t excl = sincl - slot;
-            {
+            if (spread && FAM == FAM_ALL && !SEGMODE) {
+                // every family is here: the only punts are QUIC and OpenVPN,
+                // for k_quic's list (as the fallback lane would hand them on);
+                // so a small batch launches no fallback kernel
+                if (fb) P.quic_idx[atomicAdd(P.quic_count, 1ull)] = (uint32_t)i;
+            } else {
                 const uint64_t fbm = __ballot(fb);
                 if (fbm) {
                     uint32_t fb0 = 0;
@@ -698,7 +710,11 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
                     if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
                 }
             } else {
+#ifdef MFP_PROBE_LDS_NOEMIT   // (latency probe: the length walk only)
+                if (false) {
+#else
                 if (len && fits) {
+#endif
                     Em<true> e;
                     e.begin(P.fp_arena + base + excl, out_line[lane]);
                     if (plan.ok) {

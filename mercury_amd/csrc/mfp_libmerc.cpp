@@ -174,7 +174,7 @@ MFP_EXPORT mercury_context mercury_init(const struct libmerc_config *vars, int v
 
 MFP_EXPORT int mercury_finalize(mercury_context mc) {
     if (!mc) return -1;
-    if (getenv("MFP_SHIM_STATS"))
+    if (const char *e = getenv("MFP_SHIM_STATS"); e && atoi(e) >= 2)
         for (auto &c : mc->ctx) if (c) print_kernel_stats(c);
     for (auto &c : mc->ctx) if (c) mfp_finalize(c);
     free_combiners(mc);
@@ -193,7 +193,8 @@ static mfp_context get_ctx(mercury *m, int mode) {
             mfp_analysis_set_prevalence(c, m->prev);
             mfp_analysis_report_os(c, m->report_os ? 1 : 0);
         }
-        if (getenv("MFP_SHIM_STATS")) mfp_profile_enable(c, 1);   // kernel times, printed by mercury_finalize
+        // MFP_SHIM_STATS=2: kernel times too (two events per launch: not for timing runs)
+        if (const char *e = getenv("MFP_SHIM_STATS"); e && atoi(e) >= 2) mfp_profile_enable(c, 1);
         m->ctx[mode] = c;
     }
     return m->ctx[mode];
@@ -325,16 +326,19 @@ static void fill_zero_ts(struct timespec *ts) {
 // ---------------------------------------------------------------------------
 // Combining: libmerc's API is one packet per call, one processor per thread
 // (libmerc.h:227-231).  Each call on the device path is a batch of its own --
-// a copy in, a dozen kernel launches, a copy out -- so concurrent calls of
-// different processors are combined: a call queues its packet; the first
-// caller to find no batch in flight becomes the leader, takes every queued
-// packet (its own included), runs them as one batch on the shared context and
-// completes each caller's result; callers that arrive meanwhile wait and form
-// the next batch.  One thread calling alone pays one batch per packet, N
-// threads share batches of up to N packets.  Batches keep the arrival order,
-// which orders the fingerprint-prevalence LRU updates as the reference's shared
-// classifier sees concurrent calls.  (Processors with "reassembly" keep their
-// own flow table and run their packets one by one.)
+// a copy in, a few kernel launches, one wait -- so concurrent calls of
+// different processors are combined: a call queues its packet; a caller that
+// finds fewer than max_leaders batches in flight becomes a leader, takes every
+// queued packet (its own included), runs them as one batch on a small-batch
+// slot of the shared context and completes each caller's result; callers that
+// arrive meanwhile wait and form the next batch, which may run beside it.  One
+// thread calling alone pays one batch per packet, N threads share batches.  A
+// batch keeps its packets' arrival order, and each thread's calls are decided
+// against the fingerprint-prevalence LRU in its own call order; batches in
+// flight together are decided in the order they finish, as the reference's
+// shared classifier sees concurrent threads in whichever order they reach it.
+// (Processors with "reassembly" keep their own flow table and run their
+// packets one by one.)
 // ---------------------------------------------------------------------------
 struct Req {
     const uint8_t *pkt;
@@ -386,15 +390,8 @@ struct PinnedVec {
 };
 }  // extern "C++"
 
-struct Combiner {
-    std::mutex m;
-    std::condition_variable cv;
-    std::vector<Req *> q;
-    bool busy = false;
-    // MFP_SHIM_STATS: batches, packets, nanoseconds in the device batch / the
-    // records and JSON text (printed by mercury_finalize)
-    uint64_t st_batches = 0, st_pkts = 0, st_dev_ns = 0, st_host_ns = 0;
-    // the leader's batch buffers (one leader at a time), page-locked
+// one leader's batch buffers, page-locked
+struct Bufs {
     PinnedVec<uint8_t> arena;
     PinnedVec<mfp_pkt_desc> desc;
     PinnedVec<mfp_record> rec;
@@ -405,7 +402,29 @@ struct Combiner {
     std::vector<char> out;
 };
 
-static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req *> &batch, bool json_entry) {
+struct Combiner {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<Req *> q;
+    // leaders running a batch now: up to max_leaders at once, each on a
+    // small-batch slot of its own (mfp_process_small_pinned), so the batches
+    // of concurrent callers overlap on the device instead of queueing behind
+    // one batch in flight (MFP_SHIM_LEADERS)
+    int active = 0, max_leaders = 4;
+    std::vector<Bufs *> pool;       // idle leaders' buffers
+    // MFP_SHIM_STATS: batches, packets, nanoseconds in the device batch / the
+    // records and JSON text (printed by mercury_finalize)
+    uint64_t st_batches = 0, st_pkts = 0, st_dev_ns = 0, st_host_ns = 0;
+    Combiner() {
+        if (const char *e = getenv("MFP_SHIM_LEADERS")) max_leaders = std::max(1, atoi(e));
+    }
+    ~Combiner() { for (Bufs *b : pool) delete b; }
+};
+
+struct BatchTimes { uint64_t dev_ns = 0, host_ns = 0; };
+
+static void run_batch(mercury *m, mfp_context ctx, Bufs &C, std::vector<Req *> &batch, bool json_entry,
+                      BatchTimes &bt) {
     const size_t n = batch.size();
     C.arena.clear();
     C.desc.resize(n);
@@ -436,20 +455,23 @@ static void run_batch(mercury *m, mfp_context ctx, Combiner &C, std::vector<Req 
         memset(C.ap.data(), 0, n * MFP_ATTR_DB_TAGS * sizeof(double));
     }
     const auto t0 = std::chrono::steady_clock::now();
-    const long long used = mfp_process_batch_host_ex(ctx, C.arena.data(), C.arena.size(), C.desc.data(), n, C.rec.data(),
-                                                     C.fp.data(), cap, want_an ? C.an.data() : nullptr,
-                                                     want_an ? C.ap.data() : nullptr);
+    // page-locked buffers throughout: the device writes the results into them
+    // (mfp_process_small_pinned); a buffer that could not be pinned takes the
+    // copying path
+    const bool pinned = C.arena.pinned && C.desc.pinned && C.rec.pinned && C.fp.pinned &&
+                        (!want_an || (C.an.pinned && C.ap.pinned));
+    auto *const process = pinned ? mfp_process_small_pinned : mfp_process_batch_host_ex;
+    const long long used = process(ctx, C.arena.data(), C.arena.size(), C.desc.data(), n, C.rec.data(), C.fp.data(), cap,
+                                   want_an ? C.an.data() : nullptr, want_an ? C.ap.data() : nullptr);
     const auto t1 = std::chrono::steady_clock::now();
-    C.st_batches++;
-    C.st_pkts += n;
-    C.st_dev_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    bt.dev_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     struct HostClock {
-        Combiner &C; std::chrono::steady_clock::time_point t;
+        BatchTimes &bt; std::chrono::steady_clock::time_point t;
         ~HostClock() {
-            C.st_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+            bt.host_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                 std::chrono::steady_clock::now() - t).count();
         }
-    } host_clock{C, t1};
+    } host_clock{bt, t1};
     if (used < 0) {
         log_error("%s\n", mfp_last_error());
         for (Req *r : batch) r->err = true;
@@ -521,27 +543,36 @@ static void submit(mercury *m, mfp_context ctx, int mode, Req &r) {
     std::unique_lock<std::mutex> lk(C->m);
     C->q.push_back(&r);
     while (!r.done) {
-        if (!C->busy) {
-            C->busy = true;
+        if (C->active < C->max_leaders && !C->q.empty()) {
+            C->active++;
             std::vector<Req *> batch;
             batch.swap(C->q);
+            Bufs *B = nullptr;
+            if (!C->pool.empty()) { B = C->pool.back(); C->pool.pop_back(); }
             lk.unlock();
+            BatchTimes bt;
             // the leader hands the batch back on every exit path: an exception
             // out of run_batch (an allocation of the staging vectors) fails the
-            // batch's calls instead of leaving busy set and the waiters asleep,
-            // and never crosses the extern "C" boundary (libmerc.cc:145-149
-            // turns exceptions into 0 / NULL the same way)
+            // batch's calls instead of leaving the leader counted and the
+            // waiters asleep, and never crosses the extern "C" boundary
+            // (libmerc.cc:145-149 turns exceptions into 0 / NULL the same way)
             struct Release {
-                Combiner *C; std::unique_lock<std::mutex> &lk; std::vector<Req *> &batch;
+                Combiner *C; std::unique_lock<std::mutex> &lk; std::vector<Req *> &batch; Bufs *&B; BatchTimes &bt;
                 ~Release() {
                     lk.lock();
                     for (Req *x : batch) x->done = true;
-                    C->busy = false;
+                    if (B) C->pool.push_back(B);
+                    C->active--;
+                    C->st_batches++;
+                    C->st_pkts += batch.size();
+                    C->st_dev_ns += bt.dev_ns;
+                    C->st_host_ns += bt.host_ns;
                     C->cv.notify_all();
                 }
-            } release{C, lk, batch};
+            } release{C, lk, batch, B, bt};
             try {
-                run_batch(m, ctx, *C, batch, mode == MFP_MODE_WRITE_JSON);
+                if (!B) B = new Bufs;
+                run_batch(m, ctx, *B, batch, mode == MFP_MODE_WRITE_JSON, bt);
             } catch (const std::exception &e) {
                 log_error("per-packet batch failed: %s\n", e.what());
                 for (Req *x : batch) x->err = true;
