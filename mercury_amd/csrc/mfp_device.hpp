@@ -327,6 +327,7 @@ struct Em {
     TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
     static constexpr bool emit_pass() { return EMIT; }
+    bool spans = false;      // an emitting walk that is the only walk: it also records the hello's spans
     // Pass-2 output.  The string starts 16-byte aligned and owns its slot
     // rounded up to 16 bytes.  Bytes gather in `acc`; whole 8-byte words go
     // to a per-lane line of LINEW words in LDS, and a full line leaves as
@@ -478,6 +479,7 @@ struct SegEm {
     const HdrKey *keys_req = nullptr, *keys_resp = nullptr;
     static constexpr bool PLAN = false;
     static constexpr bool emit_pass() { return false; }
+    static constexpr bool spans = false;
     uint32_t n = 0;                     // characters produced
     bool last_putc = false;
     bool ovf = false;
@@ -2397,7 +2399,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         } else {
             fp_type_prefix(b, 1);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
-            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
+            if (!E::emit_pass() || b.spans) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
         }
         return;
         }
@@ -2686,7 +2688,7 @@ DEV void udp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *base) {
         } else {
             fp_type_prefix(b, 10);
             tls_ch_fp(b, ch, (int)cfg.tls_format);
-            if (!E::emit_pass()) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
+            if (!E::emit_pass() || b.spans) tls_sni(ch.extensions, base, o.sni_off, o.sni_len, o.ua_off, o.ua_len, o.xflags);
         }
     } else if (msg == MFP_MSG_DTLS_SH) {
         Cur b2 = body;

@@ -627,6 +627,16 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
             const uint8_t *data = glob ? P.arena + dsc.offset : stg + sbase + a16;
+            // spread, a packet that leaves room in the stage for its string:
+            // a single walk that emits as it goes (`one`), the wave copying the
+            // string out afterwards, instead of a counting walk and an emitting
+            // walk one after the other (a lone packet's latency)
+            constexpr uint32_t EBUF = FP_MAX + 64;
+            constexpr bool ONE_OK = !SEGMODE && FAM == FAM_ALL;   // (the small-batch instance)
+            const uint32_t e_at = (sbase + pk_bytes + 63) & ~63u;
+            const bool one = ONE_OK && spread && !glob && e_at + EBUF <= STG;
+            uint8_t *const ebuf = stg + e_at;
+            uint64_t one_hash = 0;
 
             Out o;
             uint32_t len = 0;
@@ -647,7 +657,27 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
                     nseg = e.nseg;
                 }
             } else {
-                if (in) {
+                bool walked = false;
+                if constexpr (ONE_OK) {
+                    if (in && one) {
+                        // one pass: the string is written into the stage behind the
+                        // packet while the walk counts it (capped at FP_MAX + a line)
+                        Em<true> e;
+                        e.begin(ebuf, out_line[lane]);
+                        e.out_end = ebuf + EBUF;
+                        e.spans = true;
+                        packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
+                        e.finish();
+                        fb = e.punt;
+                        if (o.fp_type && !fb) {
+                            if (e.valid()) len = e.n;
+                            else o.fp_type = 0;    // fingerprint::final drops truncated fingerprints
+                        }
+                        one_hash = e.hash();
+                        walked = true;
+                    }
+                }
+                if (in && !walked) {
                     Em<false> e;
                     e.plan = &plan;
                     packet_walk<FAM>(e, P.cfg, o, data, dsc.caplen, dsc.linktype);
@@ -709,12 +739,20 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
                     h = wave_xor64(h);
                     if (lane == 0) *(uint64_t *)(out + ((T + 7) & ~7u)) = mfpc::hash_final(h, T);
                 }
+            } else if (ONE_OK && spread && __builtin_amdgcn_readfirstlane((int)one)) {
+                // (spread: lane 0 holds the wave's one packet) the string, with
+                // its hash behind it, from the stage to the arena by the wave
+                const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)(fits ? len : 0u));
+                if (L) {
+                    const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)excl);
+                    const uint32_t L8 = (L + 7) & ~7u;
+                    uint64_t *dw = (uint64_t *)(P.fp_arena + base + ex);
+                    const uint64_t *sw = (const uint64_t *)ebuf;
+                    for (uint32_t k = lane; 8 * k < L8; k += 64) dw[k] = sw[k];
+                    if (lane == 0) dw[L8 / 8] = one_hash;
+                }
             } else {
-#ifdef MFP_PROBE_LDS_NOEMIT   // (latency probe: the length walk only)
-                if (false) {
-#else
                 if (len && fits) {
-#endif
                     Em<true> e;
                     e.begin(P.fp_arena + base + excl, out_line[lane]);
                     if (plan.ok) {
