@@ -3020,6 +3020,12 @@ struct KParams {
     const unsigned long long *count;
     uint32_t *quic_idx;              // QUIC packets found by the walkers, for k_quic (count *quic_count)
     unsigned long long *quic_count;
+    // spread small batch written straight into page-locked host buffers
+    // (mfp_process_small_pinned): the waves count themselves done in *fin;
+    // the last copies fp_used to host_out[0..3], resets the counters for
+    // the slot's next batch and sets host_out[4] (nullptr: not this mode)
+    unsigned long long *fin;
+    unsigned long long *host_out;
 };
 // the reassembly inputs of packet i (when the caller asked for them)
 DEV void write_seg(const KParams &P, uint64_t i, const Out &o) {

@@ -48,7 +48,8 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
                                       uint32_t bin_lds_mask, uint32_t quic_format, uint8_t *quic_scratch,
-                                      uint32_t quic_grid, hipStream_t stream, mfp_prof *prof);
+                                      uint32_t quic_grid, hipStream_t stream, mfp_prof *prof,
+                                      unsigned long long *fin = nullptr, unsigned long long *host_out = nullptr);
 extern "C" size_t mfp_quic_scratch_bytes(uint32_t grid);
 
 extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst, uint32_t *local,
@@ -413,6 +414,11 @@ struct Slot {
     // (zeroed), descriptors and packets in one host-to-device transfer
     uint8_t *d_small = nullptr; size_t cap_small = 0;
     uint8_t *h_small = nullptr; size_t cap_h_small = 0;
+    // the direct small batch's device counters (fp_used 4, bins 16, waves
+    // done 1), zero between batches: the batch's last wave resets them;
+    // cnt_dirty after a batch that may not have finished them
+    unsigned long long *d_cnt = nullptr;
+    bool cnt_dirty = false;
     hipStream_t stream = nullptr;
     // pipelined device batches (mfp_analyze_batch_device_pipelined): the
     // batch's kernels done (on the caller's stream), the decision applied (on
@@ -430,6 +436,8 @@ struct Slot {
                hipMalloc(&d_bins, 16 * sizeof(unsigned long long)) == hipSuccess &&
                hipMalloc(&d_an_stats, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
                hipMemset(d_an_stats, 0, MFP_AN_STATS_WORDS * sizeof(unsigned long long)) == hipSuccess &&
+               hipMalloc(&d_cnt, 24 * sizeof(unsigned long long)) == hipSuccess &&
+               hipMemset(d_cnt, 0, 24 * sizeof(unsigned long long)) == hipSuccess &&
                hipHostMalloc((void **)&h_used, 8 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
                hipEventCreateWithFlags(&ev_kernels, hipEventDisableTiming) == hipSuccess &&
@@ -438,7 +446,7 @@ struct Slot {
     }
     void release() {
         void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
-                     d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2, d_small,
+                     d_an, d_ap, d_arena, d_desc, d_rec, d_seg, d_fp, d_fp2, d_small, d_cnt,
                      seen.slots, seen.list, seen.counters, d_sight, d_seen_bits, d_group_off, d_seq};
         for (void *x : p) if (x) (void)hipFree(x);
         for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec, (void *)h_small})
@@ -615,7 +623,8 @@ extern "C" MFP_EXPORT int mfp_reserve(mfp_context c, size_t n) {
 // d_fp_used (the small-batch staging copy); nullptr: the slot's, cleared here
 static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena, const mfp_pkt_desc *d_desc, size_t n,
                                  mfp_record *d_rec, char *d_fp_arena, size_t fp_cap, uint64_t *d_fp_used,
-                                 hipStream_t s, unsigned long long *d_bins = nullptr) {
+                                 hipStream_t s, unsigned long long *d_bins = nullptr, unsigned long long *fin = nullptr,
+                                 unsigned long long *host_out = nullptr) {
     HIPCHK(hipSetDevice(c->device));
     if (grow(S.d_work, S.cap_work, 11 * n + 2)) { mfp_set_error("device allocation failed"); return -2; }
     if ((c->select & (SEL_QUIC | SEL_OPENVPN)) && !S.d_quic &&
@@ -639,7 +648,7 @@ static int process_device_locked(mfp_context c, Slot &S, const uint8_t *d_arena,
                                c->strategy == MFP_STRATEGY_BINNED && n <= c->small_batch ? (int)MFP_STRATEGY_SMALL
                                                                                          : c->strategy,
                                c->bin_seg_mask, c->bin_lds_mask, c->quic_format, S.d_quic, c->quic_grid, s,
-                               c->prof) != 0) {
+                               c->prof, fin, host_out) != 0) {
         mfp_set_error("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
@@ -1025,6 +1034,19 @@ extern "C" MFP_EXPORT long long mfp_process_batch_host_ex(mfp_context c, const u
     return (long long)used;
 }
 
+// A small batch is done when its last kernel's flag (S.h_used[4]) lands in
+// host memory, its writes before it: no wake-up through the runtime; a batch
+// not done within 2 ms waits on the stream, which also reports a failed launch
+static int wait_done_flag(Slot &S) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; spin++) {
+        if (__atomic_load_n(&S.h_used[4], __ATOMIC_ACQUIRE) != 0) return 0;
+        if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
+    HIPCHK(hipStreamSynchronize(S.stream));
+    return 0;
+}
+
 // The per-packet shim's batch (mfp_libmerc.cpp run_batch): every buffer is
 // page-locked host memory (hipHostMalloc), so the batch is one transfer in --
 // counters (zeroed by the copy itself), descriptors and packets staged
@@ -1067,6 +1089,30 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
         }
     } give{c, k};
     Slot &S = c->small[k];
+    // Fingerprints only (no classifier, no k_quic): the walker reads the
+    // caller's page-locked packets in place and writes records and strings
+    // straight into the caller's buffers -- one launch, no copies at all
+    // (strings at their reserved, not packed, offsets; at least 64 bytes
+    // after the last packet, which the walker may read)
+    const bool direct = !analysis && !(c->select & (SEL_QUIC | SEL_OPENVPN)) && hi + 64 <= arena_len &&
+                        fp_cap >= mfp_fp_arena_bound(n, total) && !getenv("MFP_SMALL_STAGED");
+    if (direct) {
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            HIPCHK(hipSetDevice(c->device));
+            if (S.cnt_dirty) HIPCHK(hipMemsetAsync(S.d_cnt, 0, 24 * sizeof(unsigned long long), S.stream));
+            S.cnt_dirty = true;   // until the batch's last wave has reset them
+            __atomic_store_n(&S.h_used[4], 0ull, __ATOMIC_RELAXED);
+            const int r = process_device_locked(c, S, arena, desc, n, rec, fp_arena, fp_cap, (uint64_t *)S.d_cnt, S.stream,
+                                                S.d_cnt + 4, S.d_cnt + 20, S.h_used);
+            if (r) return r;
+        }
+        if (wait_done_flag(S)) return -2;
+        S.cnt_dirty = false;
+        const unsigned long long used = S.h_used[0];   // reserved bytes: strings at their slots
+        if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+        return (long long)used;
+    }
     const size_t dcap = std::max(fp_cap, mfp_fp_arena_bound(n, total));
     // staging layout: [fp counters 4 | bin counts 16 | classifier counters] [descriptors] [packets + 64]
     constexpr size_t W = 8;
@@ -1110,20 +1156,7 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
             return -3;
         }
     }
-    // the batch is done when k_compact_small's flag lands in host memory (its
-    // writes before it): no wake-up through the runtime; a batch not done
-    // within 2 ms waits on the stream, which also reports a failed launch
-    {
-        const auto t0 = std::chrono::steady_clock::now();
-        bool done = false;
-        for (uint32_t spin = 0; !done; spin++) {
-            done = __atomic_load_n(&S.h_used[4], __ATOMIC_ACQUIRE) != 0;
-            if (!done && (spin & 255) == 255 &&
-                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
-                break;
-        }
-        if (!done) HIPCHK(hipStreamSynchronize(S.stream));
-    }
+    if (wait_done_flag(S)) return -2;
     const unsigned long long used = S.h_used[2];
     if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
     // decided on the host from the records (the prevalence LRU has its own

@@ -131,7 +131,8 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
                                       uint64_t fp_cap, unsigned long long *fp_used, uint32_t *work,
                                       unsigned long long *bin_count, int strategy, uint32_t bin_seg_mask,
                                       uint32_t bin_lds_mask, uint32_t quic_format, uint8_t *quic_scratch,
-                                      uint32_t quic_grid, hipStream_t stream, mfp_prof *prof) {
+                                      uint32_t quic_grid, hipStream_t stream, mfp_prof *prof,
+                                      unsigned long long *fin, unsigned long long *host_out) {
 #define MFP_LAUNCH(name, ...)                                \
     do {                                                     \
         if (prof) mfp_prof_begin(prof, name, stream);        \
@@ -147,6 +148,7 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
     P.fp_used = fp_used;
     P.seg = seg;
     P.idx = nullptr; P.count = nullptr;
+    P.fin = nullptr; P.host_out = nullptr;
     // QUIC and OpenVPN packets (bin 8 of the classify pass, plus any a walker hands over)
     P.quic_idx = work + (uint64_t)mfp::QUIC_BIN * n;
     P.quic_count = bin_count + mfp::QUIC_BIN;
@@ -171,9 +173,13 @@ extern "C" int mfp_launch_fingerprint(uint32_t select, uint32_t block, uint32_t 
         // (one packet per wave: a batch's walk takes as long as its slowest
         // packet, not the sum of the protocols its lanes diverge over)
         P.cfg.spread = 1;
+        // (host_out: the walker's records and strings go straight to the
+        // caller's page-locked buffers, and the batch ends with this launch)
+        if (host_out && !quic) { P.fin = fin; P.host_out = host_out; }
         const uint64_t lb = n < 2048 ? n : 2048;
         if (mfp_launch_bin_all(&P, fallback, 1, "k_fp_lds/small", (uint32_t)lb, 0, stream, prof) != 0) return -1;
         P.cfg.spread = 0;
+        P.fin = nullptr; P.host_out = nullptr;
         // (spread: the walker handled its large packets and queued its QUIC
         // and OpenVPN packets itself -- no fallback lane)
         return launch_quic();

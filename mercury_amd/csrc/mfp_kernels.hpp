@@ -787,6 +787,22 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
             __builtin_amdgcn_wave_barrier();   // the stage is rewritten by the next sub-round
         }
     }
+    if (!SEGMODE && FAM == FAM_ALL && P.host_out) {
+        // (every wave of the grid gets here: each has at least one packet)
+        __threadfence_system();                       // this wave's records and strings
+        if (lane == 0 && atomicAdd(P.fin, 1ull) == gridDim.x - 1) {
+            __threadfence();
+            unsigned long long u[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) u[j] = atomicExch(&P.fp_used[j], 0ull);
+            atomicExch(P.quic_count, 0ull);
+            atomicExch(P.fin, 0ull);
+#pragma unroll
+            for (int j = 0; j < 4; j++) P.host_out[j] = u[j];
+            __threadfence_system();
+            __hip_atomic_store(&P.host_out[4], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 #ifndef MFP_LDS_STAGE

@@ -440,10 +440,10 @@ static void run_batch(mercury *m, mfp_context ctx, Bufs &C, std::vector<Req *> &
         C.ts[i] = r.t_ns;
         total += r.len;
     }
-    {
+    {   // zero padding the device may read past the last packet (mfp_process_small_pinned)
         const size_t at = C.arena.size();
-        C.arena.resize(at + 16);
-        memset(C.arena.data() + at, 0, 16);
+        C.arena.resize(at + 64);
+        memset(C.arena.data() + at, 0, 64);
     }
     const bool want_an = mfp_analysis_enabled(ctx);
     const size_t cap = mfp_fp_arena_bound(n, total);
