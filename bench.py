@@ -797,17 +797,39 @@ def main():
         ctx.set_prevalence(prev)
         ctx.defer(True)
 
+    # several ranks: the steps are pipelined -- step k's kernels are launched,
+    # then step k-1's sightings are merged across the ranks while they run
+    # (mfp_analyze_batch_device_deferred_pipelined; two sets of output buffers)
+    sets = [(d_rec, d_fp, d_used, d_an)]
+    if prev is not None:
+        sets.append((torch.empty_like(d_rec), torch.empty_like(d_fp), torch.zeros_like(d_used),
+                     torch.empty_like(d_an)))
+    nstep = [0]
+
     def step():
-        ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(), cap,
-                           d_used.data_ptr(), stream.cuda_stream)
-        if analysis:
-            ctx.analyze_device(d_arena.data_ptr(), d_desc.data_ptr(), n, d_rec.data_ptr(), d_fp.data_ptr(),
-                               d_an.data_ptr(), stream.cuda_stream)
-            if prev is not None:
-                shard.ordered_prevalence_merge(ctx, prev, rank * n)
+        r_, f_, u_, a_ = sets[nstep[0] % len(sets)]
+        ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, r_.data_ptr(), f_.data_ptr(), cap,
+                           u_.data_ptr(), stream.cuda_stream)
+        if analysis and prev is None:
+            ctx.analyze_device(d_arena.data_ptr(), d_desc.data_ptr(), n, r_.data_ptr(), f_.data_ptr(),
+                               a_.data_ptr(), stream.cuda_stream)
+        elif analysis:
+            ctx.analyze_device_deferred_pipelined(d_arena.data_ptr(), d_desc.data_ptr(), n, r_.data_ptr(),
+                                                  f_.data_ptr(), a_.data_ptr(), stream.cuda_stream)
+            if nstep[0]:
+                shard.ordered_prevalence_merge(ctx, prev, rank * n)   # step k-1, step k in flight
+        nstep[0] += 1
+
+    def drain():
+        # the last step's merge (inside the timed region)
+        if prev is not None and nstep[0]:
+            ctx.analysis_defer_newest()
+            shard.ordered_prevalence_merge(ctx, prev, rank * n)
 
     for _ in range(args.warmup):
         step()
+    drain()
+    nstep[0] = 0
     torch.cuda.synchronize()
     reserved, overflow, used, n_fallback = [int(x) for x in d_used.cpu()]
     if overflow:
@@ -820,10 +842,12 @@ def main():
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if tdist:
         tdist.barrier()
     elapsed = time.perf_counter() - t_start
+    d_rec, d_fp, d_used, d_an = sets[(args.steps - 1) % len(sets)]   # the last step's outputs
     prof = ctx.profile_read()
     ctx.profile(False)
     if tdist:
@@ -904,11 +928,11 @@ def main():
         # the same steps with the decisions pipelined (mfp_analyze_batch_device_pipelined):
         # step k's kernels run while step k-1's sightings are decided on the host
         # (stream order kept; two sets of output buffers, alternating)
-        sets = [(d_rec, d_fp, d_used, d_an),
+        psets = [(d_rec, d_fp, d_used, d_an),
                 (torch.empty_like(d_rec), torch.empty_like(d_fp), torch.zeros_like(d_used), torch.empty_like(d_an))]
 
         def pstep(k):
-            r_, f_, u_, a_ = sets[k % 2]
+            r_, f_, u_, a_ = psets[k % 2]
             ctx.process_device(d_arena.data_ptr(), d_desc.data_ptr(), n, r_.data_ptr(), f_.data_ptr(), cap,
                                u_.data_ptr(), stream.cuda_stream)
             ctx.analyze_device_pipelined(d_arena.data_ptr(), d_desc.data_ptr(), n, r_.data_ptr(), f_.data_ptr(),
@@ -926,10 +950,10 @@ def main():
         el3 = time.perf_counter() - t3
         prof3 = ctx.profile_read()
         ctx.profile(False)
-        an3 = sets[(steps2 - 1) % 2][3].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)
+        an3 = psets[(steps2 - 1) % 2][3].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)
         v3 = (an3["flags"] & 1) != 0
         st3 = np.bincount(an3["status"][v3], minlength=5)
-        del sets
+        del psets
         diverse = {"value": round(n * steps2 / el3 / 1e6, 3), "unit": "Mpkt/s", "steps": steps2,
                    "ms_per_step": round(el3 / steps2 * 1e3, 4),
                    "path": "mfp_analyze_batch_device_pipelined: step k's kernels run while step k-1's sightings are "

@@ -293,6 +293,17 @@ MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context ctx, const uint8_t
                                                   mfp_analysis *d_out, double *d_attr_prob, void *stream);
 /* decide the batch mfp_analyze_batch_device_pipelined left pending; waits */
 MFP_EXPORT int mfp_analysis_flush(mfp_context ctx);
+/* The deferred form (mfp_analysis_defer on; the shards of one stream): launches
+ * this batch's kernels and leaves the PREVIOUS batch, if undecided, as the one
+ * mfp_analysis_distinct / _sequence / _resolve / _resolve_sequence act on, so
+ * the shards' ordered merge of batch k-1 runs while the device runs batch k.
+ * Every batch must be decided before the call after next (-1 otherwise);
+ * mfp_analysis_defer_newest then selects the last batch for its decision. */
+MFP_EXPORT int mfp_analyze_batch_device_deferred_pipelined(mfp_context ctx, const uint8_t *d_arena,
+                                                           const mfp_pkt_desc *d_desc, size_t n, mfp_record *d_rec,
+                                                           const char *d_fp_arena, mfp_analysis *d_out,
+                                                           double *d_attr_prob, void *stream);
+MFP_EXPORT int mfp_analysis_defer_newest(mfp_context ctx);
 
 /* mfp_process_batch_host plus classification into analysis[n] (NULL: none)
  * and attr_prob[n * MFP_ATTR_DB_TAGS] (NULL: not wanted). */

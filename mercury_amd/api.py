@@ -93,6 +93,10 @@ def load_library():
     lib.mfp_analyze_batch_device_pipelined.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     lib.mfp_analysis_flush.restype = ctypes.c_int
     lib.mfp_analysis_flush.argtypes = [vp]
+    lib.mfp_analyze_batch_device_deferred_pipelined.restype = ctypes.c_int
+    lib.mfp_analyze_batch_device_deferred_pipelined.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.mfp_analysis_defer_newest.restype = ctypes.c_int
+    lib.mfp_analysis_defer_newest.argtypes = [vp]
     lib.mfp_process_batch_host_seg.restype = ctypes.c_longlong
     lib.mfp_process_batch_host_seg.argtypes = [vp, vp, sz, vp, sz, vp, vp, sz, vp]
     lib.mfp_reassembler_create.restype = vp
@@ -418,6 +422,22 @@ class Context:
     def analysis_flush(self):
         if self.lib.mfp_analysis_flush(self.h) != 0:
             raise MercuryAmdError("mfp_analysis_flush failed: " + _err(self.lib))
+
+    def analyze_device_deferred_pipelined(self, d_arena, d_desc, n, d_rec, d_fp, d_out, stream=0, d_attr_prob=None):
+        """mfp_analyze_batch_device_deferred_pipelined (a deferred context, the
+        shards of one stream): this batch's kernels are launched and the previous
+        batch, if undecided, is the one analysis_distinct / analysis_resolve* act
+        on -- shard.ordered_prevalence_merge decides it while the device runs
+        this one."""
+        r = self.lib.mfp_analyze_batch_device_deferred_pipelined(self.h, d_arena, d_desc, n, d_rec, d_fp, d_out,
+                                                                  d_attr_prob, stream)
+        if r != 0:
+            raise MercuryAmdError("mfp_analyze_batch_device_deferred_pipelined failed: " + _err(self.lib))
+
+    def analysis_defer_newest(self):
+        """After the last deferred pipelined call: the analysis_* calls act on its batch."""
+        if self.lib.mfp_analysis_defer_newest(self.h) != 0:
+            raise MercuryAmdError("mfp_analysis_defer_newest failed: " + _err(self.lib))
 
     def process_name(self, pid):
         if pid == NO_PROCESS:

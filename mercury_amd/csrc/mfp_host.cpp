@@ -791,6 +791,8 @@ static int slot_apply(mfp_context c, Slot &S, const uint8_t *bits, size_t nbits,
         mfp_set_error("resolve launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -3;
     }
+    HIPCHK(hipEventRecord(S.ev_resolved, s));   // (a pipelined slot's next batch waits for it)
+    S.resolved_recorded = true;
     S.pend.live = false;
     return 0;
 }
@@ -1348,6 +1350,60 @@ extern "C" MFP_EXPORT int mfp_analyze_batch_device_pipelined(mfp_context c, cons
         O.resolved_recorded = true;
         HIPCHK(hipStreamWaitEvent(us, O.ev_resolved, 0));   // later work on the caller's stream sees its records
     }
+    return 0;
+}
+
+// The deferred (shard-merge) form of the pipeline: batch k's kernels are
+// launched on slot 0 or 3 (alternating) and batch k-1, if it is still
+// pending, becomes the batch the mfp_analysis_distinct / _sequence /
+// _resolve* calls act on -- so the ranks' ordered merge of batch k-1
+// (shard.ordered_prevalence_merge) runs on the host while the device runs
+// batch k.  The slot is reused two calls later, after its decision was
+// applied (the caller's stream waits for it); mfp_analysis_defer_newest makes
+// the last batch the one the calls act on.
+extern "C" MFP_EXPORT int mfp_analyze_batch_device_deferred_pipelined(mfp_context c, const uint8_t *d_arena,
+                                                                      const mfp_pkt_desc *d_desc, size_t n,
+                                                                      mfp_record *d_rec, const char *d_fp_arena,
+                                                                      mfp_analysis *d_out, double *d_attr_prob,
+                                                                      void *stream) {
+    if (!c) { mfp_set_error("null context"); return -1; }
+    if (!c->clf) { mfp_set_error("analysis is not enabled (config needs resources=<archive>;analysis)"); return -1; }
+    if (!c->defer) {
+        mfp_set_error("mfp_analyze_batch_device_deferred_pipelined: the context decides its own batches "
+                      "(mfp_analysis_defer is off); use mfp_analyze_batch_device_pipelined");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t us = (hipStream_t)stream;
+    const int slot = c->pipe_next ? 3 : 0, other = c->pipe_next ? 0 : 3;
+    Slot &S = c->slot[slot];
+    if (S.pend.live) {
+        mfp_set_error("mfp_analyze_batch_device_deferred_pipelined: the batch two calls back was not decided "
+                      "(mfp_analysis_resolve / mfp_analysis_resolve_sequence)");
+        return -1;
+    }
+    if (S.resolved_recorded) HIPCHK(hipStreamWaitEvent(us, S.ev_resolved, 0));
+    int r = analyze_locked(c, slot, d_arena, d_desc, n, d_rec, d_fp_arena, d_out, d_attr_prob, us);
+    if (r) return r;
+    HIPCHK(hipEventRecord(S.ev_kernels, us));
+    HIPCHK(hipEventRecord(S.ev_dev, us));
+    S.dev_recorded = true;
+    HIPCHK(hipStreamWaitEvent(S.stream, S.ev_kernels, 0));
+    S.pend.stream = S.stream;
+    c->pipe_next ^= 1;
+    Slot &O = c->slot[other];
+    if (O.pend.live) c->an_slot = other;   // the calls decide the older batch first
+    return 0;
+}
+
+// the deferred calls act on the newest analysed batch (after the last
+// pipelined call, to decide it)
+extern "C" MFP_EXPORT int mfp_analysis_defer_newest(mfp_context c) {
+    if (!c || !c->clf) { mfp_set_error("analysis is not enabled"); return -1; }
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int newest = c->pipe_next ? 0 : 3;   // the slot the last pipelined call used
+    if (c->slot[newest].pend.live) c->an_slot = newest;
     return 0;
 }
 

@@ -38,22 +38,20 @@
 namespace {
 
 // LRU over 64-bit keys: linear-probing index (keys stored in the slots,
-// backward-shift deletion: no tombstones) + intrusive doubly linked list in
-// arrays (node 0 is the list head sentinel; where[n] = node n's slot)
+// backward-shift deletion: no tombstones) + intrusive doubly linked list of
+// nodes (node 0 is the list head sentinel; a node holds its key, its links
+// and its slot, so relinking a node touches one cache line per node)
 struct Lru {
     struct Slot { uint64_t key; uint32_t node; uint32_t pad; };   // node 0: empty
+    struct Node { uint64_t key; uint32_t prev, next, where, pad; };
     uint32_t cap;
-    std::vector<uint64_t> key;
-    std::vector<uint32_t> prev, next, where;
+    std::vector<Node> nd;
     std::vector<Slot> slot;
     uint64_t mask;
     uint32_t size = 0;
 
     explicit Lru(uint32_t c) : cap(c ? c : 1) {
-        key.assign((size_t)cap + 1, 0);
-        prev.assign((size_t)cap + 1, 0);
-        next.assign((size_t)cap + 1, 0);
-        where.assign((size_t)cap + 1, 0);
+        nd.assign((size_t)cap + 1, Node{0, 0, 0, 0, 0});
         uint64_t s = 16;
         while (s < 2ull * cap + 16) s <<= 1;
         slot.assign(s, Slot{0, 0, 0});
@@ -65,6 +63,14 @@ struct Lru {
     }
     uint64_t home(uint64_t k) const { return mix(k) & mask; }
     void prefetch(uint64_t k) const { __builtin_prefetch(&slot[home(k)]); }
+    // the accesses of a sequence, prefetching slots 8 ahead (a second stage
+    // prefetching the hit's node measured slower)
+    void run(const uint64_t *hash, size_t s, size_t e, uint8_t *seen) {
+        for (size_t j = s; j < e; j++) {
+            if (j + 8 < e) prefetch(hash[j + 8]);
+            seen[j] = access(hash[j]) ? 1 : 0;
+        }
+    }
     // slot of k (found), or the empty slot that ends its probe
     uint64_t find(uint64_t k, bool &found) const {
         uint64_t i = home(k);
@@ -85,21 +91,27 @@ struct Lru {
             const bool stay = (i <= j) ? (h > i && h <= j) : (h > i || h <= j);
             if (!stay) {
                 slot[i] = slot[j];
-                where[slot[i].node] = (uint32_t)i;
+                nd[slot[i].node].where = (uint32_t)i;
                 i = j;
             }
         }
         slot[i].node = 0;
     }
-    void unlink(uint32_t n) { next[prev[n]] = next[n]; prev[next[n]] = prev[n]; }
-    void push_front(uint32_t n) { next[n] = next[0]; prev[n] = 0; prev[next[0]] = n; next[0] = n; }
-    void push_back(uint32_t n) { prev[n] = prev[0]; next[n] = 0; next[prev[0]] = n; prev[0] = n; }
+    void unlink(uint32_t n) { nd[nd[n].prev].next = nd[n].next; nd[nd[n].next].prev = nd[n].prev; }
+    void push_front(uint32_t n) {
+        const uint32_t f = nd[0].next;
+        nd[n].next = f; nd[n].prev = 0; nd[f].prev = n; nd[0].next = n;
+    }
+    void push_back(uint32_t n) {
+        const uint32_t b = nd[0].prev;
+        nd[n].prev = b; nd[n].next = 0; nd[b].next = n; nd[0].prev = n;
+    }
     bool contains(uint64_t k) const { bool f; find(k, f); return f; }
     uint32_t insert_at(uint64_t i, uint64_t k) {   // i: the empty slot find() returned
         const uint32_t n = ++size;                 // nodes 1..size are live (evictions reuse theirs)
-        key[n] = k;
+        nd[n].key = k;
         slot[i] = Slot{k, n, 0};
-        where[n] = (uint32_t)i;
+        nd[n].where = (uint32_t)i;
         return n;
     }
     // fingerprint_prevalence::update (analysis.h:386-408); returns whether k
@@ -109,17 +121,17 @@ struct Lru {
         uint64_t i = find(k, found);
         if (found) {
             const uint32_t n = slot[i].node;
-            if (next[0] != n) { unlink(n); push_front(n); }
+            if (nd[0].next != n) { unlink(n); push_front(n); }
             return true;
         }
         if (size == cap) {                         // evict the least recently used, reuse its node
-            const uint32_t t = prev[0];
+            const uint32_t t = nd[0].prev;
             unlink(t);
-            erase_slot(where[t]);
+            erase_slot(nd[t].where);
             i = find(k, found);                    // the shift may have moved k's empty slot
-            key[t] = k;
+            nd[t].key = k;
             slot[i] = Slot{k, t, 0};
-            where[t] = (uint32_t)i;
+            nd[t].where = (uint32_t)i;
             push_front(t);
             return false;
         }
@@ -139,7 +151,7 @@ struct Lru {
     // the keys from least to most recently used
     void export_keys(std::vector<uint64_t> &out) const {
         out.clear();
-        for (uint32_t n = prev[0]; n != 0; n = prev[n]) out.push_back(key[n]);
+        for (uint32_t n = nd[0].prev; n != 0; n = nd[n].prev) out.push_back(nd[n].key);
     }
 };
 
@@ -226,10 +238,7 @@ static void decide(Lru &L, const uint64_t *hash, size_t m, uint8_t *seen) {
     if (const char *e = getenv("MFP_LRU_THREADS")) tmax = std::max<size_t>(1, std::min<size_t>(tmax, strtoul(e, nullptr, 10)));
     size_t T = std::min<size_t>(m / (8 * (size_t)L.cap), tmax);
     if (T <= 1) {
-        for (size_t j = 0; j < m; j++) {
-            if (j + 8 < m) L.prefetch(hash[j + 8]);
-            seen[j] = L.access(hash[j]) ? 1 : 0;
-        }
+        L.run(hash, 0, m, seen);
         return;
     }
     std::vector<uint64_t> init;
@@ -250,10 +259,7 @@ static void decide(Lru &L, const uint64_t *hash, size_t m, uint8_t *seen) {
             } else if (t == 0) {
                 lru_at(C, hash, 0, init, 0);
             }
-            for (size_t j = s; j < e; j++) {
-                if (j + 8 < e) C.prefetch(hash[j + 8]);
-                seen[j] = C.access(hash[j]) ? 1 : 0;
-            }
+            C.run(hash, s, e, seen);
             std::lock_guard<std::mutex> lk(dmu);
             sets[t] = std::move(C);
             done[t] = 1;
@@ -267,7 +273,7 @@ static void decide(Lru &L, const uint64_t *hash, size_t m, uint8_t *seen) {
 // the keys of `older` from its most recent down, up to the capacity
 static void set_from(Lru &out, const uint64_t *recent, size_t n, const Lru &older) {
     for (size_t i = 0; i < n && out.size < out.cap; i++) out.append_lru(recent[i]);
-    for (uint32_t k = older.next[0]; k != 0 && out.size < out.cap; k = older.next[k]) out.append_lru(older.key[k]);
+    for (uint32_t k = older.nd[0].next; k != 0 && out.size < out.cap; k = older.nd[k].next) out.append_lru(older.nd[k].key);
 }
 
 extern "C" {
@@ -287,7 +293,7 @@ MFP_EXPORT long long mfp_prevalence_summary(mfp_prevalence p, const uint64_t *ha
     Lru S(p->lru.cap);
     for (size_t i = m; i-- > 0 && S.size < S.cap;) S.append_lru(hash[i]);
     long long k = 0;
-    for (uint32_t n = S.next[0]; n != 0; n = S.next[n]) out[k++] = S.key[n];
+    for (uint32_t n = S.nd[0].next; n != 0; n = S.nd[n].next) out[k++] = S.nd[n].key;
     return k;
 }
 

@@ -7,19 +7,22 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
 
-def test_bench_spawns_ranks_dry_run():
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
-                         capture_output=True, text=True, timeout=180, cwd=ROOT)
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_spawns_ranks_dry_run(world):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dry-run"],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
-    assert line["dry_run"] and line["n_gpus"] == 2 and line["backend"] == "gloo"
-    assert sorted(r["rank"] for r in line["ranks"]) == [0, 1]
-    assert sorted(r["local_rank"] for r in line["ranks"]) == [0, 1]
-    assert len({r["pid"] for r in line["ranks"]}) == 2
+    assert line["dry_run"] and line["n_gpus"] == world and line["backend"] == "gloo"
+    assert sorted(r["rank"] for r in line["ranks"]) == list(range(world))
+    assert sorted(r["local_rank"] for r in line["ranks"]) == list(range(world))
+    assert len({r["pid"] for r in line["ranks"]}) == world
 
 
 def test_bench_under_launcher_env_uses_world_size():

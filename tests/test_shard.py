@@ -231,13 +231,95 @@ def test_ordered_prevalence_merge_world2_hip():
     assert res[0][1] == res[1][1] and res[0][2] > 0
 
 
-def _scale_worker(rank, world, port, q, m, steps):
+def _gpu_pipe_worker(rank, world, port, q):
+    """bench.py's pipelined multi-rank step on cuda:0: each step's kernels are
+    launched (process_device + analyze_device_deferred_pipelined), then the
+    previous step's sightings are decided across the ranks
+    (shard.ordered_prevalence_merge) while the device runs this one."""
+    import torch
+    import torch.distributed as dist
+    import mercury_amd
+    from tests.test_prevalence import REF_ARCHIVE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, d = synth.lru_batch(synth.lru_keys())
+        ctx = mercury_amd.Context(f"select=tls;resources={REF_ARCHIVE};analysis", device=0)
+        prev = mercury_amd.Prevalence(100000)
+        ctx.set_prevalence(prev)
+        ctx.defer(True)
+        step, cap = 17000, 48 * 1024 * 1024
+        stream = torch.cuda.current_stream()
+        d_arena = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        sets = [dict(rec=torch.empty(step * 32, dtype=torch.uint8, device="cuda"),
+                     fp=torch.empty(cap, dtype=torch.uint8, device="cuda"),
+                     used=torch.zeros(4, dtype=torch.int64, device="cuda"),
+                     an=torch.empty(step * mercury_amd.ANALYSIS_DTYPE.itemsize, dtype=torch.uint8, device="cuda"))
+                for _ in range(2)]
+        bases = list(range(0, len(d), world * step))
+        got, descs = [], [None, None]
+
+        def decide(k):
+            shard.ordered_prevalence_merge(ctx, prev, bases[k] + rank * step)
+            got.append(ctx.last_analysis()["status"].astype(np.uint8))
+
+        for k, lo in enumerate(bases):
+            s_lo = lo + rank * step
+            dd = np.ascontiguousarray(d[s_lo:s_lo + step])
+            b = sets[k % 2]
+            descs[k % 2] = torch.from_numpy(dd.view(np.uint8)).cuda()
+            ctx.process_device(d_arena.data_ptr(), descs[k % 2].data_ptr(), len(dd), b["rec"].data_ptr(),
+                               b["fp"].data_ptr(), cap, b["used"].data_ptr(), stream.cuda_stream)
+            ctx.analyze_device_deferred_pipelined(d_arena.data_ptr(), descs[k % 2].data_ptr(), len(dd),
+                                                  b["rec"].data_ptr(), b["fp"].data_ptr(), b["an"].data_ptr(),
+                                                  stream.cuda_stream)
+            if k:
+                decide(k - 1)     # step k-1's merge, with step k's kernels in flight
+        ctx.analysis_defer_newest()
+        decide(len(bases) - 1)
+        torch.cuda.synchronize()
+        q.put((rank, np.concatenate(got).tobytes(), prev.keys().tobytes()))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ordered_prevalence_merge_pipelined_world2_hip():
+    """The pipelined multi-rank step (bench.py --gpus N): two gloo ranks on
+    cuda:0, step k's kernels launched before step k-1's ordered merge; the
+    statuses, in stream order, equal the reference's
+    (tests/golden/lru_status.bin.gz), and both ranks end with the same LRU."""
+    import multiprocessing as mp
+    from tests.test_prevalence import golden_status
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ps = [ctxm.Process(target=_gpu_pipe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (np.frombuffer(s, np.uint8), k) for r, s, k in [q.get(timeout=600) for _ in ps]}
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    step = 17000
+    got = np.concatenate([res[r][0][k * step:(k + 1) * step] for k in range(5) for r in range(2)])
+    want = golden_status()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} statuses differ, first at {bad[:5]}"
+    assert res[0][1] == res[1][1]
+
+
+def _scale_worker(rank, world, port, q, m, steps, threads=2):
     """One rank at the realistic-diversity leg's scale: m unknown-TLS sightings
     per step (mostly distinct fingerprints, cycling the 100 000-entry LRU),
     decided with shard.ordered_prevalence_merge; reports the merge's wall time
-    per step.  Two LRU threads per rank (MFP_LRU_THREADS), so world 4 fills
-    this host's 8 cores and no more."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo", MFP_LRU_THREADS="2")
+    per step.  `threads` LRU threads per rank (MFP_LRU_THREADS): world x
+    threads stays within the host's cores."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo",
+                      MFP_LRU_THREADS=str(threads))
     import time
     import torch.distributed as dist
     import mercury_amd
@@ -266,14 +348,14 @@ def _scale_worker(rank, world, port, q, m, steps):
         dist.destroy_process_group()
 
 
-def _run_scale(world, m, steps):
+def _run_scale(world, m, steps, threads=2):
     import multiprocessing as mp
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    ps = [ctxm.Process(target=_scale_worker, args=(r, world, port, q, m, steps)) for r in range(world)]
+    ps = [ctxm.Process(target=_scale_worker, args=(r, world, port, q, m, steps, threads)) for r in range(world)]
     for p in ps:
         p.start()
     res = {r: (t, c, k) for r, t, c, k in [q.get(timeout=600) for _ in ps]}
@@ -283,17 +365,19 @@ def _run_scale(world, m, steps):
     return res
 
 
-def test_ordered_prevalence_merge_scale_world2_world4():
+def test_ordered_prevalence_merge_scale_world2_4_8():
     """SURVEY 8(e) at the diversity leg's scale: 17.5 M sightings per rank per
-    step.  The sequence form decides every sighting once, on its own rank, so
-    the merge's time per step does not grow with the number of ranks (the
-    earlier form resolved all ranks' sightings on every rank: 4x the work at
-    world 4).  Every rank ends each step with the same LRU."""
+    step, world 2, 4 and 8 (one LRU thread per rank: 8 ranks fill this host's
+    8 cores).  The sequence form decides every sighting once, on its own rank,
+    so the merge's time per step does not grow with the number of ranks (the
+    earlier form resolved all ranks' sightings on every rank: 8x the work at
+    world 8).  Every rank ends each step with the same LRU.  The per-rank time
+    at the GPU box's thread share: tools/merge_scale.py (profiles/)."""
     m, steps = 17_500_000, 2
     t = {}
-    for world in (2, 4):
-        res = _run_scale(world, m, steps)
+    for world in (2, 4, 8):
+        res = _run_scale(world, m, steps, threads=1)
         assert len({tuple(v[2]) for v in res.values()}) == 1      # same LRU on every rank
         t[world] = max(max(v[0][1:]) for v in res.values())      # steady state (the first step warms up)
-    print(f"merge per step: world 2 {t[2]:.2f} s, world 4 {t[4]:.2f} s")
-    assert t[4] < 1.6 * t[2], t
+    print("merge per step (1 LRU thread per rank): " + ", ".join(f"world {w} {x:.2f} s" for w, x in t.items()))
+    assert t[4] < 1.6 * t[2] and t[8] < 1.8 * t[2], t
