@@ -698,7 +698,7 @@ def main():
                     help="config 5: host-resident (H2D/D2H-inclusive) packets per job, split over the ranks; 0 = skip")
     ap.add_argument("--e2e-buffer", type=int, default=10_000_000,
                     help="packets in each rank's page-locked source buffer (looped up to its share)")
-    ap.add_argument("--e2e-chunk", type=int, default=2_000_000)
+    ap.add_argument("--e2e-chunk", type=int, default=1_000_000)
     ap.add_argument("--no-json-leg", action="store_true")
     ap.add_argument("--diverse-leg", type=float, default=1.0,
                     help="fraction of TLS ClientHellos with per-packet cipher suites in the realistic-diversity "

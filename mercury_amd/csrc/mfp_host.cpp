@@ -57,6 +57,9 @@ extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *sr
                                   mfp_prof *prof);
 
 
+extern "C" int mfp_launch_compact_to(const mfp_record *rec, mfp_record *rec_out, uint64_t n, const uint8_t *src,
+                                     uint8_t *dst, uint64_t cap, uint32_t *local, unsigned long long *block_sum,
+                                     unsigned long long *ctr, hipStream_t stream, mfp_prof *prof);
 extern "C" int mfp_launch_compact_small(const mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst_host,
                                         uint64_t cap, mfp_record *rec_host, const unsigned long long *used,
                                         unsigned long long *used_host, const mfp_analysis *an, mfp_analysis *an_host,
@@ -429,6 +432,10 @@ struct Slot {
     // caller's stream (mfp_process_batch_device, mfp_analyze_batch_device*):
     // a host batch staged on the slot's own stream waits for it
     hipEvent_t ev_dev = nullptr;
+    // host pipeline: the chunk's copy in done (on the copy stream), and the
+    // slot's chunk done with its packet buffers (on the slot's stream)
+    hipEvent_t ev_in = nullptr, ev_free = nullptr;
+    bool free_recorded = false;
     bool dev_recorded = false;
 
     bool init() {
@@ -442,7 +449,9 @@ struct Slot {
                hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
                hipEventCreateWithFlags(&ev_kernels, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&ev_resolved, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_dev, hipEventDisableTiming) == hipSuccess;
+               hipEventCreateWithFlags(&ev_dev, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_in, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_free, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         void *p[] = {d_used, d_bins, d_quic, d_work, d_an_stats, d_pending, d_work_items, d_lanel, d_deferred, d_huge, d_segn,
@@ -452,7 +461,7 @@ struct Slot {
         for (void *x : {(void *)h_used, (void *)h_seq, (void *)h_gbits, (void *)h_dec, (void *)h_small})
             if (x) (void)hipHostFree(x);
         if (stream) (void)hipStreamDestroy(stream);
-        for (hipEvent_t e : {ev_kernels, ev_resolved, ev_dev}) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {ev_kernels, ev_resolved, ev_dev, ev_in, ev_free}) if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -479,7 +488,10 @@ struct mfp_context_s {
     bool defer = false;                  // mfp_analysis_defer
     bool report_os = false;              // libmerc_config.report_os (mfp_analysis_report_os)
     bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
-    Slot slot[4];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2: host pipeline
+    Slot slot[5];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2, 4: host pipeline
+    unsigned long long *d_pipe = nullptr;   // the host pipeline's stream counters (packed bytes, overflow)
+    hipStream_t in_stream = nullptr;        // the host pipeline's copy stream (MFP_PIPE_INSTREAM)
+    hipEvent_t ev_pipe[3] = {nullptr, nullptr, nullptr};   // a pipeline slot's compaction scan done
     // the per-packet shim's concurrent small batches (mfp_process_small_pinned):
     // each on a slot of its own, so batches of different callers overlap on the
     // device; taken and returned under mu, waited for outside it
@@ -573,6 +585,9 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (c->own_prev) mfp_prevalence_destroy(c->own_prev);
     for (Slot &S : c->slot) S.release();
     for (int j = 0; j < mfp_context_s::NSMALL; j++) if (c->small_init[j]) c->small[j].release();
+    if (c->d_pipe) (void)hipFree(c->d_pipe);
+    if (c->in_stream) (void)hipStreamDestroy(c->in_stream);
+    for (hipEvent_t e : c->ev_pipe) if (e) (void)hipEventDestroy(e);
     delete c->prof;
     delete c;
 }
@@ -931,13 +946,28 @@ static int batch_span(const uint8_t *arena, size_t arena_len, const mfp_pkt_desc
 // on the slot's stream; descriptors keep their offsets: the device arena
 // pointer handed to the kernels is the staging buffer minus the (256-byte
 // aligned) start of the copied span
+// the pipelined host path's compaction target (mfp_process_pipelined when the
+// caller's arena and records are page-locked): strings and records straight
+// into them at their stream offsets, after the previous chunk's scan
+struct PipeOut {
+    uint8_t *dst; uint64_t cap;       // the caller's fp arena (device-visible pointer)
+    mfp_record *rec_out;              // the chunk's records in the caller's array (device-visible pointer)
+    unsigned long long *ctr;          // c->d_pipe
+    hipEvent_t wait;                  // the previous chunk's scan (nullptr: the first chunk)
+    hipEvent_t done;                  // recorded after this chunk's compaction
+};
 static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
-                            size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false) {
+                            size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false,
+                            const PipeOut *po = nullptr, const uint64_t *staged = nullptr) {
     Slot &S = c->slot[slot];
     // device-pointer calls may still be using this slot's scratch on the caller's stream
     if (S.dev_recorded) { HIPCHK(hipStreamWaitEvent(S.stream, S.ev_dev, 0)); S.dev_recorded = false; }
     uint64_t lo, hi, total;
-    if (batch_span(arena, arena_len, desc, n, lo, hi, total)) return -1;
+    if (staged) {   // (stage_copy ran: {lo, hi, total}, the copies queued behind ev_in)
+        lo = staged[0]; hi = staged[1]; total = staged[2];
+    } else if (batch_span(arena, arena_len, desc, n, lo, hi, total)) {
+        return -1;
+    }
     // the device arena holds the strings at their reserved slots (the TLS
     // ClientHello bin reserves by an upper bound, k_fp_tls1): sized by the
     // bound, whatever the caller's dense capacity; the callers check that the
@@ -946,16 +976,21 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     const uint64_t span = hi - lo;
     // 64 bytes of padding after the span: the kernels read the aligned block
     // that holds a packet's last byte
-    if (grow(S.d_arena, S.cap_arena, span + 64) || grow(S.d_desc, S.cap_desc, n + 1) || grow(S.d_rec, S.cap_rec, n + 1) ||
+    if ((!staged && (grow(S.d_arena, S.cap_arena, span + 64) || grow(S.d_desc, S.cap_desc, n + 1))) ||
+        grow(S.d_rec, S.cap_rec, n + 1) ||
         grow(S.d_fp, S.cap_fp, dcap + 64) || grow(S.d_fp2, S.cap_fp2, dcap + 64) ||
         (analysis && grow(S.d_an, S.cap_an, n + 1)) ||
         (analysis && attr_prob && grow(S.d_ap, S.cap_ap, MFP_ATTR_DB_TAGS * (n + 1)))) {
         mfp_set_error("device allocation failed");
         return -2;
     }
-    const uint64_t copy = std::min<uint64_t>(span + 16, arena_len - lo);
-    if (copy) HIPCHK(hipMemcpyAsync(S.d_arena, arena + lo, copy, hipMemcpyHostToDevice, S.stream));
-    if (n) HIPCHK(hipMemcpyAsync(S.d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, S.stream));
+    if (staged) {
+        HIPCHK(hipStreamWaitEvent(S.stream, S.ev_in, 0));
+    } else {
+        const uint64_t copy = std::min<uint64_t>(span + 16, arena_len - lo);
+        if (copy) HIPCHK(hipMemcpyAsync(S.d_arena, arena + lo, copy, hipMemcpyHostToDevice, S.stream));
+        if (n) HIPCHK(hipMemcpyAsync(S.d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, S.stream));
+    }
     const uint8_t *d_base = S.d_arena - lo;
     int r = process_device_locked(c, S, d_base, S.d_desc, n, S.d_rec, S.d_fp, dcap, (uint64_t *)S.d_used, S.stream);
     if (r) return r;
@@ -965,6 +1000,22 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
         // the synchronous host batch decides its unknown-TLS sightings now;
         // pipeline slots when they retire (chunk order), on the host copies
         if (slot == 0 && !c->defer && !host_resolve) { r = slot_resolve(c, S); if (r) return r; }
+    }
+    if (staged) {   // the packets and descriptors are read by now: the copy of the slot's next chunk may start
+        HIPCHK(hipEventRecord(S.ev_free, S.stream));
+        S.free_recorded = true;
+    }
+    if (po) {
+        if (po->wait) HIPCHK(hipStreamWaitEvent(S.stream, po->wait, 0));
+        if (n && mfp_launch_compact_to(S.d_rec, po->rec_out, n, (const uint8_t *)S.d_fp, po->dst, po->cap, S.d_work,
+                                       (unsigned long long *)(S.d_work + ((n + 3) & ~(size_t)1)), po->ctr, S.stream,
+                                       c->prof) != 0) {
+            mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return -3;
+        }
+        HIPCHK(hipEventRecord(po->done, S.stream));
+        if (analysis) S.pend.fp = S.d_fp;   // the device records still index it
+        return 0;
     }
     // strings to a dense arena in packet order (d_fp2, d_used[2] bytes), records re-pointed;
     // the bin lists in d_work are dead by now and hold the scan scratch
@@ -1220,23 +1271,138 @@ extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8
         // an error path may leave copies into the caller's buffers queued on
         // either pipeline stream: drain both before the caller reuses them
         // (the error string of the failure is kept)
-        for (int s = 1; s <= 2; s++) (void)hipStreamSynchronize(c->slot[s].stream);
+        for (int s : {1, 2, 4}) (void)hipStreamSynchronize(c->slot[s].stream);
     }
     return r;
+}
+
+// a pipeline chunk's copy in, queued on the copy stream `cs` as soon as the
+// slot's previous chunk has read its packets (ev_free) -- before the host waits
+// for that chunk -- so consecutive chunks' copies follow each other on the
+// link; span = {lo, hi, total} for stage_and_launch
+static int stage_copy(mfp_context c, Slot &S, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                      size_t n, hipStream_t cs, uint64_t span[3]) {
+    if (batch_span(arena, arena_len, desc, n, span[0], span[1], span[2])) return -1;
+    const uint64_t lo = span[0], sp = span[1] - span[0];
+    if (S.free_recorded) { HIPCHK(hipStreamWaitEvent(cs, S.ev_free, 0)); S.free_recorded = false; }
+    // (growing frees the old buffers: hipFree waits for the device)
+    if (grow(S.d_arena, S.cap_arena, sp + 64) || grow(S.d_desc, S.cap_desc, n + 1)) {
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
+    const uint64_t copy = std::min<uint64_t>(sp + 16, arena_len - lo);
+    if (copy) HIPCHK(hipMemcpyAsync(S.d_arena, arena + lo, copy, hipMemcpyHostToDevice, cs));
+    if (n) HIPCHK(hipMemcpyAsync(S.d_desc, desc, n * sizeof(mfp_pkt_desc), hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(S.ev_in, cs));
+    (void)c;
+    return 0;
+}
+
+// the device-visible address of [p, p + len) when all of it is page-locked
+// host memory (hipHostMalloc / hipHostRegister), else nullptr
+static void *device_view(const void *p, size_t len) {
+    if (!p || !len) return nullptr;
+    hipPointerAttribute_t a, b;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    const uint8_t *e = (const uint8_t *)p + len - 1;
+    if (hipPointerGetAttributes(&b, e) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    if (b.type != hipMemoryTypeHost) return nullptr;
+    return (uint8_t *)a.devicePointer + ((const uint8_t *)p - (const uint8_t *)a.hostPointer);
+}
+
+// mfp_process_pipelined into page-locked outputs: three chunks in flight on
+// three slots; each chunk's compaction writes its strings and records straight
+// into the caller's buffers at their stream offsets (the scan continues the
+// previous chunk's, across streams), so a chunk retires without a copy queued
+// behind the host's wait; the host waits for a chunk only to decide its
+// unknown-TLS sightings, two chunks later
+static long long pipelined_direct(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
+                                  size_t n, mfp_record *rec, mfp_record *rec_dev, char *fp_arena, uint8_t *fp_dev,
+                                  size_t fp_cap, mfp_analysis *analysis, double *attr_prob, size_t chunk) {
+    constexpr int NP = 3;
+    static constexpr int slot_of[NP] = {1, 2, 4};
+    if (!c->d_pipe && hipMalloc(&c->d_pipe, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        c->d_pipe = nullptr;
+        mfp_set_error("device allocation failed");
+        return -2;
+    }
+    for (hipEvent_t &e : c->ev_pipe)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipMemset(c->d_pipe, 0, 2 * sizeof(unsigned long long)));
+    struct Inflight { bool live; size_t lo, hi; };
+    Inflight inf[NP] = {};
+    auto retire = [&](int s) -> int {
+        Slot &S = c->slot[slot_of[s]];
+        HIPCHK(hipStreamSynchronize(S.stream));
+        if (analysis) {   // (the pipeline decides its chunks itself, in order)
+            const int r = slot_resolve_host(c, S, analysis + inf[s].lo, rec + inf[s].lo);
+            if (r) return r;
+        }
+        inf[s].live = false;
+        return 0;
+    };
+    const size_t nch = (n + chunk - 1) / chunk;
+    int prev = -1;
+    for (size_t k = 0; k < nch; k++) {
+        const int s = (int)(k % NP);
+        Slot &S = c->slot[slot_of[s]];
+        if (inf[s].live) { int r = retire(s); if (r) return r; }
+        const size_t lo = k * chunk, hi = std::min(n, lo + chunk), m = hi - lo;
+        uint64_t bytes = 0;
+        for (size_t i = lo; i < hi; i++) bytes += desc[i].caplen;
+        const PipeOut po{fp_dev, fp_cap, rec_dev + lo, c->d_pipe, prev >= 0 ? c->ev_pipe[prev] : nullptr, c->ev_pipe[s]};
+        int r = stage_and_launch(c, slot_of[s], arena, arena_len, desc + lo, m, mfp_fp_arena_bound(m, bytes),
+                                 analysis != nullptr, attr_prob != nullptr, false, &po);
+        if (r) return r;
+        if (analysis) HIPCHK(hipMemcpyAsync(analysis + lo, S.d_an, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
+        if (analysis && attr_prob && m)
+            HIPCHK(hipMemcpyAsync(attr_prob + lo * MFP_ATTR_DB_TAGS, S.d_ap, m * MFP_ATTR_DB_TAGS * sizeof(double),
+                                  hipMemcpyDeviceToHost, S.stream));
+        inf[s] = {true, lo, hi};
+        prev = s;
+    }
+    for (size_t k = nch > NP ? nch - NP : 0; k < nch; k++) {   // the chunks still in flight, oldest first
+        const int s = (int)(k % NP);
+        if (inf[s].live) { int r = retire(s); if (r) return r; }
+    }
+    unsigned long long ctr[2];
+    HIPCHK(hipMemcpy(ctr, c->d_pipe, sizeof ctr, hipMemcpyDeviceToHost));
+    if (ctr[1] || ctr[0] > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
+    return (long long)ctr[0];
 }
 
 static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                                   size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
                                   double *attr_prob, size_t chunk) {
     if (chunk == 0) chunk = (size_t)1 << 20;
+    // MFP_PIPE_DIRECT=1: the compaction writes into page-locked outputs
+    // (pipelined_direct; measured slower: the byte stores over PCIe take
+    // ~10 ms per 2M chunk on the GPU, tools/e2e_probe.py)
+    if (const char *e = getenv("MFP_PIPE_DIRECT"); e && e[0] == '1') {
+        auto *fp_dev = (uint8_t *)device_view(fp_arena, fp_cap);
+        auto *rec_dev = (mfp_record *)device_view(rec, n * sizeof(mfp_record));
+        if (fp_dev && rec_dev && n)
+            return pipelined_direct(c, arena, arena_len, desc, n, rec, rec_dev, fp_arena, fp_dev, fp_cap, analysis,
+                                    attr_prob, chunk);
+    }
+    // NP chunks in flight on NP slots (MFP_PIPE_SLOTS, 2 or 3); MFP_PIPE_INSTREAM=1:
+    // the host-to-device copies go one after the other on one stream, so the
+    // first chunk's kernels start after its own copy, not after a share of all
+    int NP = 2;
+    if (const char *e = getenv("MFP_PIPE_SLOTS")) NP = atoi(e) == 3 ? 3 : 2;
+    static constexpr int slot_of[3] = {1, 2, 4};
+    bool instream = true;
+    if (const char *e = getenv("MFP_PIPE_INSTREAM")) instream = e[0] == '1';
+    if (instream && !c->in_stream) HIPCHK(hipStreamCreateWithFlags(&c->in_stream, hipStreamNonBlocking));
     struct Inflight { bool live; size_t lo, hi; };
-    Inflight inf[2] = {{false, 0, 0}, {false, 0, 0}};
+    Inflight inf[3] = {};
     uint64_t fp_base = 0;
     // wait for the chunk in pipeline slot s, queue the copy of its packed
     // fingerprints to the caller's arena (chunk order; the slot's next chunk
     // queues behind it on the same stream) and rebase its records
     auto retire = [&](int s) -> int {
-        Slot &S = c->slot[1 + s];
+        Slot &S = c->slot[slot_of[s]];
         HIPCHK(hipStreamSynchronize(S.stream));
         if (analysis) {   // (the pipeline always decides its chunks itself, in order)
             const int r = slot_resolve_host(c, S, analysis + inf[s].lo, rec + inf[s].lo);
@@ -1252,14 +1418,20 @@ static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t ar
     };
     const size_t nch = (n + chunk - 1) / chunk;
     for (size_t k = 0; k < nch; k++) {
-        const int s = (int)(k & 1);
-        Slot &S = c->slot[1 + s];
-        if (inf[s].live) { int r = retire(s); if (r) return r; }
+        const int s = (int)(k % NP);
+        Slot &S = c->slot[slot_of[s]];
         const size_t lo = k * chunk, hi = std::min(n, lo + chunk), m = hi - lo;
+        uint64_t span[3];
+        if (instream) {   // the copy in first, then the wait for the slot's previous chunk
+            const int r = stage_copy(c, S, arena, arena_len, desc + lo, m, c->in_stream, span);
+            if (r) return r;
+        }
+        if (inf[s].live) { int r = retire(s); if (r) return r; }
         uint64_t bytes = 0;
         for (size_t i = lo; i < hi; i++) bytes += desc[i].caplen;
         const size_t cap = mfp_fp_arena_bound(m, bytes);
-        int r = stage_and_launch(c, 1 + s, arena, arena_len, desc + lo, m, cap, analysis != nullptr, attr_prob != nullptr);
+        int r = stage_and_launch(c, slot_of[s], arena, arena_len, desc + lo, m, cap, analysis != nullptr,
+                                 attr_prob != nullptr, false, nullptr, instream ? span : nullptr);
         if (r) return r;
         if (analysis) HIPCHK(hipMemcpyAsync(analysis + lo, S.d_an, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
         if (analysis && attr_prob && m)
@@ -1269,10 +1441,11 @@ static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t ar
         HIPCHK(hipMemcpyAsync(S.h_used, S.d_used, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S.stream));
         inf[s] = {true, lo, hi};
     }
-    // the older of the (up to) two chunks still in flight first
-    if (nch >= 2 && inf[nch & 1].live) { int r = retire((int)(nch & 1)); if (r) return r; }
-    for (int s = 0; s < 2; s++) if (inf[s].live) { int r = retire(s); if (r) return r; }
-    for (int s = 0; s < 2; s++) HIPCHK(hipStreamSynchronize(c->slot[1 + s].stream));   // the last string copies
+    for (size_t k = nch > (size_t)NP ? nch - NP : 0; k < nch; k++) {   // the chunks still in flight, oldest first
+        const int s = (int)(k % NP);
+        if (inf[s].live) { int r = retire(s); if (r) return r; }
+    }
+    for (int s = 0; s < NP; s++) HIPCHK(hipStreamSynchronize(c->slot[slot_of[s]].stream));   // the last string copies
     return (long long)fp_base;
 }
 

@@ -267,6 +267,39 @@ def test_pipelined_host_path_vs_reference(chunk):
     assert (rec3["fp_type"] == rec1["fp_type"]).all() and (rec3["flags"] == rec1["flags"]).all()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [1000, 4096])
+def test_pipelined_page_locked_outputs_equal_pageable(chunk):
+    """mfp_process_pipelined into page-locked outputs (three chunks in flight,
+    strings and records written by the device straight into them): the same
+    records, fingerprint arena and classifier results, byte for byte, as into
+    pageable outputs (the copying pipeline), and the reference's results."""
+    import torch
+    a, d = synth_batch()
+    ref = load_ref_an("an_synth.tsv.gz")
+    cfg = f"select={SELECT};resources={os.path.join(GOLD, 'synth_resources.tgz')};analysis"
+    runs = []
+    for pinned in (False, True):
+        ctx = mercury_amd.Context(cfg, device=0, mode=mercury_amd.api.MODE_ANALYSIS)
+        try:
+            cap = ctx.fp_arena_bound(d)
+            if pinned:
+                out = (torch.zeros(len(d) * 32, dtype=torch.uint8, pin_memory=True).numpy().view(mercury_amd.RECORD_DTYPE),
+                       torch.zeros(cap, dtype=torch.uint8, pin_memory=True).numpy(),
+                       np.zeros(len(d), mercury_amd.ANALYSIS_DTYPE))
+            else:
+                out = (np.zeros(len(d), mercury_amd.RECORD_DTYPE), np.zeros(cap, np.uint8),
+                       np.zeros(len(d), mercury_amd.ANALYSIS_DTYPE))
+            rec, used, an = ctx.process_pipelined(a, d, chunk=chunk, analysis=True, out=out)
+            names = [ctx.process_name(int(p)) for p in an["process"]]
+            runs.append((rec.tobytes(), out[1][:used].tobytes(), an.tobytes()))
+        finally:
+            ctx.close()
+    assert runs[0] == runs[1]
+    bad = compare(ref, rec, an, names)
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+
+
 # ---------------------------------------------------------------------------
 # encrypted resource archives (encrypted_file enc_file_reader.h:86-231):
 # tests/golden/resources-test.tgz.enc is resources-test.tgz under AES-128-CBC
