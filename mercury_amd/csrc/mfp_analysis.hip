@@ -1973,7 +1973,8 @@ extern "C" size_t mfp_analysis_huge_bytes(uint32_t max_nproc) {
 // neither's last round leaves CUs idle (5 and 4 blocks per CU on 256 CUs: 5120;
 // the flat 2048 was 1.6 rounds of k_analyze).  MFP_GRID_ROUND=0: 2048.
 static uint64_t seg_block_cap() {
-    static const uint64_t cap = [] {
+    static std::atomic<uint64_t> cap_cache[64];
+    const uint64_t cap = (uint64_t)mfp_per_device(cap_cache, [] {
         const char *e = getenv("MFP_GRID_ROUND");
         if (e && e[0] == '0') return (uint64_t)2048;
         int dev = 0, cus = 0, a = 0, f = 0;
@@ -1991,7 +1992,7 @@ static uint64_t seg_block_cap() {
         uint64_t l = ra / x * rf;
         if (const char *r = getenv("MFP_SEG_ROUNDS")) l *= strtoul(r, nullptr, 10) ? strtoul(r, nullptr, 10) : 1;
         return l <= 32768 ? l : (uint64_t)2048;
-    }();
+    });
     return cap;
 }
 
@@ -1999,7 +2000,8 @@ static uint64_t seg_block_cap() {
 // 5 waves per SIMD), over the segments with a stride; the flat 1024 ran it at 2
 // waves per SIMD.  MFP_GRID_ROUND=0: 1024.
 static uint32_t score_grid(uint32_t blocks) {
-    static const uint32_t res = [] {
+    static std::atomic<uint64_t> res_cache[64];
+    const uint32_t res = (uint32_t)mfp_per_device(res_cache, [] {
         const char *e = getenv("MFP_GRID_ROUND");
         if (e && e[0] == '0') return 1024u;
         int dev = 0, cus = 0, nb = 0;
@@ -2011,7 +2013,7 @@ static uint32_t score_grid(uint32_t blocks) {
             return 1024u;
         }
         return (uint32_t)(cus * nb);
-    }();
+    });
     return blocks < res ? blocks : res;
 }
 
@@ -2020,7 +2022,8 @@ static uint32_t score_grid(uint32_t blocks) {
 // one block per 1024 groups (763 blocks at 50 M packets: three quarters of the
 // CUs).  MFP_GRID_ROUND=0: one block per 1024 groups, at most 1024.
 static uint64_t seen_grid(uint64_t groups) {
-    static const uint64_t res = [] {
+    static std::atomic<uint64_t> res_cache[64];
+    const uint64_t res = (uint64_t)mfp_per_device(res_cache, [] {
         const char *e = getenv("MFP_GRID_ROUND");
         if (e && e[0] == '0') return (uint64_t)0;
         int dev = 0, cus = 0, nb = 0;
@@ -2032,7 +2035,7 @@ static uint64_t seen_grid(uint64_t groups) {
             return (uint64_t)0;
         }
         return (uint64_t)cus * (uint64_t)nb;
-    }();
+    });
     uint64_t sb = (groups + 1023) / 1024;
     if (sb > 1024) sb = 1024;
     if (res) {

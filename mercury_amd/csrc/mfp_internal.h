@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <string>
 
 #include "../../include/mfp.h"
@@ -40,3 +41,21 @@ bool mfp_hello_alpn(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, co
 long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                                    size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
                                    double *attr_prob);
+
+// A launch-shape value computed once per device (occupancy x CUs): cached per
+// hipGetDevice index, so contexts on different devices of one process each get
+// their own device's value (0 in a slot means not computed yet)
+template <class F>
+inline uint64_t mfp_per_device(std::atomic<uint64_t> (&cache)[64], F compute) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return (uint64_t)compute();
+    }
+    uint64_t v = cache[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+        v = (uint64_t)compute() + 1;
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v - 1;
+}

@@ -572,7 +572,8 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
 #ifdef MFP_PROBE_REPEAT   // (latency probe: the whole walk R times in the same wave)
     for (int rep_ = 0; rep_ < MFP_PROBE_REPEAT; rep_++)
 #endif
-    const bool spread = P.cfg.spread != 0;   // (P.idx == nullptr then)
+    // (P.idx == nullptr then; only the small-batch all-family instance spreads)
+    const bool spread = FAM == FAM_ALL && !SEGMODE && P.cfg.spread != 0;
     for (uint64_t g = blockIdx.x; (spread ? g : g * 64) < count; g += gridDim.x) {
         const uint64_t t = spread ? g : g * 64 + lane;
         const bool live = spread ? lane == 0 : t < count;
@@ -818,7 +819,8 @@ __global__ __launch_bounds__(64) void k_fp_lds(KParams P, uint32_t *fallback) {
 // round on two thirds of the CUs.  MFP_GRID_ROUND=0: the grid as given.
 template <auto KERN>
 inline uint32_t round_grid(uint32_t want) {
-    static const uint32_t res = [] {
+    static std::atomic<uint64_t> res_cache[64];
+    const uint32_t res = (uint32_t)mfp_per_device(res_cache, [] {
         const char *e = getenv("MFP_GRID_ROUND");
         if (e && e[0] == '0') return 0u;
         int dev = 0, cus = 0, nb = 0;
@@ -829,7 +831,7 @@ inline uint32_t round_grid(uint32_t want) {
             return 0u;
         }
         return (uint32_t)(cus * nb);
-    }();
+    });
     return res && want > res ? want / res * res : want;
 }
 
