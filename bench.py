@@ -1013,6 +1013,21 @@ def main():
             if len(pl) == len(names) and all(abs(prof[k][0] / args.steps - 1.0) < 1e-9 for k in names):
                 for k, x in zip(names, pl):
                     traffic[k] = x["hbm_bytes"]
+        # the step split into the fingerprint kernels and the classifier's (whose
+        # table re-reads are mostly cache-resident, so its traffic/bytes ratio
+        # reads differently from the walkers')
+        def step_part(pred):
+            ks = [k for k in kern_ms if pred(k)]
+            ms = sum(kern_ms[k] for k in ks)
+            ab = sum(kbytes.get(k, 0) or 0 for k in ks)
+            tb = (sum(traffic[k] for k in ks) if isinstance(traffic, dict) and ks and all(k in traffic for k in ks)
+                  else None)
+            ach = ab / (ms * 1e-3) / 1e9 if ms else 0.0
+            return {"kernels": len(ks), "kernel_ms": round(ms, 4), "algorithmic_bytes": ab, "achieved": round(ach, 2),
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tb,
+                    "traffic_per_algorithmic_byte": round(tb / ab, 3) if tb and ab else None}
+        is_clf = lambda k: k.startswith(("k_analyze", "k_an_", "k_seen"))   # noqa: E731
+        step_split = {"walkers": step_part(lambda k: not is_clf(k)), "classifier": step_part(is_clf)}
         n_fp = int((rec["fp_type"] > 0).sum())
         if workload == "mixed":
             wl = ("config 4: 50M mixed TLS/HTTP/SSH/TCP, protocol-ident + fingerprint + --analysis classifier "
@@ -1067,7 +1082,8 @@ def main():
                 "step": {"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "kernel_ms": round(step_kern_ms, 4), "algorithmic_bytes": alg_bytes,
                          "traffic": traffic if not isinstance(traffic, dict) else traffic.get("step"),
-                         "what": "every kernel of one step, back to back on one stream"},
+                         "what": "every kernel of one step, back to back on one stream",
+                         "split": step_split},
             },
             "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4),
                             "algorithmic_bytes": kbytes.get(k),
