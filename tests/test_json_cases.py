@@ -116,3 +116,57 @@ def test_hello_meta_analysis_context():
     lib.mercury_packet_processor_destruct(p)
     lib.mercury_finalize(mc)
     assert not bad, f"{len(bad)} mismatches: {bad[:6]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,limit", [("edge", None), ("corpus", None), ("fuzz0", 3000)])
+def test_shim_write_json_per_packet_vs_reference(name, limit):
+    """mercury_packet_processor_write_json_linktype packet by packet from 8
+    threads at once (one processor each: their calls are combined into
+    concurrent small batches, mfp_process_small_pinned; frames past the
+    walker's LDS stage -- the 65 535/70 000-byte edge cases -- are walked from
+    memory by their own wave): every record equals the reference's write_json
+    line for that packet."""
+    from concurrent.futures import ThreadPoolExecutor
+    arena, desc = cases.batch(cases.CASES[name][0]())
+    want = cases.load_json_golden(name, 0)
+    n = len(desc) if limit is None else min(limit, len(desc))
+    lib = mercury_amd.load_library()
+    vp = ctypes.c_void_p
+
+    class Timespec(ctypes.Structure):
+        _fields_ = [("tv_sec", ctypes.c_long), ("tv_nsec", ctypes.c_long)]
+
+    lib.mercury_init.restype = vp
+    lib.mercury_init.argtypes = [ctypes.POINTER(_LibmercConfig), ctypes.c_int]
+    lib.mercury_packet_processor_construct.restype = vp
+    lib.mercury_packet_processor_construct.argtypes = [vp]
+    lib.mercury_packet_processor_destruct.argtypes = [vp]
+    lib.mercury_finalize.argtypes = [vp]
+    f = lib.mercury_packet_processor_write_json_linktype
+    f.restype = ctypes.c_size_t
+    f.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(Timespec), ctypes.c_uint16]
+    cfg = _LibmercConfig()
+    cfg.packet_filter_cfg = cfg_string(0).encode()
+    mc = lib.mercury_init(ctypes.byref(cfg), 0)
+    assert mc
+    threads = 8
+
+    def work(t):
+        p = lib.mercury_packet_processor_construct(mc)
+        buf = ctypes.create_string_buffer(1 << 20)
+        bad = []
+        for i in range(t, n, threads):
+            off, ln = int(desc[i]["offset"]), int(desc[i]["caplen"])
+            pkt = ctypes.create_string_buffer(arena[off:off + ln].tobytes() + bytes(16))
+            ts = Timespec(TS // 1_000_000_000, TS % 1_000_000_000)
+            k = f(p, buf, len(buf), pkt, ln, ctypes.byref(ts), int(desc[i]["linktype"]))
+            if buf.raw[:k] != (want[i] + b"\n" if want[i] else b""):
+                bad.append(i)
+        lib.mercury_packet_processor_destruct(p)
+        return bad
+
+    with ThreadPoolExecutor(threads) as ex:
+        bad = sorted(sum(ex.map(work, range(threads)), []))
+    lib.mercury_finalize(mc)
+    assert not bad, f"{len(bad)} of {n} packets differ, first {bad[:8]}"
