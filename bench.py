@@ -743,6 +743,10 @@ def main():
         if tdist:
             tdist.destroy_process_group()
         return
+    if os.environ.get("MFP_BENCH_DEVICE0") == "1":
+        # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0
+        # (never a bench line: the ranks share one GPU)
+        local = 0
     torch.cuda.set_device(local)
 
     workload = args.workload
