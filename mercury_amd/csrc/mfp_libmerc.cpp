@@ -844,6 +844,10 @@ MFP_EXPORT int mercury_packet_processor_get_analysis_context_fdc(mercury_packet_
     log_error("mercury_packet_processor_get_analysis_context_fdc: FDC output is not provided by libmercury_amd\n");
     return -4;                   // fdc_return::UNKNOWN_ERROR
 }
+// the MFP_MSG_OTHER packets counted by note_other
+MFP_EXPORT uint64_t mercury_amd_other_packets(mercury_context mc) {
+    return mc ? mc->other.load(std::memory_order_relaxed) : 0;
+}
 MFP_EXPORT const char *mercury_get_license_string(void) {
     return "libmercury_amd: MI355X fingerprint/classify path for the libmerc API";
 }
