@@ -66,3 +66,51 @@ def test_selection_with_other_protocols_vs_reference(key):
     claimed = [i for i, s in enumerate(sources) if str(s).startswith(("other:http.rdp", "other:udp.wg.50000.443"))]
     if key != "mix":
         assert all(int(rec["msg"][i]) == OTHER for i in claimed), [(i, int(rec["msg"][i])) for i in claimed]
+
+
+@pytest.mark.gpu
+def test_shim_counts_packets_claimed_by_other_protocols():
+    """The libmerc shim under "all": per-packet write_json returns 0 for every
+    packet the device marks MFP_MSG_OTHER, and mercury_amd_other_packets
+    counts them (the records the reference writes and this library does not)."""
+    import ctypes
+    from tests.test_json import _LibmercConfig
+    arena, desc, _ = load()
+    ctx = mercury_amd.Context(MANIFEST["all"]["config"], device=0)
+    try:
+        rec, _ = ctx.process_host(arena, desc)
+    finally:
+        ctx.close()
+    idx = [i for i in range(len(desc)) if int(rec["msg"][i]) == OTHER][:200]
+    assert len(idx) >= 50
+    lib = mercury_amd.load_library()
+    vp = ctypes.c_void_p
+
+    class Timespec(ctypes.Structure):
+        _fields_ = [("tv_sec", ctypes.c_long), ("tv_nsec", ctypes.c_long)]
+
+    lib.mercury_init.restype = vp
+    lib.mercury_init.argtypes = [ctypes.POINTER(_LibmercConfig), ctypes.c_int]
+    lib.mercury_packet_processor_construct.restype = vp
+    lib.mercury_packet_processor_construct.argtypes = [vp]
+    lib.mercury_packet_processor_destruct.argtypes = [vp]
+    lib.mercury_finalize.argtypes = [vp]
+    lib.mercury_amd_other_packets.restype = ctypes.c_uint64
+    lib.mercury_amd_other_packets.argtypes = [vp]
+    f = lib.mercury_packet_processor_write_json_linktype
+    f.restype = ctypes.c_size_t
+    f.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(Timespec), ctypes.c_uint16]
+    cfg = _LibmercConfig()
+    cfg.packet_filter_cfg = MANIFEST["all"]["config"].encode()
+    mc = lib.mercury_init(ctypes.byref(cfg), 0)
+    assert mc and lib.mercury_amd_other_packets(mc) == 0
+    p = lib.mercury_packet_processor_construct(mc)
+    buf = ctypes.create_string_buffer(1 << 16)
+    for i in idx:
+        off, ln = int(desc[i]["offset"]), int(desc[i]["caplen"])
+        pkt = ctypes.create_string_buffer(arena[off:off + ln].tobytes() + bytes(16))
+        ts = Timespec(TS // 10**9, 0)
+        assert f(p, buf, len(buf), pkt, ln, ctypes.byref(ts), int(desc[i]["linktype"])) == 0, i
+    assert lib.mercury_amd_other_packets(mc) == len(idx)
+    lib.mercury_packet_processor_destruct(p)
+    lib.mercury_finalize(mc)
