@@ -362,10 +362,30 @@ struct Em {
         if (out_end && out + 8 * ((words + 1) & ~1u) > out_end) return;   // (an over-long string: dropped anyway)
         for (uint32_t k = 0; 2 * k < words; k++) o4[k] = l4[k];
     }
+    // LINEW == 2: the pending word stays in registers and every second word
+    // leaves with one 16-byte store (no LDS line): lanes reach a store at
+    // different pushes, and a wave then issues one store instruction there
+    // instead of an 8-word line's four LDS reads and four stores
+    uint64_t w0 = 0;
     DEV void put_word() {
         h ^= mfpc::word_term(acc, wi++);
+        if constexpr (LINEW == 2) {
+            if (nw == 0) { w0 = acc; nw = 1; return; }
+            store2(acc);
+            out += 16;
+            nw = 0;
+            return;
+        }
         line[nw++] = acc;
         if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
+    }
+    DEV void store2(uint64_t w1) {
+#ifdef MFP_PROBE_NOSTORE
+        if (w1 == 0x0123456789abcdefull) *(volatile uint8_t *)out = 0;
+        return;
+#endif
+        if (out_end && out + 16 > out_end) return;   // (an over-long string: dropped anyway)
+        *(uint4 *)out = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
     }
     DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
         if (EMIT) {
@@ -385,6 +405,11 @@ struct Em {
     }
     DEV void finish() {
         if (EMIT) {
+            if constexpr (LINEW == 2) {
+                if (nacc) { put_word(); nacc = 0; }
+                if (nw) store2(0);
+                return;
+            }
             if (nacc) { h ^= mfpc::word_term(acc, wi++); line[nw++] = acc; nacc = 0; }
             if (nw) flush_line(nw);
         }

@@ -26,6 +26,54 @@ namespace mfp {
 
 constexpr int TILE = 256;
 
+// Tile order by length (k_fp_tls1: MFP_TLS_SORT, k_fp_seg: MFP_SEG_SORT).  A
+// lane-per-packet wave runs every loop for its longest packet and every
+// branch its lanes take, so the tile's packets are handed to its lanes in
+// caplen order: packets of one length are mostly one client's hello or one
+// request template, so a wave's lanes walk and emit alike.  The rank of each
+// packet is the count of smaller (caplen, lane) keys, read four at a time
+// from LDS (every lane reads the same words: broadcast, no bank conflict);
+// the tile's live packets stay the first lanes.  Output placement does not
+// change meaning: the records address their strings.
+#ifndef MFP_TLS_SORT
+#define MFP_TLS_SORT 1
+#endif
+#ifndef MFP_SEG_SORT
+#define MFP_SEG_SORT 0
+#endif
+struct TileSort {
+    uint32_t key[TILE] __attribute__((aligned(16)));
+    uint32_t idx[TILE];
+    mfp_pkt_desc desc[TILE];
+};
+template <bool ALIASED = false>   // ALIASED: s overlays LDS the walk writes (a barrier after the reads)
+DEV void tile_take(const KParams &P, uint64_t tile, uint64_t count, TileSort &s, int tid, uint64_t &i,
+                   mfp_pkt_desc &dsc, bool &live) {
+    const uint64_t t = tile * TILE + tid;
+    live = t < count;
+    const uint32_t i0 = live ? P.idx[t] : 0u;
+    mfp_pkt_desc d0;
+    if (live) d0 = P.desc[i0];
+    else { d0.offset = 0; d0.caplen = 0; d0.linktype = 0xffff; d0.flags = 0; }
+    const uint32_t cl = d0.caplen < 0xfffffeu ? d0.caplen : 0xfffffeu;
+    const uint32_t mk = ((live ? cl : 0xffffffu) << 8) | (uint32_t)tid;
+    s.key[tid] = mk;
+    __syncthreads();
+    uint32_t r = 0;
+#pragma unroll 8
+    for (int j = 0; j < TILE; j += 4) {
+        const uint4 v = *(const uint4 *)&s.key[j];
+        r += (v.x < mk ? 1u : 0u) + (v.y < mk ? 1u : 0u) + (v.z < mk ? 1u : 0u) + (v.w < mk ? 1u : 0u);
+    }
+    s.idx[r] = i0;
+    s.desc[r] = d0;
+    __syncthreads();
+    i = s.idx[tid];
+    dsc = s.desc[tid];
+    if (ALIASED) __syncthreads();
+    // (otherwise the caller's end-of-tile barrier orders these reads before the next tile's writes)
+}
+
 // k_fingerprint -- lane-per-packet walker straight from HBM, grid-stride
 // over tiles of TILE packets.  The fallback lane of the other bin kernels
 // (packets larger than k_fp_lds's stage, segment lists that overflow); with
@@ -192,6 +240,11 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
 #ifndef MFP_TLS_ONEPASS
 #define MFP_TLS_ONEPASS 1
 #endif
+// emission line in words: 8 (a 64-byte LDS line per lane, four 16-byte
+// stores per full line) or 2 (no LDS line: one 16-byte store per two words)
+#ifndef MFP_TLS_LINEW
+#define MFP_TLS_LINEW 8
+#endif
 template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
@@ -199,17 +252,28 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
     __shared__ uint16_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
     __shared__ uint8_t ext_ord[FMT ? TILE : 1][FAST_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
+#if MFP_TLS_SORT   // over the emission lines (the extension windows are written right after the take)
+    static_assert(sizeof(TileSort) <= sizeof(out_line), "TileSort in out_line");
+    TileSort &tsort = *reinterpret_cast<TileSort *>(&out_line[0][0]);
+#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     KPH_DECL
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
+#if MFP_TLS_SORT
+        uint64_t i;
+        bool live;
+        mfp_pkt_desc dsc;
+        tile_take<true>(P, tile, count, tsort, tid, i, dsc, live);
+#else
         const uint64_t t = tile * TILE + tid;
         const bool live = t < count;
         const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
         mfp_pkt_desc dsc;
         if (live) dsc = P.desc[i];
         else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
+#endif
         const uint8_t *data = P.arena + dsc.offset;
 
         // reservation from the bound: one atomic per tile
@@ -289,7 +353,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
 #else
         if (len && fits) {
 #endif
-            Em<true, -1, 8, MFP_LEBLOCK16 != 0> e;   // the packet is in HBM
+            Em<true, -1, MFP_TLS_LINEW, MFP_LEBLOCK16 != 0> e;   // the packet is in HBM
             e.begin(P.fp_arena + base + excl, out_line[tid]);
             tls_ch_emit_fast<FMT>(e, plan);
             e.finish();
@@ -345,7 +409,10 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
 #endif
 constexpr int SEG_STRIDE = SEG_MAX + 1;   // odd word stride: lane-private lists are bank-conflict free
 constexpr uint32_t SEG_STAGE = 2048;      // packets up to this (minus alignment) are staged in LDS for expansion
-constexpr int SEG_LINEW = 4;              // lane emission: words per LDS line
+#ifndef MFP_SEG_LINEW
+#define MFP_SEG_LINEW 4
+#endif
+constexpr int SEG_LINEW = MFP_SEG_LINEW;  // lane emission: words per LDS line (2: no LDS line, Em)
 template <uint32_t FAM = FAM_HTTP>
 __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32_t *fallback) {
     __shared__ uint32_t segs[TILE * SEG_STRIDE];
@@ -357,9 +424,16 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
     __shared__ uint8_t s_slots[(1 << REQ_BITS) + (1 << RESP_BITS)];
 #endif
 #if MFP_SEG_LANE
-    __shared__ uint64_t out_line[TILE][SEG_LINEW];
+    __shared__ __attribute__((aligned(16))) uint64_t out_line[TILE][SEG_LINEW];
+#if MFP_SEG_SORT   // the emission lines are free while the tile is taken (a barrier precedes the emission)
+    static_assert(sizeof(TileSort) <= sizeof(out_line), "TileSort in out_line");
+    TileSort &tsort = *reinterpret_cast<TileSort *>(&out_line[0][0]);
+#endif
 #else
     __shared__ uint4 stage[TILE / 64][SEG_STAGE / 16];   // per wave: the packet being expanded
+#if MFP_SEG_SORT
+    __shared__ TileSort tsort;
+#endif
 #endif
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
@@ -379,12 +453,19 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     KPH_DECL
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
+#if MFP_SEG_SORT
+        uint64_t i;
+        bool live;
+        mfp_pkt_desc dsc;
+        tile_take(P, tile, count, tsort, tid, i, dsc, live);
+#else
         const uint64_t t = tile * TILE + tid;
         const bool live = t < count;
         const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
         mfp_pkt_desc dsc;
         if (live) dsc = P.desc[i];
         else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
+#endif
         const uint8_t *data = P.arena + dsc.offset;
 
         Out o;
