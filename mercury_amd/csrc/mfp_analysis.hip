@@ -780,11 +780,28 @@ __global__ __launch_bounds__(64 * AW) void k_analyze(AParams P) {
 #ifndef MFP_AN_FEAT_MINW
 #define MFP_AN_FEAT_MINW 4   // 4 waves/SIMD: 10.4 -> 9.0 ms (r03l A/B), no spill
 #endif
+// MFP_AN_FEAT_PREF: a batch's work items, records and descriptors arrive in
+// LDS by direct-to-LDS 16-byte loads (global_load_lds_dwordx4: no VGPRs) one
+// batch ahead -- the work items two batches ahead, since the records' addresses
+// come from them -- so a batch starts from its packet bytes and entry, two
+// dependent memory round trips fewer per batch
+#ifndef MFP_AN_FEAT_PREF
+#define MFP_AN_FEAT_PREF 1
+#endif
+ADEV void lds_load16(const void *src, void *lds_base) {   // lane l's 16 bytes at lds_base + 16 l
+    __builtin_amdgcn_global_load_lds(src, (void __attribute__((address_space(3))) *)lds_base, 16, 0, 0);
+}
 __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(AParams P) {
     const uint32_t lane = lane_id();
     const int wid = (int)rfl(threadIdx.x >> 6);
     const mfp_classifier_dev &D = P.D;
     const uint32_t seg = (uint32_t)(blockIdx.x * AW + wid);
+#if MFP_AN_FEAT_PREF
+    static_assert(sizeof(WorkItem) == 16 && sizeof(mfp_record) == 32 && sizeof(mfp_pkt_desc) == 16, "16-byte rows");
+    __shared__ __attribute__((aligned(16))) uint4 pf_w[AW][2][64];   // work items, by batch parity
+    __shared__ __attribute__((aligned(16))) uint4 pf_r[AW][2][64];   // the batch's records, two halves
+    __shared__ __attribute__((aligned(16))) uint4 pf_d[AW][64];      // the batch's descriptors
+#endif
     if (seg >= P.nseg) return;
     const WorkItem *wk = P.work + (uint64_t)seg * P.seg_cap;
     Deferred *ll = P.lanel + (uint64_t)seg * P.seg_cap;
@@ -792,19 +809,51 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
     const uint32_t total = rfl(P.seg_n[3 * seg]);
     uint32_t n_l = 0, n_d = 0;       // wave-uniform list counts
     uint32_t n_look = 0;             // feature-table lookups issued by this lane (mfp_analysis_counters [10])
+#if MFP_AN_FEAT_PREF
+    // the records and descriptors of the work item at pf_w[wid][par][lane]
+    auto pref_rows = [&](uint32_t par) {
+        const WorkItem x = *(const WorkItem *)&pf_w[wid][par][lane];
+        const uint8_t *rp = (const uint8_t *)(P.rec + x.i);
+        lds_load16(rp, &pf_r[wid][0][0]);
+        lds_load16(rp + 16, &pf_r[wid][1][0]);
+        lds_load16(P.desc + x.i, &pf_d[wid][0]);
+    };
+    if (lane < total) lds_load16(wk + lane, &pf_w[wid][0][0]);
+    if (64 + lane < total) lds_load16(wk + 64 + lane, &pf_w[wid][1][0]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane < total) pref_rows(0);
+#endif
     for (uint32_t b0 = 0; b0 < total; b0 += 64) {
         const bool live = b0 + lane < total;
         WorkItem w;
+        mfp_record r;
+#if MFP_AN_FEAT_PREF
+        const uint32_t par = (b0 >> 6) & 1u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this batch's rows, the next batch's items
+        uint64_t doff = 0;
+        if (live) {
+            w = *(const WorkItem *)&pf_w[wid][par][lane];
+            const uint4 r0 = pf_r[wid][0][lane], r1 = pf_r[wid][1][lane];
+            uint4 rr[2] = {r0, r1};
+            __builtin_memcpy(&r, rr, 32);
+            doff = ((const mfp_pkt_desc *)&pf_d[wid][lane])->offset;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the next batch's rows land
+        if (b0 + 64 + lane < total) pref_rows(par ^ 1u);
+        if (b0 + 128 + lane < total) lds_load16(wk + b0 + 128 + lane, &pf_w[wid][par][0]);
+#else
         if (live) w = wk[b0 + lane];
-        else { w.i = 0; w.entry = 0xffffffffu; w.flags = 0; w.pad = 0; }
+#endif
+        if (!live) { w.i = 0; w.entry = 0xffffffffu; w.flags = 0; w.pad = 0; }
         const uint64_t i = w.i;
         const bool xcheck = w.flags & WK_XCHECK, pending = w.flags & WK_PENDING;
         bool scored = w.flags & WK_SCORE;
         const uint32_t entry = w.entry;
-        mfp_record r;
+#if !MFP_AN_FEAT_PREF
         if (live) r = P.rec[i];
-        else { r.fp_len = 0; r.fp_type = 0; r.flags = 0; r.fp_offset = 0; r.net = 0; r.msg = 0;
-               r.sni_off = 0; r.sni_len = 0xffff; r.ua_off = 0; r.ua_len = 0xffff; r.dst_port = 0; r.xflags = 0; }
+#endif
+        if (!live) { r.fp_len = 0; r.fp_type = 0; r.flags = 0; r.fp_offset = 0; r.net = 0; r.msg = 0;
+                     r.sni_off = 0; r.sni_len = 0xffff; r.ua_off = 0; r.ua_len = 0xffff; r.dst_port = 0; r.xflags = 0; }
         const uint8_t *fp = P.fp_arena + r.fp_offset;
         mfp_entry E;
         E.proc_off = 0; E.nproc = 0; E.malware_db = 0; E.generic_dmz = 0;
@@ -824,7 +873,11 @@ __global__ __launch_bounds__(64 * AW, MFP_AN_FEAT_MINW) void k_an_features(APara
         bool has[3] = {false, false, false};
         // ---- destination context (destination_context::init, result.h:346)
         // and the classifier-agnostic attributes of a ClientHello
+#if MFP_AN_FEAT_PREF
+        const uint8_t *pkt = P.arena + (scored || xcheck ? doff : 0);
+#else
         const uint8_t *pkt = P.arena + (scored || xcheck ? P.desc[i].offset : 0);
+#endif
         // server name / user agent: packet bytes, or the QUIC sidecar behind the string's hash
         const uint8_t *sbase = (r.flags & MFP_FLAG_SIDECAR) ? fp + ((r.fp_len + 7) & ~7u) + 8 : pkt;
         Dst dd;

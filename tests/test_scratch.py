@@ -68,13 +68,14 @@ def kernel_scratch():
 # waves/SIMD with register caps below what the whole parser family wants, and
 # spill; these are their current bounds (bytes per lane), so a growth shows up
 # here.  FAM: 2 SSH, 4 HTTP, 16 DTLS, 63 all (the fallback lane).  k_an_features
-# runs at 4 waves/SIMD with a 12-byte spill (faster than 3 waves without; round 5:
-# the six feature probes' home slots loaded together, 8 -> 12 bytes, 8.55 -> 8.18 ms).
+# runs at 4 waves/SIMD with a 20-byte spill (faster than 3 waves without; round 5:
+# the six feature probes' home slots loaded together, 8 -> 12 bytes, 8.55 -> 8.18 ms;
+# the batch's items, records and descriptors prefetched into LDS, 12 -> 20 bytes, 8.22 -> 8.00 ms).
 # The HTTP and fallback walkers carry the checks for selected protocols outside
 # the path (tcp_other_matcher & co., round 4): +8 and +32 bytes.  k_fp_tls1
 # (one instance per TLS format, round 4: plan length by arithmetic, uniform
 # emitter) spills nothing for formats 0 and 1 and 8 bytes for format 2.
-BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8, "k_an_features": 12, "k_fingerprintILj2E": 176, "k_fingerprintILj4E": 36,
+BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8, "k_an_features": 20, "k_fingerprintILj2E": 176, "k_fingerprintILj4E": 36,
                   "k_fingerprintILj16E": 496, "k_fingerprintILj63E": 944, "k_fp_ldsILb0ELj36864ELj63E": 176,
                   "k_fp_ldsILb0ELj36864ELj2E": 176,
                   # the one-parse transport parameter sort (round 4): the LDS TLS walker +12, the DTLS
