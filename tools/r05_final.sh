@@ -11,6 +11,7 @@ T=${TAG:-r05f}
 O=gpurun_out/$T
 mkdir -p $O
 TAG=$T BENCH="--diverse-leg 0" bash tools/gpu_traffic.sh || exit 1
+cp $O/traffic.json profiles/${T}_traffic_50M_analysis_survey.json   # (the box copy: the bench below reports it)
 B="python3 bench.py --packets 10000000 --steps 3 --warmup 1 --no-cpu-baseline --e2e-total 0 --diverse-leg 0 --no-other-paths"
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_INSTS_SMEM -f csv -d $O/p1 -o p1 -- $B > $O/p1.out 2>&1 || { tail -5 $O/p1.out; exit 1; }
 echo "sq pass 1 done"
