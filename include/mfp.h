@@ -370,6 +370,14 @@ MFP_EXPORT long long mfp_process_batch_reassembly(mfp_context ctx, mfp_reassembl
                                                   const uint64_t *ts_ns, mfp_record *rec, char *fp_arena,
                                                   size_t fp_cap, uint16_t *props, mfp_pkt_desc *out_desc);
 MFP_EXPORT const uint8_t *mfp_reassembler_frames(mfp_reassembler r, size_t *len);
+/* Per packet of the last batch (*n of them): 1 when the reference's
+ * tcp_reassembler::dump_pkt is set after that packet (stateful_pkt_proc::dump_pkt
+ * pkt_proc.cc:1842-1845) -- its data went into the flow table (TCP segments
+ * pkt_proc.cc:852-866, QUIC / DTLS reassembly.hpp:931-1009,1074-1079); a packet
+ * that does not reach the IP layer keeps the value of the packet before it, as
+ * the reference does.  The filtered pcap writer writes these packets too
+ * (pkt_processing.h:104,250).  Valid until the reassembler's next call. */
+MFP_EXPORT const uint8_t *mfp_reassembler_dumped(mfp_reassembler r, size_t *n);
 /* With --analysis (a context with resources=...;analysis;reassembly): the same,
  * then the records the reference writes -- packets with a record, the
  * reassembled messages -- fingerprinted and classified once more in stream
@@ -500,7 +508,10 @@ MFP_EXPORT int mfp_process_os_info(mfp_context ctx, uint32_t proc_slot, uint32_t
 
 /* last analysis batch: [0] packets classified, [1] unknown-TLS sightings,
  * [2] fingerprints with more processes than the kernel handles (512),
- * [3] fingerprints in the context's prevalence LRU */
+ * [3] fingerprints in the context's prevalence LRU.  "Last batch" means the
+ * last batch of the batch API (slots 0-4); the per-packet libmerc shim's
+ * concurrent small batches run on slots of their own and are not counted
+ * here or in mfp_analysis_counters. */
 MFP_EXPORT int mfp_analysis_stats(mfp_context ctx, uint64_t out[4]);
 
 /* the last analysis batch's counters, up to n of: [0] packets classified,

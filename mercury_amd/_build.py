@@ -9,7 +9,12 @@ LIB = os.path.join(HERE, "libmercury_amd.so")
 OBJ = os.path.join(HERE, "_obj")
 
 SOURCES = ["mfp_kernels.hip", "mfp_k_tls.hip", "mfp_k_http.hip", "mfp_k_small.hip", "mfp_k_all.hip", "mfp_analysis.hip", "mfp_compact.hip", "mfp_host.cpp", "mfp_classifier.cpp", "mfp_libmerc.cpp",
-           "mfp_pcap.cpp", "mfp_json.cpp", "mfp_prevalence.cpp", "mfp_quic.hip", "mfp_reassembly.cpp"]
+           "mfp_pcap.cpp", "mfp_json.cpp", "mfp_prevalence.cpp", "mfp_quic.hip", "mfp_reassembly.cpp",
+           "mfp_pktproc.cpp"]
+# the pcap -> JSON / filtered-pcap driver over the batch packet processors
+# (mercury_amd/csrc/mfp_drv.cpp), linked against the library beside it
+DRV_SRC = os.path.join(CSRC, "mfp_drv.cpp")
+DRV = os.path.join(HERE, "mercury-amd")
 ARCH = os.environ.get("MFP_OFFLOAD_ARCH", "gfx950")
 
 
@@ -53,6 +58,12 @@ def build(verbose=False):
             raise subprocess.CalledProcessError(p.returncode, cmd)
     if _newer(LIB, objs):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lcrypto"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    if _newer(DRV, sorted(_includes(DRV_SRC)) + [LIB]):
+        cmd = ["g++", "-O2", "-std=c++17", "-Wall", DRV_SRC, "-o", DRV, "-L" + HERE, "-lmercury_amd",
+               "-Wl,-rpath,$ORIGIN", "-lpthread"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -212,8 +212,94 @@ def load_library():
     lib.mfp_analysis_last.argtypes = [vp, vp, sz]
     lib.mfp_analysis_resolve_sequence.restype = ctypes.c_int
     lib.mfp_analysis_resolve_sequence.argtypes = [vp, vp, sz]
+    # batch packet processors (include/mfp_pkt_proc.h)
+    lib.mfp_pkt_proc_create.restype = vp
+    lib.mfp_pkt_proc_create.argtypes = [vp, ctypes.c_int, ctypes.POINTER(PktProcOpts), SINK_FN, vp]
+    lib.mfp_pkt_proc_apply.restype = ctypes.c_int
+    lib.mfp_pkt_proc_apply.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint16, vp]
+    for f in ("mfp_pkt_proc_flush", "mfp_pkt_proc_drain", "mfp_pkt_proc_finalize"):
+        getattr(lib, f).restype = ctypes.c_int
+        getattr(lib, f).argtypes = [vp]
+    lib.mfp_pkt_proc_destroy.argtypes = [vp]
+    lib.mfp_pkt_proc_stats.restype = ctypes.c_int
+    lib.mfp_pkt_proc_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), sz]
+    lib.mfp_pcap_file_header.restype = sz
+    lib.mfp_pcap_file_header.argtypes = [vp]
+    lib.mfp_reassembler_dumped.restype = vp
+    lib.mfp_reassembler_dumped.argtypes = [vp, ctypes.POINTER(sz)]
     _lib = lib
     return lib
+
+
+class PktProcOpts(ctypes.Structure):
+    """mfp_pkt_proc_opts (include/mfp_pkt_proc.h)."""
+    _fields_ = [("batch_pkts", ctypes.c_size_t), ("arena_bytes", ctypes.c_size_t), ("flush_us", ctypes.c_uint32),
+                ("json_threads", ctypes.c_int), ("chunk", ctypes.c_size_t)]
+
+
+SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+PKT_PROC_JSON, PKT_PROC_FILTER_PCAP = 0, 1
+PKT_PROC_STATS = ["packets", "batches", "records", "bytes", "device_ns", "writer_ns", "skipped"]
+
+
+def pcap_file_header():
+    """The 24-byte header of a `mercury -w` output file (mfp_pcap_file_header)."""
+    lib = load_library()
+    b = ctypes.create_string_buffer(24)
+    assert lib.mfp_pcap_file_header(b) == 24
+    return b.raw
+
+
+class PacketProcessor:
+    """A batch packet processor (include/mfp_pkt_proc.h) over a context made
+    with MODE_WRITE_JSON: kind PKT_PROC_JSON (pkt_proc_json_writer_llq's
+    output) or PKT_PROC_FILTER_PCAP (`mercury -w`).  apply() takes one
+    packet, as pkt_proc::apply does; the output collects in `self.out`."""
+
+    def __init__(self, ctx, kind=PKT_PROC_JSON, batch_pkts=0, arena_bytes=0, flush_us=0, json_threads=0, chunk=0):
+        self.lib = ctx.lib
+        self.out = bytearray()
+        self.calls = 0
+
+        def sink(_user, data, n):
+            self.out += ctypes.string_at(data, n)
+            self.calls += 1
+            return 0
+        self._sink = SINK_FN(sink)          # kept alive as long as the processor
+        opts = PktProcOpts(batch_pkts, arena_bytes, flush_us, json_threads, chunk)
+        self.h = self.lib.mfp_pkt_proc_create(ctx.h, kind, ctypes.byref(opts), self._sink, None)
+        if not self.h:
+            raise MercuryAmdError("mfp_pkt_proc_create failed: " + _err(self.lib))
+
+    def _check(self, r, what):
+        if r:
+            raise MercuryAmdError(f"{what} failed ({r}): " + _err(self.lib))
+
+    def apply(self, packet, ts_sec=0, ts_nsec=0, linktype=1, length=None):
+        b = bytes(packet)
+        n = len(b)
+        self._check(self.lib.mfp_pkt_proc_apply(self.h, ts_sec, ts_nsec, n, n if length is None else length,
+                                                linktype, b), "mfp_pkt_proc_apply")
+
+    def flush(self):
+        self._check(self.lib.mfp_pkt_proc_flush(self.h), "mfp_pkt_proc_flush")
+
+    def drain(self):
+        self._check(self.lib.mfp_pkt_proc_drain(self.h), "mfp_pkt_proc_drain")
+
+    def finalize(self):
+        self._check(self.lib.mfp_pkt_proc_finalize(self.h), "mfp_pkt_proc_finalize")
+
+    def stats(self):
+        v = (ctypes.c_uint64 * len(PKT_PROC_STATS))()
+        self._check(self.lib.mfp_pkt_proc_stats(self.h, v, len(PKT_PROC_STATS)), "mfp_pkt_proc_stats")
+        return dict(zip(PKT_PROC_STATS, list(v)))
+
+    def close(self):
+        if self.h:
+            self.lib.mfp_pkt_proc_destroy(self.h)
+            self.h = None
 
 
 def _err(lib):

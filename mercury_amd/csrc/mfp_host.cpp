@@ -1125,7 +1125,12 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
         for (int j = 0; j < mfp_context_s::NSMALL && k < 0; j++) {
             if (c->small_busy[j]) continue;
             if (!c->small_init[j]) {
-                if (!c->small[j].init()) { mfp_set_error("small-batch slot: HIP allocation failed"); return -2; }
+                if (!c->small[j].init()) {
+                    c->small[j].release();        // what init() allocated before it failed
+                    c->small[j] = Slot{};
+                    mfp_set_error("small-batch slot: HIP allocation failed");
+                    return -2;
+                }
                 c->small_init[j] = true;
             }
             c->small_busy[j] = true;
@@ -1147,8 +1152,13 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
     // straight into the caller's buffers -- one launch, no copies at all
     // (strings at their reserved, not packed, offsets; at least 64 bytes
     // after the last packet, which the walker may read)
+    // Only the SMALL strategy's last wave copies the counters out, resets them
+    // and sets the done flag (process_device_locked picks it for binned
+    // contexts at n <= small_batch); any other strategy takes the staged path,
+    // whose k_compact_small does that work
     const bool direct = !analysis && !(c->select & (SEL_QUIC | SEL_OPENVPN)) && hi + 64 <= arena_len &&
-                        fp_cap >= mfp_fp_arena_bound(n, total) && !getenv("MFP_SMALL_STAGED");
+                        c->strategy == MFP_STRATEGY_BINNED && fp_cap >= mfp_fp_arena_bound(n, total) &&
+                        !getenv("MFP_SMALL_STAGED");
     if (direct) {
         {
             std::lock_guard<std::mutex> lk(c->mu);
@@ -1161,6 +1171,13 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
             if (r) return r;
         }
         if (wait_done_flag(S)) return -2;
+        if (__atomic_load_n(&S.h_used[4], __ATOMIC_ACQUIRE) == 0) {
+            // the stream drained without the walker's done flag: the counters
+            // were neither copied out nor reset (cnt_dirty stays set, so the
+            // next batch clears them)
+            mfp_set_error("small batch finished without its done flag");
+            return -3;
+        }
         S.cnt_dirty = false;
         const unsigned long long used = S.h_used[0];   // reserved bytes: strings at their slots
         if (S.h_used[1] || used > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
@@ -1272,6 +1289,7 @@ extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8
         // either pipeline stream: drain both before the caller reuses them
         // (the error string of the failure is kept)
         for (int s : {1, 2, 4}) (void)hipStreamSynchronize(c->slot[s].stream);
+        if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);   // chunk copies still reading the arena
     }
     return r;
 }

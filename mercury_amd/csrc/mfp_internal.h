@@ -42,6 +42,14 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
                                    size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
                                    double *attr_prob);
 
+// the JSON writer (mfp_json.cpp) handing its text to a sink in packet order:
+// the batch packet processors (mfp_pktproc.cpp); props / analysis optional
+typedef int (*mfp_json_sink)(void *user, const void *data, size_t len);
+long long mfp_write_json_to_sink(mfp_context ctx, const uint16_t *props, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                 size_t n, const mfp_record *rec, const char *fp_arena, const mfp_analysis *analysis,
+                                 const double *attr_prob, const uint64_t *ts_ns, uint64_t *line_end, uint64_t *skipped,
+                                 int threads, mfp_json_sink sink, void *user);
+
 // A launch-shape value computed once per device (occupancy x CUs): cached per
 // hipGetDevice index, so contexts on different devices of one process each get
 // their own device's value (0 in a slot means not computed yet)

@@ -1157,12 +1157,14 @@ bool mfp_hello_alpn(const uint8_t *pkt, uint32_t caplen, const mfp_record &r, co
     return found;
 }
 
+// sink != nullptr: the threads' parts go to sink in packet order instead of
+// into out (the batch packet processors, mfp_pktproc.cpp); out_cap unused
 static long long write_json_batch(mfp_context ctx, const uint16_t *props, const uint8_t *arena, const mfp_pkt_desc *desc,
                                    size_t n,
                                    const mfp_record *rec, const char *fp_arena, const mfp_analysis *an, const double *ap,
                                    const uint64_t *ts_ns, char *out, size_t out_cap, uint64_t *line_end,
-                                   uint64_t *skipped, int threads) {
-    if ((n && (!arena || !desc || !rec || !fp_arena || !line_end)) || (out_cap && !out)) {
+                                   uint64_t *skipped, int threads, mfp_json_sink sink = nullptr, void *user = nullptr) {
+    if ((n && (!arena || !desc || !rec || !fp_arena || !line_end)) || (out_cap && !out && !sink)) {
         mfp_set_error("mfp_write_json_batch: null argument");
         return -1;
     }
@@ -1222,6 +1224,16 @@ static long long write_json_batch(mfp_context ctx, const uint16_t *props, const 
         std::lock_guard<std::mutex> lk(pool_mu);
         if (pool.size() < part.size()) pool.swap(part);
     };
+    if (sink) {
+        for (int t = 0; t < threads; t++)
+            if (part[(size_t)t].len && sink(user, part[(size_t)t].buf.get(), part[(size_t)t].len) != 0) {
+                give_back();
+                mfp_set_error("JSON output: the sink failed");
+                return -3;
+            }
+        give_back();
+        return (long long)total;
+    }
     if (total > out_cap) {
         give_back();
         mfp_set_error("mfp_write_json_batch: output buffer too small (need %llu bytes)", (unsigned long long)total);
@@ -1286,4 +1298,15 @@ MFP_EXPORT long long mfp_write_json_batch_reassembly_analysis(mfp_context ctx, c
     if (n && (!props || !analysis)) { mfp_set_error("mfp_write_json_batch_reassembly_analysis: null argument"); return -1; }
     return write_json_batch(ctx, props, arena, desc, n, rec, fp_arena, analysis, attr_prob, ts_ns, out, out_cap,
                             line_end, skipped, threads);
+}
+
+// the batch packet processors' form (mfp_pktproc.cpp): any of the four
+// writers above, the text handed to sink in packet order
+long long mfp_write_json_to_sink(mfp_context ctx, const uint16_t *props, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                 size_t n, const mfp_record *rec, const char *fp_arena, const mfp_analysis *analysis,
+                                 const double *attr_prob, const uint64_t *ts_ns, uint64_t *line_end, uint64_t *skipped,
+                                 int threads, mfp_json_sink sink, void *user) {
+    if (analysis && (!ctx || !mfp_analysis_enabled(ctx))) { mfp_set_error("the context has no classifier"); return -1; }
+    return write_json_batch(analysis ? ctx : nullptr, props, arena, desc, n, rec, fp_arena, analysis, attr_prob, ts_ns,
+                            nullptr, 0, line_end, skipped, threads, sink, user);
 }

@@ -296,6 +296,8 @@ struct mfp_reassembler_s {
     std::vector<size_t> who;                        // packet index of each rebuilt frame
     std::vector<uint16_t> who_props;
     std::vector<uint8_t> quiet;                     // 1: a segment that writes no record (return false)
+    std::vector<uint8_t> dump;                      // 1: the packet fed the flow table (tcp_reassembler::dump_pkt)
+    uint8_t dump_carry = 0;                         // dump_pkt after the last packet of the previous batch
     std::vector<uint8_t> merged;                    // arena ++ frames (the classifier pass)
     std::vector<mfp_pkt_desc> desc3;
     QCrypto qc;                                     // the current QUIC Initial's crypto buffer
@@ -305,6 +307,15 @@ struct mfp_reassembler_s {
 extern "C" MFP_EXPORT mfp_reassembler mfp_reassembler_create(void) { return new mfp_reassembler_s; }
 extern "C" MFP_EXPORT void mfp_reassembler_destroy(mfp_reassembler r) { delete r; }
 extern "C" MFP_EXPORT uint64_t mfp_reassembler_flows(mfp_reassembler r) { return r ? r->table.size() : 0; }
+// tcp_reassembler::dump_pkt after each packet of the last batch
+// (stateful_pkt_proc::dump_pkt pkt_proc.cc:1842-1845): set where the reference
+// hands the packet's data to process_tcp_data_pkt / process_udp_data_pkt
+// (pkt_proc.cc:852-866, reassembly.hpp:931-1009,1074-1079), cleared for every
+// other packet (ip_write_json pkt_proc.cc:1078-1080)
+extern "C" MFP_EXPORT const uint8_t *mfp_reassembler_dumped(mfp_reassembler r, size_t *n) {
+    if (n) *n = r ? r->dump.size() : 0;
+    return r && !r->dump.empty() ? r->dump.data() : nullptr;
+}
 extern "C" MFP_EXPORT const uint8_t *mfp_reassembler_frames(mfp_reassembler r, size_t *len) {
     if (len) *len = r ? r->frames.size() : 0;
     return r && !r->frames.empty() ? r->frames.data() : nullptr;
@@ -468,6 +479,7 @@ static void dtls_fragment(mfp_reassembler R, size_t i, const uint8_t *arena, con
     if (it != R->table.end() && !cid_ok(it->second.f)) return;      // another message on this 5-tuple: standalone
     if (it == R->table.end() && !more_bytes) return;                 // a later fragment without a flow: standalone
     const bool first = it == R->table.end();                         // udp_segment{init_seg = true} (:1071-1080)
+    R->dump[i] = 1;                                                  // dump_pkt (:1074, :1079)
     housekeeping(R, sec);                                            // process_udp_data_pkt's own check_flow
     it = R->table.find(k);
     if (it != R->table.end() && !cid_ok(it->second.f)) { no_record(i); return; }
@@ -665,9 +677,11 @@ static void quic_initial(mfp_reassembler R, size_t i, const uint8_t *arena, cons
     if (fresh) {
         if (!missing) {
             segment(true, crypto_offset, crypto_len);
+            R->dump[i] = 1;                                  // dump_pkt (reassembly.hpp:931)
         } else {
             if (q.count == 0 || q.first == 0xffff) return;
             if (q.first >= q.count) return;                  // frames[first_frame_idx] past the list: not restated
+            R->dump[i] = 1;                                  // dump_pkt (reassembly.hpp:981)
             const uint32_t ff = q.first;
             if (q.flen[ff] < 10) {                           // min_crypto_data (quic.h:1571-1578)
                 const uint64_t fo = q.foff[ff];
@@ -686,8 +700,10 @@ static void quic_initial(mfp_reassembler R, size_t i, const uint8_t *arena, cons
         if (it->second.f.state != S_PROGRESS) { no_record(i); return; }   // success / truncated: return false
         if (!missing) {
             segment(false, crypto_offset, crypto_len);
+            R->dump[i] = 1;                                  // dump_pkt (reassembly.hpp:988)
         } else {
             if (q.count == 0) return;
+            R->dump[i] = 1;                                  // dump_pkt (reassembly.hpp:1009)
             for (uint32_t x = 0; x < q.count; x++)
                 if (usable(x)) segment(false, q.foff[x], q.flen[x]);
         }
@@ -718,6 +734,7 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
     // 2. the flow table in stream order (process_tcp_data pkt_proc.cc:773-893)
     R->frames.clear(); R->desc2.clear(); R->who.clear(); R->who_props.clear();
     R->quiet.assign(n, 0);
+    R->dump.assign(n, 0);
     auto no_record = [&](size_t i) {                        // process_tcp_data returned false
         rec[i].flags &= (uint8_t)~MFP_FLAG_EMIT; rec[i].fp_type = 0; rec[i].fp_len = 0; R->quiet[i] = 1;
     };
@@ -767,6 +784,7 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
             if (supp) continue;                             // not in reassembly: taken as complete
             if (!more_bytes) { no_record(i); continue; }
         }
+        R->dump[i] = 1;                                     // dump_pkt (pkt_proc.cc:852, 862, 866)
         // 0: in order, after the flow's contiguous bytes (pkt_proc.cc:856-861)
         const uint32_t seq = had && !s.seq ? (uint32_t)it->second.f.contiguous : s.seq;
         // process_tcp_data_pkt (reassembly.hpp:717-746): its own check_flow, then
@@ -794,6 +812,14 @@ static long long reassemble(mfp_context ctx, mfp_reassembler R, const uint8_t *a
             if (an_path) R->more_state = true;              // in_progress (pkt_proc.cc:1636-1638)
         }
         if (more) more[i] = R->more_state;
+    }
+    // dump_pkt is cleared only by packets that reach the IP layer
+    // (ip_write_json pkt_proc.cc:1078-1080, analyze_ip_packet :1611-1613); a
+    // packet that does not (ARP, an unsupported ethertype) keeps the value the
+    // packet before it left
+    for (size_t i = 0; i < n; i++) {
+        if (R->seg[i].kind & MFP_SEG_IP) R->dump_carry = R->dump[i];
+        else R->dump[i] = R->dump_carry;
     }
     // 3. the reassembled messages through the device; their records replace
     // the completing packets' (their strings follow the batch's)

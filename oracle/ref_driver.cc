@@ -15,6 +15,13 @@
 //   idx  valid  fp_type  status  process  score  malware  p_malware  more  fp_string
 // Mode "json": the write_json record text, one line per packet (empty line
 // when the reference writes nothing).
+// Mode "pcapw": the filtered pcap writer of `mercury -w` (pkt_proc_filter_pcap_writer[_llq],
+// src/pkt_processing.h:92-121,230-259): each packet through the processor's
+// Ethernet write_json (pkt_proc.cc:1258-1326, an LLQ_MAX_MSG_SIZE buffer, the
+// packet's link type NOT passed, as there) and written in classic pcap format
+// when a record was written or dump_pkt() is set (pkt_proc.cc:1842-1845), with
+// the output file's header first (write_pcap_file_header pcap_file_io.c:88-104,
+// pcap_queue_write :540-579).  The pcap bytes go to stdout.
 // Mode "meta": analysis_context path, one TSV line per packet:
 //   idx  valid  server_name(hex)  user_agent(hex)   ("-" = NULL)
 // Mode "attr": analysis_context path, the accessors the embedders read, one
@@ -240,6 +247,30 @@ int main(int argc, char **argv) {
                                                                    (uint8_t *)pkts[i].data, pkts[i].len, &ts, pkts[i].linktype);
             fwrite(out.data(), 1, n, stdout);
             if (n == 0 || out[n - 1] != '\n') fputc('\n', stdout);
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "pcapw") {
+        // the pcap structs as pcap_file_io.c:41-61 lays them out (little-endian
+        // host, never byte-swapped when writing)
+        auto put32 = [](uint8_t *d, uint32_t v) { memcpy(d, &v, 4); };
+        auto put16 = [](uint8_t *d, uint16_t v) { memcpy(d, &v, 2); };
+        uint8_t fh[24];
+        put32(fh, 0xa1b2c3d4u); put16(fh + 4, 2); put16(fh + 6, 4); put32(fh + 8, 0); put32(fh + 12, 0);
+        put32(fh + 16, 65535); put32(fh + 20, 1);                     // snaplen 65535, LINKTYPE_ETHERNET
+        fwrite(fh, 1, sizeof fh, stdout);
+        std::vector<uint8_t> big(1 << 20);                            // LLQ_MAX_MSG_SIZE (llq.h:17)
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        for (size_t i = 0; i < pkts.size(); i++) {
+            struct timespec ts{(time_t)tsv[i], 0};
+            const size_t n = p->write_json(big.data(), big.size(), (uint8_t *)pkts[i].data, pkts[i].len, &ts);
+            if (n == 0 && !p->dump_pkt()) continue;
+            // (the _llq form `mercury -w` builds, pkt_processing.cc:35-38: an empty
+            // packet still gets its 16-byte header, pcap_queue_write :555-569)
+            uint8_t ph[16];
+            put32(ph, (uint32_t)ts.tv_sec); put32(ph + 4, (uint32_t)(ts.tv_nsec / 1000));
+            put32(ph + 8, pkts[i].len); put32(ph + 12, pkts[i].len);
+            fwrite(ph, 1, sizeof ph, stdout);
+            fwrite(pkts[i].data, 1, pkts[i].len, stdout);
         }
         mercury_packet_processor_destruct(p);
     } else if (mode == "an" || mode == "anr") {
