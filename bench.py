@@ -84,6 +84,130 @@ def build_device_batch(torch, n, workload, draw_seed, unique, diverse_tls=0.0):
     return ua, ud, d_arena, desc, d_desc
 
 
+GOLD = os.path.join(ROOT, "tests", "golden")
+OUTPUT_TOL = 1e-6   # score / p_malware (the reference's fp32 expf)
+
+
+def golden_applies(n, unique, workload, analysis, resources_kind, draw_seed):
+    """bench_sample.npz / bench_diverse_status.bin.gz hold the reference's
+    output for the default config-4 batch of rank 0 (tests/golden/make_golden_bench.py)."""
+    m = json.load(open(os.path.join(GOLD, "bench_manifest.json")))
+    return (analysis and workload == "mixed" and resources_kind == "survey" and n == m["packets"] and
+            unique == m["unique"] and draw_seed == m["draw_seed"])
+
+
+def check_step_output(torch, ctx, rec, an, d_fp, n, u):
+    """The timed step's records at 24 000 seeded positions (one per sampled
+    unique packet, in a seeded period of the 50 M) against the reference's:
+    emit flag, fingerprint type and bytes, analysis validity, status, process,
+    malware flag; score and p_malware within OUTPUT_TOL."""
+    g = dict(np.load(os.path.join(GOLD, "bench_sample.npz")))   # (an NpzFile decompresses on every access)
+    rows = g["rows"].astype(np.int64)
+    reps = n // u
+    k = np.random.default_rng(0x5EED0B1D).integers(0, reps, len(rows))
+    idx = rows + k * u
+    r, a = rec[idx], an[idx]
+    # the sampled strings, gathered on the device (the arena is tens of GB)
+    lens = r["fp_len"].astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    gidx = np.repeat(r["fp_offset"].astype(np.int64) - starts, lens) + np.arange(int(lens.sum()), dtype=np.int64)
+    blob = d_fp[torch.from_numpy(gidx).to(d_fp.device)].cpu().numpy().tobytes() if len(gidx) else b""
+    ends = np.concatenate([[0], g["fp_ends"].astype(np.int64)])
+    gblob = g["fp_blob"].tobytes()
+    names = g["proc_names"].tobytes().decode().split("\n")
+    bad = []
+    for j in range(len(rows)):
+        fi = int(g["fp_idx"][j])
+        want_fp = gblob[ends[fi]:ends[fi + 1]]
+        got_fp = blob[starts[j]:starts[j] + lens[j]]
+        emit = int(r["flags"][j] & 1)
+        if (emit, int(r["fp_type"][j]), got_fp) != (int(g["emit"][j]), int(g["fp_type"][j]), want_fp):
+            bad.append((int(idx[j]), "fingerprint"))
+            continue
+        valid = int(a["flags"][j] & 1)
+        if valid != int(g["valid"][j]):
+            bad.append((int(idx[j]), "valid"))
+            continue
+        if not valid:
+            continue
+        name = ctx.process_name(int(a["process"][j]))
+        mal = int((a["flags"][j] >> 1) & 1)
+        pm = float(a["malware_prob"][j]) if a["flags"][j] & 4 else 0.0
+        want_name = names[int(g["proc_idx"][j])]
+        if (int(a["status"][j]) != int(g["status"][j]) or name != want_name or mal != int(g["malware"][j]) or
+                abs(float(a["score"][j]) - float(g["score"][j])) > OUTPUT_TOL or
+                (want_name and abs(pm - float(g["p_malware"][j])) > OUTPUT_TOL)):
+            bad.append((int(idx[j]), "analysis"))
+    return {"ok": not bad, "records_checked": len(rows), "classified_checked": int(g["valid"].sum()),
+            "mismatches": len(bad), "first": bad[:5],
+            "against": "tests/golden/bench_sample.npz (reference libmerc, make_golden_bench.py)"}
+
+
+def check_diverse_statuses(an):
+    """The diversity leg's first step: every unknown-TLS sighting's status
+    (randomized / unlabeled) in stream order against the reference's 17.5 M
+    decisions (tests/golden/bench_diverse_status.bin.gz)."""
+    import gzip
+    m = json.load(open(os.path.join(GOLD, "bench_manifest.json")))
+    with gzip.open(os.path.join(GOLD, "bench_diverse_status.bin.gz"), "rb") as f:
+        want = np.unpackbits(np.frombuffer(f.read(), np.uint8))[:m["diverse_sightings"]]
+    valid = (an["flags"] & 1) != 0
+    st = an["status"]
+    sight = valid & ((st == 2) | (st == 3))
+    got = (st[sight] == 3).astype(np.uint8)
+    ok = len(got) == len(want) and bool(np.array_equal(got, want))
+    first = None
+    if not ok and len(got) == len(want):
+        first = int(np.flatnonzero(got != want)[0])
+    return {"ok": ok, "sightings": int(len(got)), "reference_sightings": int(len(want)),
+            "unlabeled": int(got.sum()), "first_mismatch": first,
+            "against": "tests/golden/bench_diverse_status.bin.gz (reference libmerc, make_golden_bench.py)"}
+
+
+def diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, tdist, world, rank):
+    """The realistic-diversity leg on several ranks: each rank's batch carries
+    per-packet cipher suites (350 k distinct unknown-TLS fingerprints per rank
+    and step, the LRU cycling), every step pipelined -- step k's kernels
+    launched, then step k-1's sightings decided across the ranks in shard
+    order (shard.ordered_prevalence_merge) while they run; the last step's
+    merge inside the timed region.  Reports the job rate and each rank's
+    merge time beside its kernel time."""
+    from mercury_amd import shard
+    steps2 = max(1, min(args.steps, 10))
+    step()
+    drain()
+    nstep[0] = 0
+    torch.cuda.synchronize()
+    del merge_s[:]
+    ctx.profile(True)
+    tdist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps2):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    el_local = time.perf_counter() - t
+    tdist.barrier()
+    el = shard.max_over_ranks(el_local)
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    kern = sum(v[1] for v in prof.values()) / steps2
+    merges = [round(x * 1e3, 3) for x in merge_s]
+    per_rank = [None] * world
+    tdist.all_gather_object(per_rank, {"rank": rank, "kernel_ms_per_step": round(kern, 4),
+                                       "ms_per_step": round(el_local / steps2 * 1e3, 4),
+                                       "merge_ms": merges,
+                                       "merge_ms_mean": round(float(np.mean(merge_s)) * 1e3, 3) if merge_s else None})
+    return {"value": round(n * world * steps2 / el / 1e6, 3), "unit": "Mpkt/s", "steps": steps2,
+            "ms_per_step": round(el / steps2 * 1e3, 4), "n_gpus": world,
+            "path": "mfp_analyze_batch_device_deferred_pipelined + shard.ordered_prevalence_merge of step k-1 while "
+                    "step k runs (each sighting decided once, on its own rank, from the earlier shards' LRU "
+                    "summaries); the last step's merge inside the timed region",
+            "diverse_tls_fraction": args.diverse_leg, "per_rank": per_rank,
+            "what": "the diversity leg's batch on every rank (its own draw), max over ranks"}
+
+
 def replicate_npz(torch, path, n):
     """The packets of a committed fixture (tests/golden/*.npz: arena + desc),
     replicated on the device to n packets."""
@@ -763,7 +887,13 @@ def main():
         if args.resources == "survey":
             from tests import synth_db
             t1 = time.time()
-            resources = synth_db.build_survey()      # every rank builds the same file; the write is atomic
+            # rank 0 builds the archive (~30 s of host work), the others wait at
+            # a gloo barrier and find the file (build_survey's write is atomic)
+            if rank == 0:
+                resources = synth_db.build_survey()
+            if tdist:
+                tdist.barrier()
+            resources = synth_db.build_survey()
             log(f"[rank {rank}] survey archive {os.path.getsize(resources) / 1e6:.1f} MB ({time.time() - t1:.1f} s)")
         else:
             resources = TEST_RESOURCES
@@ -809,6 +939,12 @@ def main():
         sets.append((torch.empty_like(d_rec), torch.empty_like(d_fp), torch.zeros_like(d_used),
                      torch.empty_like(d_an)))
     nstep = [0]
+    merge_s = []          # host seconds of each ordered cross-rank merge (several ranks)
+
+    def timed_merge():
+        tm = time.perf_counter()
+        shard.ordered_prevalence_merge(ctx, prev, rank * n)
+        merge_s.append(time.perf_counter() - tm)
 
     def step():
         r_, f_, u_, a_ = sets[nstep[0] % len(sets)]
@@ -821,14 +957,14 @@ def main():
             ctx.analyze_device_deferred_pipelined(d_arena.data_ptr(), d_desc.data_ptr(), n, r_.data_ptr(),
                                                   f_.data_ptr(), a_.data_ptr(), stream.cuda_stream)
             if nstep[0]:
-                shard.ordered_prevalence_merge(ctx, prev, rank * n)   # step k-1, step k in flight
+                timed_merge()   # step k-1, step k in flight
         nstep[0] += 1
 
     def drain():
         # the last step's merge (inside the timed region)
         if prev is not None and nstep[0]:
             ctx.analysis_defer_newest()
-            shard.ordered_prevalence_merge(ctx, prev, rank * n)
+            timed_merge()
 
     for _ in range(args.warmup):
         step()
@@ -876,6 +1012,10 @@ def main():
         an_info = {"classified": int(valid.sum()),
                    "status": {mercury_amd.api.STATUS_NAMES[i]: int(st[i]) for i in range(5)},
                    "malware": int(((an["flags"] & 2) != 0).sum())}
+    output_check = None
+    if rank == 0 and golden_applies(n, args.unique, workload, analysis, args.resources, draw_seed):
+        output_check = check_step_output(torch, ctx, rec, an, d_fp, n, len(ud))
+        log(f"[rank 0] timed step's output vs the reference: {output_check}")
     kern_ms = {k: v[1] / args.steps for k, v in prof.items()}
     step_kern_ms = sum(kern_ms.values())
     dominant = max(kern_ms, key=kern_ms.get)
@@ -899,6 +1039,12 @@ def main():
                     (an_counters if an_counters is not None else {})[f"{tu}_phase_clocks"] = [int(x) for x in words[:5]]
     kbytes = kernel_bytes(rec, desc, an if analysis else None, n_fallback, an_counters)
     diverse = None
+    if analysis and args.diverse_leg > 0 and world > 1:
+        del d_arena, d_desc
+        torch.cuda.empty_cache()
+        _, _, d_arena, _, d_desc = build_device_batch(torch, n, workload, draw_seed, args.unique,
+                                                      diverse_tls=args.diverse_leg)
+        diverse = diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, tdist, world, rank)
     if analysis and args.diverse_leg > 0 and world == 1:
         # realistic diversity: the same step over a batch whose TLS ClientHellos
         # carry per-packet cipher suites -- hundreds of thousands of distinct
@@ -911,6 +1057,12 @@ def main():
         distinct2 = len(set(mercury_amd.fingerprints(rec2u, fp2u)) - {""})
         step()
         torch.cuda.synchronize()
+        diverse_check = None
+        if golden_applies(n, args.unique, workload, analysis, args.resources, draw_seed):
+            # the first diversity step follows the main leg's steps: its 17.5 M
+            # LRU decisions against the reference's
+            diverse_check = check_diverse_statuses(sets[0][3].cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE))
+            log(f"[rank 0] diversity step's LRU decisions vs the reference: {diverse_check}")
         ctx.profile(True)
         # (as many steps as the main leg, up to 10: the pipelined form's last
         # decision -- mfp_analysis_flush, one step's host decision -- is the
@@ -975,6 +1127,7 @@ def main():
                    "status_sync": {mercury_amd.api.STATUS_NAMES[i]: int(st2[i]) for i in range(5)},
                    "synchronous": sync_leg,
                    "lru_entries": int(ctx.analysis_stats()[3]),
+                   "reference_check": diverse_check,
                    "what": "same step, same archive; the unique packets' TLS ClientHellos get random first two "
                            "cipher suites (tests/synth.py diverse_tls), replicated like the main leg"}
     e2e = None
@@ -1075,6 +1228,7 @@ def main():
             "fingerprints_per_step": n_fp,
             "fallback_packets_per_step": n_fallback,
             "analysis": an_info,
+            "output_check": output_check,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(kbytes.get(dominant, 0) / (kern_ms[dominant] * 1e-3) / 1e9, 2),
@@ -1104,6 +1258,12 @@ def main():
             "other_paths": others,
             "per_packet_shim": shim,
         }
+        checks = [c for c in (output_check, (diverse or {}).get("reference_check")) if c]
+        if any(not c["ok"] for c in checks):
+            # the records the line times differ from the reference's: no line
+            log(json.dumps(out))
+            log("bench: the timed output differs from the reference (output_check / diversity.reference_check)")
+            sys.exit(3)
         print(json.dumps(out), flush=True)
     ctx.close()
     if tdist:

@@ -22,6 +22,17 @@
 // when a record was written or dump_pkt() is set (pkt_proc.cc:1842-1845), with
 // the output file's header first (write_pcap_file_header pcap_file_io.c:88-104,
 // pcap_queue_write :540-579).  The pcap bytes go to stdout.
+// Modes "wjan" and "stat" run a TILED stream: MERC_TILE="u1:N" makes the
+// stream packets [0, u1) once, then packets [u1, total) repeated until the
+// stream holds N packets (bench.py's device batch is such a tiling of its unique
+// packets).  Both use the write_json path with the classifier (the analysis
+// result the record's "analysis" object prints, pkt_proc.cc:1195-1213).
+//   "wjan": one TSV line per stream index listed in MERC_ROWS_FILE (sorted
+//     little-endian u64):  idx  emit  fp_type  valid  status  process  score
+//     malware  p_malware  fp_string
+//   "stat": for the tiled part [u1, N), one bit per packet whose status is
+//     randomized or unlabeled (an unknown-TLS sighting, analysis.h:1043-1083):
+//     1 = unlabeled; packed MSB first (numpy.packbits) to stdout.
 // Mode "meta": analysis_context path, one TSV line per packet:
 //   idx  valid  server_name(hex)  user_agent(hex)   ("-" = NULL)
 // Mode "attr": analysis_context path, the accessors the embedders read, one
@@ -224,7 +235,65 @@ int main(int argc, char **argv) {
         for (size_t i = 0; i < pkts.size() && 8 * i + 8 <= tb.size(); i++) memcpy(&tsv[i], tb.data() + 8 * i, 8);
     }
     std::vector<char> out(1 << 16);
-    if (mode == "fp") {
+    // the stream order of the tiled modes
+    size_t tile_u1 = 0, tile_n = pkts.size();
+    if (const char *t = getenv("MERC_TILE")) {
+        unsigned long long a = 0, b = 0;
+        if (sscanf(t, "%llu:%llu", &a, &b) != 2 || a > pkts.size() || (b > a && a == pkts.size())) {
+            fprintf(stderr, "bad MERC_TILE\n");
+            return 2;
+        }
+        tile_u1 = a; tile_n = b;
+    }
+    auto stream_pkt = [&](size_t i) -> const pkt & {
+        if (i < tile_u1) return pkts[i];
+        return pkts[tile_u1 + (i - tile_u1) % (pkts.size() - tile_u1)];
+    };
+    if (mode == "wjan" || mode == "stat") {
+        std::vector<uint64_t> rows;
+        if (const char *rf = getenv("MERC_ROWS_FILE")) {
+            auto rb = slurp(rf);
+            rows.resize(rb.size() / 8);
+            memcpy(rows.data(), rb.data(), rows.size() * 8);
+        }
+        size_t next_row = 0;
+        std::vector<uint8_t> bits;
+        uint8_t acc = 0;
+        int nb = 0;
+        mercury_packet_processor p = mercury_packet_processor_construct(mc);
+        for (size_t i = 0; i < tile_n; i++) {
+            const pkt &k = stream_pkt(i);
+            struct timespec ts{(time_t)1700000000, 0};
+            const size_t n = mercury_packet_processor_write_json_linktype(p, out.data(), out.size(), (uint8_t *)k.data,
+                                                                         k.len, &ts, k.linktype);
+            const bool valid = n > 0 && p->analysis.result.is_valid();
+            const analysis_context *ac = valid ? &p->analysis : nullptr;
+            const int status = ac ? (int)analysis_context_get_fingerprint_status(ac) : 0;
+            if (mode == "stat") {
+                if (i >= tile_u1 && (status == 2 || status == 3)) {
+                    acc = (uint8_t)(acc << 1 | (status == 3));
+                    if (++nb == 8) { bits.push_back(acc); acc = 0; nb = 0; }
+                }
+                continue;
+            }
+            if (next_row >= rows.size() || rows[next_row] != i) continue;
+            next_row++;
+            const int t = n > 0 ? p->analysis.fp.get_type() : 0;
+            const char *proc = ""; double score = 0; bool mal = false; double pm = 0;
+            if (ac) {
+                analysis_context_get_process_info(ac, &proc, &score);
+                analysis_context_get_malware_info(ac, &mal, &pm);
+            }
+            printf("%zu\t%d\t%d\t%d\t%d\t%s\t%.17g\t%d\t%.17g\t%s\n", i, n > 0, t, (int)valid, status,
+                   proc ? proc : "", score, (int)mal, pm, t ? p->analysis.fp.string() : "");
+        }
+        if (mode == "stat") {
+            fprintf(stderr, "sightings %zu\n", bits.size() * 8 + nb);
+            if (nb) bits.push_back((uint8_t)(acc << (8 - nb)));
+            fwrite(bits.data(), 1, bits.size(), stdout);
+        }
+        mercury_packet_processor_destruct(p);
+    } else if (mode == "fp") {
         mercury_packet_processor p = mercury_packet_processor_construct(mc);
         for (size_t i = 0; i < pkts.size(); i++) {
             struct timespec ts{(time_t)tsv[i], 0};
