@@ -164,7 +164,7 @@ def check_diverse_statuses(an):
             "against": "tests/golden/bench_diverse_status.bin.gz (reference libmerc, make_golden_bench.py)"}
 
 
-def diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, tdist, world, rank):
+def diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, merge_ph, tdist, world, rank):
     """The realistic-diversity leg on several ranks: each rank's batch carries
     per-packet cipher suites (350 k distinct unknown-TLS fingerprints per rank
     and step, the LRU cycling), every step pipelined -- step k's kernels
@@ -174,11 +174,13 @@ def diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, tdist, 
     merge time beside its kernel time."""
     from mercury_amd import shard
     steps2 = max(1, min(args.steps, 10))
+    nstep[0] = 0          # the main leg's last step was decided by its drain()
     step()
     drain()
     nstep[0] = 0
     torch.cuda.synchronize()
     del merge_s[:]
+    del merge_ph[:]
     ctx.profile(True)
     tdist.barrier()
     torch.cuda.synchronize()
@@ -198,7 +200,10 @@ def diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, tdist, 
     tdist.all_gather_object(per_rank, {"rank": rank, "kernel_ms_per_step": round(kern, 4),
                                        "ms_per_step": round(el_local / steps2 * 1e3, 4),
                                        "merge_ms": merges,
-                                       "merge_ms_mean": round(float(np.mean(merge_s)) * 1e3, 3) if merge_s else None})
+                                       "merge_ms_mean": round(float(np.mean(merge_s)) * 1e3, 3) if merge_s else None,
+                                       "merge_phase_ms_mean": {k: round(float(np.mean([p.get(k, 0.0) for p in merge_ph]))
+                                                                        * 1e3, 3)
+                                                               for k in (merge_ph[0] if merge_ph else {})}})
     return {"value": round(n * world * steps2 / el / 1e6, 3), "unit": "Mpkt/s", "steps": steps2,
             "ms_per_step": round(el / steps2 * 1e3, 4), "n_gpus": world,
             "path": "mfp_analyze_batch_device_deferred_pipelined + shard.ordered_prevalence_merge of step k-1 while "
@@ -940,11 +945,13 @@ def main():
                      torch.empty_like(d_an)))
     nstep = [0]
     merge_s = []          # host seconds of each ordered cross-rank merge (several ranks)
+    merge_ph = []         # ... and its phases (shard.last_merge_phases)
 
     def timed_merge():
         tm = time.perf_counter()
         shard.ordered_prevalence_merge(ctx, prev, rank * n)
         merge_s.append(time.perf_counter() - tm)
+        merge_ph.append(dict(shard.last_merge_phases))
 
     def step():
         r_, f_, u_, a_ = sets[nstep[0] % len(sets)]
@@ -1044,7 +1051,7 @@ def main():
         torch.cuda.empty_cache()
         _, _, d_arena, _, d_desc = build_device_batch(torch, n, workload, draw_seed, args.unique,
                                                       diverse_tls=args.diverse_leg)
-        diverse = diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, tdist, world, rank)
+        diverse = diverse_multi_rank(torch, ctx, args, n, step, drain, nstep, merge_s, merge_ph, tdist, world, rank)
     if analysis and args.diverse_leg > 0 and world == 1:
         # realistic diversity: the same step over a batch whose TLS ClientHellos
         # carry per-packet cipher suites -- hundreds of thousands of distinct

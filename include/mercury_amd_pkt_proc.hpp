@@ -81,6 +81,10 @@ public:
                                  pi->linktype, eth));
     }
     void flush() override { check(mfp_pkt_proc_flush(p_)); }
+    // a whole block of packets (mfp_pkt_proc_apply_batch)
+    void apply_batch(const uint8_t *arena, const mfp_pkt_desc *desc, size_t n, const uint64_t *ts_ns) {
+        check(mfp_pkt_proc_apply_batch(p_, arena, desc, n, ts_ns));
+    }
     void finalize() override { check(mfp_pkt_proc_finalize(p_)); }
 
     // [MFP_PKT_PROC_NSTATS] counters (include/mfp_pkt_proc.h)

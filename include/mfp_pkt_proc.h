@@ -68,10 +68,12 @@ enum {
 };
 
 typedef struct {
-    size_t   batch_pkts;     /* packets per batch (0: 262144)                         */
+    size_t   batch_pkts;     /* packets per batch (0: 131072)                         */
     size_t   arena_bytes;    /* page-locked bytes per batch arena (0: 1 KiB per packet,
-                                at least 64 MiB); a packet that does not fit starts
-                                the next batch                                          */
+                                at least 64 MiB; at most 2 GiB); a packet that does not
+                                fit starts the next batch.  Three batches' arenas and
+                                result buffers (the fingerprint arena by
+                                mfp_fp_arena_bound) are page-locked at create       */
     uint32_t flush_us;       /* hand a batch over once its first packet waited this
                                 long (checked in apply; 0: only when full / flush)   */
     int      json_threads;   /* host threads rendering JSON text (0: 16)              */
@@ -96,6 +98,13 @@ MFP_EXPORT mfp_pkt_proc mfp_pkt_proc_create(mfp_context ctx, int kind, const mfp
  * 0, or < 0 after an error (the processor's first error is kept). */
 MFP_EXPORT int mfp_pkt_proc_apply(mfp_pkt_proc p, int64_t tv_sec, int64_t tv_nsec, uint32_t caplen, uint32_t len,
                                   uint16_t linktype, const uint8_t *packet);
+
+/* apply() for n packets at once (a TPACKET_V3 block walked by
+ * mfp_tpacket3_block, or a block of a pcap file read by mfp_pcap_read_batch:
+ * process_all_packets_in_block af_packet_v3.c:174-210 without its per-packet
+ * call); ts_ns[i] = tv_sec * 1e9 + tv_nsec (NULL: "now").  Returns 0 or < 0. */
+MFP_EXPORT int mfp_pkt_proc_apply_batch(mfp_pkt_proc p, const uint8_t *arena, const mfp_pkt_desc *desc, size_t n,
+                                        const uint64_t *ts_ns);
 
 /* pkt_proc::flush(): hand the packets buffered so far to the device thread
  * (the capture loop calls it before it waits, af_packet_v3.c:744-754);

@@ -9,7 +9,9 @@
 // A summary line (packets, seconds, Mpkt/s, records, bytes) goes to stderr.
 //
 // usage: mercury-amd -r IN.pcap (-f OUT.json | -w OUT.pcap) [-c packet_filter_cfg]
-//                    [-d device] [-b batch_pkts] [-t json_threads] [-l loop_count]
+//                    [-d device] [-b batch_pkts] [-t json_threads] [-l loop_count] [-B]
+// -B: hand each block read from the file to mfp_pkt_proc_apply_batch instead
+//     of one apply() per packet (the AF_PACKET block form)
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,7 +26,7 @@
 static void usage(const char *a0) {
     fprintf(stderr,
             "usage: %s -r IN.pcap (-f OUT.json | -w OUT.pcap) [-c packet_filter_cfg] [-d device]\n"
-            "          [-b batch_pkts] [-t json_threads] [-l loop_count]\n",
+            "          [-b batch_pkts] [-t json_threads] [-l loop_count] [-B]\n",
             a0);
     exit(2);
 }
@@ -33,6 +35,7 @@ int main(int argc, char **argv) {
     const char *in = nullptr, *json_out = nullptr, *pcap_out = nullptr;
     std::string cfg;                      // "" = the reference's default selection ("all")
     int device = 0, loops = 1;
+    bool bulk = false;
     mfp_pkt_proc_opts o{};
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
@@ -45,6 +48,7 @@ int main(int argc, char **argv) {
         else if (a == "-b") o.batch_pkts = (size_t)strtoull(val(), nullptr, 10);
         else if (a == "-t") o.json_threads = atoi(val());
         else if (a == "-l") loops = atoi(val());
+        else if (a == "-B") bulk = true;
         else usage(argv[0]);
     }
     if (!in || (!json_out == !pcap_out) || loops < 1) usage(argv[0]);
@@ -59,9 +63,9 @@ int main(int argc, char **argv) {
 
     int rc = 0;
     uint64_t pkts = 0, st[MFP_PKT_PROC_NSTATS] = {};
-    double secs = 0;
+    double secs = 0, read_s = 0;
     try {
-        mercury_amd::gpu_batch_proc *proc;
+        mercury_amd::gpu_batch_proc *proc;   // (bulk: its handle, through mfp_pkt_proc_apply_batch)
         if (json_out) proc = new mercury_amd::pkt_proc_gpu_json_writer(ctx, out, &o);
         else proc = new mercury_amd::pkt_proc_gpu_filter_pcap_writer(ctx, out, &o);
         // the file is read in blocks (mfp_pcap_read_batch: the reference's
@@ -77,9 +81,16 @@ int main(int argc, char **argv) {
             if (!pc) { fprintf(stderr, "mercury-amd: %s\n", mfp_last_error()); rc = 1; break; }
             for (;;) {
                 size_t used = 0;
+                const auto tr = std::chrono::steady_clock::now();
                 const long long n = mfp_pcap_read_batch(pc, arena.data(), cap, desc.data(), max_pkts, ts.data(), &used);
+                read_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
                 if (n < 0) { fprintf(stderr, "mercury-amd: %s\n", mfp_last_error()); rc = 1; break; }
                 if (n == 0) break;
+                if (bulk) {
+                    proc->apply_batch(arena.data(), desc.data(), (size_t)n, ts.data());
+                    pkts += (uint64_t)n;
+                    continue;
+                }
                 for (long long i = 0; i < n; i++) {
                     packet_info pi;
                     pi.ts.tv_sec = (time_t)(ts[i] / 1000000000ull);
@@ -105,8 +116,8 @@ int main(int argc, char **argv) {
     mfp_finalize(ctx);
     fprintf(stderr,
             "{\"packets\": %llu, \"seconds\": %.6f, \"mpps\": %.3f, \"records\": %llu, \"bytes_out\": %llu, "
-            "\"batches\": %llu, \"device_s\": %.6f, \"writer_s\": %.6f, \"skipped\": %llu}\n",
+            "\"batches\": %llu, \"device_s\": %.6f, \"writer_s\": %.6f, \"read_s\": %.6f, \"skipped\": %llu}\n",
             (unsigned long long)pkts, secs, secs > 0 ? pkts / secs / 1e6 : 0.0, (unsigned long long)st[2],
-            (unsigned long long)st[3], (unsigned long long)st[1], st[4] / 1e9, st[5] / 1e9, (unsigned long long)st[6]);
+            (unsigned long long)st[3], (unsigned long long)st[1], st[4] / 1e9, st[5] / 1e9, read_s, (unsigned long long)st[6]);
     return rc;
 }

@@ -1225,6 +1225,10 @@ static long long write_json_batch(mfp_context ctx, const uint16_t *props, const 
         if (pool.size() < part.size()) pool.swap(part);
     };
     if (sink) {
+        for (int t = 1; t < threads; t++) {   // line ends in the stream of this call
+            const size_t lo = (size_t)t * per, hi = lo + per < n ? lo + per : n;
+            for (size_t i = lo; i < hi; i++) line_end[i] += base[(size_t)t];
+        }
         for (int t = 0; t < threads; t++)
             if (part[(size_t)t].len && sink(user, part[(size_t)t].buf.get(), part[(size_t)t].len) != 0) {
                 give_back();

@@ -314,8 +314,9 @@ extern "C" MFP_EXPORT mfp_pkt_proc mfp_pkt_proc_create(mfp_context ctx, int kind
     p->ctx = ctx;
     p->kind = kind;
     if (opts) p->o = *opts;
-    if (!p->o.batch_pkts) p->o.batch_pkts = 262144;
+    if (!p->o.batch_pkts) p->o.batch_pkts = 131072;
     if (!p->o.arena_bytes) p->o.arena_bytes = std::max<size_t>((size_t)64 << 20, p->o.batch_pkts * 1024);
+    p->o.arena_bytes = std::min<size_t>(p->o.arena_bytes, (size_t)2 << 30);
     p->o.arena_bytes = std::max<size_t>(p->o.arena_bytes, 65536 + 16);   // any one packet fits
     if (p->o.json_threads <= 0) p->o.json_threads = 16;
     p->sink = sink;
@@ -323,9 +324,16 @@ extern "C" MFP_EXPORT mfp_pkt_proc mfp_pkt_proc_create(mfp_context ctx, int kind
     p->reassembly = mfp_reassembly_enabled(ctx) != 0;
     p->analysis = mfp_analysis_enabled(ctx) != 0;
     if (p->reassembly) p->R = mfp_reassembler_create();
+    // every page-locked buffer up front (pinning gigabytes takes a while: not in
+    // the capture loop's path); the fingerprint arena by its bound for a full batch
+    size_t fp_cap = mfp_fp_arena_bound(p->o.batch_pkts, p->o.arena_bytes);
+    if (p->reassembly) fp_cap += mfp_fp_arena_bound(p->o.batch_pkts, p->o.batch_pkts * (size_t)8400);
+    const bool an = p->analysis && kind == MFP_PKT_PROC_JSON;
     for (int k = 0; k < mfp_pkt_proc_s::NB; k++) {
         Batch &B = p->b[k];
-        if (!B.arena.reserve(p->o.arena_bytes + kPad) || !B.desc.reserve(p->o.batch_pkts + 1)) {
+        if (!B.arena.reserve(p->o.arena_bytes + kPad) || !B.desc.reserve(p->o.batch_pkts + 1) ||
+            !B.rec.reserve(p->o.batch_pkts + 1) || !B.fp.reserve(fp_cap) ||
+            (an && (!B.an.reserve(p->o.batch_pkts + 1) || !B.ap.reserve((p->o.batch_pkts + 1) * MFP_ATTR_DB_TAGS)))) {
             for (auto &x : p->b) x.release();
             if (p->R) mfp_reassembler_destroy(p->R);
             delete p;
@@ -372,6 +380,18 @@ extern "C" MFP_EXPORT int mfp_pkt_proc_apply(mfp_pkt_proc p, int64_t tv_sec, int
     B->ts_usec.push_back((uint32_t)(tv_nsec / 1000));
     B->n++;
     p->st_pkts++;
+    return 0;
+}
+
+extern "C" MFP_EXPORT int mfp_pkt_proc_apply_batch(mfp_pkt_proc p, const uint8_t *arena, const mfp_pkt_desc *desc,
+                                                   size_t n, const uint64_t *ts_ns) {
+    if (!p || (n && (!arena || !desc))) { mfp_set_error("null argument"); return -1; }
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t t = ts_ns ? ts_ns[i] : 0;
+        const int r = mfp_pkt_proc_apply(p, (int64_t)(t / 1000000000ull), (int64_t)(t % 1000000000ull), desc[i].caplen,
+                                         desc[i].caplen, desc[i].linktype, arena + desc[i].offset);
+        if (r) return r;
+    }
     return 0;
 }
 

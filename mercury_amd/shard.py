@@ -108,6 +108,9 @@ def _all_gather_rows(arr, group=None):
     return [o.numpy().view(np.uint8)[:int(k.item()) * 8].view(arr.dtype) for o, k in zip(outs, ns)]
 
 
+last_merge_phases = {}   # seconds per phase of the last ordered_prevalence_merge (bench.py reports them)
+
+
 def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
     """Decide the unknown-TLS sightings of this rank's last analysed batch
     (ctx deferred, see Context.defer) in stream order across the ranks of
@@ -116,25 +119,43 @@ def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
     rank applies the same decisions to its own copy).  The exchange is two or
     three fixed-size int64 all_gathers (no pickling).  Returns the number of
     distinct fingerprints exchanged (or sightings, on the sequence path)."""
+    import time
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    ph = last_merge_phases
+    ph.clear()
+    t0 = time.perf_counter()
+
+    def lap(name):
+        nonlocal t0
+        t = time.perf_counter()
+        ph[name] = ph.get(name, 0.0) + (t - t0)
+        t0 = t
     dl = ctx.analysis_distinct()
+    lap("distinct_export")
     # [distinct count or -1 (table overflow), this shard's stream base]
     hdr = torch.tensor([-1 if dl is None else len(dl), int(shard_base)], dtype=torch.int64)
     hdrs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(hdrs, hdr, group=group)
-    if all(int(h[0]) >= 0 for h in hdrs):
+    lap("header_gather")
+    # the distinct form is exact only when no eviction can happen inside the
+    # step; with more distinct fingerprints in the step than the LRU holds it
+    # cannot be (every rank sees the same counts, so all take the same path)
+    if all(int(h[0]) >= 0 for h in hdrs) and sum(int(h[0]) for h in hdrs) <= prev.capacity:
         lists = _all_gather_rows(dl if dl is not None else np.zeros(0, SIGHTING_DTYPE), group)
         for x, h in zip(lists, hdrs):
             x["first"] += np.uint64(int(h[1]))
             x["last"] += np.uint64(int(h[1]))
         allv = np.concatenate(lists) if lists else np.zeros(0, SIGHTING_DTYPE)
+        lap("distinct_gather")
         if prev.resolve_distinct(allv):
             k = sum(len(x) for x in lists[:rank])
             ctx.analysis_resolve(allv[k:k + len(lists[rank])])
+            lap("distinct_resolve")
             return len(allv)
+        lap("distinct_resolve")
     # the sequence form, decided once: each rank decides its own sightings,
     # from the set that the earlier shards leave; a shard's effect on any later
     # one is its summary -- its distinct fingerprints by last sighting, at most
@@ -142,8 +163,16 @@ def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
     # exchange summaries, not sightings, and the work per rank does not grow
     # with the number of ranks
     seq = np.ascontiguousarray(ctx.analysis_sequence(), np.uint64)
-    summaries = _all_gather_rows(prev.summary(seq), group)
+    lap("sequence_export")
+    mine = prev.summary(seq)
+    lap("summary")
+    summaries = _all_gather_rows(mine, group)
+    lap("summary_gather")
     prior = np.concatenate(summaries[:rank][::-1]) if rank else np.zeros(0, np.uint64)
-    ctx.analysis_resolve_sequence(prev.resolve_shard(seq, prior))
+    seen = prev.resolve_shard(seq, prior)
+    lap("resolve_shard")
+    ctx.analysis_resolve_sequence(seen)
+    lap("apply")
     prev.advance(np.concatenate(summaries[::-1]))
+    lap("advance")
     return sum(len(x) for x in summaries)

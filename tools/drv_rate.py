@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--unique", type=int, default=1_000_000)
     ap.add_argument("--loops", type=int, default=5)
     ap.add_argument("--tmp", default="/tmp")
-    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--batch", type=int, nargs="*", default=[0])
     ap.add_argument("--analysis", action="store_true")
     args = ap.parse_args()
     from tests import synth
@@ -46,16 +46,19 @@ def main():
             f.write(a[o:o + int(d["caplen"][i])].tobytes())
     print(f"pcap: {len(d)} packets, {os.path.getsize(src) / 1e9:.2f} GB ({time.time() - t0:.1f} s)", file=sys.stderr,
           flush=True)
-    cfg = "select=tls,dtls,ssh,http,tcp,tcp.syn_ack"
+    cfg = "tls,dtls,ssh,http,tcp,tcp.syn_ack"   # a bare list ("select=..." needs the key=value form's ';')
     if args.analysis:
         from tests import synth_db
-        cfg += f";resources={synth_db.build_survey()};analysis"
+        cfg = f"select={cfg};resources={synth_db.build_survey()};analysis"
     drv = os.path.join(ROOT, "mercury_amd", "mercury-amd")
-    for flag, name in (("-f", "drv_out.json"), ("-w", "drv_out.pcap")):
-        out = os.path.join(args.tmp, name)
-        cmd = [drv, "-r", src, flag, out, "-c", cfg, "-l", str(args.loops)]
-        if args.batch:
-            cmd += ["-b", str(args.batch)]
+    runs = []
+    for b in args.batch:
+        runs += [("-f", os.path.join(args.tmp, "drv_out.json"), b, False), ("-f", "/dev/null", b, False),
+                 ("-w", "/dev/null", b, False), ("-f", "/dev/null", b, True)]
+    for flag, out, batch, bulk in runs:
+        cmd = [drv, "-r", src, flag, out, "-c", cfg, "-l", str(args.loops)] + (["-B"] if bulk else [])
+        if batch:
+            cmd += ["-b", str(batch)]
         t = time.time()
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         wall = time.time() - t
@@ -63,11 +66,14 @@ def main():
             print(r.stderr, file=sys.stderr)
             sys.exit(r.returncode)
         st = json.loads(r.stderr.strip().splitlines()[-1])
-        st.update({"output": "json" if flag == "-f" else "pcap", "analysis": args.analysis,
-                   "output_bytes": os.path.getsize(out), "wall_s": round(wall, 3),
+        st.update({"output": ("json" if flag == "-f" else "pcap") + (" -> file" if out != "/dev/null" else " -> /dev/null"),
+                   "apply": "apply_batch per file block" if bulk else "apply() per packet",
+                   "analysis": args.analysis, "batch_pkts": batch or 131072, "wall_s": round(wall, 3),
                    "input_gb_per_loop": round(os.path.getsize(src) / 1e9, 3)})
+        if out != "/dev/null":
+            st["output_bytes"] = os.path.getsize(out)
+            os.remove(out)
         print(json.dumps(st), flush=True)
-        os.remove(out)
     os.remove(src)
 
 
