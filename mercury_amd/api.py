@@ -625,6 +625,16 @@ class Context:
         self.lib.mfp_analysis_distinct(self.h, out.ctypes.data, n)
         return out[:n]
 
+    def analysis_distinct_count(self):
+        """How many distinct unknown-TLS fingerprints the last deferred batch
+        has (its table's counter; no export), or None when too many for it."""
+        n = self.lib.mfp_analysis_distinct(self.h, None, 0)
+        if n == -3:
+            return None
+        if n < 0:
+            raise MercuryAmdError(_err(self.lib))
+        return int(n)
+
     def analysis_sequence(self):
         n = self.lib.mfp_analysis_sequence(self.h, None, 0)
         if n < 0:

@@ -119,84 +119,6 @@ __global__ __launch_bounds__(256) void k_compact_copy(mfp_record *rec, uint64_t 
     }
 }
 
-// The pipelined host path's form (mfp_process_pipelined, chunk after chunk):
-// the exclusive scan continues the stream's running total ctr[0] (the
-// previous chunk's scan is waited for, across streams); the strings go
-// straight into the caller's page-locked arena at their stream offsets, the
-// re-pointed records to rec_out (the device records, with their own offsets
-// and hashes, stay as the classifier's decision kernels read them).  Nothing
-// is written past `cap`: ctr[1] flags the overflow.
-__global__ __launch_bounds__(1024) void k_block_scan_base(unsigned long long *block_sum, uint64_t nb,
-                                                         unsigned long long *ctr, uint64_t cap) {
-    __shared__ unsigned long long carry;
-    __shared__ unsigned long long wsum[16];
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x == 0) carry = ctr[0];
-    __syncthreads();
-    for (uint64_t b0 = 0; b0 < nb; b0 += 1024) {
-        const uint64_t k = b0 + threadIdx.x;
-        const unsigned long long v = k < nb ? block_sum[k] : 0ull;
-        unsigned long long incl = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const unsigned long long y = __shfl_up(incl, d, 64);
-            if (lane >= (uint32_t)d) incl += y;
-        }
-        if (lane == 63) wsum[wid] = incl;
-        __syncthreads();
-        unsigned long long base = carry, tot = 0;
-        for (uint32_t w = 0; w < 16; w++) {
-            if (w < wid) base += wsum[w];
-            tot += wsum[w];
-        }
-        if (k < nb) block_sum[k] = base + incl - v;
-        __syncthreads();
-        if (threadIdx.x == 0) carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        ctr[0] = carry;
-        if (carry > cap) ctr[1] = 1;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_compact_copy_to(const mfp_record *rec, mfp_record *rec_out, uint64_t n,
-                                                         const uint32_t *local, const unsigned long long *block_sum,
-                                                         const uint8_t *src, uint8_t *dst, uint64_t cap) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t g = wave; g * 64 < n; g += nw) {
-        const uint64_t i = g * 64 + lane;
-        uint64_t so = 0, dof = 0;
-        uint32_t len = 0;
-        mfp_record r;
-        if (i < n) {
-            r = rec[i];
-            len = packed_len(r, src);
-            so = r.fp_offset;
-            dof = block_sum[i / B] + local[i];
-            if (dof + len > cap) len = 0;   // (overflow: flagged by the scan)
-        }
-        for (int j = 0; j < 64; j++) {
-            const uint32_t lj = (uint32_t)__shfl((int)len, j, 64);
-            if (!lj) continue;
-            const uint64_t sj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(so >> 32), j, 64) << 32) |
-                                (uint32_t)__shfl((int)(uint32_t)so, j, 64);
-            const uint64_t dj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dof >> 32), j, 64) << 32) |
-                                (uint32_t)__shfl((int)(uint32_t)dof, j, 64);
-            for (uint32_t k = lane; k < lj; k += 64) dst[dj + k] = src[sj + k];
-        }
-        if (i < n) {
-            // (a record without a string moves by the chunk's base, block_sum[0],
-            // as the copying pipeline rebases every record of a chunk)
-            if (len) { r.fp_offset = dof; r.flags &= (uint8_t)~MFP_FLAG_HASHED; }
-            else r.fp_offset += block_sum[0];
-            rec_out[i] = r;
-        }
-    }
-}
-
 // A small batch (the per-packet API, n <= 1024) in one launch: the scan in
 // LDS, then the packed strings, the re-pointed records, the classifier's
 // results and the counters written straight into the caller's page-locked
@@ -289,20 +211,3 @@ extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *sr
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// k_compact_copy_to's launch: dst and rec_out may be page-locked host memory;
-// ctr (device): [0] the stream's packed bytes so far, [1] overflow
-extern "C" int mfp_launch_compact_to(const mfp_record *rec, mfp_record *rec_out, uint64_t n, const uint8_t *src,
-                                     uint8_t *dst, uint64_t cap, uint32_t *local, unsigned long long *block_sum,
-                                     unsigned long long *ctr, hipStream_t stream, mfp_prof *prof) {
-    if (n == 0) return 0;
-    const uint64_t nb = (n + mfpk::B - 1) / mfpk::B;
-    if (prof) mfp_prof_begin(prof, "k_compact", stream);
-    hipLaunchKernelGGL(mfpk::k_len_scan, dim3((uint32_t)nb), dim3(mfpk::B), 0, stream, rec, n, src, local, block_sum);
-    hipLaunchKernelGGL(mfpk::k_block_scan_base, dim3(1), dim3(1024), 0, stream, block_sum, nb, ctr, cap);
-    uint64_t cb = (n + 255) / 256;
-    if (cb > 2048) cb = 2048;
-    hipLaunchKernelGGL(mfpk::k_compact_copy_to, dim3((uint32_t)cb), dim3(256), 0, stream, rec, rec_out, n, local,
-                       block_sum, src, dst, cap);
-    if (prof) mfp_prof_end(prof, stream);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}

@@ -57,9 +57,6 @@ extern "C" int mfp_launch_compact(mfp_record *rec, uint64_t n, const uint8_t *sr
                                   mfp_prof *prof);
 
 
-extern "C" int mfp_launch_compact_to(const mfp_record *rec, mfp_record *rec_out, uint64_t n, const uint8_t *src,
-                                     uint8_t *dst, uint64_t cap, uint32_t *local, unsigned long long *block_sum,
-                                     unsigned long long *ctr, hipStream_t stream, mfp_prof *prof);
 extern "C" int mfp_launch_compact_small(const mfp_record *rec, uint64_t n, const uint8_t *src, uint8_t *dst_host,
                                         uint64_t cap, mfp_record *rec_host, const unsigned long long *used,
                                         unsigned long long *used_host, const mfp_analysis *an, mfp_analysis *an_host,
@@ -404,6 +401,11 @@ struct Slot {
         uint64_t n = 0;
         const mfp_record *rec = nullptr; const char *fp = nullptr; mfp_analysis *out = nullptr;
         hipStream_t stream = nullptr;
+        // the last mfp_analysis_sequence / _distinct result of this batch (the
+        // count query and the export that follows it share one device pass)
+        long long seq_m = -1;
+        std::vector<mfp_sighting> dist;
+        long long dist_u = -5;
     } pend;
     uint8_t *d_arena = nullptr; size_t cap_arena = 0;
     mfp_pkt_desc *d_desc = nullptr; size_t cap_desc = 0;
@@ -488,10 +490,8 @@ struct mfp_context_s {
     bool defer = false;                  // mfp_analysis_defer
     bool report_os = false;              // libmerc_config.report_os (mfp_analysis_report_os)
     bool reassembly = false;             // "reassembly" in the config: mfp_process_batch_reassembly
-    Slot slot[5];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2, 4: host pipeline
-    unsigned long long *d_pipe = nullptr;   // the host pipeline's stream counters (packed bytes, overflow)
-    hipStream_t in_stream = nullptr;        // the host pipeline's copy stream (MFP_PIPE_INSTREAM)
-    hipEvent_t ev_pipe[3] = {nullptr, nullptr, nullptr};   // a pipeline slot's compaction scan done
+    Slot slot[4];                        // 0: synchronous calls (and 3: pipelined device batches); 1, 2: host pipeline
+    hipStream_t in_stream = nullptr;        // the host pipeline's copy stream
     // the per-packet shim's concurrent small batches (mfp_process_small_pinned):
     // each on a slot of its own, so batches of different callers overlap on the
     // device; taken and returned under mu, waited for outside it
@@ -585,9 +585,7 @@ extern "C" MFP_EXPORT void mfp_finalize(mfp_context c) {
     if (c->own_prev) mfp_prevalence_destroy(c->own_prev);
     for (Slot &S : c->slot) S.release();
     for (int j = 0; j < mfp_context_s::NSMALL; j++) if (c->small_init[j]) c->small[j].release();
-    if (c->d_pipe) (void)hipFree(c->d_pipe);
     if (c->in_stream) (void)hipStreamDestroy(c->in_stream);
-    for (hipEvent_t e : c->ev_pipe) if (e) (void)hipEventDestroy(e);
     delete c->prof;
     delete c;
 }
@@ -734,6 +732,8 @@ static int analyze_locked(mfp_context c, int slot, const uint8_t *d_arena, const
     if (r) return r;
     c->an_slot = slot;
     S.pend.live = true;
+    S.pend.seq_m = -1;
+    S.pend.dist_u = -5;
     S.pend.n = n; S.pend.rec = d_rec; S.pend.fp = d_fp_arena; S.pend.out = d_out; S.pend.stream = s;
     return 0;
 }
@@ -946,19 +946,9 @@ static int batch_span(const uint8_t *arena, size_t arena_len, const mfp_pkt_desc
 // on the slot's stream; descriptors keep their offsets: the device arena
 // pointer handed to the kernels is the staging buffer minus the (256-byte
 // aligned) start of the copied span
-// the pipelined host path's compaction target (mfp_process_pipelined when the
-// caller's arena and records are page-locked): strings and records straight
-// into them at their stream offsets, after the previous chunk's scan
-struct PipeOut {
-    uint8_t *dst; uint64_t cap;       // the caller's fp arena (device-visible pointer)
-    mfp_record *rec_out;              // the chunk's records in the caller's array (device-visible pointer)
-    unsigned long long *ctr;          // c->d_pipe
-    hipEvent_t wait;                  // the previous chunk's scan (nullptr: the first chunk)
-    hipEvent_t done;                  // recorded after this chunk's compaction
-};
 static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                             size_t n, size_t fp_cap, bool analysis, bool attr_prob, bool host_resolve = false,
-                            const PipeOut *po = nullptr, const uint64_t *staged = nullptr) {
+                            const uint64_t *staged = nullptr) {
     Slot &S = c->slot[slot];
     // device-pointer calls may still be using this slot's scratch on the caller's stream
     if (S.dev_recorded) { HIPCHK(hipStreamWaitEvent(S.stream, S.ev_dev, 0)); S.dev_recorded = false; }
@@ -1004,18 +994,6 @@ static int stage_and_launch(mfp_context c, int slot, const uint8_t *arena, size_
     if (staged) {   // the packets and descriptors are read by now: the copy of the slot's next chunk may start
         HIPCHK(hipEventRecord(S.ev_free, S.stream));
         S.free_recorded = true;
-    }
-    if (po) {
-        if (po->wait) HIPCHK(hipStreamWaitEvent(S.stream, po->wait, 0));
-        if (n && mfp_launch_compact_to(S.d_rec, po->rec_out, n, (const uint8_t *)S.d_fp, po->dst, po->cap, S.d_work,
-                                       (unsigned long long *)(S.d_work + ((n + 3) & ~(size_t)1)), po->ctr, S.stream,
-                                       c->prof) != 0) {
-            mfp_set_error("compaction launch failed: %s", hipGetErrorString(hipGetLastError()));
-            return -3;
-        }
-        HIPCHK(hipEventRecord(po->done, S.stream));
-        if (analysis) S.pend.fp = S.d_fp;   // the device records still index it
-        return 0;
     }
     // strings to a dense arena in packet order (d_fp2, d_used[2] bytes), records re-pointed;
     // the bin lists in d_work are dead by now and hold the scan scratch
@@ -1112,7 +1090,7 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
                                    size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
                                    double *attr_prob) {
     if (!c) { mfp_set_error("null context"); return -1; }
-    if (n == 0 || n > c->small_batch || n > 1024 || c->defer || (analysis && !c->clf) || getenv("MFP_SMALL_COPIES"))
+    if (n == 0 || n > c->small_batch || n > 1024 || c->defer || (analysis && !c->clf))
         return mfp_process_batch_host_ex(c, arena, arena_len, desc, n, rec, fp_arena, fp_cap, analysis, attr_prob);
     if (fp_cap < mfp_fp_arena_bound(0, 0)) { mfp_set_error("fp_cap below mfp_fp_arena_bound"); return -1; }
     uint64_t lo, hi, total;
@@ -1157,8 +1135,7 @@ long long mfp_process_small_pinned(mfp_context c, const uint8_t *arena, size_t a
     // contexts at n <= small_batch); any other strategy takes the staged path,
     // whose k_compact_small does that work
     const bool direct = !analysis && !(c->select & (SEL_QUIC | SEL_OPENVPN)) && hi + 64 <= arena_len &&
-                        c->strategy == MFP_STRATEGY_BINNED && fp_cap >= mfp_fp_arena_bound(n, total) &&
-                        !getenv("MFP_SMALL_STAGED");
+                        c->strategy == MFP_STRATEGY_BINNED && fp_cap >= mfp_fp_arena_bound(n, total);
     if (direct) {
         {
             std::lock_guard<std::mutex> lk(c->mu);
@@ -1288,7 +1265,7 @@ extern "C" MFP_EXPORT long long mfp_process_pipelined(mfp_context c, const uint8
         // an error path may leave copies into the caller's buffers queued on
         // either pipeline stream: drain both before the caller reuses them
         // (the error string of the failure is kept)
-        for (int s : {1, 2, 4}) (void)hipStreamSynchronize(c->slot[s].stream);
+        for (int s : {1, 2}) (void)hipStreamSynchronize(c->slot[s].stream);
         if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);   // chunk copies still reading the arena
     }
     return r;
@@ -1316,105 +1293,18 @@ static int stage_copy(mfp_context c, Slot &S, const uint8_t *arena, size_t arena
     return 0;
 }
 
-// the device-visible address of [p, p + len) when all of it is page-locked
-// host memory (hipHostMalloc / hipHostRegister), else nullptr
-static void *device_view(const void *p, size_t len) {
-    if (!p || !len) return nullptr;
-    hipPointerAttribute_t a, b;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
-    const uint8_t *e = (const uint8_t *)p + len - 1;
-    if (hipPointerGetAttributes(&b, e) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-    if (b.type != hipMemoryTypeHost) return nullptr;
-    return (uint8_t *)a.devicePointer + ((const uint8_t *)p - (const uint8_t *)a.hostPointer);
-}
-
-// mfp_process_pipelined into page-locked outputs: three chunks in flight on
-// three slots; each chunk's compaction writes its strings and records straight
-// into the caller's buffers at their stream offsets (the scan continues the
-// previous chunk's, across streams), so a chunk retires without a copy queued
-// behind the host's wait; the host waits for a chunk only to decide its
-// unknown-TLS sightings, two chunks later
-static long long pipelined_direct(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
-                                  size_t n, mfp_record *rec, mfp_record *rec_dev, char *fp_arena, uint8_t *fp_dev,
-                                  size_t fp_cap, mfp_analysis *analysis, double *attr_prob, size_t chunk) {
-    constexpr int NP = 3;
-    static constexpr int slot_of[NP] = {1, 2, 4};
-    if (!c->d_pipe && hipMalloc(&c->d_pipe, 2 * sizeof(unsigned long long)) != hipSuccess) {
-        c->d_pipe = nullptr;
-        mfp_set_error("device allocation failed");
-        return -2;
-    }
-    for (hipEvent_t &e : c->ev_pipe)
-        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipMemset(c->d_pipe, 0, 2 * sizeof(unsigned long long)));
-    struct Inflight { bool live; size_t lo, hi; };
-    Inflight inf[NP] = {};
-    auto retire = [&](int s) -> int {
-        Slot &S = c->slot[slot_of[s]];
-        HIPCHK(hipStreamSynchronize(S.stream));
-        if (analysis) {   // (the pipeline decides its chunks itself, in order)
-            const int r = slot_resolve_host(c, S, analysis + inf[s].lo, rec + inf[s].lo);
-            if (r) return r;
-        }
-        inf[s].live = false;
-        return 0;
-    };
-    const size_t nch = (n + chunk - 1) / chunk;
-    int prev = -1;
-    for (size_t k = 0; k < nch; k++) {
-        const int s = (int)(k % NP);
-        Slot &S = c->slot[slot_of[s]];
-        if (inf[s].live) { int r = retire(s); if (r) return r; }
-        const size_t lo = k * chunk, hi = std::min(n, lo + chunk), m = hi - lo;
-        uint64_t bytes = 0;
-        for (size_t i = lo; i < hi; i++) bytes += desc[i].caplen;
-        const PipeOut po{fp_dev, fp_cap, rec_dev + lo, c->d_pipe, prev >= 0 ? c->ev_pipe[prev] : nullptr, c->ev_pipe[s]};
-        int r = stage_and_launch(c, slot_of[s], arena, arena_len, desc + lo, m, mfp_fp_arena_bound(m, bytes),
-                                 analysis != nullptr, attr_prob != nullptr, false, &po);
-        if (r) return r;
-        if (analysis) HIPCHK(hipMemcpyAsync(analysis + lo, S.d_an, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
-        if (analysis && attr_prob && m)
-            HIPCHK(hipMemcpyAsync(attr_prob + lo * MFP_ATTR_DB_TAGS, S.d_ap, m * MFP_ATTR_DB_TAGS * sizeof(double),
-                                  hipMemcpyDeviceToHost, S.stream));
-        inf[s] = {true, lo, hi};
-        prev = s;
-    }
-    for (size_t k = nch > NP ? nch - NP : 0; k < nch; k++) {   // the chunks still in flight, oldest first
-        const int s = (int)(k % NP);
-        if (inf[s].live) { int r = retire(s); if (r) return r; }
-    }
-    unsigned long long ctr[2];
-    HIPCHK(hipMemcpy(ctr, c->d_pipe, sizeof ctr, hipMemcpyDeviceToHost));
-    if (ctr[1] || ctr[0] > fp_cap) { mfp_set_error("fingerprint arena overflow (cap %zu)", fp_cap); return -4; }
-    return (long long)ctr[0];
-}
-
 static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t arena_len, const mfp_pkt_desc *desc,
                                   size_t n, mfp_record *rec, char *fp_arena, size_t fp_cap, mfp_analysis *analysis,
                                   double *attr_prob, size_t chunk) {
     if (chunk == 0) chunk = (size_t)1 << 20;
-    // MFP_PIPE_DIRECT=1: the compaction writes into page-locked outputs
-    // (pipelined_direct; measured slower: the byte stores over PCIe take
-    // ~10 ms per 2M chunk on the GPU, tools/e2e_probe.py)
-    if (const char *e = getenv("MFP_PIPE_DIRECT"); e && e[0] == '1') {
-        auto *fp_dev = (uint8_t *)device_view(fp_arena, fp_cap);
-        auto *rec_dev = (mfp_record *)device_view(rec, n * sizeof(mfp_record));
-        if (fp_dev && rec_dev && n)
-            return pipelined_direct(c, arena, arena_len, desc, n, rec, rec_dev, fp_arena, fp_dev, fp_cap, analysis,
-                                    attr_prob, chunk);
-    }
-    // NP chunks in flight on NP slots (MFP_PIPE_SLOTS, 2 or 3); MFP_PIPE_INSTREAM=1:
-    // the host-to-device copies go one after the other on one stream, so the
+    // two chunks in flight on pipeline slots 1 and 2 (three were slower, r05_e2e); the
+    // host-to-device copies go one after the other on the copy stream, so the
     // first chunk's kernels start after its own copy, not after a share of all
-    int NP = 2;
-    if (const char *e = getenv("MFP_PIPE_SLOTS")) NP = atoi(e) == 3 ? 3 : 2;
-    static constexpr int slot_of[3] = {1, 2, 4};
-    bool instream = true;
-    if (const char *e = getenv("MFP_PIPE_INSTREAM")) instream = e[0] == '1';
-    if (instream && !c->in_stream) HIPCHK(hipStreamCreateWithFlags(&c->in_stream, hipStreamNonBlocking));
+    constexpr int NP = 2;
+    static constexpr int slot_of[NP] = {1, 2};
+    if (!c->in_stream) HIPCHK(hipStreamCreateWithFlags(&c->in_stream, hipStreamNonBlocking));
     struct Inflight { bool live; size_t lo, hi; };
-    Inflight inf[3] = {};
+    Inflight inf[NP] = {};
     uint64_t fp_base = 0;
     // wait for the chunk in pipeline slot s, queue the copy of its packed
     // fingerprints to the caller's arena (chunk order; the slot's next chunk
@@ -1440,7 +1330,7 @@ static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t ar
         Slot &S = c->slot[slot_of[s]];
         const size_t lo = k * chunk, hi = std::min(n, lo + chunk), m = hi - lo;
         uint64_t span[3];
-        if (instream) {   // the copy in first, then the wait for the slot's previous chunk
+        {   // the copy in first, then the wait for the slot's previous chunk
             const int r = stage_copy(c, S, arena, arena_len, desc + lo, m, c->in_stream, span);
             if (r) return r;
         }
@@ -1449,7 +1339,7 @@ static long long pipelined_locked(mfp_context c, const uint8_t *arena, size_t ar
         for (size_t i = lo; i < hi; i++) bytes += desc[i].caplen;
         const size_t cap = mfp_fp_arena_bound(m, bytes);
         int r = stage_and_launch(c, slot_of[s], arena, arena_len, desc + lo, m, cap, analysis != nullptr,
-                                 attr_prob != nullptr, false, nullptr, instream ? span : nullptr);
+                                 attr_prob != nullptr, false, span);
         if (r) return r;
         if (analysis) HIPCHK(hipMemcpyAsync(analysis + lo, S.d_an, m * sizeof(mfp_analysis), hipMemcpyDeviceToHost, S.stream));
         if (analysis && attr_prob && m)
@@ -1639,10 +1529,19 @@ extern "C" MFP_EXPORT long long mfp_analysis_distinct(mfp_context c, mfp_sightin
     Slot *S = deferred_slot(c);
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
-    std::vector<mfp_sighting> d;
-    const long long u = slot_distinct(c, *S, d);
+    if (!out && S->pend.dist_u == -5) {   // the count alone: the table's counters, no export
+        unsigned int cnt[4];
+        HIPCHK(hipMemcpyAsync(cnt, S->seen.counters, sizeof cnt, hipMemcpyDeviceToHost, S->pend.stream));
+        HIPCHK(hipStreamSynchronize(S->pend.stream));
+        return cnt[1] || cnt[0] > S->seen.list_cap ? -3 : (long long)cnt[0];
+    }
+    if (S->pend.dist_u == -5) {   // once per pending batch
+        S->pend.dist_u = slot_distinct(c, *S, S->pend.dist);
+        if (S->pend.dist_u == -2) { const long long e = S->pend.dist_u; S->pend.dist_u = -5; return e; }
+    }
+    const long long u = S->pend.dist_u;
     if (u < 0) return u;
-    if (out) memcpy(out, d.data(), std::min<size_t>(cap, d.size()) * sizeof(mfp_sighting));
+    if (out) memcpy(out, S->pend.dist.data(), std::min<size_t>(cap, S->pend.dist.size()) * sizeof(mfp_sighting));
     return u;
 }
 
@@ -1652,8 +1551,12 @@ extern "C" MFP_EXPORT long long mfp_analysis_sequence(mfp_context c, uint64_t *h
     Slot *S = deferred_slot(c);
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
-    const long long m = slot_sequence(c, *S);
-    if (m < 0) return m;
+    long long m = S->pend.seq_m;
+    if (m < 0) {   // once per pending batch (h_seq keeps it until the slot's next sequence)
+        m = slot_sequence(c, *S);
+        if (m < 0) return m;
+        S->pend.seq_m = m;
+    }
     if (hash) memcpy(hash, S->h_seq, std::min<size_t>(cap, (size_t)m) * 8);
     return m;
 }
@@ -1704,8 +1607,12 @@ extern "C" MFP_EXPORT int mfp_analysis_resolve_sequence(mfp_context c, const uin
     Slot *S = deferred_slot(c);
     if (!S) return -1;
     HIPCHK(hipSetDevice(c->device));
-    const long long ms = slot_sequence(c, *S);   // leaves the group offsets on the device
+    // the group offsets the resolve kernel reads: left on the device by this
+    // batch's sequence (mfp_analysis_sequence), or computed now
+    long long ms = S->pend.seq_m;
+    if (ms < 0) ms = slot_sequence(c, *S);
     if (ms < 0) return (int)ms;
+    S->pend.seq_m = ms;
     if ((size_t)ms != m) { mfp_set_error("sequence length %zu, batch has %lld sightings", m, ms); return -1; }
     const int r = slot_apply(c, *S, seen, m, true);
     if (r == 0) HIPCHK(hipStreamSynchronize(S->pend.stream));

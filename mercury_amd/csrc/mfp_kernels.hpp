@@ -26,7 +26,7 @@ namespace mfp {
 
 constexpr int TILE = 256;
 
-// Tile order by length (k_fp_tls1: MFP_TLS_SORT, k_fp_seg: MFP_SEG_SORT).  A
+// Tile order by length (k_fp_tls1).  A
 // lane-per-packet wave runs every loop for its longest packet and every
 // branch its lanes take, so the tile's packets are handed to its lanes in
 // caplen order: packets of one length are mostly one client's hello or one
@@ -35,12 +35,8 @@ constexpr int TILE = 256;
 // from LDS (every lane reads the same words: broadcast, no bank conflict);
 // the tile's live packets stay the first lanes.  Output placement does not
 // change meaning: the records address their strings.
-#ifndef MFP_TLS_SORT
-#define MFP_TLS_SORT 1
-#endif
-#ifndef MFP_SEG_SORT
-#define MFP_SEG_SORT 0
-#endif
+// (The same order for the HTTP request bin was slower, 9.91 -> 10.18 ms, and
+// an order over two tiles gained 0.08 ms only: neither is kept, r05_ab/r05s*.)
 struct TileSort {
     uint32_t key[TILE] __attribute__((aligned(16)));
     uint32_t idx[TILE];
@@ -72,47 +68,6 @@ DEV void tile_take(const KParams &P, uint64_t tile, uint64_t count, TileSort &s,
     dsc = s.desc[tid];
     if (ALIASED) __syncthreads();
     // (otherwise the caller's end-of-tile barrier orders these reads before the next tile's writes)
-}
-
-// MFP_TLS_SORT 2: the order over a window of two tiles (512 ClientHellos), the
-// sorted window then walked as two tiles; each lane keeps its second packet in
-// registers while the first tile's walk reuses the LDS
-struct TileSort2 {
-    uint32_t key[2 * TILE] __attribute__((aligned(16)));
-    uint32_t idx[2 * TILE];
-    mfp_pkt_desc desc[2 * TILE];
-};
-DEV void tile_take2(const KParams &P, uint64_t win, uint64_t count, TileSort2 &s, int tid, uint64_t &i0,
-                    mfp_pkt_desc &d0, bool &l0, uint64_t &i1, mfp_pkt_desc &d1, bool &l1) {
-    uint32_t mk[2], ix[2];
-    mfp_pkt_desc dd[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const uint64_t t = win * 2 * TILE + (uint64_t)(h * TILE + tid);
-        const bool live = t < count;
-        ix[h] = live ? P.idx[t] : 0u;
-        if (live) dd[h] = P.desc[ix[h]];
-        else { dd[h].offset = 0; dd[h].caplen = 0; dd[h].linktype = 0xffff; dd[h].flags = 0; }
-        const uint32_t cl = dd[h].caplen < 0x7ffffeu ? dd[h].caplen : 0x7ffffeu;
-        mk[h] = ((live ? cl : 0x7fffffu) << 9) | (uint32_t)(h * TILE + tid);
-        s.key[h * TILE + tid] = mk[h];
-    }
-    __syncthreads();
-    uint32_t r0 = 0, r1 = 0;
-#pragma unroll 8
-    for (int j = 0; j < 2 * TILE; j += 4) {
-        const uint4 v = *(const uint4 *)&s.key[j];
-        r0 += (v.x < mk[0] ? 1u : 0u) + (v.y < mk[0] ? 1u : 0u) + (v.z < mk[0] ? 1u : 0u) + (v.w < mk[0] ? 1u : 0u);
-        r1 += (v.x < mk[1] ? 1u : 0u) + (v.y < mk[1] ? 1u : 0u) + (v.z < mk[1] ? 1u : 0u) + (v.w < mk[1] ? 1u : 0u);
-    }
-    __syncthreads();   // (idx / desc share no words with key, but the ranks are read from key above)
-    s.idx[r0] = ix[0]; s.desc[r0] = dd[0];
-    s.idx[r1] = ix[1]; s.desc[r1] = dd[1];
-    __syncthreads();
-    const uint64_t nlive = count - win * 2 * TILE;
-    i0 = s.idx[tid]; d0 = s.desc[tid]; l0 = (uint64_t)tid < nlive;
-    i1 = s.idx[TILE + tid]; d1 = s.desc[TILE + tid]; l1 = (uint64_t)(TILE + tid) < nlive;
-    __syncthreads();   // s overlays LDS the walk writes
 }
 
 // k_fingerprint -- lane-per-packet walker straight from HBM, grid-stride
@@ -293,45 +248,18 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
     __shared__ uint16_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
     __shared__ uint8_t ext_ord[FMT ? TILE : 1][FAST_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
-#if MFP_TLS_SORT == 2
-    static_assert(sizeof(TileSort2) <= sizeof(out_line), "TileSort2 in out_line");
-    TileSort2 &tsort2 = *reinterpret_cast<TileSort2 *>(&out_line[0][0]);
-#elif MFP_TLS_SORT   // over the emission lines (the extension windows are written right after the take)
+    // the tile order over the emission lines (the extension windows are written right after the take)
     static_assert(sizeof(TileSort) <= sizeof(out_line), "TileSort in out_line");
     TileSort &tsort = *reinterpret_cast<TileSort *>(&out_line[0][0]);
-#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     KPH_DECL
-#if MFP_TLS_SORT == 2
-    for (uint64_t win = blockIdx.x; win * 2 * TILE < count; win += gridDim.x) {
-      uint64_t i_w0, i_w1;
-      mfp_pkt_desc d_w0, d_w1;
-      bool l_w0, l_w1;
-      tile_take2(P, win, count, tsort2, tid, i_w0, d_w0, l_w0, i_w1, d_w1, l_w1);
-#pragma unroll 1
-      for (int sub = 0; sub < 2; sub++) {
-        const uint64_t i = sub ? i_w1 : i_w0;
-        const bool live = sub ? l_w1 : l_w0;
-        const mfp_pkt_desc dsc = sub ? d_w1 : d_w0;
-#else
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
-#endif
-#if MFP_TLS_SORT == 2
-#elif MFP_TLS_SORT
         uint64_t i;
         bool live;
         mfp_pkt_desc dsc;
         tile_take<true>(P, tile, count, tsort, tid, i, dsc, live);
-#else
-        const uint64_t t = tile * TILE + tid;
-        const bool live = t < count;
-        const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
-        mfp_pkt_desc dsc;
-        if (live) dsc = P.desc[i];
-        else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
-#endif
         const uint8_t *data = P.arena + dsc.offset;
 
         // reservation from the bound: one atomic per tile
@@ -444,9 +372,6 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         }
         __syncthreads();   // tile_base / wave_tot reuse
         KPH(4);
-#if MFP_TLS_SORT == 2
-      }
-#endif
     }
     KPH_FLUSH();
 }
@@ -486,15 +411,8 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
 #endif
 #if MFP_SEG_LANE
     __shared__ __attribute__((aligned(16))) uint64_t out_line[TILE][SEG_LINEW];
-#if MFP_SEG_SORT   // the emission lines are free while the tile is taken (a barrier precedes the emission)
-    static_assert(sizeof(TileSort) <= sizeof(out_line), "TileSort in out_line");
-    TileSort &tsort = *reinterpret_cast<TileSort *>(&out_line[0][0]);
-#endif
 #else
     __shared__ uint4 stage[TILE / 64][SEG_STAGE / 16];   // per wave: the packet being expanded
-#if MFP_SEG_SORT
-    __shared__ TileSort tsort;
-#endif
 #endif
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
@@ -514,19 +432,12 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
     const uint64_t count = (uint64_t)__hip_atomic_load(P.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     KPH_DECL
     for (uint64_t tile = blockIdx.x; tile * TILE < count; tile += gridDim.x) {
-#if MFP_SEG_SORT
-        uint64_t i;
-        bool live;
-        mfp_pkt_desc dsc;
-        tile_take(P, tile, count, tsort, tid, i, dsc, live);
-#else
         const uint64_t t = tile * TILE + tid;
         const bool live = t < count;
         const uint64_t i = live ? (uint64_t)P.idx[t] : 0;
         mfp_pkt_desc dsc;
         if (live) dsc = P.desc[i];
         else { dsc.offset = 0; dsc.caplen = 0; dsc.linktype = 0xffff; dsc.flags = 0; }
-#endif
         const uint8_t *data = P.arena + dsc.offset;
 
         Out o;

@@ -16,7 +16,10 @@
 // Timestamps are reported as tv_sec * 1e9 + tv_usec * 1000 ns
 // (packet_info_init_from_pkthdr, pcap_file_io.c:462-468).
 #include <linux/if_packet.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
@@ -41,7 +44,45 @@ struct mfp_pcap_s {
     FILE *f = nullptr;
     bool swap = false;
     uint32_t linktype = 0;
-    std::vector<char> iobuf;
+    // the file is read in large blocks into buf (two small freads per packet,
+    // each taking the stream's lock, cost more than the copy); [pos, end) unread
+    std::vector<uint8_t> buf;
+    const uint8_t *data = nullptr;       // the unread bytes: buf, or the mapped file
+    size_t pos = 0, end = 0;
+    bool eof = false;
+    void *map = nullptr;                 // a regular file is mapped whole (no copy through a buffer)
+    size_t map_len = 0;
+    // at least `need` unread bytes, unless the file ends first
+    bool avail(size_t need) {
+        if (map) return end - pos >= need;
+        while (end - pos < need && !eof) {
+            if (pos) { memmove(buf.data(), buf.data() + pos, end - pos); end -= pos; pos = 0; }
+            const size_t got = fread(buf.data() + end, 1, buf.size() - end, f);
+            if (got == 0) eof = true;
+            end += got;
+        }
+        return end - pos >= need;
+    }
+    bool try_map() {
+        struct stat st;
+        if (fstat(fileno(f), &st) != 0 || !S_ISREG(st.st_mode) || st.st_size <= 0) return false;
+        void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fileno(f), 0);
+        if (m == MAP_FAILED) return false;
+        (void)madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+        map = m;
+        map_len = (size_t)st.st_size;
+        data = (const uint8_t *)m;
+        end = map_len;
+        return true;
+    }
+    // skip k bytes of the file: what is buffered, then the rest by seeking
+    bool skip(size_t k) {
+        if (map) { pos += std::min(k, end - pos); return true; }   // (fseek past the end succeeds too)
+        const size_t b = std::min(k, end - pos);
+        pos += b;
+        k -= b;
+        return k == 0 || fseek(f, (long)k, SEEK_CUR) == 0;
+    }
     bool have_hdr = false;               // record header read, its data not yet taken
     uint32_t ts_sec = 0, ts_usec = 0, incl = 0;
     bool done = false, failed = false;
@@ -49,6 +90,7 @@ struct mfp_pcap_s {
 
 extern "C" MFP_EXPORT void mfp_pcap_close(mfp_pcap p) {
     if (!p) return;
+    if (p->map) munmap(p->map, p->map_len);
     if (p->f) fclose(p->f);
     delete p;
 }
@@ -59,14 +101,18 @@ extern "C" MFP_EXPORT mfp_pcap mfp_pcap_open(const char *path) {
     if (!f) { mfp_set_error("%s: error opening read file %s", strerror(errno), path); return nullptr; }
     auto *p = new mfp_pcap_s;
     p->f = f;
-    p->iobuf.resize(4u << 20);
-    setvbuf(f, p->iobuf.data(), _IOFBF, p->iobuf.size());
+    if (!p->try_map()) {
+        p->buf.resize(8u << 20);   // > BUFLEN + a record header
+        p->data = p->buf.data();
+    }
     uint8_t h[24];
-    if (fread(h, sizeof h, 1, f) != 1) {
+    if (!p->avail(sizeof h)) {
         mfp_set_error("could not read PCAP file header");
         mfp_pcap_close(p);
         return nullptr;
     }
+    memcpy(h, p->data + p->pos, sizeof h);
+    p->pos += sizeof h;
     uint32_t magic;
     memcpy(&magic, h, 4);
     if (magic == kMagic || magic == kCigam) {
@@ -102,8 +148,9 @@ extern "C" MFP_EXPORT long long mfp_pcap_read_batch(mfp_pcap p, uint8_t *arena, 
     size_t used = 0, n = 0;
     while (n < max_pkts && !p->done) {
         if (!p->have_hdr) {
-            uint8_t h[16];
-            if (fread(h, sizeof h, 1, p->f) != 1) { p->done = true; break; }   // no more data
+            if (!p->avail(16)) { p->done = true; break; }   // no (whole) record header: no more data
+            const uint8_t *h = p->data + p->pos;
+            p->pos += 16;
             p->ts_sec = rd32(h, p->swap);
             p->ts_usec = rd32(h + 4, p->swap);
             p->incl = rd32(h + 8, p->swap);
@@ -117,12 +164,14 @@ extern "C" MFP_EXPORT long long mfp_pcap_read_batch(mfp_pcap p, uint8_t *arena, 
             }
             break;                       // next batch starts with this record
         }
-        if (take && fread(arena + used, take, 1, p->f) != 1) {
+        if (take && !p->avail(take)) {
             mfp_set_error("could not read packet with caplen %u", take);
             p->done = p->failed = true;
             break;
         }
-        if (p->incl > take && fseek(p->f, (long)(p->incl - take), SEEK_CUR) != 0) {
+        if (take) memcpy(arena + used, p->data + p->pos, take);
+        p->pos += take;
+        if (p->incl > take && !p->skip(p->incl - take)) {
             mfp_set_error("could not advance file pointer");
             p->done = p->failed = true;  // the truncated packet itself is still delivered
         }

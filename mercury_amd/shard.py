@@ -133,10 +133,10 @@ def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
         t = time.perf_counter()
         ph[name] = ph.get(name, 0.0) + (t - t0)
         t0 = t
-    dl = ctx.analysis_distinct()
-    lap("distinct_export")
+    nd = ctx.analysis_distinct_count()
+    lap("distinct_count")
     # [distinct count or -1 (table overflow), this shard's stream base]
-    hdr = torch.tensor([-1 if dl is None else len(dl), int(shard_base)], dtype=torch.int64)
+    hdr = torch.tensor([-1 if nd is None else nd, int(shard_base)], dtype=torch.int64)
     hdrs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(hdrs, hdr, group=group)
     lap("header_gather")
@@ -144,6 +144,8 @@ def ordered_prevalence_merge(ctx, prev, shard_base, group=None):
     # step; with more distinct fingerprints in the step than the LRU holds it
     # cannot be (every rank sees the same counts, so all take the same path)
     if all(int(h[0]) >= 0 for h in hdrs) and sum(int(h[0]) for h in hdrs) <= prev.capacity:
+        dl = ctx.analysis_distinct()
+        lap("distinct_export")
         lists = _all_gather_rows(dl if dl is not None else np.zeros(0, SIGHTING_DTYPE), group)
         for x, h in zip(lists, hdrs):
             x["first"] += np.uint64(int(h[1]))

@@ -109,7 +109,10 @@ class _ShardCtx:
         self.seen = None
 
     def analysis_distinct(self):
-        return self.dl.copy()
+        return None if self.dl is None else self.dl.copy()
+
+    def analysis_distinct_count(self):
+        return None if self.dl is None else len(self.dl)
 
     def analysis_sequence(self):
         return self.seq
@@ -337,7 +340,7 @@ def _scale_worker(rank, world, port, q, m, steps, threads=2):
             c = _ShardCtx.__new__(_ShardCtx)
             c.seq = (keys.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0x5EED)
             c.dl, c.seen = None, None
-            c.analysis_distinct = lambda: None                       # the table overflowed: sequence form
+            # (dl None: the table overflowed: the sequence form)
             dist.barrier()
             t0 = time.perf_counter()
             shard.ordered_prevalence_merge(c, prev, rank * m)
