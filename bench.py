@@ -324,13 +324,13 @@ def other_paths(torch, steps):
     ts = np.full(len(desc), 1700000000 * 10**9, np.uint64)
     # warm-up at the timed size (the context's device buffers grow to it),
     # then a fresh flow table for each timed call (the same stream each time)
-    ctx.process_host_reassembly(arena, desc, ts_ns=ts)
+    ctx.process_host_reassembly(arena, desc, ts_ns=ts, merged=False)
     els = []
     for _ in range(3):
         ctx.lib.mfp_reassembler_destroy(ctx.reasm)
         ctx.reasm = None
         t0 = time.perf_counter()
-        rec, fp, props, _, _ = ctx.process_host_reassembly(arena, desc, ts_ns=ts)
+        rec, fp, props, _, _ = ctx.process_host_reassembly(arena, desc, ts_ns=ts, merged=False)
         els.append(time.perf_counter() - t0)
     el = float(np.mean(els))
     ctx.close()

@@ -365,11 +365,12 @@ class Context:
             raise MercuryAmdError("mfp_process_batch_host_seg failed: " + _err(self.lib))
         return rec, fp[:used].tobytes(), seg[:n]
 
-    def process_host_reassembly(self, arena, desc, ts_ns=None, analysis=False):
+    def process_host_reassembly(self, arena, desc, ts_ns=None, analysis=False, merged=True):
         """A host batch in stream order through the context's TCP reassembler
         (config with "reassembly"; state persists across calls) -> (records,
         fp arena bytes, props (uint16, REASM_* bits), arena ++ rebuilt frames,
-        desc indexing it)."""
+        desc indexing it).  merged=False: None in place of arena ++ frames (a
+        caller that renders no JSON skips the copy)."""
         if not self.lib.mfp_reassembly_enabled(self.h):
             raise MercuryAmdError("the configuration has no \"reassembly\"")
         if not getattr(self, "reasm", None):
@@ -398,11 +399,14 @@ class Context:
                                                          out_desc.ctypes.data)
         if used < 0:
             raise MercuryAmdError("mfp_process_batch_reassembly failed: " + _err(self.lib))
-        flen = ctypes.c_size_t(0)
-        ptr = self.lib.mfp_reassembler_frames(self.reasm, ctypes.byref(flen))
-        frames = np.ctypeslib.as_array((ctypes.c_uint8 * flen.value).from_address(ptr)).copy() if flen.value else \
-            np.zeros(0, np.uint8)
-        out = (rec, fp[:used].tobytes(), props[:n], np.concatenate([arena, frames]), out_desc[:n])
+        joined = None
+        if merged:
+            flen = ctypes.c_size_t(0)
+            ptr = self.lib.mfp_reassembler_frames(self.reasm, ctypes.byref(flen))
+            frames = np.ctypeslib.as_array((ctypes.c_uint8 * flen.value).from_address(ptr)) if flen.value else \
+                np.zeros(0, np.uint8)
+            joined = np.concatenate([arena, frames])
+        out = (rec, fp[:used].tobytes(), props[:n], joined, out_desc[:n])
         return out + (an[:n], ap[:n]) if analysis else out
 
     def analyze_host_reassembly(self, arena, desc, ts_ns=None, analysis=True):

@@ -1,13 +1,13 @@
 #!/bin/bash
-# GPU box, round-5 closing profiles on the final tree: rocprofv3 kernel-trace
+# GPU box, round-6 closing profiles on the final tree: rocprofv3 kernel-trace
 # stats + FETCH_SIZE / WRITE_SIZE passes over config 4 (tools/gpu_traffic.sh),
 # two SQ counter passes over 10 M packets, the FETCH/WRITE calibration
 # kernels (tools/calib_fetch), then the default bench line.
-#   TAG=r05f bash tools/r05_final.sh
+#   TAG=r06g bash tools/r06_final.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
-T=${TAG:-r05f}
+T=${TAG:-r06g}
 O=gpurun_out/$T
 mkdir -p $O
 TAG=$T BENCH="--diverse-leg 0" bash tools/gpu_traffic.sh || exit 1
