@@ -710,12 +710,18 @@ def arena_slots(rec, desc):
     return int(np.where(rec["msg"] == 1, np.maximum(exact, by_bound), exact).sum())
 
 
-def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
+def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None, tables=None):
     """Algorithmic HBM bytes per step of each kernel:
     what the kernel must read and write at least, from the packets' own
     sizes.  k_classify: descriptor + the packet's first 128 bytes + the bin id
     and index; a bin kernel: index + descriptor + the whole packet + record +
-    the fingerprint (+ its 8-byte hash); the classifier kernels: see below."""
+    the fingerprint (+ its 8-byte hash); the classifier kernels: see below.
+    Reads of the archive's tables (the pool copies strings are verified
+    against, feature-table slots, priors, update lists) are NOT algorithmic
+    bytes: a step re-reads the same few thousand entries millions of times and
+    the caches serve them; `tables` (a dict), when given, receives them per
+    kernel."""
+    tb = tables if tables is not None else {}
     cap = desc["caplen"].astype(np.int64)
     fl = rec["fp_len"].astype(np.int64)
     hashed = np.where((rec["flags"] & 4) != 0, 8, 0)
@@ -744,8 +750,9 @@ def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
         # k_analyze: record in, analysis record out; per classified packet the
         # stored string hash and the fingerprint verified against its pool copy;
         # the 16-B work item of each packet with more to do; the sighting bitmap
-        out["k_analyze"] = int(len(rec) * (32 + A) + (valid * (8 + 2 * fl)).sum() +
+        out["k_analyze"] = int(len(rec) * (32 + A) + (valid * (8 + fl)).sum() +
                                16 * st.get("work_items", 0) + 8 * ngroups)
+        tb["k_analyze"] = int((valid * fl).sum())
         # k_seen_scan: the bitmap, each sighting's record and hash, one 24-B
         # sighting-slot update per distinct fingerprint per block
         out["k_seen_scan"] = int(8 * ngroups + st.get("pending", 0) * (32 + 8) + 24 * st.get("seen_merges", 0))
@@ -753,16 +760,16 @@ def kernel_bytes(rec, desc, an, n_fallback=0, an_stats=None):
         # window of each work item; server name and user agent with their pool
         # copies (scored packets); one 32-B slot per feature lookup; the 64-B
         # entry written to the lane or wave scorer's list
-        out["k_an_features"] = int(st.get("work_items", 0) * (16 + 32 + 16 + 40) + (scored * 2 * (sn + ua)).sum() +
-                                   32 * st.get("feature_slots", 0) +
+        out["k_an_features"] = int(st.get("work_items", 0) * (16 + 32 + 16 + 40) + (scored * (sn + ua)).sum() +
                                    64 * (st.get("lane_scored", 0) + st.get("deferred", 0)))
+        tb["k_an_features"] = int((scored * (sn + ua)).sum() + 32 * st.get("feature_slots", 0))
         # k_an_score: list entry, fingerprint entry, priors, update entries and
         # the analysis record of each lane-scored packet
-        out["k_an_score"] = int(st.get("lane_scored", 0) * (64 + 32 + A) + 8 * st.get("lane_priors", 0) +
-                                12 * st.get("lane_updates", 0))
+        out["k_an_score"] = int(st.get("lane_scored", 0) * (64 + 32 + A))
+        tb["k_an_score"] = int(8 * st.get("lane_priors", 0) + 12 * st.get("lane_updates", 0))
         # k_analyze_wave: the same for each wave-scored packet
-        out["k_analyze_wave"] = int(st.get("deferred", 0) * (64 + 32 + A) + 8 * st.get("wave_priors", 0) +
-                                    12 * st.get("wave_updates", 0))
+        out["k_analyze_wave"] = int(st.get("deferred", 0) * (64 + 32 + A))
+        tb["k_analyze_wave"] = int(8 * st.get("wave_priors", 0) + 12 * st.get("wave_updates", 0))
         # k_analyze_resolve: one 8-byte sighting bitmap word per 64 packets, and per
         # pending sighting its record, its sighting-table slot (24 B) and its result
         out["k_analyze_resolve"] = int(8 * ngroups + st.get("pending", 0) * (32 + 24 + A))
@@ -1013,16 +1020,10 @@ def main():
     caplen_bytes = int(desc["caplen"].astype(np.int64).sum())
     fp_bytes = int(rec["fp_len"].astype(np.int64).sum())
     assert fp_bytes == used
-    # algorithmic bytes per step: every packet
-    # read once, its descriptor, its 32-B record and its fingerprint written;
-    # the classifier re-reads the record and the fingerprint of each
-    # classified packet and writes a 32-B analysis record per packet
-    alg_bytes = caplen_bytes + 16 * n + 32 * n + fp_bytes
     an_info = None
     if analysis:
         an = d_an.cpu().numpy().view(mercury_amd.ANALYSIS_DTYPE)
         valid = (an["flags"] & 1) != 0
-        alg_bytes += 32 * n + mercury_amd.ANALYSIS_DTYPE.itemsize * n + int(rec["fp_len"][valid].astype(np.int64).sum())
         st = np.bincount(an["status"][valid], minlength=5)
         an_info = {"classified": int(valid.sum()),
                    "status": {mercury_amd.api.STATUS_NAMES[i]: int(st[i]) for i in range(5)},
@@ -1034,7 +1035,6 @@ def main():
     kern_ms = {k: v[1] / args.steps for k, v in prof.items()}
     step_kern_ms = sum(kern_ms.values())
     dominant = max(kern_ms, key=kern_ms.get)
-    achieved = alg_bytes / (step_kern_ms * 1e-3) / 1e9
 
     total_pkts = n * world
     value = total_pkts * args.steps / elapsed / 1e6
@@ -1052,7 +1052,12 @@ def main():
                 words = (ctypes.c_uint64 * 8)()
                 if fn(words) == 0:
                     (an_counters if an_counters is not None else {})[f"{tu}_phase_clocks"] = [int(x) for x in words[:5]]
-    kbytes = kernel_bytes(rec, desc, an if analysis else None, n_fallback, an_counters)
+    ktables = {}
+    kbytes = kernel_bytes(rec, desc, an if analysis else None, n_fallback, an_counters, ktables)
+    # the step's algorithmic bytes: the same per-kernel definition summed over
+    # the kernels the step launched (so roofline.step and its split agree)
+    alg_bytes = sum(kbytes.get(k, 0) or 0 for k in kern_ms)
+    achieved = alg_bytes / (step_kern_ms * 1e-3) / 1e9
     diverse = None
     if analysis and args.diverse_leg > 0 and world > 1:
         del d_arena, d_desc
@@ -1200,6 +1205,7 @@ def main():
             ach = ab / (ms * 1e-3) / 1e9 if ms else 0.0
             return {"kernels": len(ks), "kernel_ms": round(ms, 4), "algorithmic_bytes": ab, "achieved": round(ach, 2),
                     "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tb,
+                    "table_read_bytes": sum(ktables.get(k, 0) for k in ks),
                     "traffic_per_algorithmic_byte": round(tb / ab, 3) if tb and ab else None}
         is_clf = lambda k: k.startswith(("k_analyze", "k_an_", "k_seen"))   # noqa: E731
         step_split = {"walkers": step_part(lambda k: not is_clf(k)), "classifier": step_part(is_clf)}
@@ -1258,11 +1264,14 @@ def main():
                 "step": {"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "kernel_ms": round(step_kern_ms, 4), "algorithmic_bytes": alg_bytes,
                          "traffic": traffic if not isinstance(traffic, dict) else traffic.get("step"),
-                         "what": "every kernel of one step, back to back on one stream",
+                         "what": "every kernel of one step, back to back on one stream; algorithmic bytes = the "
+                                 "sum of the kernels' own (kernels[*].algorithmic_bytes: inputs read once, outputs "
+                                 "written once; archive-table re-reads excluded, kernels[*].table_read_bytes)",
                          "split": step_split},
             },
             "kernels": {k: {"launches_per_step": prof[k][0] / args.steps, "ms_per_step": round(v, 4),
                             "algorithmic_bytes": kbytes.get(k),
+                            "table_read_bytes": ktables.get(k),
                             "hbm_bytes": traffic.get(k) if traffic else None,
                             "achieved_gb_s": round(kbytes[k] / (v * 1e-3) / 1e9, 2) if kbytes.get(k) and v else None}
                         for k, v in kern_ms.items()},

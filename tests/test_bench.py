@@ -50,15 +50,18 @@ def test_kernel_bytes_accounting():
     an["process"] = [7, 0xFFFFFFFF, 0xFFFFFFFF]
     st = {"work_items": 1, "lane_scored": 1, "feature_slots": 5, "lane_priors": 4, "lane_updates": 10,
           "pending": 0, "deferred": 0, "seen_merges": 0}
-    kb = bench.kernel_bytes(rec, desc, an, an_stats=st)
+    tb = {}
+    kb = bench.kernel_bytes(rec, desc, an, an_stats=st, tables=tb)
     assert kb["k_fp_tls1/tls_ch"] == 4 + 16 + 600 + 32 + 300
     assert kb["k_fp_seg/http_req"] == 4 + 16 + 200 + 32 + 100 + 8
     assert kb["k_fingerprint/tcp_syn"] == 4 + 16 + 60 + 32 + 40
     assert kb["k_classify"] == 3 * (16 + 5) + 128 + 128 + 60
-    assert kb["k_analyze"] == 3 * (32 + 32) + (8 + 2 * 300) + 16 + 8   # record + 32-B analysis record
-    assert kb["k_an_features"] == (16 + 32 + 16 + 40) + 2 * 20 + 32 * 5 + 64
-    assert kb["k_an_score"] == (64 + 32 + 32) + 8 * 4 + 12 * 10
+    assert kb["k_analyze"] == 3 * (32 + 32) + (8 + 300) + 16 + 8   # record + 32-B analysis record
+    assert kb["k_an_features"] == (16 + 32 + 16 + 40) + 20 + 64
+    assert kb["k_an_score"] == 64 + 32 + 32
     assert kb["k_seen_scan"] == 8
+    # the archive's tables: the verified strings' pool copies, feature slots, priors and update lists
+    assert tb == {"k_analyze": 300, "k_an_features": 20 + 32 * 5, "k_an_score": 8 * 4 + 12 * 10, "k_analyze_wave": 0}
 
 
 def _bench():
