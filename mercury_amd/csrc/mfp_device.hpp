@@ -1266,6 +1266,7 @@ struct TlsPlan {
     uint16_t *off_row = nullptr;
     uint8_t *ord_row = nullptr;
     uint8_t *win = nullptr;    // (k_fp_tls1) the extension-header window in LDS (ExtWin::wv)
+    uint8_t *win2 = nullptr;   // (k_fp_tls1, MFP_EXT_WIN_BLOCKS > 4) its blocks from the fifth on
     uint32_t win_lane = 0;
 };
 
@@ -1437,6 +1438,10 @@ DEV bool key32_grease(uint32_t k, int fmt) { return fmt == 1 ? (k >> 16) == 0x0a
 #ifndef MFP_EXT_WIN
 #define MFP_EXT_WIN 2
 #endif
+// 16-byte blocks in the window (MFP_EXT_WIN 2): 4 = 64 bytes per lane
+#ifndef MFP_EXT_WIN_BLOCKS
+#define MFP_EXT_WIN_BLOCKS 4
+#endif
 // MFP_EXT_WIN 2: the blocks go straight to LDS (global_load_lds_dwordx4, no
 // VGPRs); the wave's window area is 4 x 1 KiB, block k of lane l at
 // wv + 1024 k + 16 l (the instruction writes lane l's 16 bytes at the
@@ -1446,23 +1451,26 @@ struct ExtWin {
     uint8_t *wv;                 // the wave's window area in LDS (4 KiB; MFP_EXT_WIN 1: the lane's 64-byte row)
     uint32_t lane;
     const uint8_t *base;         // the window's first byte (16-byte aligned); nullptr: empty
+    uint8_t *wv2;                // blocks 4.. of the window (MFP_EXT_WIN_BLOCKS > 4)
+    DEV uint8_t *blk(uint32_t b) const { return b < 4 ? wv + 1024 * b : wv2 + 1024 * (b - 4); }
     DEV const uint32_t *dw(uint32_t k) const {
-        return MFP_EXT_WIN == 2 ? (const uint32_t *)(wv + 1024 * (k >> 2) + 16 * lane + 4 * (k & 3))
+        return MFP_EXT_WIN == 2 ? (const uint32_t *)(blk(k >> 2) + 16 * lane + 4 * (k & 3))
                                 : (const uint32_t *)wv + k;
     }
 };
 // the 4 bytes at a, big-endian (a < end; bytes at or past end are garbage)
 DEV uint32_t win_be32(ExtWin &wn, const uint8_t *a, const uint8_t *end) {
     uint64_t o = (uint64_t)(a - wn.base);
-    if (wn.base == nullptr || a < wn.base || o > 56) {
+    constexpr uint32_t NB = MFP_EXT_WIN == 2 ? MFP_EXT_WIN_BLOCKS : 4;
+    if (wn.base == nullptr || a < wn.base || o > 16 * NB - 8) {
         const uint8_t *b = (const uint8_t *)((uintptr_t)a & ~(uintptr_t)15);
         const uint4 *s = (const uint4 *)b;
         if (MFP_EXT_WIN == 2) {
 #pragma unroll
-            for (int k = 0; k < 4; k++)
+            for (uint32_t k = 0; k < NB; k++)
                 if (k == 0 || b + 16 * k < end)
                     __builtin_amdgcn_global_load_lds((const void *)(s + k),
-                                                     (void __attribute__((address_space(3))) *)(wn.wv + 1024 * k),
+                                                     (void __attribute__((address_space(3))) *)(wn.blk(k)),
                                                      16, 0, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
@@ -1509,7 +1517,7 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
     uint32_t cnt = 0;
     bool rare = false;
     Cur p = ch.extensions;
-    ExtWin wn{pl.win, pl.win_lane, nullptr};
+    ExtWin wn{pl.win, pl.win_lane, nullptr, pl.win2};
     while (clen(p) > 0) {
         const uint8_t *start = p.d;
         Ext x = ext_parse_win(p, wn);

@@ -248,6 +248,9 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
     __shared__ uint16_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
     __shared__ uint8_t ext_ord[FMT ? TILE : 1][FAST_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
+#if MFP_EXT_WIN == 2 && MFP_EXT_WIN_BLOCKS > 4
+    __shared__ __attribute__((aligned(16))) uint8_t ext_win2[TILE / 64][1024 * (MFP_EXT_WIN_BLOCKS - 4)];
+#endif
     // the tile order over the emission lines (the extension windows are written right after the take)
     static_assert(sizeof(TileSort) <= sizeof(out_line), "TileSort in out_line");
     TileSort &tsort = *reinterpret_cast<TileSort *>(&out_line[0][0]);
@@ -302,6 +305,9 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         // free until the emission: the extension-header window (ExtWin)
         plan.win = MFP_EXT_WIN == 2 ? (uint8_t *)&out_line[0][0] + 4096 * wid : (uint8_t *)out_line[tid];
         plan.win_lane = (uint32_t)lane;
+#if MFP_EXT_WIN == 2 && MFP_EXT_WIN_BLOCKS > 4
+        plan.win2 = ext_win2[wid];
+#endif
         {
             Em<false, FMT> e;
             e.plan = &plan;

@@ -357,6 +357,10 @@ extern "C" MFP_EXPORT int mfp_pkt_proc_apply(mfp_pkt_proc p, int64_t tv_sec, int
     if (p->err) { std::lock_guard<std::mutex> lk(p->mu); return report(p); }
     const uint32_t L = std::min(len, caplen);
     if (L && !packet) { mfp_set_error("null packet"); return -1; }
+    if (L > p->o.arena_bytes) {   // (no batch could hold it; the readers cap records at 65 536 bytes)
+        mfp_set_error("a %u-byte packet is larger than the %zu-byte batch arena", L, p->o.arena_bytes);
+        return -1;
+    }
     Batch *B = &p->b[p->fill];
     if (B->n == p->o.batch_pkts || B->used + L > p->o.arena_bytes ||
         (p->o.flush_us && B->n && (B->n & 63) == 0 &&
