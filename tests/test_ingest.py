@@ -193,3 +193,30 @@ def test_pcap_ingest_to_device(tmp_path):
     ctx.close()
     want = [row[3] for row in cases.load_golden("binmix", 0, "fp")]
     assert got == want and sum(1 for s in got if s) > 5000
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+def test_pcap_from_a_pipe_equals_the_file(tmp_path, big_endian):
+    """A regular file is mapped whole; a pipe (or any stream) goes through the
+    reader's block buffer (mfp_pcap.cpp): the same packets, times and
+    truncation (a 70 000-byte record, BUFLEN = 65 536) either way, including
+    records that straddle the buffer's refills."""
+    import threading
+    pk = packets(2500, seed=7) + [bytes(range(256)) * 274]          # the last: 70 144 bytes
+    p = tmp_path / "a.pcap"
+    write_pcap(p, pk, big_endian=big_endian, network_field=(1 if not big_endian else 0x00010000))
+    want = read_all(p, max_pkts=64, arena_bytes=4 << 20)
+    fifo = tmp_path / "a.fifo"
+    os.mkfifo(fifo)
+    blob = open(p, "rb").read()
+
+    def feed():
+        with open(fifo, "wb") as f:
+            for k in range(0, len(blob), 100_003):    # odd-sized writes
+                f.write(blob[k:k + 100_003])
+    t = threading.Thread(target=feed)
+    t.start()
+    got = read_all(fifo, max_pkts=64, arena_bytes=4 << 20)
+    t.join()
+    assert got == want
+    assert len(got[1]) == len(pk) and got[1][-1] == pk[-1][:65536]
