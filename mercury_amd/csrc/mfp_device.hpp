@@ -1261,9 +1261,10 @@ struct TlsPlan {
     Cur version, ciphers, exts;
     uint32_t n, type, fmt;
     bool ok;
-    // the fast plan (k_fp_tls1): the lane's rows in LDS -- offsets of the
-    // kept extensions by wire index, and the emission order as wire indices
-    uint16_t *off_row = nullptr;
+    // the fast plan (k_fp_tls1): the lane's rows in LDS -- the kept
+    // extensions by wire index (ext_row: header and offset), and the emission
+    // order as wire indices
+    uint32_t *off_row = nullptr;   // ext_row entries (below)
     uint8_t *ord_row = nullptr;
     uint8_t *win = nullptr;    // (k_fp_tls1) the extension-header window in LDS (ExtWin::wv)
     uint8_t *win2 = nullptr;   // (k_fp_tls1, MFP_EXT_WIN_BLOCKS > 4) its blocks from the fifth on
@@ -1504,6 +1505,20 @@ DEV Ext ext_parse_win(Cur &p, ExtWin &wn) {
     return x;
 }
 
+// A kept extension in the plan's LDS row (k_fp_tls1), so the emission reads
+// no extension header again: a static extension (its value is printed) as
+// 1 << 31 | type code << 22 | length << 11 | offset in the extension block
+// (type code: the type, below 64, or 63 for 21760; length and offset at most
+// 2047, else the plan is left unset); any other as its 16-bit type (only the
+// type is printed)
+DEV uint32_t ext_row(uint32_t t, uint32_t vl, uint32_t off, bool st) {
+    return st ? (1u << 31) | ((t < 64 ? t : 63u) << 22) | (vl << 11) | off : t;
+}
+DEV uint32_t ext_row_type(uint32_t er) {
+    if (!(er >> 31)) return er & 0xffff;
+    const uint32_t tc = (er >> 22) & 63u;
+    return tc == 63 ? 21760u : tc;
+}
 template <int FMT, class E>
 DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const uint8_t *base,
                           uint32_t &sni_off, uint32_t &sni_len, uint32_t &alpn_off, uint32_t &alpn_len) {
@@ -1550,7 +1565,12 @@ DEV void tls_ch_plan_fast(E &b, TlsPlan &pl, const Ch &ch, uint32_t type, const 
             if (c3 >= 3) continue;
         }
         if (cnt >= (uint32_t)FAST_EXT || x.type == 0x39 || x.type == 0xffa5) { rare = true; continue; }
-        pl.off_row[cnt] = (uint16_t)(start - ch.extensions.d);
+        {
+            const uint32_t off = (uint32_t)(start - ch.extensions.d);
+            const bool st = static_ext_bit(x.type);
+            if (st && (off > 2047 || x.length > 2047)) { rare = true; continue; }
+            pl.off_row[cnt] = ext_row(x.type, x.length, off, st);
+        }
         if (FMT != 0) {
             bool fits;
             const uint32_t v = ext_key32(x, FMT, bucket, cnt, fits);
@@ -1600,20 +1620,13 @@ DEV void tls_ch_emit_fast(E &b, TlsPlan &pl) {
     }
     hex_run<true>(b, pl.ciphers.d, (uint32_t)clen(pl.ciphers) & ~1u);
     b.push(')' | ((FMT ? '[' : '(') << 8), 2);
-    // the next extension's header is loaded while this one is written (its
-    // load's latency hidden behind an extension's emission)
-    uint32_t off_next = pl.n ? pl.off_row[FMT == 0 ? 0 : pl.ord_row[0]] : 0u;
-    uint32_t th_next = pl.n ? ld_be32n(pl.exts.d + off_next, 4) : 0u;
+    // the extension headers come from the plan's rows (no packet loads)
     for (uint32_t j = 0; j < pl.n; j++) {
-        const uint32_t off = off_next;
-        const uint8_t *h = pl.exts.d + off;
-        const uint32_t th = th_next;                       // type << 16 | length (the plan kept whole extensions)
-        if (j + 1 < pl.n) {
-            off_next = pl.off_row[FMT == 0 ? j + 1 : pl.ord_row[j + 1]];
-            th_next = ld_be32n(pl.exts.d + off_next, 4);
-        }
-        const uint32_t t = th >> 16, vl = th & 0xffff;
-        const bool st = static_ext_bit(t);
+        const uint32_t er = pl.off_row[FMT == 0 ? j : pl.ord_row[j]];
+        const bool st = er >> 31;
+        const uint32_t t = ext_row_type(er), vl = st ? (er >> 11) & 2047u : 0u;
+        const uint8_t *h = pl.exts.d + (er & 2047u);
+        const uint32_t th = (t << 16) | vl;                // type << 16 | length (the plan kept whole extensions)
         uint32_t w;                                        // head: type, length as a little-endian word
         if (FMT == 0) {
             w = degrease_pairs(__builtin_bswap32(th));     // hex_degrease of type and length (tls.h:1560-1600)

@@ -245,7 +245,7 @@ template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
     __shared__ __attribute__((aligned(16))) uint64_t out_line[TILE][8];   // emission staging, one 64-byte line per lane
-    __shared__ uint16_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: offsets by wire index (odd stride)
+    __shared__ uint32_t ext_off[TILE][FAST_EXT + 1];   // the plan's rows: ext_row entries by wire index (odd stride)
     __shared__ uint8_t ext_ord[FMT ? TILE : 1][FAST_EXT + 4];   // emission order (formats 1/2)
     __shared__ unsigned long long tile_base;
 #if MFP_EXT_WIN == 2 && MFP_EXT_WIN_BLOCKS > 4
@@ -263,7 +263,6 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         bool live;
         mfp_pkt_desc dsc;
         tile_take<true>(P, tile, count, tsort, tid, i, dsc, live);
-        const uint8_t *data = P.arena + dsc.offset;
 
         // reservation from the bound: one atomic per tile
         const uint32_t bound = live ? (2 * dsc.caplen + 64 < FP_MAX ? 2 * dsc.caplen + 64 : FP_MAX) : 0u;
@@ -303,6 +302,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
         plan.off_row = ext_off[tid];
         plan.ord_row = ext_ord[FMT ? tid : 0];
         // free until the emission: the extension-header window (ExtWin)
+        const uint8_t *data = P.arena + dsc.offset;
         plan.win = MFP_EXT_WIN == 2 ? (uint8_t *)&out_line[0][0] + 4096 * wid : (uint8_t *)out_line[tid];
         plan.win_lane = (uint32_t)lane;
 #if MFP_EXT_WIN == 2 && MFP_EXT_WIN_BLOCKS > 4

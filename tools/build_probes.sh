@@ -1,7 +1,8 @@
 #!/bin/bash
 # profiling variants of libmercury_amd.so (never shipped: mercury_amd/_probe/)
 # usage: tools/build_probes.sh NAME:MACRO[,MACRO] ...
-#   an_*: mfp_analysis.hip only; tls_* / http_*: that family's walker TU only; quic_*: mfp_quic.hip;
+#   an_*: mfp_analysis.hip only; tls_* / http_*: that family's walker TU only (tlsk_* / httpk_*: and
+#   mfp_kernels.hip, k_classify); quic_*: mfp_quic.hip;
 #   anything else: every walker TU
 set -e
 cd "$(dirname "$0")/.."
@@ -19,7 +20,8 @@ for spec in "$@"; do
   (  # fingerprint probes: recompile the walker translation units
     objs=""
     tus="mfp_kernels mfp_k_tls mfp_k_http mfp_k_small mfp_k_all"
-    case $name in tls_*) tus=mfp_k_tls ;; http_*) tus=mfp_k_http ;; quic_*) tus=mfp_quic ;; esac   # probes of one family
+    case $name in tls_*) tus=mfp_k_tls ;; tlsk_*) tus="mfp_k_tls mfp_kernels" ;; http_*) tus=mfp_k_http ;;
+                  httpk_*) tus="mfp_k_http mfp_kernels" ;; quic_*) tus=mfp_quic ;; esac   # probes of one family (+ k_classify)
     for k in $tus; do
       hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $defs -c mercury_amd/csrc/$k.hip \
         -o mercury_amd/_probe/k_${name}_$k.o & objs="$objs mercury_amd/_probe/k_${name}_$k.o"
