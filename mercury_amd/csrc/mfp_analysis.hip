@@ -131,43 +131,8 @@ ADEV uint64_t word_at(const uint8_t *s, uint32_t len, uint32_t j) {
 // string-relative 8-byte words j0 .. j0+B-1 of s[0, len) (bytes past len read
 // as 0), from B+1 aligned 8-byte loads issued together: one memory round
 // trip per 8*B bytes; never reads an aligned word past the last byte
-// MFP_AN_LW16: from B/2+1 aligned 16-byte loads instead of B+1 8-byte ones (the
-// lane-per-item kernels are bound by their scattered vector-memory accesses);
-// reads up to 15 bytes past the last byte (the pool is padded, packets'
-// last 16-byte blocks are readable, include/mfp.h)
-#ifndef MFP_AN_LW16
-#define MFP_AN_LW16 0
-#endif
 template <int B>
 ADEV void load_words(const uint8_t *s, uint32_t len, uint32_t j0, uint64_t (&w)[B]) {
-#if MFP_AN_LW16
-    static_assert(B % 2 == 0, "B even");
-    {
-        const uintptr_t p0 = (uintptr_t)s + 8 * (uintptr_t)j0;
-        const uintptr_t base = p0 & ~(uintptr_t)15;
-        const uint32_t q = (uint32_t)(p0 >> 3) & 1u, sh = (uint32_t)(p0 & 7) * 8;
-        const uintptr_t end = (uintptr_t)s + len;
-        uint64_t a[B + 2];
-#pragma unroll
-        for (int k = 0; k <= B / 2; k++) {
-            const uintptr_t p = base + 16 * (uintptr_t)k;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (p < end) v = *(const uint4 *)p;
-            a[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-            a[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        }
-#pragma unroll
-        for (int k = 0; k < B; k++) {
-            const uint64_t lo = q ? a[k + 1] : a[k], hi = q ? a[k + 2] : a[k + 1];
-            uint64_t x = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
-            const uint32_t pos = 8 * (j0 + k);
-            if (pos >= len) x = 0;
-            else if (len - pos < 8) x &= (1ull << (8 * (len - pos))) - 1;
-            w[k] = x;
-        }
-        return;
-    }
-#endif
     const uintptr_t base = (uintptr_t)s & ~(uintptr_t)7;
     const uint32_t sh = (uint32_t)((uintptr_t)s & 7) * 8;
     const uintptr_t end = (uintptr_t)s + len;

@@ -1237,7 +1237,6 @@ int mfp_classifier_upload(mfp_classifier *c, int device) {
         insert_string_slot(t.dom_slots, mfpc::str_hash((const uint8_t *)kv.first.data(), (uint32_t)kv.first.size()),
                            kv.second, pool_add(t, kv.first), (uint32_t)kv.first.size());
     if (t.pool.empty()) t.pool.push_back(0);
-    t.pool.insert(t.pool.end(), 16, 0);   // (16-byte loads of a string's last block stay inside)
     if (t.upd.empty()) t.upd.push_back(mfp_update{0, 0, 0});
     if (t.prior.empty()) { t.prior.push_back(0); t.proc_id.push_back(0); t.proc_mal.push_back(0); t.proc_attr.push_back(0); }
     if (t.entry.empty()) t.entry.push_back(mfp_entry{0, 0, 0, 0, 0, 0, 0, 0});

@@ -212,39 +212,11 @@ DEV uint64_t swar_alpha(uint64_t w) {                  // isalpha (ASCII)
 #ifndef MFP_SWB
 #define MFP_SWB 4
 #endif
-// MFP_SWAR16: the 32 bytes of a round trip from two aligned 16-byte loads
-#ifndef MFP_SWAR16
-#define MFP_SWAR16 0
-#endif
 // (w0: when given, receives the first round's words, from p & ~7)
 template <class F>
 DEV const uint8_t *swar_find(const uint8_t *p, const uint8_t *e, F flag, uint64_t *w0 = nullptr) {
     if (!p || p >= e) return e;
     const uintptr_t ee = (uintptr_t)e;
-#if MFP_SWAR16
-    {
-        const uintptr_t pp = (uintptr_t)p;
-        uintptr_t a = pp & ~(uintptr_t)15;
-        while (true) {
-            const uint4 z = make_uint4(0, 0, 0, 0);
-            const uint4 x0 = *(const uint4 *)a, x1 = a + 16 < ee ? *(const uint4 *)(a + 16) : z;
-            const uint64_t w[4] = {(uint64_t)x0.x | (uint64_t)x0.y << 32, (uint64_t)x0.z | (uint64_t)x0.w << 32,
-                                   (uint64_t)x1.x | (uint64_t)x1.y << 32, (uint64_t)x1.z | (uint64_t)x1.w << 32};
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uintptr_t ak = a + 8 * k;
-                if (ak >= ee) return e;
-                if (ak + 8 <= pp) continue;                      // (first round) wholly before p
-                uint64_t m = flag(w[k]);
-                if (ak < pp) m &= ~0ull << (8 * (pp - ak));
-                const uintptr_t in = ee - ak;
-                if (in < 8) m &= (1ull << (8 * in)) - 1;
-                if (m) return (const uint8_t *)(ak + (__builtin_ctzll(m) >> 3));
-            }
-            a += 32;
-        }
-    }
-#endif
     uintptr_t a = (uintptr_t)p & ~(uintptr_t)7;
     uint64_t m0 = ~0ull << (8 * ((uintptr_t)p & 7));   // bytes before p in the first word
     while (true) {
