@@ -83,8 +83,9 @@ BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8
                   "k_fp_ldsILb0ELj36864ELj1E": 12,
                   # the HTTP segment walker with the header loop's windowed delimiter tests
                   # (MFP_HTTP_FAST 2, round 4): 8 bytes at its 128-VGPR cap; the HTTP HBM
-                  # lane walker (not a default bin kernel) with both delimiter paths 28 -> 36
-                  "k_fp_segILj4E": 8}
+                  # lane walker (not a default bin kernel) with both delimiter paths 28 -> 36;
+                  # round 6: the ':' search's words kept for the value and delimiter (MFP_HTTP_WIN) 8 -> 16
+                  "k_fp_segILj4E": 16}
 
 
 def test_classifier_and_crypto_kernels_use_no_scratch():
