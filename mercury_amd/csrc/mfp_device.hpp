@@ -258,6 +258,74 @@ DEV uint32_t cparse_to_delims(Cur &dst, Cur &r, uint8_t d1, uint8_t d2) {   // d
     dst.e = r.e;
     return 0;
 }
+// A lane's last SWB loaded words (from a, words at or past the range end e
+// left zero) kept across searches of one line: swar_find_w looks there first
+// when p lies inside, and records the last round it loads (MFP_HTTP_WIN).
+// Precondition: the later searches' ends do not pass the recorded e.
+struct SWin {
+    uint64_t w[MFP_SWB];
+    uintptr_t a = 0, e = 0;
+};
+template <class F>
+DEV const uint8_t *swar_find_w(const uint8_t *p, const uint8_t *e, F flag, SWin &W) {
+    if (!p || p >= e) return e;
+    const uintptr_t pp = (uintptr_t)p, ee = (uintptr_t)e;
+    uintptr_t a;
+    uint64_t m0;
+    if (W.a && pp >= W.a && pp < W.a + 8 * MFP_SWB && ee <= W.e) {
+#pragma unroll
+        for (int k = 0; k < MFP_SWB; k++) {
+            const uintptr_t ak = W.a + 8 * (uintptr_t)k;
+            if (ak + 8 <= pp) continue;
+            if (ak >= ee) return e;
+            uint64_t m = flag(W.w[k]);
+            if (ak < pp) m &= ~0ull << (8 * (pp - ak));
+            const uintptr_t in = ee - ak;
+            if (in < 8) m &= (1ull << (8 * in)) - 1;
+            if (m) return (const uint8_t *)(ak + (__builtin_ctzll(m) >> 3));
+        }
+        a = W.a + 8 * MFP_SWB;
+        m0 = ~0ull;
+        if (a >= ee) return e;
+    } else {
+        a = pp & ~(uintptr_t)7;
+        m0 = ~0ull << (8 * (pp & 7));
+    }
+    while (true) {
+#pragma unroll
+        for (int k = 0; k < MFP_SWB; k++) W.w[k] = a + 8 * k < ee ? *(const uint64_t *)(a + 8 * k) : 0ull;
+        W.a = a;
+        W.e = ee;
+#pragma unroll
+        for (int k = 0; k < MFP_SWB; k++) {
+            const uintptr_t ak = a + 8 * k;
+            if (ak >= ee) return e;
+            uint64_t m = flag(W.w[k]) & (k == 0 ? m0 : ~0ull);
+            const uintptr_t in = ee - ak;
+            if (in < 8) m &= (1ull << (8 * in)) - 1;
+            if (m) return (const uint8_t *)(ak + (__builtin_ctzll(m) >> 3));
+        }
+        a += 8 * MFP_SWB;
+        m0 = ~0ull;
+    }
+}
+// cparse_to_delim / cparse_to_delims through the window (the delimiter's value is not read)
+DEV void cparse_to_delim_w(Cur &dst, Cur &r, uint8_t delim, SWin &W) {
+    if (!cnotempty(r)) { cset_null(r); cset_null(dst); return; }
+    dst.d = r.d;
+    const uint8_t *q = swar_find_w(r.d, r.e, [=](uint64_t w) { return swar_eq(w, delim); }, W);
+    if (q < r.e) { dst.e = r.d = q; return; }
+    dst.e = r.e;
+}
+DEV void cparse_to_delims_w(Cur &dst, Cur &r, uint8_t d1, uint8_t d2, SWin &W) {
+    dst.d = r.d;
+    if (r.d) {
+        const uint8_t *q = swar_find_w(r.d, r.e, [=](uint64_t w) { return swar_eq(w, d1) | swar_eq(w, d2); }, W);
+        r.d = q;
+        if (q < r.e) { dst.e = q; return; }
+    }
+    dst.e = r.e;
+}
 DEV bool ccompare_n(Cur c, const uint8_t *x, long n) {        // datum::compare_nbytes datum.h:873
     if (!(c.d && clen(c) >= n)) return false;
     for (long i = 0; i < n; i++) if (ld(c.d + i) != ld(x + i)) return false;
@@ -1686,21 +1754,37 @@ DEV void name_list_parse(Cur &nl, Cur &p) {             // name_list::parse ssh.
     if (l > 2048) { if (p.d) p.d = p.e; return; }
     cparse(nl, p, (long)l);
 }
-template <class E>
-DEV bool ssh_kex_fp(E *b, Cur payload) {                // ssh_kex_init::fingerprint ssh.h:240
-    Cur p = payload, t, nl[10];
+// The 10 name-lists of a KEXINIT, parsed once for the check and the
+// fingerprint: each as offset << 16 | length from the payload's start, ~0u
+// when null (ssh_kex_init::parse ssh.h:190; a payload is at most 16 KiB, a
+// list at most 2048 bytes)
+struct SshKex {
+    uint32_t nl[10];
+    bool ok;                                            // the kex_algorithms list is not empty
+};
+DEV SshKex ssh_kex_parse(Cur payload) {
+    SshKex k;
+    Cur p = payload, t;
     cparse(t, p, 1);
     cparse(t, p, 16);
-    for (int i = 0; i < 10; i++) { cset_null(nl[i]); name_list_parse(nl[i], p); }
-    if (!cnotempty(nl[0])) return false;
-    if (b) {
-        for (int i = 0; i < 10; i++) {
-            b->putc('(');
-            if (cnotempty(nl[i])) b->hex(nl[i].d, clen(nl[i]));
-            b->putc(')');
-        }
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        Cur l;
+        cset_null(l);
+        name_list_parse(l, p);
+        k.nl[i] = cnull(l) ? ~0u : ((uint32_t)(l.d - payload.d) << 16) | (uint32_t)clen(l);
     }
-    return true;
+    k.ok = k.nl[0] != ~0u && (k.nl[0] & 0xffff) != 0;
+    return k;
+}
+template <class E>
+DEV void ssh_kex_fp(E &b, Cur payload, const SshKex &k) {   // ssh_kex_init::fingerprint ssh.h:240
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        b.putc('(');
+        if (k.nl[i] != ~0u && (k.nl[i] & 0xffff)) b.hex(payload.d + (k.nl[i] >> 16), (long)(k.nl[i] & 0xffff));
+        b.putc(')');
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2235,9 +2319,13 @@ template <class E>
 DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
     Cur f1, f2, f3;   // req: method, protocol ; resp: version, status, reason
     cset_null(f1); cset_null(f2); cset_null(f3);
+    // (MFP_HTTP_WIN, segment walker) the line's searches share their loaded words
+    constexpr bool LW = E::SEG && MFP_HTTP_WIN && MFP_HTTP_FAST < 3;
+    SWin W;
     if (req) {
         Cur uri;
-        cparse_to_delim(f1, p, ' ');
+        if (LW) cparse_to_delim_w(f1, p, ' ', W);
+        else cparse_to_delim(f1, p, ' ');
         long ml = clen(f1);
         if (ml < 3 || ml > 16) return false;
 #if MFP_HTTP_FAST >= 3
@@ -2259,6 +2347,19 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         cparse_to_delims(f2, p, '\r', '\n');
         if (!(f2.d && clen(f2) >= 5 && h5 == 0x2f50545448ull)) return false;   // "HTTP/"
 #else
+        if constexpr (LW) {
+            if (swar_find_w(f1.d, f1.e, [](uint64_t w) { return ~swar_upper(w) & 0x8080808080808080ull; }, W) < f1.e)
+                return false;
+            cskip(p, 1);
+            cparse_to_delim_w(uri, p, ' ', W);
+            cskip(p, 1);
+            cparse_to_delims_w(f2, p, '\r', '\n', W);
+            if (!(f2.d && clen(f2) >= 5)) return false;
+            const uintptr_t fa = (uintptr_t)f2.d;
+            const uint64_t h5 = W.a && fa >= W.a && fa + 8 <= W.a + 8 * MFP_SWB ? win_get8(W.w, W.a, fa)
+                                                                               : ld_le8n(f2.d, 5);
+            if ((h5 & 0xffffffffffull) != 0x2f50545448ull) return false;   // "HTTP/" (f2 holds 5 bytes)
+        } else {
         if (swar_find(f1.d, f1.e, [](uint64_t w) { return ~swar_upper(w) & 0x8080808080808080ull; }) < f1.e) return false;
         cskip(p, 1);
         cparse_to_delim(uri, p, ' ');
@@ -2267,7 +2368,15 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         if (!(f2.d && clen(f2) >= 5 && ld(f2.d) == 'H' && ld(f2.d + 1) == 'T' && ld(f2.d + 2) == 'T' &&
               ld(f2.d + 3) == 'P' && ld(f2.d + 4) == '/'))
             return false;
+        }
 #endif
+    } else if constexpr (LW) {
+        cparse_to_delim_w(f1, p, ' ', W);
+        cskip(p, 1);
+        cparse_to_delim_w(f2, p, ' ', W);
+        cskip(p, 1);
+        cparse_to_delims_w(f3, p, '\r', '\n', W);
+        if (!cnotempty(f2)) return false;
     } else {
         cparse_to_delim(f1, p, ' ');
         cskip(p, 1);
@@ -2277,7 +2386,8 @@ DEV bool http_msg(E &b, Cur p, bool req, Out &o, const uint8_t *base) {
         if (!cnotempty(f2)) return false;
     }
     Cur delim; delim.d = p.d;
-    if (p.d) p.d = swar_find(p.d, p.e, [](uint64_t w) { return swar_alpha(w); });
+    if (p.d) p.d = LW ? swar_find_w(p.d, p.e, [](uint64_t w) { return swar_alpha(w); }, W)
+                      : swar_find(p.d, p.e, [](uint64_t w) { return swar_alpha(w); });
     delim.e = p.d;
     fp_type_prefix(b, req ? 3 : 4);
     b.putc('('); b.hex(f1.d, clen(f1)); b.putc(')');
@@ -2539,9 +2649,11 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         cskip(p, 1);
         bool kex = false;
         SshBin bin; cset_null(bin.payload); bin.more = 0;
+        SshKex kx;
+        kx.ok = false;
         if (cnotempty(p)) {
             bin = ssh_bin_parse(p);
-            if (cnotempty(bin.payload)) kex = ssh_kex_fp<E>(nullptr, bin.payload);
+            if (cnotempty(bin.payload)) { kx = ssh_kex_parse(bin.payload); kex = kx.ok; }
         }
         uint64_t more = kex ? bin.more : 8192;
         if (more) o.flags |= MFP_FLAG_TRUNCATED;
@@ -2551,7 +2663,7 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         if (kex) {
             o.fp_type = server ? 18 : 5;
             fp_type_prefix(b, o.fp_type);
-            ssh_kex_fp(&b, bin.payload);
+            ssh_kex_fp(b, bin.payload, kx);
         } else {
             o.fp_type = server ? 20 : 17;
             fp_type_prefix(b, o.fp_type);
@@ -2584,11 +2696,12 @@ DEV void tcp_data(E &b, const Cfg &cfg, Out &o, Cur pkt, const uint8_t *tcph, co
         if (bin.more) o.flags |= MFP_FLAG_TRUNCATED;
         if (bin.more) o.more = (uint32_t)bin.more;     // pkt_proc.cc:563-569
         else o.seg_kind |= MFP_SEG_SUPPLEMENTARY;
-        if (!ssh_kex_fp<E>(nullptr, bin.payload)) return;
+        const SshKex kx = ssh_kex_parse(bin.payload);
+        if (!kx.ok) return;
         o.flags |= MFP_FLAG_EMIT;
         o.fp_type = server ? 19 : 6;
         fp_type_prefix(b, o.fp_type);
-        ssh_kex_fp(&b, bin.payload);
+        ssh_kex_fp(b, bin.payload, kx);
         return;
         }
     }
