@@ -56,30 +56,6 @@ DEV uint64_t ld_be(const uint8_t *p, int n) {          // n = 1..8
     if (n <= 4) return ld_be32n(p, n);
     return ((uint64_t)ld_be32n(p, 4) << (8 * (n - 4))) | ld_be32n(p + 4, n - 4);
 }
-// consecutive little-endian 4-byte groups of p[0, len): one aligned dword
-// load per group
-struct LeStream {
-    const uint32_t *q;
-    uint32_t sh, prev;
-    long left;
-    DEV void init(const uint8_t *p, long len) {
-        const uintptr_t a = (uintptr_t)p;
-        q = (const uint32_t *)(a & ~(uintptr_t)3);
-        sh = (uint32_t)(a & 3) * 8;
-        left = len;
-        prev = len > 0 ? q[0] : 0u;
-    }
-    DEV uint32_t next() {                      // bytes past the end read as garbage; callers mask
-        const long take = left < 4 ? left : 4;
-        const bool need_hi = left > 4 || (sh && (long)(sh / 8) + take > 4);
-        const uint32_t hi = need_hi ? q[1] : 0u;
-        const uint32_t v = sh ? (prev >> sh) | (hi << (32 - sh)) : prev;
-        prev = hi;
-        q++;
-        left -= 4;
-        return v;
-    }
-};
 // up to 32 bytes of p[0, len) as eight little-endian 4-byte groups, from the
 // aligned dwords that hold them, all loads issued before any is used (one
 // memory round trip per 32 bytes instead of one per 4); groups past len hold
@@ -97,38 +73,6 @@ struct LeBlock {
         for (int k = 0; k < 9; k++) w[k] = k < ndw ? q[k] : 0u;
 #pragma unroll
         for (int k = 0; k < 8; k++) v[k] = sh ? (w[k] >> sh) | (w[k + 1] << (32 - sh)) : w[k];
-    }
-};
-// LeBlock from the aligned 16-byte blocks that hold the bytes (at most 3 load
-// instructions per 32 bytes instead of 9), realigned in registers.  Global
-// memory only (k_fp_tls1 / k_fp_seg emission: Em's WIDE parameter,
-// MFP_LEBLOCK16); the LDS-staged walker keeps LeBlock.
-#ifndef MFP_LEBLOCK16
-#define MFP_LEBLOCK16 0
-#endif
-struct LeBlock16 {
-    uint32_t v[8];
-    DEV void load(const uint8_t *p, long len) {
-        const uintptr_t a = (uintptr_t)p;
-        const uint4 *q4 = (const uint4 *)(a & ~(uintptr_t)15);
-        const uint32_t off = (uint32_t)(a & 15);
-        const long nb = len < 32 ? len : 32;
-        const uint32_t nq = (uint32_t)((off + nb + 15) >> 4);   // 1..3
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        const uint4 x0 = q4[0], x1 = nq > 1 ? q4[1] : z, x2 = nq > 2 ? q4[2] : z;
-        // scalars, not an array: a select between two array elements would
-        // become a load from a selected address (private memory)
-#define MFP_LB16_W(i)                                                                                   \
-    ((i) == 0 ? x0.x : (i) == 1 ? x0.y : (i) == 2 ? x0.z : (i) == 3 ? x0.w : (i) == 4 ? x1.x : (i) == 5 ? x1.y \
-     : (i) == 6 ? x1.z : (i) == 7 ? x1.w : (i) == 8 ? x2.x : (i) == 9 ? x2.y : (i) == 10 ? x2.z : x2.w)
-        const uint32_t s4 = off >> 2, sb = off & 3;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t lo = s4 == 0 ? MFP_LB16_W(k) : s4 == 1 ? MFP_LB16_W(k + 1) : s4 == 2 ? MFP_LB16_W(k + 2) : MFP_LB16_W(k + 3);
-            const uint32_t hi = s4 == 0 ? MFP_LB16_W(k + 1) : s4 == 1 ? MFP_LB16_W(k + 2) : s4 == 2 ? MFP_LB16_W(k + 3) : MFP_LB16_W(k + 4);
-            v[k] = __builtin_amdgcn_alignbyte(hi, lo, sb);
-        }
-#undef MFP_LB16_W
     }
 };
 // 4 bytes (b0 lowest) -> 8 lowercase hex characters, little-endian (b0's high nibble first)
@@ -355,14 +299,13 @@ struct TlsPlan;
 // FAST >= 0 (k_fp_tls1, TLS format FAST): pass 1 records the ClientHello plan
 // with the string's length by arithmetic (tls_ch_plan_fast), pass 2 emits it
 // with tls_ch_emit_fast
-template <bool EMIT, int FAST_FMT = -1, int LINEW = 8, bool WIDE = false>
+template <bool EMIT, int FAST_FMT = -1, int LINEW = 8>
 struct Em {
     uint32_t n = 0;          // bytes produced
     bool last_putc = false;
     bool punt = false;       // the message needs a parser family this walker lacks
     DEV void punt_pkt() { punt = true; }
     static constexpr int FAST = FAST_FMT;
-    static constexpr bool WIDE_LOADS = WIDE;   // hex_run reads global memory with LeBlock16
     static constexpr bool PLAN = !EMIT;   // pass 1 records a ClientHello plan (TlsPlan) in *plan
     TlsPlan *plan = nullptr;              // set by every kernel that runs pass 1 on TLS/DTLS packets
     static constexpr bool SEG = false;
@@ -402,30 +345,10 @@ struct Em {
         if (out_end && out + 8 * ((words + 1) & ~1u) > out_end) return;   // (an over-long string: dropped anyway)
         for (uint32_t k = 0; 2 * k < words; k++) o4[k] = l4[k];
     }
-    // LINEW == 2: the pending word stays in registers and every second word
-    // leaves with one 16-byte store (no LDS line): lanes reach a store at
-    // different pushes, and a wave then issues one store instruction there
-    // instead of an 8-word line's four LDS reads and four stores
-    uint64_t w0 = 0;
     DEV void put_word() {
         h ^= mfpc::word_term(acc, wi++);
-        if constexpr (LINEW == 2) {
-            if (nw == 0) { w0 = acc; nw = 1; return; }
-            store2(acc);
-            out += 16;
-            nw = 0;
-            return;
-        }
         line[nw++] = acc;
         if (nw == (uint32_t)LINEW) { flush_line(LINEW); out += 8 * LINEW; nw = 0; }
-    }
-    DEV void store2(uint64_t w1) {
-#ifdef MFP_PROBE_NOSTORE
-        if (w1 == 0x0123456789abcdefull) *(volatile uint8_t *)out = 0;
-        return;
-#endif
-        if (out_end && out + 16 > out_end) return;   // (an over-long string: dropped anyway)
-        *(uint4 *)out = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
     }
     DEV void push(uint64_t v, uint32_t k) {     // append k (1..8) bytes, little-endian in v (zero above)
         if (EMIT) {
@@ -445,11 +368,6 @@ struct Em {
     }
     DEV void finish() {
         if (EMIT) {
-            if constexpr (LINEW == 2) {
-                if (nacc) { put_word(); nacc = 0; }
-                if (nw) store2(0);
-                return;
-            }
             if (nacc) { h ^= mfpc::word_term(acc, wi++); line[nw++] = acc; nacc = 0; }
             if (nw) flush_line(nw);
         }
@@ -538,7 +456,6 @@ DEV uint32_t seg_src(uint32_t s) { return s >> 15; }
 struct HdrKey;
 struct SegEm {
     static constexpr bool SEG = true;
-    static constexpr bool WIDE_LOADS = false;
     // (MFP_HTTP_NAMEWIN) LDS copies of the header-name tables, set by k_fp_seg
     const uint8_t *slots_req = nullptr, *slots_resp = nullptr;
     const HdrKey *keys_req = nullptr, *keys_resp = nullptr;
@@ -702,21 +619,10 @@ DEV uint64_t low_chars(uint64_t v, uint32_t k) { return k >= 8 ? v : (v & ((1ull
 // even) of p[0, len), 4 bytes -> 8 characters per push
 template <bool DEGREASE, class E>
 DEV void hex_run(E &b, const uint8_t *p, uint32_t len) {
-#ifdef MFP_HEXRUN_STREAM   // (A/B: one dword load per 4 bytes)
-    LeStream s;
-    s.init(p, (long)len);
-    for (uint32_t i = 0; i < len; i += 4) {
-        uint32_t w = s.next();
-        if (DEGREASE) w = degrease_pairs(w);
-        const uint32_t c = len - i >= 4 ? 8u : 2 * (len - i);
-        b.push(low_chars(hex4(w), c), c);
-    }
-    return;
-#endif
     // 32 bytes per round trip: the block's dword loads are all issued before
     // the first is used (LeBlock), then 8 characters per push
     for (uint32_t i0 = 0; i0 < len; i0 += 32) {
-        typename std::conditional<E::WIDE_LOADS, LeBlock16, LeBlock>::type blk;
+        LeBlock blk;
 #ifdef MFP_PROBE_HEXRUN_NOLOAD   // (profiling probe only: the value loads' cost)
 #pragma unroll
         for (int k = 0; k < 8; k++) blk.v[k] = (uint32_t)(uintptr_t)p + i0 + k;

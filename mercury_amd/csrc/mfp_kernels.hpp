@@ -236,11 +236,6 @@ __global__ __launch_bounds__(TILE, FAM == FAM_TLS ? MFP_TLS_MINW : MFP_LANE_MINW
 #ifndef MFP_TLS_ONEPASS
 #define MFP_TLS_ONEPASS 1
 #endif
-// emission line in words: 8 (a 64-byte LDS line per lane, four 16-byte
-// stores per full line) or 2 (no LDS line: one 16-byte store per two words)
-#ifndef MFP_TLS_LINEW
-#define MFP_TLS_LINEW 8
-#endif
 template <int FMT>
 __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint32_t *fallback) {
     __shared__ uint32_t wave_tot[TILE / 64];
@@ -345,7 +340,7 @@ __global__ __launch_bounds__(TILE, MFP_TLS_MINW) void k_fp_tls1(KParams P, uint3
 #else
         if (len && fits) {
 #endif
-            Em<true, -1, MFP_TLS_LINEW, MFP_LEBLOCK16 != 0> e;   // the packet is in HBM
+            Em<true> e;                                          // the packet is in HBM
             e.begin(P.fp_arena + base + excl, out_line[tid]);
             tls_ch_emit_fast<FMT>(e, plan);
             e.finish();
@@ -404,7 +399,7 @@ constexpr uint32_t SEG_STAGE = 2048;      // packets up to this (minus alignment
 #ifndef MFP_SEG_LINEW
 #define MFP_SEG_LINEW 4
 #endif
-constexpr int SEG_LINEW = MFP_SEG_LINEW;  // lane emission: words per LDS line (2: no LDS line, Em)
+constexpr int SEG_LINEW = MFP_SEG_LINEW;  // lane emission: words per LDS line
 template <uint32_t FAM = FAM_HTTP>
 __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32_t *fallback) {
     __shared__ uint32_t segs[TILE * SEG_STRIDE];
@@ -510,7 +505,7 @@ __global__ __launch_bounds__(TILE, MFP_SEG_MINW) void k_fp_seg(KParams P, uint32
         KPH(1);
 #if MFP_SEG_LANE
         if (len && fits) {
-            Em<true, -1, SEG_LINEW, MFP_LEBLOCK16 != 0> em;   // the packet is in HBM
+            Em<true, -1, SEG_LINEW> em;                          // the packet is in HBM
             em.begin(P.fp_arena + base + excl, out_line[tid]);
             seg_emit_lane(em, segs + tid * SEG_STRIDE, e.nseg, data, pool);
             em.finish();
