@@ -57,22 +57,28 @@ DEV uint64_t ld_be(const uint8_t *p, int n) {          // n = 1..8
     return ((uint64_t)ld_be32n(p, 4) << (8 * (n - 4))) | ld_be32n(p + 4, n - 4);
 }
 // up to 32 bytes of p[0, len) as eight little-endian 4-byte groups, from the
-// aligned dwords that hold them, all loads issued before any is used (one
-// memory round trip per 32 bytes instead of one per 4); groups past len hold
-// garbage the caller masks.  Only dwords holding requested bytes are read.
+// aligned 8-byte words that hold them (at most 5 loads per 32 bytes: the lane
+// walkers are bound by their scattered accesses, round 6 r06/r06aa_*), all
+// issued before any is used and realigned with static word indices; groups past
+// len hold garbage the caller masks.  Only words holding requested bytes are
+// read (within the 16-byte block of a packet's last byte, include/mfp.h).
 struct LeBlock {
     uint32_t v[8];
     DEV void load(const uint8_t *p, long len) {
         const uintptr_t a = (uintptr_t)p;
-        const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(a & 3) * 8;
+        const uint64_t *q = (const uint64_t *)(a & ~(uintptr_t)7);
+        const uint32_t sh = (uint32_t)(a & 7) * 8;
         const long nb = len < 32 ? len : 32;
-        const int ndw = (int)(((long)(sh / 8) + nb + 3) / 4);   // 1..9
-        uint32_t w[9];
+        const int nqw = (int)(((long)(sh / 8) + nb + 7) / 8);   // 1..5
+        uint64_t w[5];
 #pragma unroll
-        for (int k = 0; k < 9; k++) w[k] = k < ndw ? q[k] : 0u;
+        for (int k = 0; k < 5; k++) w[k] = k < nqw ? q[k] : 0ull;
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = sh ? (w[k] >> sh) | (w[k + 1] << (32 - sh)) : w[k];
+        for (int j = 0; j < 4; j++) {
+            const uint64_t x = sh ? (w[j] >> sh) | (w[j + 1] << (64 - sh)) : w[j];
+            v[2 * j] = (uint32_t)x;
+            v[2 * j + 1] = (uint32_t)(x >> 32);
+        }
     }
 };
 // 4 bytes (b0 lowest) -> 8 lowercase hex characters, little-endian (b0's high nibble first)

@@ -75,7 +75,9 @@ def kernel_scratch():
 # the path (tcp_other_matcher & co., round 4): +8 and +32 bytes.  k_fp_tls1
 # (one instance per TLS format, round 4: plan length by arithmetic, uniform
 # emitter) spills nothing for formats 0 and 1 and 8 bytes for format 2.
-BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8, "k_an_features": 20, "k_fingerprintILj2E": 176, "k_fingerprintILj4E": 36,
+BOUNDED_SCRATCH = {"k_fp_tls1ILi0E": 0, "k_fp_tls1ILi1E": 0, "k_fp_tls1ILi2E": 8, "k_an_features": 20, "k_fingerprintILj2E": 176,
+                  # the HTTP HBM lane walker (not a default bin kernel): 36 -> 64 with the 8-byte-word hex loads (round 6)
+                  "k_fingerprintILj4E": 64,
                   "k_fingerprintILj16E": 496, "k_fingerprintILj63E": 944, "k_fp_ldsILb0ELj36864ELj63E": 176,
                   "k_fp_ldsILb0ELj36864ELj2E": 176,
                   # the one-parse transport parameter sort (round 4): the LDS TLS walker +12, the DTLS
